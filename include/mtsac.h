@@ -1,0 +1,186 @@
+/*
+ * mtsac.h -- C-ABI of the MI355X multi-task SAC update engine (libmtsac.so).
+ *
+ * Drop-in boundary for the reference's MTSAC hot path.  Every entry point
+ * cites the reference interface it replaces (paths relative to the
+ * reginald-mclean/mtrl tree):
+ *
+ *   mtsac_create / mtsac_destroy   MTSAC.initialize      mtrl/rl/algorithms/mtsac.py:153-284
+ *                                  (device state instead of a flax PyTree)
+ *   mtsac_set_params/get_params    TrainState params / opt_state leaves
+ *                                  mtrl/rl/algorithms/utils.py:11-46, mtsac.py:197-256
+ *   mtsac_buffer_add               MultiTaskReplayBuffer.add        mtrl/rl/buffers.py:426-474
+ *   mtsac_buffer_write             MultiTaskReplayBuffer.load_checkpoint data  buffers.py:326-335
+ *   mtsac_buffer_read              MultiTaskReplayBuffer.checkpoint data       buffers.py:308-324
+ *   mtsac_buffer_set/get_state     pos / full fields                buffers.py:306,337-343
+ *   mtsac_rng_set / mtsac_rng_get  buffer _rng PCG64 state          buffers.py:260,323,335
+ *   mtsac_sample                   MultiTaskReplayBuffer.sample(int) buffers.py:494-549
+ *   mtsac_update                   MTSAC.update -> _update_inner     mtsac.py:1173-1251
+ *   mtsac_get_logs                 the update's LogDict              mtsac.py:1241-1247
+ *   mtsac_eval_action              MTSAC.eval_action / _eval_action  mtsac.py:80-84,306-311
+ *   mtsac_sample_action            MTSAC.sample_action               mtsac.py:70-77,298-304
+ *   mtsac_comm_*                   (new) task-sharded data parallelism over RCCL; the
+ *                                  reference is single-device
+ *
+ * Conventions
+ *   - Return value: 0 on success, a negative errno-style code on failure; the
+ *     thread-local message is available from mtsac_last_error().  Nothing aborts.
+ *   - The engine owns all device memory.  Callers own every pointer they pass;
+ *     pointers are borrowed for the duration of the call only.  Data pointers may
+ *     be host or device (HIP unified addressing: hipMemcpyDefault).
+ *   - One engine per GPU per process.  All work of an engine is serialised on its
+ *     own HIP stream; mtsac_get_logs / mtsac_sample / mtsac_get_params are the
+ *     synchronisation points.
+ *   - Parameter vectors use the flax leaf order (ravel_pytree order) of the
+ *     reference networks: head bias, head kernel, layer_0 bias, layer_0 kernel,
+ *     layer_1 ... (critic leaves carry the leading ensemble axis).  With task
+ *     sharding (task_count < num_tasks) the head leaves hold only the local tasks.
+ */
+#ifndef MTSAC_H_
+#define MTSAC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTSAC_ABI_VERSION 1
+#define MTSAC_NUM_LOGS 10
+
+/* log slots, order of mtsac.py:1241-1247 (critic, actor, alpha logs) */
+enum mtsac_log_slot {
+  MTSAC_LOG_QF_VALUES = 0,          /* losses/qf_values                */
+  MTSAC_LOG_QF_LOSS = 1,            /* losses/qf_loss                  */
+  MTSAC_LOG_CRITIC_GRAD_NORM = 2,   /* metrics/critic_grad_magnitude   */
+  MTSAC_LOG_CRITIC_PARAMS_NORM = 3, /* metrics/critic_params_norm      */
+  MTSAC_LOG_ACTOR_LOSS = 4,         /* losses/actor_loss               */
+  MTSAC_LOG_ACTOR_GRAD_NORM = 5,    /* metrics/actor_grad_magnitude    */
+  MTSAC_LOG_ACTOR_PARAMS_NORM = 6,  /* metrics/actor_params_norm       */
+  MTSAC_LOG_EXPLORE_LOSS = 7,       /* metrics/explore_loss (always 0) */
+  MTSAC_LOG_ALPHA_LOSS = 8,         /* losses/alpha_loss               */
+  MTSAC_LOG_ALPHA = 9               /* alpha = sum(exp(log_alpha))     */
+};
+
+/* which parameter / optimizer vector mtsac_{get,set}_params addresses */
+enum mtsac_tensor {
+  MTSAC_ACTOR = 0,
+  MTSAC_CRITIC = 1,
+  MTSAC_CRITIC_TARGET = 2,
+  MTSAC_LOG_ALPHA_PARAMS = 3,
+  MTSAC_ACTOR_ADAM_MU = 4,
+  MTSAC_ACTOR_ADAM_NU = 5,
+  MTSAC_CRITIC_ADAM_MU = 6,
+  MTSAC_CRITIC_ADAM_NU = 7,
+  MTSAC_ALPHA_ADAM_MU = 8,
+  MTSAC_ALPHA_ADAM_NU = 9
+};
+
+enum mtsac_precision {
+  MTSAC_FP32 = 0 /* exact-f32 MFMA (v_mfma_f32_32x32x2_f32), fp32 everywhere */
+};
+
+/* Hyper-parameters: MTSACConfig (mtsac.py:116-127) + AlgorithmConfig
+ * (config/rl.py:16-22) + ContinuousActionPolicyConfig / QValueFunctionConfig
+ * (config/networks.py:6-31) + MultiHeadConfig (config/nn.py:8-31,63) +
+ * OptimizerConfig (config/optim.py:14-43) + OffPolicyTrainingConfig
+ * (config/rl.py:47-50). */
+typedef struct mtsac_config {
+  int32_t num_tasks;        /* T: width of the one-hot at the end of obs       */
+  int32_t task_begin;       /* first task owned by this engine (sharding)      */
+  int32_t task_count;       /* tasks owned by this engine (= T unsharded)      */
+  int32_t obs_dim;          /* observation width incl. one-hot (39 + T)        */
+  int32_t action_dim;       /* A (4)                                           */
+  int32_t actor_width, actor_depth;
+  int32_t critic_width, critic_depth;
+  int32_t num_critics;      /* ensemble size (2)                               */
+  int32_t batch_per_task;   /* B / T (128)                                     */
+  int64_t capacity;         /* slots per task = buffer_size // T               */
+  float gamma, tau;
+  float actor_lr, critic_lr, alpha_lr;
+  float actor_max_grad_norm, critic_max_grad_norm, alpha_max_grad_norm; /* <=0: no clip */
+  float adam_b1, adam_b2, adam_eps;
+  float initial_temperature;
+  float log_std_min, log_std_max;
+  int32_t clip;             /* clip y and Q to +-5000 (mtsac.py:557-560)        */
+  int32_t use_task_weights; /* mtsac.py:103-113                                 */
+  int32_t normalize_rewards;/* per-task min/max (buffers.py:534-538)            */
+  int32_t precision;        /* enum mtsac_precision                             */
+  uint64_t noise_seed;      /* device N(0,1) stream used when no eps is injected */
+} mtsac_config;
+
+/* A batch laid out like ReplayBufferSamples (types.py:49-54): rows of this
+ * engine's tasks, row = i * task_count + local_task. */
+typedef struct mtsac_batch {
+  const float* observations;      /* [B_local][obs_dim]    */
+  const float* actions;           /* [B_local][action_dim] */
+  const float* next_observations; /* [B_local][obs_dim]    */
+  const float* dones;             /* [B_local]             */
+  const float* rewards;           /* [B_local]             */
+} mtsac_batch;
+
+typedef struct mtsac_engine mtsac_engine;
+
+const char* mtsac_last_error(void);
+int mtsac_abi_version(void);
+void mtsac_default_config(mtsac_config* cfg, int32_t num_tasks);
+
+int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out);
+void mtsac_destroy(mtsac_engine* h);
+
+/* parameters / optimizer state, flax leaf order, fp32 */
+int64_t mtsac_param_count(const mtsac_engine* h, int which);
+int mtsac_set_params(mtsac_engine* h, int which, const float* src, int64_t n);
+int mtsac_get_params(mtsac_engine* h, int which, float* dst, int64_t n);
+int mtsac_set_adam_count(mtsac_engine* h, int which /*0 actor,1 critic,2 alpha*/, int32_t count);
+int mtsac_get_adam_count(mtsac_engine* h, int which, int32_t* count);
+
+/* replay buffer (device resident; layout documented in DESIGN.md) */
+int mtsac_buffer_add(mtsac_engine* h, const float* obs, const float* next_obs, const float* actions,
+                     const float* rewards, const float* dones);
+int mtsac_buffer_write(mtsac_engine* h, int64_t slot_begin, int64_t n_slots, const float* obs,
+                       const float* next_obs, const float* actions, const float* rewards,
+                       const float* dones);
+int mtsac_buffer_read(mtsac_engine* h, int64_t slot_begin, int64_t n_slots, float* obs, float* next_obs,
+                      float* actions, float* rewards, float* dones);
+int mtsac_buffer_fill_synthetic(mtsac_engine* h, uint64_t seed);
+int mtsac_buffer_set_state(mtsac_engine* h, int64_t pos, int32_t full);
+int mtsac_buffer_get_state(mtsac_engine* h, int64_t* pos, int32_t* full);
+int mtsac_buffer_set_reward_stats(mtsac_engine* h, const double* min_r, const double* max_r);
+int mtsac_rng_set(mtsac_engine* h, uint64_t state_hi, uint64_t state_lo, uint64_t inc_hi,
+                  uint64_t inc_lo, int32_t has_uint32, uint32_t uinteger);
+int mtsac_rng_get(mtsac_engine* h, uint64_t* state_hi, uint64_t* state_lo, uint64_t* inc_hi,
+                  uint64_t* inc_lo, int32_t* has_uint32, uint32_t* uinteger);
+/* draw one batch with the device index stream and copy it (and the indices) out */
+int mtsac_sample(mtsac_engine* h, int64_t* indices, float* obs, float* actions, float* next_obs,
+                 float* dones, float* rewards);
+
+/* one gradient step.  batch == NULL: sample from the device buffer.
+ * eps_next / eps_cur ([B_local][A] N(0,1) noise for a' ~ pi(.|s') and a ~ pi(.|s));
+ * both NULL: device counter-based normal stream. */
+int mtsac_update(mtsac_engine* h, const mtsac_batch* batch, const float* eps_next, const float* eps_cur);
+/* run `steps` device-sampled, device-noise updates (hipGraph replay when enabled) */
+int mtsac_update_many(mtsac_engine* h, int32_t steps);
+int mtsac_get_logs(mtsac_engine* h, float* logs /* MTSAC_NUM_LOGS */);
+int mtsac_enable_graph(mtsac_engine* h, int32_t enable);
+int mtsac_synchronize(mtsac_engine* h);
+
+/* rollout side */
+int mtsac_eval_action(mtsac_engine* h, const float* obs, int32_t n, float* actions);
+int mtsac_sample_action(mtsac_engine* h, const float* obs, int32_t n, const float* eps, float* actions);
+
+/* multi-GPU: RCCL communicator over the shared-trunk gradients */
+int mtsac_comm_unique_id_size(void);
+int mtsac_comm_get_unique_id(void* id_out);
+int mtsac_comm_init(mtsac_engine* h, const void* unique_id, int32_t nranks, int32_t rank);
+
+/* measurement: per-kernel-family HIP event timing of the last update_many call */
+int mtsac_set_timing(mtsac_engine* h, int32_t enable);
+int mtsac_get_timing(mtsac_engine* h, int32_t family, double* total_ms, int32_t* launches,
+                     double* flops);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTSAC_H_ */

@@ -1,0 +1,1173 @@
+// engine.cpp -- the MTSAC update engine behind include/mtsac.h (C-ABI).
+//
+// Orchestrates one multi-task SAC gradient step (reference _update_inner,
+// mtrl/rl/algorithms/mtsac.py:1173-1247) as a fixed sequence of HIP kernels on one
+// stream: device index stream + gather, actor forward on s' (a', logpi'), target
+// critic (y), critic forward/backward, clip+Adam+Polyak, actor forward, critic
+// forward with the UPDATED critic, critic data-grad into the action columns,
+// actor backward, clip+Adam, temperature update.  Every pointer is fixed at
+// creation, so the whole step is captured once into a hipGraph and replayed.
+//
+// Task sharding (multi-GPU): an engine owns tasks [task_begin, task_begin+task_count);
+// trunk parameters are replicated, heads are local.  Per network one RCCL
+// all-reduce(sum) runs over the contiguous trunk-gradient range plus a small
+// scalar tail (local head |g|^2, loss sums, temperature grads), so the global
+// clip norm and the logged losses equal the single-device ones.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mtsac.h"
+#include "../../include/mtsac_debug.h"
+#include "kernels.h"
+
+using namespace mtsac;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      return fail(-5, std::string(#expr) + ": " + hipGetErrorString(_e));                  \
+  } while (0)
+
+constexpr int MAXD = 8;
+constexpr long long ALIGN = 64;  // floats (256 B)
+constexpr int EXTRA = 128;       // scalar tail of each gradient buffer (all-reduced with the trunk)
+constexpr int PART = 1024;       // max partial-sum blocks
+
+long long align_up(long long x, long long a) { return (x + a - 1) / a * a; }
+
+struct Net {
+  int in_dim = 0, in_ld = 0, width = 0, depth = 0, T_l = 0, hd = 0, E = 1;
+  long long off_hb = 0, off_hW = 0, off_b[MAXD] = {}, off_W[MAXD] = {};
+  long long ms_hb = 0, ms_hW = 0, ms_b = 0, ms_W[MAXD] = {};  // member strides
+  long long n_flat = 0, trunk_off = 0, n_params = 0;
+  std::vector<std::pair<long long, long long>> leaves;  // (offset, count) in flax order
+  float *p = nullptr, *g = nullptr, *m = nullptr, *v = nullptr, *tgt = nullptr;
+  OptScalars* sc = nullptr;
+
+  void layout(int in, int in_ld_, int W, int D, int T, int hd_, int E_) {
+    in_dim = in; in_ld = in_ld_; width = W; depth = D; T_l = T; hd = hd_; E = E_;
+    long long o = 0;
+    auto leaf = [&](long long member, long long& off, long long& ms) {
+      off = o;
+      ms = member;
+      leaves.push_back({o, member * E});
+      n_params += member * E;
+      o = align_up(o + member * E, ALIGN);
+    };
+    leaf((long long)T * hd, off_hb, ms_hb);
+    leaf((long long)T * W * hd, off_hW, ms_hW);
+    trunk_off = o;
+    int fan = in;
+    for (int i = 0; i < D; ++i) {
+      leaf(W, off_b[i], ms_b);
+      leaf((long long)fan * W, off_W[i], ms_W[i]);
+      fan = W;
+    }
+    n_flat = o;
+  }
+};
+
+}  // namespace
+
+struct mtsac_engine {
+  mtsac_config cfg{};
+  int device = 0;
+  hipStream_t st = nullptr;
+  int T_l = 0, T_g = 0, A = 0, D = 0, B = 0, n = 0, R = 0, ld_a = 0, ld_c = 0, B_glob = 0;
+  Net actor, critic;
+  // replay
+  float* store = nullptr;
+  long long* buf_size = nullptr;  // device: pos or capacity
+  long long h_pos = 0;
+  int h_full = 0;
+  PcgDev* rng = nullptr;
+  unsigned long long* jump = nullptr;
+  int* idx = nullptr;
+  double *rmin = nullptr, *rmax = nullptr;
+  std::vector<double> h_rmin, h_rmax;
+  // inputs
+  float *xa = nullptr, *xan = nullptr, *xc = nullptr, *xcn = nullptr, *xcp = nullptr;
+  float *rew = nullptr, *done = nullptr, *tw = nullptr;
+  int* task = nullptr;
+  int *counts = nullptr, *rows = nullptr;
+  // user-batch staging
+  float *u_obs = nullptr, *u_act = nullptr, *u_nobs = nullptr, *u_done = nullptr, *u_rew = nullptr;
+  float *eps_n = nullptr, *eps_c = nullptr;
+  // activations / grads
+  float* ha[MAXD] = {};
+  float* hc[MAXD] = {};
+  float *dza[2] = {}, *dzc[2] = {};
+  float *logpi_n = nullptr, *logpi = nullptr, *y = nullptr, *dq = nullptr, *row_a = nullptr, *row_b = nullptr,
+        *row_c = nullptr, *alpha_w = nullptr, *cache = nullptr, *dout_a = nullptr;
+  float* partials = nullptr;
+  float* log_alpha = nullptr;
+  float *la_m = nullptr, *la_v = nullptr;
+  OptScalars* sc_alpha = nullptr;
+  float* logs = nullptr;
+  unsigned long long* counter = nullptr;
+  int* err = nullptr;
+  // rollout
+  int roll_max = 0;
+  float *r_obs = nullptr, *r_x = nullptr, *r_eps = nullptr, *r_act = nullptr, *r_lp = nullptr, *r_dummy = nullptr;
+  float* r_h[MAXD] = {};
+  int* r_task = nullptr;
+  // graph
+  bool use_graph = true;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  bool graph_timed = false;
+  // comm
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  // timing
+  bool timing = false;
+  struct TimedLaunch {
+    int family;
+    double flops;
+    hipEvent_t a, b;
+  };
+  std::vector<TimedLaunch> tl;
+  size_t tl_next = 0;
+  std::vector<void*> allocs;
+
+  ~mtsac_engine() {
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    if (graph) (void)hipGraphDestroy(graph);
+    for (auto& t : tl) {
+      (void)hipEventDestroy(t.a);
+      (void)hipEventDestroy(t.b);
+    }
+    if (comm) ncclCommDestroy(comm);
+    for (void* p : allocs) (void)hipFree(p);
+    if (st) (void)hipStreamDestroy(st);
+  }
+
+  template <typename T>
+  int alloc(T** p, size_t count) {
+    void* q = nullptr;
+    size_t bytes = std::max<size_t>(count * sizeof(T), 256);
+    bytes = (bytes + 255) / 256 * 256;
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess) return fail(-12, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+    e = hipMemset(q, 0, bytes);
+    if (e != hipSuccess) return fail(-5, std::string("hipMemset failed: ") + hipGetErrorString(e));
+    allocs.push_back(q);
+    *p = reinterpret_cast<T*>(q);
+    return 0;
+  }
+
+  // ------------------------------------------------------------ timing hooks
+  void t_begin(int family, double flops) {
+    if (!timing) return;
+    if (tl_next >= tl.size()) {
+      TimedLaunch x{};
+      (void)hipEventCreate(&x.a);
+      (void)hipEventCreate(&x.b);
+      tl.push_back(x);
+    }
+    tl[tl_next].family = family;
+    tl[tl_next].flops = flops;
+    (void)hipEventRecord(tl[tl_next].a, st);
+  }
+  void t_end() {
+    if (!timing) return;
+    (void)hipEventRecord(tl[tl_next].b, st);
+    ++tl_next;
+  }
+
+  void gemm(const GemmParams& p, GemmKind kind, int epi, int batch) {
+    t_begin((int)kind, 2.0 * (double)p.M * p.N * p.K * batch);
+    gemm_f32(p, kind, epi, batch, st);
+    t_end();
+  }
+
+  // ------------------------------------------------------------ trunk passes
+  // acts[i] = relu(in_i @ W_i + b_i) for every member (batched over the ensemble)
+  void trunk_forward(Net& net, const float* params, const float* X, int ldx, float** acts, int M) {
+    for (int i = 0; i < net.depth; ++i) {
+      GemmParams g{};
+      g.A = (i == 0) ? X : acts[i - 1];
+      g.lda = (i == 0) ? ldx : net.width;
+      g.sA = (i == 0) ? 0 : (long long)M * net.width;
+      g.B = params + net.off_W[i];
+      g.ldb = net.width;
+      g.sB = net.ms_W[i];
+      g.C = acts[i];
+      g.ldc = net.width;
+      g.sC = (long long)M * net.width;
+      g.bias = params + net.off_b[i];
+      g.sBias = net.ms_b;
+      g.M = M;
+      g.N = net.width;
+      g.K = (i == 0) ? net.in_dim : net.width;
+      gemm(g, GEMM_NN, EPI_BIAS_RELU, net.E);
+    }
+  }
+
+  // dz_top: grad at the last trunk layer's pre-activation.  Walks down computing weight
+  // grads (if wgrad) and dz of lower layers; returns the buffer holding dz of layer 0.
+  float* trunk_backward(Net& net, const float* params, const float* X, int ldx, float** acts, float* dz_top,
+                        float** dzbuf, bool wgrad, int M) {
+    float* dz = dz_top;
+    int which = (dz_top == dzbuf[0]) ? 1 : 0;
+    for (int i = net.depth - 1; i >= 0; --i) {
+      if (wgrad) {
+        GemmParams g{};
+        g.A = (i == 0) ? X : acts[i - 1];  // [K=rows][M=fan_in] storage -> TA
+        g.lda = (i == 0) ? ldx : net.width;
+        g.sA = (i == 0) ? 0 : (long long)M * net.width;
+        g.B = dz;
+        g.ldb = net.width;
+        g.sB = (long long)M * net.width;
+        g.C = net.g + net.off_W[i];
+        g.ldc = net.width;
+        g.sC = net.ms_W[i];
+        g.db = net.g + net.off_b[i];
+        g.sDb = net.ms_b;
+        g.M = (i == 0) ? net.in_dim : net.width;
+        g.N = net.width;
+        g.K = M;
+        gemm(g, GEMM_TN, EPI_STORE, net.E);
+      }
+      if (i > 0) {
+        GemmParams g{};
+        g.A = dz;
+        g.lda = net.width;
+        g.sA = (long long)M * net.width;
+        g.B = params + net.off_W[i];  // W_i (fan_in x W) == [N=fan_in][K=W]
+        g.ldb = net.width;
+        g.sB = net.ms_W[i];
+        g.C = dzbuf[which];
+        g.ldc = net.width;
+        g.sC = (long long)M * net.width;
+        g.mask = acts[i - 1];
+        g.ldm = net.width;
+        g.sMask = (long long)M * net.width;
+        g.M = M;
+        g.N = net.width;
+        g.K = net.width;
+        gemm(g, GEMM_NT, EPI_RELU_MASK, net.E);
+        dz = dzbuf[which];
+        which ^= 1;
+      }
+    }
+    return dz;
+  }
+
+  HeadParams head(Net& net, const float* params, const float* h, int M, const int* tsk) {
+    HeadParams hp{};
+    hp.h = h;
+    hp.Wh = params + net.off_hW;
+    hp.bh = params + net.off_hb;
+    hp.task = tsk;
+    hp.B = M;
+    hp.W = net.width;
+    hp.hd = net.hd;
+    hp.E = net.E;
+    hp.sWh = net.ms_hW;
+    hp.sbh = net.ms_hb;
+    hp.sh = (long long)M * net.width;
+    return hp;
+  }
+
+  void allreduce(float* buf, size_t count) {
+    if (comm == nullptr || nranks <= 1) return;
+    ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm, st);
+  }
+
+  // clip + Adam (+ Polyak) over one network; gradient already complete (and reduced)
+  void optimize(Net& net, float lr, float max_norm, bool polyak) {
+    float* extra = net.g + net.n_flat;
+    int np = sumsq_partials(net.g + net.trunk_off, net.n_flat - net.trunk_off, partials, PART, st);
+    grad_norm_finalize(partials, np, extra + 0, max_norm, net.sc, st);
+    AdamParams a{};
+    a.p = net.p;
+    a.m = net.m;
+    a.v = net.v;
+    a.g = net.g;
+    a.target = polyak ? net.tgt : nullptr;
+    a.n = net.n_flat;
+    a.lr = lr;
+    a.b1 = cfg.adam_b1;
+    a.b2 = cfg.adam_b2;
+    a.eps = cfg.adam_eps;
+    a.tau = cfg.tau;
+    a.sc = net.sc;
+    a.p_partials = partials;
+    int na = adam_update(a, max_norm, PART, st);
+    param_norm_finalize(partials, na, net.sc, st);
+  }
+
+  void head_sq(Net& net) {  // local |g_head|^2 into the scalar tail
+    int np = sumsq_partials(net.g, net.trunk_off, partials, PART, st);
+    sum_partials(partials, np, net.g + net.n_flat + 0, st);
+  }
+
+  // ------------------------------------------------------------ one gradient step
+  void step(bool device_batch, bool device_noise) {
+    const int Bl = B;
+    GatherParams gp = gather_params();
+    if (device_batch) {
+      replay_indices(rng, jump, buf_size, n, idx, st);
+      replay_gather(gp, st);
+    } else {
+      batch_scatter(gp, u_obs, u_act, u_nobs, u_done, u_rew, Bl, st);
+    }
+    task_rows(task, Bl, T_l, counts, rows, Bl, st);
+    if (cfg.use_task_weights) row_alpha(task, cfg.task_begin, log_alpha, T_g, Bl, 1, row_c, tw, st);
+    const float* twp = cfg.use_task_weights ? tw : nullptr;
+
+    // ---- critic update (mtsac.py:513-621)
+    trunk_forward(actor, actor.p, xan, ld_a, ha, Bl);
+    PolicyParams pp{};
+    pp.head = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
+    pp.eps = device_noise ? nullptr : eps_n;
+    pp.seed = cfg.noise_seed;
+    pp.counter = counter;
+    pp.stream_id = 1;
+    pp.A = A;
+    pp.ls_min = cfg.log_std_min;
+    pp.ls_max = cfg.log_std_max;
+    pp.a_out = xcn;
+    pp.ld_a_out = ld_c;
+    pp.logpi = logpi_n;
+    policy_head(pp, st);
+
+    trunk_forward(critic, critic.tgt, xcn, ld_c, hc, Bl);
+    CriticHeadParams ch{};
+    ch.head = head(critic, critic.tgt, hc[critic.depth - 1], Bl, task);
+    ch.mode = CH_TARGET;
+    ch.rew = rew;
+    ch.done = done;
+    ch.logpi = logpi_n;
+    ch.log_alpha = log_alpha;
+    ch.task = task;
+    ch.task_begin = cfg.task_begin;
+    ch.y_out = y;
+    ch.tw = twp;
+    ch.gamma = cfg.gamma;
+    ch.clip = cfg.clip;
+    ch.T_glob = T_g;
+    critic_head(ch, st);
+
+    trunk_forward(critic, critic.p, xc, ld_c, hc, Bl);
+    ch.head = head(critic, critic.p, hc[critic.depth - 1], Bl, task);
+    ch.mode = CH_CRITIC;
+    ch.y = y;
+    ch.dq = dq;
+    ch.row_a = row_a;
+    ch.row_b = row_b;
+    ch.inv_norm = 1.0f / ((float)critic.E * (float)B_glob);
+    critic_head(ch, st);
+
+    HeadParams chp = head(critic, critic.p, hc[critic.depth - 1], Bl, task);
+    head_backward_weight(chp, dq, Bl, counts, rows, Bl, critic.g + critic.off_hW, critic.g + critic.off_hb, st);
+    head_backward_data(chp, dq, Bl, dzc[0], st);
+    trunk_backward(critic, critic.p, xc, ld_c, hc, dzc[0], dzc, true, Bl);
+    {
+      const float* ins[2] = {row_a, row_b};
+      reduce_rows(ins, 2, Bl, critic.g + critic.n_flat + 1, st);
+    }
+    head_sq(critic);
+    allreduce(critic.g + critic.trunk_off, (size_t)(critic.n_flat - critic.trunk_off + EXTRA));
+    optimize(critic, cfg.critic_lr, cfg.critic_max_grad_norm, true);
+
+    // ---- actor update (mtsac.py:623-711), critic params already updated
+    trunk_forward(actor, actor.p, xa, ld_a, ha, Bl);
+    pp.head = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
+    pp.eps = device_noise ? nullptr : eps_c;
+    pp.stream_id = 2;
+    pp.a_out = xcp;
+    pp.logpi = logpi;
+    pp.cache = cache;
+    policy_head(pp, st);
+
+    trunk_forward(critic, critic.p, xcp, ld_c, hc, Bl);
+    ch.head = head(critic, critic.p, hc[critic.depth - 1], Bl, task);
+    ch.mode = CH_ACTOR;
+    ch.logpi = logpi;
+    ch.dq = dq;
+    ch.row_a = row_c;
+    ch.alpha_w = alpha_w;
+    ch.inv_norm = 1.0f / (float)B_glob;
+    critic_head(ch, st);
+    head_backward_data(ch.head, dq, Bl, dzc[0], st);
+    float* dz0 = trunk_backward(critic, critic.p, xcp, ld_c, hc, dzc[0], dzc, false, Bl);
+    ActionGradParams ag{};
+    ag.dz1 = dz0;
+    ag.W0 = critic.p + critic.off_W[0];
+    ag.s_dz = (long long)Bl * critic.width;
+    ag.s_W0 = critic.ms_W[0];
+    ag.E = critic.E;
+    ag.B = Bl;
+    ag.Wc = critic.width;
+    ag.A = A;
+    ag.cache = cache;
+    ag.alpha_w = alpha_w;
+    ag.ls_min = cfg.log_std_min;
+    ag.ls_max = cfg.log_std_max;
+    ag.dout = dout_a;
+    action_grad(ag, st);
+
+    HeadParams ahp = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
+    head_backward_weight(ahp, dout_a, 0, counts, rows, Bl, actor.g + actor.off_hW, actor.g + actor.off_hb, st);
+    head_backward_data(ahp, dout_a, 0, dza[0], st);
+    trunk_backward(actor, actor.p, xa, ld_a, ha, dza[0], dza, true, Bl);
+    {
+      const float* ins[1] = {row_c};
+      reduce_rows(ins, 1, Bl, actor.g + actor.n_flat + 1, st);
+    }
+    // temperature gradient rides in the actor's scalar tail: [2] loss part, [3..] grad
+    AlphaParams al = alpha_params();
+    alpha_grad(al, st);
+    head_sq(actor);
+    allreduce(actor.g + actor.trunk_off, (size_t)(actor.n_flat - actor.trunk_off + EXTRA));
+    optimize(actor, cfg.actor_lr, cfg.actor_max_grad_norm, false);
+
+    // ---- temperature (mtsac.py:713-731)
+    alpha_adam(al, cfg.alpha_lr, cfg.adam_b1, cfg.adam_b2, cfg.adam_eps, cfg.alpha_max_grad_norm, st);
+
+    LogParams lp{};
+    lp.critic_sums = critic.g + critic.n_flat + 1;
+    lp.actor_sums = actor.g + actor.n_flat + 1;
+    lp.critic = critic.sc;
+    lp.actor = actor.sc;
+    lp.alpha_loss_sum = actor.g + actor.n_flat + 2;
+    lp.log_alpha = log_alpha;
+    lp.T_glob = T_g;
+    lp.inv_critic = 1.0f / ((float)critic.E * (float)B_glob);
+    lp.inv_actor = 1.0f / (float)B_glob;
+    lp.inv_b = 1.0f / (float)B_glob;
+    lp.logs = logs;
+    write_logs(lp, st);
+    bump_counter(counter, st);
+  }
+
+  AlphaParams alpha_params() {
+    AlphaParams al{};
+    al.logpi = logpi;
+    al.counts = counts;
+    al.rows = rows;
+    al.max_rows = B;
+    al.T_l = T_l;
+    al.task_begin = cfg.task_begin;
+    al.T_glob = T_g;
+    al.B_glob = B_glob;
+    al.target_entropy = -(float)A;
+    al.log_alpha = log_alpha;
+    al.m = la_m;
+    al.v = la_v;
+    al.grad = actor.g + actor.n_flat + 3;
+    al.loss_part = actor.g + actor.n_flat + 2;
+    al.sc = sc_alpha;
+    return al;
+  }
+
+  GatherParams gather_params() {
+    GatherParams gp{};
+    gp.store = store;
+    gp.idx = idx;
+    gp.n = n;
+    gp.T_l = T_l;
+    gp.R = R;
+    gp.obs_dim = D;
+    gp.act_dim = A;
+    gp.T_glob = T_g;
+    gp.task_begin = cfg.task_begin;
+    gp.ld_a = ld_a;
+    gp.ld_c = ld_c;
+    gp.xa = xa;
+    gp.xa_next = xan;
+    gp.xc = xc;
+    gp.xc_next = xcn;
+    gp.xc_pi = xcp;
+    gp.rew = rew;
+    gp.done = done;
+    gp.task = task;
+    gp.rmin = cfg.normalize_rewards ? rmin : nullptr;
+    gp.rmax = cfg.normalize_rewards ? rmax : nullptr;
+    gp.norm_eps = 1e-8;
+    gp.err = err;
+    return gp;
+  }
+
+  int check_err() {
+    int e = 0;
+    HIP_TRY(hipMemcpyAsync(&e, err, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (e) {
+      int z = 0;
+      HIP_TRY(hipMemcpy(err, &z, sizeof(int), hipMemcpyHostToDevice));
+      return fail(-22,
+                  "batch rows must end in an exact one-hot task id owned by this engine (obs and next_obs agree)");
+    }
+    return 0;
+  }
+};
+
+// ================================================================ C-ABI
+extern "C" {
+
+const char* mtsac_last_error(void) { return g_last_error.c_str(); }
+int mtsac_abi_version(void) { return MTSAC_ABI_VERSION; }
+
+void mtsac_default_config(mtsac_config* c, int32_t T) {
+  std::memset(c, 0, sizeof(*c));
+  c->num_tasks = T;
+  c->task_begin = 0;
+  c->task_count = T;
+  c->obs_dim = 39 + T;
+  c->action_dim = 4;
+  c->actor_width = 400;
+  c->actor_depth = 3;
+  c->critic_width = 400;
+  c->critic_depth = 3;
+  c->num_critics = 2;
+  c->batch_per_task = 128;
+  c->capacity = 100000;
+  c->gamma = 0.99f;
+  c->tau = 0.005f;
+  c->actor_lr = c->critic_lr = c->alpha_lr = 3e-4f;
+  c->actor_max_grad_norm = 1.0f;
+  c->critic_max_grad_norm = 1.0f;
+  c->alpha_max_grad_norm = 0.0f;
+  c->adam_b1 = 0.9f;
+  c->adam_b2 = 0.999f;
+  c->adam_eps = 1e-5f;
+  c->initial_temperature = 1.0f;
+  c->log_std_min = -20.0f;
+  c->log_std_max = 2.0f;
+  c->precision = MTSAC_FP32;
+  c->noise_seed = 2;
+}
+
+static int pcg_jump_table(unsigned long long* out /* 65*4 */) {
+  // state_{j} = A_j s + C_j inc;  A_0 = 1, C_0 = 0;  A_{j+1} = M A_j, C_{j+1} = M C_j + 1
+  typedef unsigned __int128 u128h;
+  const u128h M = ((u128h)0x2360ED051FC65DA4ull << 64) | (u128h)0x4385DF649FCCF645ull;
+  u128h a = 1, c = 0;
+  for (int j = 0; j <= 64; ++j) {
+    out[4 * j + 0] = (unsigned long long)(a >> 64);
+    out[4 * j + 1] = (unsigned long long)a;
+    out[4 * j + 2] = (unsigned long long)(c >> 64);
+    out[4 * j + 3] = (unsigned long long)c;
+    a = a * M;
+    c = c * M + 1;
+  }
+  return 0;
+}
+
+int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
+  if (!cfg || !out) return fail(-22, "null argument");
+  *out = nullptr;
+  const mtsac_config& c = *cfg;
+  if (c.num_tasks < 1 || c.task_count < 1 || c.task_begin < 0 || c.task_begin + c.task_count > c.num_tasks)
+    return fail(-22, "invalid task range");
+  if (c.task_count > 64) return fail(-22, "at most 64 tasks per engine");
+  if (c.num_tasks > EXTRA - 8) return fail(-22, "num_tasks too large");
+  if (c.action_dim < 1 || c.action_dim > 4) return fail(-22, "action_dim must be in [1, 4]");
+  if (c.obs_dim < c.num_tasks) return fail(-22, "obs_dim must include the one-hot task id");
+  if (c.actor_width % 4 || c.critic_width % 4 || c.actor_width <= 0 || c.critic_width <= 0)
+    return fail(-22, "network widths must be positive multiples of 4");
+  if (c.actor_depth < 1 || c.actor_depth > MAXD || c.critic_depth < 1 || c.critic_depth > MAXD)
+    return fail(-22, "depth must be in [1, 8]");
+  if (c.num_critics < 1 || c.num_critics > 4) return fail(-22, "num_critics must be in [1, 4]");
+  if (c.batch_per_task < 1) return fail(-22, "batch_per_task must be positive");
+  if (c.capacity < c.batch_per_task || c.capacity >= (1ll << 31))
+    return fail(-22, "capacity must be in [batch_per_task, 2^31)");
+  if (c.precision != MTSAC_FP32) return fail(-22, "unsupported precision");
+  hipError_t he = hipSetDevice(hip_device);
+  if (he != hipSuccess) return fail(-19, std::string("hipSetDevice: ") + hipGetErrorString(he));
+
+  auto* e = new mtsac_engine();
+  e->cfg = c;
+  e->device = hip_device;
+  e->T_l = c.task_count;
+  e->T_g = c.num_tasks;
+  e->A = c.action_dim;
+  e->D = c.obs_dim;
+  e->n = c.batch_per_task;
+  e->B = c.batch_per_task * c.task_count;
+  e->B_glob = c.batch_per_task * c.num_tasks;
+  e->R = (int)align_up(2LL * e->D + e->A + 2, 4);
+  e->ld_a = (int)align_up(e->D, 4);
+  e->ld_c = (int)align_up(e->D + e->A, 4);
+  e->roll_max = std::max(64, c.num_tasks);
+  int rc = 0;
+  auto bad = [&](int r) {
+    delete e;
+    return r;
+  };
+  if (hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) != hipSuccess) return bad(fail(-5, "stream"));
+
+  e->actor.layout(e->D, e->ld_a, c.actor_width, c.actor_depth, e->T_l, 2 * e->A, 1);
+  e->critic.layout(e->D + e->A, e->ld_c, c.critic_width, c.critic_depth, e->T_l, 1, c.num_critics);
+  for (Net* net : {&e->actor, &e->critic}) {
+    if ((rc = e->alloc(&net->p, net->n_flat))) return bad(rc);
+    if ((rc = e->alloc(&net->g, net->n_flat + EXTRA))) return bad(rc);
+    if ((rc = e->alloc(&net->m, net->n_flat))) return bad(rc);
+    if ((rc = e->alloc(&net->v, net->n_flat))) return bad(rc);
+    if ((rc = e->alloc(&net->sc, 1))) return bad(rc);
+  }
+  if ((rc = e->alloc(&e->critic.tgt, e->critic.n_flat))) return bad(rc);
+
+  const int B = e->B;
+  if ((rc = e->alloc(&e->store, (size_t)c.capacity * e->T_l * e->R))) return bad(rc);
+  if ((rc = e->alloc(&e->buf_size, 1))) return bad(rc);
+  if ((rc = e->alloc(&e->rng, 1))) return bad(rc);
+  if ((rc = e->alloc(&e->jump, 65 * 4))) return bad(rc);
+  if ((rc = e->alloc(&e->idx, e->n))) return bad(rc);
+  if ((rc = e->alloc(&e->rmin, e->T_l))) return bad(rc);
+  if ((rc = e->alloc(&e->rmax, e->T_l))) return bad(rc);
+  if ((rc = e->alloc(&e->xa, (size_t)B * e->ld_a))) return bad(rc);
+  if ((rc = e->alloc(&e->xan, (size_t)B * e->ld_a))) return bad(rc);
+  if ((rc = e->alloc(&e->xc, (size_t)B * e->ld_c))) return bad(rc);
+  if ((rc = e->alloc(&e->xcn, (size_t)B * e->ld_c))) return bad(rc);
+  if ((rc = e->alloc(&e->xcp, (size_t)B * e->ld_c))) return bad(rc);
+  for (float** p : {&e->rew, &e->done, &e->tw, &e->logpi_n, &e->logpi, &e->y, &e->row_a, &e->row_b, &e->row_c,
+                    &e->alpha_w, &e->u_done, &e->u_rew})
+    if ((rc = e->alloc(p, B))) return bad(rc);
+  if ((rc = e->alloc(&e->task, B))) return bad(rc);
+  if ((rc = e->alloc(&e->counts, e->T_l))) return bad(rc);
+  if ((rc = e->alloc(&e->rows, (size_t)e->T_l * B))) return bad(rc);
+  if ((rc = e->alloc(&e->u_obs, (size_t)B * e->D))) return bad(rc);
+  if ((rc = e->alloc(&e->u_nobs, (size_t)B * e->D))) return bad(rc);
+  if ((rc = e->alloc(&e->u_act, (size_t)B * e->A))) return bad(rc);
+  if ((rc = e->alloc(&e->eps_n, (size_t)B * e->A))) return bad(rc);
+  if ((rc = e->alloc(&e->eps_c, (size_t)B * e->A))) return bad(rc);
+  for (int i = 0; i < c.actor_depth; ++i)
+    if ((rc = e->alloc(&e->ha[i], (size_t)B * c.actor_width))) return bad(rc);
+  for (int i = 0; i < c.critic_depth; ++i)
+    if ((rc = e->alloc(&e->hc[i], (size_t)c.num_critics * B * c.critic_width))) return bad(rc);
+  for (int i = 0; i < 2; ++i) {
+    if ((rc = e->alloc(&e->dza[i], (size_t)B * c.actor_width))) return bad(rc);
+    if ((rc = e->alloc(&e->dzc[i], (size_t)c.num_critics * B * c.critic_width))) return bad(rc);
+  }
+  if ((rc = e->alloc(&e->dq, (size_t)c.num_critics * B))) return bad(rc);
+  if ((rc = e->alloc(&e->cache, (size_t)B * 5 * e->A))) return bad(rc);
+  if ((rc = e->alloc(&e->dout_a, (size_t)B * 2 * e->A))) return bad(rc);
+  if ((rc = e->alloc(&e->partials, PART))) return bad(rc);
+  if ((rc = e->alloc(&e->log_alpha, e->T_g))) return bad(rc);
+  if ((rc = e->alloc(&e->la_m, e->T_g))) return bad(rc);
+  if ((rc = e->alloc(&e->la_v, e->T_g))) return bad(rc);
+  if ((rc = e->alloc(&e->sc_alpha, 1))) return bad(rc);
+  if ((rc = e->alloc(&e->logs, MTSAC_NUM_LOGS))) return bad(rc);
+  if ((rc = e->alloc(&e->counter, 1))) return bad(rc);
+  if ((rc = e->alloc(&e->err, 1))) return bad(rc);
+  // rollout workspace
+  const int rm = e->roll_max;
+  if ((rc = e->alloc(&e->r_obs, (size_t)rm * e->D))) return bad(rc);
+  if ((rc = e->alloc(&e->r_x, (size_t)rm * e->ld_a))) return bad(rc);
+  if ((rc = e->alloc(&e->r_eps, (size_t)rm * e->A))) return bad(rc);
+  if ((rc = e->alloc(&e->r_act, (size_t)rm * e->A))) return bad(rc);
+  if ((rc = e->alloc(&e->r_lp, rm))) return bad(rc);
+  if ((rc = e->alloc(&e->r_dummy, (size_t)rm * (e->ld_c + 4)))) return bad(rc);
+  if ((rc = e->alloc(&e->r_task, rm))) return bad(rc);
+  for (int i = 0; i < c.actor_depth; ++i)
+    if ((rc = e->alloc(&e->r_h[i], (size_t)rm * c.actor_width))) return bad(rc);
+
+  unsigned long long jt[65 * 4];
+  pcg_jump_table(jt);
+  if (hipMemcpy(e->jump, jt, sizeof(jt), hipMemcpyHostToDevice) != hipSuccess) return bad(fail(-5, "jump table"));
+  std::vector<float> la(e->T_g, std::log(c.initial_temperature));
+  if (hipMemcpy(e->log_alpha, la.data(), sizeof(float) * e->T_g, hipMemcpyHostToDevice) != hipSuccess)
+    return bad(fail(-5, "log_alpha"));
+  e->h_rmin.assign(e->T_l, INFINITY);
+  e->h_rmax.assign(e->T_l, -INFINITY);
+  *out = e;
+  return 0;
+}
+
+void mtsac_destroy(mtsac_engine* h) { delete h; }
+
+static Net* net_of(mtsac_engine* h, int which, float** buf) {
+  switch (which) {
+    case MTSAC_ACTOR: *buf = h->actor.p; return &h->actor;
+    case MTSAC_CRITIC: *buf = h->critic.p; return &h->critic;
+    case MTSAC_CRITIC_TARGET: *buf = h->critic.tgt; return &h->critic;
+    case MTSAC_ACTOR_ADAM_MU: *buf = h->actor.m; return &h->actor;
+    case MTSAC_ACTOR_ADAM_NU: *buf = h->actor.v; return &h->actor;
+    case MTSAC_CRITIC_ADAM_MU: *buf = h->critic.m; return &h->critic;
+    case MTSAC_CRITIC_ADAM_NU: *buf = h->critic.v; return &h->critic;
+    default: return nullptr;
+  }
+}
+
+static float* alpha_buf(mtsac_engine* h, int which) {
+  switch (which) {
+    case MTSAC_LOG_ALPHA_PARAMS: return h->log_alpha;
+    case MTSAC_ALPHA_ADAM_MU: return h->la_m;
+    case MTSAC_ALPHA_ADAM_NU: return h->la_v;
+    default: return nullptr;
+  }
+}
+
+int64_t mtsac_param_count(const mtsac_engine* hc, int which) {
+  auto* h = const_cast<mtsac_engine*>(hc);
+  if (!h) return fail(-22, "null engine");
+  if (alpha_buf(h, which)) return h->T_g;
+  float* b = nullptr;
+  Net* net = net_of(h, which, &b);
+  if (!net) return fail(-22, "unknown tensor id");
+  return net->n_params;
+}
+
+static int copy_params(mtsac_engine* h, int which, float* host, int64_t n, bool to_device) {
+  if (!h || !host) return fail(-22, "null argument");
+  if (float* ab = alpha_buf(h, which)) {
+    if (n != h->T_g) return fail(-22, "size mismatch");
+    HIP_TRY(hipStreamSynchronize(h->st));
+    HIP_TRY(to_device ? hipMemcpy(ab, host, sizeof(float) * n, hipMemcpyDefault)
+                      : hipMemcpy(host, ab, sizeof(float) * n, hipMemcpyDefault));
+    return 0;
+  }
+  float* buf = nullptr;
+  Net* net = net_of(h, which, &buf);
+  if (!net) return fail(-22, "unknown tensor id");
+  if (n != net->n_params) return fail(-22, "size mismatch: expected " + std::to_string(net->n_params));
+  HIP_TRY(hipStreamSynchronize(h->st));
+  long long o = 0;
+  for (auto& lf : net->leaves) {
+    if (to_device)
+      HIP_TRY(hipMemcpy(buf + lf.first, host + o, sizeof(float) * lf.second, hipMemcpyDefault));
+    else
+      HIP_TRY(hipMemcpy(host + o, buf + lf.first, sizeof(float) * lf.second, hipMemcpyDefault));
+    o += lf.second;
+  }
+  return 0;
+}
+
+int mtsac_set_params(mtsac_engine* h, int which, const float* src, int64_t n) {
+  return copy_params(h, which, const_cast<float*>(src), n, true);
+}
+int mtsac_get_params(mtsac_engine* h, int which, float* dst, int64_t n) { return copy_params(h, which, dst, n, false); }
+
+static OptScalars* sc_of(mtsac_engine* h, int which) {
+  return which == 0 ? h->actor.sc : which == 1 ? h->critic.sc : which == 2 ? h->sc_alpha : nullptr;
+}
+int mtsac_set_adam_count(mtsac_engine* h, int which, int32_t count) {
+  if (!h) return fail(-22, "null engine");
+  OptScalars* s = sc_of(h, which);
+  if (!s) return fail(-22, "which must be 0 (actor), 1 (critic) or 2 (alpha)");
+  HIP_TRY(hipStreamSynchronize(h->st));
+  HIP_TRY(hipMemcpy(&s->count, &count, sizeof(int), hipMemcpyHostToDevice));
+  return 0;
+}
+int mtsac_get_adam_count(mtsac_engine* h, int which, int32_t* count) {
+  if (!h || !count) return fail(-22, "null argument");
+  OptScalars* s = sc_of(h, which);
+  if (!s) return fail(-22, "which must be 0 (actor), 1 (critic) or 2 (alpha)");
+  HIP_TRY(hipStreamSynchronize(h->st));
+  HIP_TRY(hipMemcpy(count, &s->count, sizeof(int), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// ---------------------------------------------------------------- buffer
+static int upload_size(mtsac_engine* h) {
+  long long sz = h->h_full ? h->cfg.capacity : h->h_pos;
+  HIP_TRY(hipMemcpyAsync(h->buf_size, &sz, sizeof(sz), hipMemcpyHostToDevice, h->st));
+  HIP_TRY(hipStreamSynchronize(h->st));
+  return 0;
+}
+
+static int write_slots(mtsac_engine* h, int64_t s0, int64_t ns, const float* obs, const float* nobs, const float* act,
+                       const float* rew, const float* done) {
+  const int T = h->T_l, D = h->D, A = h->A, R = h->R;
+  std::vector<float> rec((size_t)ns * T * R, 0.0f);
+  for (int64_t s = 0; s < ns; ++s)
+    for (int t = 0; t < T; ++t) {
+      float* r = &rec[((size_t)s * T + t) * R];
+      const size_t row = (size_t)s * T + t;
+      std::memcpy(r, obs + row * D, sizeof(float) * D);
+      std::memcpy(r + D, act + row * A, sizeof(float) * A);
+      r[D + A] = rew[row];
+      r[D + A + 1] = done[row];
+      std::memcpy(r + D + A + 2, nobs + row * D, sizeof(float) * D);
+    }
+  HIP_TRY(hipStreamSynchronize(h->st));
+  HIP_TRY(hipMemcpy(h->store + (size_t)s0 * T * R, rec.data(), sizeof(float) * rec.size(), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int mtsac_buffer_add(mtsac_engine* h, const float* obs, const float* next_obs, const float* actions,
+                     const float* rewards, const float* dones) {
+  if (!h || !obs || !next_obs || !actions || !rewards || !dones) return fail(-22, "null argument");
+  int rc = write_slots(h, h->h_pos, 1, obs, next_obs, actions, rewards, dones);
+  if (rc) return rc;
+  if (h->cfg.normalize_rewards) {  // buffers.py:460-462
+    for (int t = 0; t < h->T_l; ++t) {
+      h->h_rmin[t] = std::min(h->h_rmin[t], (double)rewards[t]);
+      h->h_rmax[t] = std::max(h->h_rmax[t], (double)rewards[t]);
+    }
+    HIP_TRY(hipMemcpy(h->rmin, h->h_rmin.data(), sizeof(double) * h->T_l, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(h->rmax, h->h_rmax.data(), sizeof(double) * h->T_l, hipMemcpyHostToDevice));
+  }
+  // _advance_position(1)  (buffers.py:337-343)
+  long long np = h->h_pos + 1;
+  if (np >= h->cfg.capacity) h->h_full = 1;
+  h->h_pos = np % h->cfg.capacity;
+  return upload_size(h);
+}
+
+int mtsac_buffer_write(mtsac_engine* h, int64_t s0, int64_t ns, const float* obs, const float* next_obs,
+                       const float* actions, const float* rewards, const float* dones) {
+  if (!h || !obs || !next_obs || !actions || !rewards || !dones) return fail(-22, "null argument");
+  if (s0 < 0 || ns < 0 || s0 + ns > h->cfg.capacity) return fail(-22, "slot range out of bounds");
+  const int64_t chunk = 4096;
+  for (int64_t s = 0; s < ns; s += chunk) {
+    const int64_t k = std::min(chunk, ns - s);
+    const size_t row = (size_t)s * h->T_l;
+    int rc = write_slots(h, s0 + s, k, obs + row * h->D, next_obs + row * h->D, actions + row * h->A, rewards + row,
+                         dones + row);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+int mtsac_buffer_read(mtsac_engine* h, int64_t s0, int64_t ns, float* obs, float* next_obs, float* actions,
+                      float* rewards, float* dones) {
+  if (!h) return fail(-22, "null engine");
+  if (s0 < 0 || ns < 0 || s0 + ns > h->cfg.capacity) return fail(-22, "slot range out of bounds");
+  const int T = h->T_l, D = h->D, A = h->A, R = h->R;
+  std::vector<float> rec((size_t)ns * T * R);
+  HIP_TRY(hipStreamSynchronize(h->st));
+  HIP_TRY(hipMemcpy(rec.data(), h->store + (size_t)s0 * T * R, sizeof(float) * rec.size(), hipMemcpyDeviceToHost));
+  for (int64_t s = 0; s < ns; ++s)
+    for (int t = 0; t < T; ++t) {
+      const float* r = &rec[((size_t)s * T + t) * R];
+      const size_t row = (size_t)s * T + t;
+      if (obs) std::memcpy(obs + row * D, r, sizeof(float) * D);
+      if (actions) std::memcpy(actions + row * A, r + D, sizeof(float) * A);
+      if (rewards) rewards[row] = r[D + A];
+      if (dones) dones[row] = r[D + A + 1];
+      if (next_obs) std::memcpy(next_obs + row * D, r + D + A + 2, sizeof(float) * D);
+    }
+  return 0;
+}
+
+int mtsac_buffer_fill_synthetic(mtsac_engine* h, uint64_t seed) {
+  if (!h) return fail(-22, "null engine");
+  fill_synthetic(h->store, h->cfg.capacity, h->T_l, h->R, h->D, h->A, h->T_g, h->cfg.task_begin, seed, h->st);
+  HIP_TRY(hipGetLastError());
+  h->h_pos = 0;
+  h->h_full = 1;
+  return upload_size(h);
+}
+
+int mtsac_buffer_set_state(mtsac_engine* h, int64_t pos, int32_t full) {
+  if (!h) return fail(-22, "null engine");
+  if (pos < 0 || pos >= h->cfg.capacity) return fail(-22, "pos out of range");
+  h->h_pos = pos;
+  h->h_full = full ? 1 : 0;
+  return upload_size(h);
+}
+
+int mtsac_buffer_get_state(mtsac_engine* h, int64_t* pos, int32_t* full) {
+  if (!h || !pos || !full) return fail(-22, "null argument");
+  *pos = h->h_pos;
+  *full = h->h_full;
+  return 0;
+}
+
+int mtsac_buffer_set_reward_stats(mtsac_engine* h, const double* mn, const double* mx) {
+  if (!h || !mn || !mx) return fail(-22, "null argument");
+  h->h_rmin.assign(mn, mn + h->T_l);
+  h->h_rmax.assign(mx, mx + h->T_l);
+  HIP_TRY(hipMemcpy(h->rmin, mn, sizeof(double) * h->T_l, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->rmax, mx, sizeof(double) * h->T_l, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int mtsac_rng_set(mtsac_engine* h, uint64_t shi, uint64_t slo, uint64_t ihi, uint64_t ilo, int32_t has32, uint32_t u) {
+  if (!h) return fail(-22, "null engine");
+  PcgDev s{shi, slo, ihi, ilo, has32 ? 1 : 0, u};
+  HIP_TRY(hipStreamSynchronize(h->st));
+  HIP_TRY(hipMemcpy(h->rng, &s, sizeof(s), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int mtsac_rng_get(mtsac_engine* h, uint64_t* shi, uint64_t* slo, uint64_t* ihi, uint64_t* ilo, int32_t* has32,
+                  uint32_t* u) {
+  if (!h || !shi || !slo || !ihi || !ilo || !has32 || !u) return fail(-22, "null argument");
+  PcgDev s{};
+  HIP_TRY(hipStreamSynchronize(h->st));
+  HIP_TRY(hipMemcpy(&s, h->rng, sizeof(s), hipMemcpyDeviceToHost));
+  *shi = s.state_hi;
+  *slo = s.state_lo;
+  *ihi = s.inc_hi;
+  *ilo = s.inc_lo;
+  *has32 = s.has_uint32;
+  *u = s.uinteger;
+  return 0;
+}
+
+int mtsac_sample(mtsac_engine* h, int64_t* indices, float* obs, float* actions, float* next_obs, float* dones,
+                 float* rewards) {
+  if (!h) return fail(-22, "null engine");
+  replay_indices(h->rng, h->jump, h->buf_size, h->n, h->idx, h->st);
+  GatherParams gp = h->gather_params();
+  replay_gather(gp, h->st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(h->st));
+  const int B = h->B, D = h->D, A = h->A;
+  if (indices) {
+    std::vector<int> tmp(h->n);
+    HIP_TRY(hipMemcpy(tmp.data(), h->idx, sizeof(int) * h->n, hipMemcpyDeviceToHost));
+    for (int i = 0; i < h->n; ++i) indices[i] = tmp[i];
+  }
+  if (obs) HIP_TRY(hipMemcpy2D(obs, sizeof(float) * D, h->xa, sizeof(float) * h->ld_a, sizeof(float) * D, B,
+                               hipMemcpyDeviceToHost));
+  if (next_obs) HIP_TRY(hipMemcpy2D(next_obs, sizeof(float) * D, h->xan, sizeof(float) * h->ld_a, sizeof(float) * D,
+                                    B, hipMemcpyDeviceToHost));
+  if (actions) HIP_TRY(hipMemcpy2D(actions, sizeof(float) * A, h->xc, sizeof(float) * h->ld_c, sizeof(float) * A, B,
+                                   hipMemcpyDeviceToHost));
+  if (dones) HIP_TRY(hipMemcpy(dones, h->done, sizeof(float) * B, hipMemcpyDeviceToHost));
+  if (rewards) HIP_TRY(hipMemcpy(rewards, h->rew, sizeof(float) * B, hipMemcpyDeviceToHost));
+  return h->check_err();
+}
+
+// ---------------------------------------------------------------- update
+int mtsac_update(mtsac_engine* h, const mtsac_batch* b, const float* eps_next, const float* eps_cur) {
+  if (!h) return fail(-22, "null engine");
+  if ((eps_next == nullptr) != (eps_cur == nullptr)) return fail(-22, "inject both eps_next and eps_cur or neither");
+  const int B = h->B, D = h->D, A = h->A;
+  if (b) {
+    if (!b->observations || !b->actions || !b->next_observations || !b->dones || !b->rewards)
+      return fail(-22, "incomplete batch");
+    HIP_TRY(hipMemcpyAsync(h->u_obs, b->observations, sizeof(float) * B * D, hipMemcpyDefault, h->st));
+    HIP_TRY(hipMemcpyAsync(h->u_nobs, b->next_observations, sizeof(float) * B * D, hipMemcpyDefault, h->st));
+    HIP_TRY(hipMemcpyAsync(h->u_act, b->actions, sizeof(float) * B * A, hipMemcpyDefault, h->st));
+    HIP_TRY(hipMemcpyAsync(h->u_done, b->dones, sizeof(float) * B, hipMemcpyDefault, h->st));
+    HIP_TRY(hipMemcpyAsync(h->u_rew, b->rewards, sizeof(float) * B, hipMemcpyDefault, h->st));
+  }
+  if (eps_next) {
+    HIP_TRY(hipMemcpyAsync(h->eps_n, eps_next, sizeof(float) * B * A, hipMemcpyDefault, h->st));
+    HIP_TRY(hipMemcpyAsync(h->eps_c, eps_cur, sizeof(float) * B * A, hipMemcpyDefault, h->st));
+  }
+  h->tl_next = 0;
+  h->step(b == nullptr, eps_next == nullptr);
+  HIP_TRY(hipGetLastError());
+  if (b || eps_next) HIP_TRY(hipStreamSynchronize(h->st));  // borrowed host pointers
+  return 0;
+}
+
+int mtsac_update_many(mtsac_engine* h, int32_t steps) {
+  if (!h) return fail(-22, "null engine");
+  if (steps <= 0) return 0;
+  if (!h->use_graph) {
+    for (int s = 0; s < steps; ++s) {
+      h->tl_next = 0;
+      h->step(true, true);
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+  if (h->gexec && h->graph_timed != h->timing) {
+    (void)hipGraphExecDestroy(h->gexec);
+    (void)hipGraphDestroy(h->graph);
+    h->gexec = nullptr;
+    h->graph = nullptr;
+  }
+  if (!h->gexec) {
+    h->tl_next = 0;
+    HIP_TRY(hipStreamBeginCapture(h->st, hipStreamCaptureModeThreadLocal));
+    h->step(true, true);
+    hipError_t ce = hipStreamEndCapture(h->st, &h->graph);
+    if (ce != hipSuccess) return fail(-5, std::string("graph capture: ") + hipGetErrorString(ce));
+    HIP_TRY(hipGraphInstantiate(&h->gexec, h->graph, nullptr, nullptr, 0));
+    h->graph_timed = h->timing;
+  }
+  for (int s = 0; s < steps; ++s) HIP_TRY(hipGraphLaunch(h->gexec, h->st));
+  return 0;
+}
+
+int mtsac_get_logs(mtsac_engine* h, float* logs) {
+  if (!h || !logs) return fail(-22, "null argument");
+  HIP_TRY(hipMemcpyAsync(logs, h->logs, sizeof(float) * MTSAC_NUM_LOGS, hipMemcpyDeviceToHost, h->st));
+  HIP_TRY(hipStreamSynchronize(h->st));
+  return h->check_err();
+}
+
+int mtsac_enable_graph(mtsac_engine* h, int32_t enable) {
+  if (!h) return fail(-22, "null engine");
+  h->use_graph = enable != 0;
+  return 0;
+}
+
+int mtsac_synchronize(mtsac_engine* h) {
+  if (!h) return fail(-22, "null engine");
+  HIP_TRY(hipStreamSynchronize(h->st));
+  return h->check_err();
+}
+
+// ---------------------------------------------------------------- rollout
+static int act(mtsac_engine* h, const float* obs, int n, const float* eps, float* out, bool zero_eps) {
+  if (!h || !obs || !out) return fail(-22, "null argument");
+  if (n < 1 || n > h->roll_max) return fail(-22, "row count out of range");
+  const int D = h->D, A = h->A;
+  HIP_TRY(hipMemcpyAsync(h->r_obs, obs, sizeof(float) * n * D, hipMemcpyDefault, h->st));
+  if (zero_eps)
+    HIP_TRY(hipMemsetAsync(h->r_eps, 0, sizeof(float) * n * A, h->st));
+  else
+    HIP_TRY(hipMemcpyAsync(h->r_eps, eps, sizeof(float) * n * A, hipMemcpyDefault, h->st));
+  GatherParams gp{};
+  gp.T_l = h->T_l;
+  gp.obs_dim = D;
+  gp.act_dim = A;
+  gp.T_glob = h->T_g;
+  gp.task_begin = h->cfg.task_begin;
+  gp.ld_a = h->ld_a;
+  gp.ld_c = h->ld_c;
+  gp.xa = h->r_x;
+  gp.xa_next = h->r_dummy;
+  gp.xc = h->r_dummy;
+  gp.xc_next = h->r_dummy;
+  gp.xc_pi = h->r_dummy;
+  gp.rew = h->r_lp;
+  gp.done = h->r_lp;
+  gp.task = h->r_task;
+  gp.err = h->err;
+  // obs doubles as next_obs; the action / reward / done inputs are ignored scratch
+  batch_scatter(gp, h->r_obs, h->r_eps, h->r_obs, h->r_lp, h->r_lp, n, h->st);
+  h->trunk_forward(h->actor, h->actor.p, h->r_x, h->ld_a, h->r_h, n);
+  PolicyParams pp{};
+  pp.head = h->head(h->actor, h->actor.p, h->r_h[h->actor.depth - 1], n, h->r_task);
+  pp.eps = h->r_eps;
+  pp.A = A;
+  pp.ls_min = h->cfg.log_std_min;
+  pp.ls_max = h->cfg.log_std_max;
+  pp.a_out = h->r_act;
+  pp.ld_a_out = A;
+  pp.logpi = h->r_lp;
+  policy_head(pp, h->st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, h->r_act, sizeof(float) * n * A, hipMemcpyDefault, h->st));
+  HIP_TRY(hipStreamSynchronize(h->st));
+  return h->check_err();
+}
+
+int mtsac_eval_action(mtsac_engine* h, const float* obs, int32_t n, float* actions) {
+  return act(h, obs, n, nullptr, actions, true);  // mode() = tanh(mu)
+}
+int mtsac_sample_action(mtsac_engine* h, const float* obs, int32_t n, const float* eps, float* actions) {
+  if (!eps) return fail(-22, "eps required");
+  return act(h, obs, n, eps, actions, false);
+}
+
+// ---------------------------------------------------------------- comm
+int mtsac_comm_unique_id_size(void) { return (int)sizeof(ncclUniqueId); }
+int mtsac_comm_get_unique_id(void* id_out) {
+  if (!id_out) return fail(-22, "null argument");
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return fail(-5, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  std::memcpy(id_out, &id, sizeof(id));
+  return 0;
+}
+int mtsac_comm_init(mtsac_engine* h, const void* unique_id, int32_t nranks, int32_t rank) {
+  if (!h || !unique_id) return fail(-22, "null argument");
+  if (nranks <= 1) return 0;
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id, sizeof(id));
+  HIP_TRY(hipSetDevice(h->device));
+  ncclResult_t r = ncclCommInitRank(&h->comm, nranks, id, rank);
+  if (r != ncclSuccess) return fail(-5, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  h->nranks = nranks;
+  h->rank = rank;
+  if (h->gexec) {
+    (void)hipGraphExecDestroy(h->gexec);
+    (void)hipGraphDestroy(h->graph);
+    h->gexec = nullptr;
+    h->graph = nullptr;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------- timing
+int mtsac_set_timing(mtsac_engine* h, int32_t enable) {
+  if (!h) return fail(-22, "null engine");
+  h->timing = enable != 0;
+  return 0;
+}
+int mtsac_get_timing(mtsac_engine* h, int32_t family, double* total_ms, int32_t* launches, double* flops) {
+  if (!h || !total_ms || !launches || !flops) return fail(-22, "null argument");
+  HIP_TRY(hipStreamSynchronize(h->st));
+  double ms = 0.0, fl = 0.0;
+  int nl = 0;
+  for (size_t i = 0; i < h->tl_next && i < h->tl.size(); ++i) {
+    if (h->tl[i].family != family) continue;
+    float t = 0.f;
+    HIP_TRY(hipEventElapsedTime(&t, h->tl[i].a, h->tl[i].b));
+    ms += t;
+    fl += h->tl[i].flops;
+    ++nl;
+  }
+  *total_ms = ms;
+  *launches = nl;
+  *flops = fl;
+  return 0;
+}
+
+// ---------------------------------------------------------------- debug (include/mtsac_debug.h)
+int mtsac_debug_gemm(int kind, int epi, int batch, int M, int N, int K, const float* A, int lda, int a_shared,
+                     const float* B, int ldb, float* C, int ldc, const float* bias, const float* mask, int ldm,
+                     float* db) {
+  if (kind < 0 || kind > 2 || batch < 1 || M < 1 || N < 1 || K < 1) return fail(-22, "bad gemm arguments");
+  const bool ta = kind == 2, tb = kind == 1;
+  const long long a_rows = ta ? K : M, b_rows = tb ? N : K;
+  const long long sA = a_rows * lda, sB = b_rows * ldb, sC = (long long)M * ldc;
+  float *dA = nullptr, *dB = nullptr, *dC = nullptr, *dbias = nullptr, *dmask = nullptr, *ddb = nullptr;
+  auto cleanup = [&]() {
+    for (float* p : {dA, dB, dC, dbias, dmask, ddb})
+      if (p) (void)hipFree(p);
+  };
+  const long long nA = a_shared ? sA : sA * batch;
+  bool ok = hipMalloc(&dA, sizeof(float) * nA) == hipSuccess && hipMalloc(&dB, sizeof(float) * sB * batch) == hipSuccess &&
+            hipMalloc(&dC, sizeof(float) * sC * batch) == hipSuccess;
+  if (ok && bias) ok = hipMalloc(&dbias, sizeof(float) * N * batch) == hipSuccess;
+  if (ok && mask) ok = hipMalloc(&dmask, sizeof(float) * (long long)M * ldm * batch) == hipSuccess;
+  if (ok && db) ok = hipMalloc(&ddb, sizeof(float) * N * batch) == hipSuccess;
+  if (!ok) {
+    cleanup();
+    return fail(-12, "hipMalloc failed");
+  }
+  (void)hipMemcpy(dA, A, sizeof(float) * nA, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dB, B, sizeof(float) * sB * batch, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dC, C, sizeof(float) * sC * batch, hipMemcpyHostToDevice);
+  if (bias) (void)hipMemcpy(dbias, bias, sizeof(float) * N * batch, hipMemcpyHostToDevice);
+  if (mask) (void)hipMemcpy(dmask, mask, sizeof(float) * (long long)M * ldm * batch, hipMemcpyHostToDevice);
+  GemmParams g{};
+  g.A = dA; g.lda = lda; g.sA = a_shared ? 0 : sA;
+  g.B = dB; g.ldb = ldb; g.sB = sB;
+  g.C = dC; g.ldc = ldc; g.sC = sC;
+  g.bias = dbias; g.sBias = N;
+  g.mask = dmask; g.ldm = ldm; g.sMask = (long long)M * ldm;
+  g.db = ddb; g.sDb = N;
+  g.M = M; g.N = N; g.K = K;
+  gemm_f32(g, (GemmKind)kind, epi, batch, nullptr);
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(C, dC, sizeof(float) * sC * batch, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && db) e = hipMemcpy(db, ddb, sizeof(float) * N * batch, hipMemcpyDeviceToHost);
+  cleanup();
+  if (e != hipSuccess) return fail(-5, std::string("debug gemm: ") + hipGetErrorString(e));
+  return 0;
+}
+
+}  // extern "C"

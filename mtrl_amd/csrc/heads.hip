@@ -1,0 +1,347 @@
+// heads.hip -- per-task heads, tanh-Gaussian policy, SAC losses, head backward.
+//
+// Reference: MultiHeadNetwork head selection (mtrl/nn/multi_head.py:50-66),
+// ContinuousActionPolicy + TanhMultivariateNormalDiag (mtrl/rl/networks.py:28-45,
+// mtrl/nn/distributions.py:6-16), critic / actor losses (mtsac.py:538-566,
+// 631-675).  The reference evaluates ALL T heads on every row and then picks the
+// row's own head; here only the selected head is computed (same dot product).
+// One wavefront per batch row; the head kernels stream the last trunk activation
+// (W floats per row) exactly once.
+#include "devrng.h"
+#include "kernels.h"
+
+namespace mtsac {
+
+namespace {
+
+constexpr float LOG2F = 0.69314718055994530942f;
+constexpr float HALF_LOG_2PI = 0.91893853320467274178f;
+
+__device__ inline float wsum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ inline float softplusf(float z) {  // jax.nn.softplus = logaddexp(z, 0)
+  return fmaxf(z, 0.f) + log1pf(expf(-fabsf(z)));
+}
+
+// d clip(v, lo, hi) / dv with jax's maximum/minimum tie rule (0.5 at the bounds)
+__device__ inline float clip_grad(float v, float lo, float hi) {
+  if (v > lo && v < hi) return 1.f;
+  if (v == lo || v == hi) return 0.5f;
+  return 0.f;
+}
+
+// out[o] = sum_w h[w] * Wt[w*HD + o], reduced over the wave (every lane gets the sums)
+template <int HD>
+__device__ inline void head_dot(const float* __restrict__ h, const float* __restrict__ Wt, int W, float (&acc)[HD]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 0; o < HD; ++o) acc[o] = 0.f;
+  for (int w = lane; w < W; w += 64) {
+    const float hv = h[w];
+    if (HD == 8) {
+      const float4 a = *reinterpret_cast<const float4*>(Wt + w * 8);
+      const float4 c = *reinterpret_cast<const float4*>(Wt + w * 8 + 4);
+      acc[0] += hv * a.x; acc[1] += hv * a.y; acc[2] += hv * a.z; acc[3] += hv * a.w;
+      acc[4 % HD] += hv * c.x; acc[5 % HD] += hv * c.y; acc[6 % HD] += hv * c.z; acc[7 % HD] += hv * c.w;
+    } else {
+#pragma unroll
+      for (int o = 0; o < HD; ++o) acc[o] += hv * Wt[w * HD + o];
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < HD; ++o) acc[o] = wsum(acc[o]);
+}
+
+// ------------------------------------------------------------------ actor head + policy
+template <int HD>
+__global__ __launch_bounds__(256) void policy_head_kernel(PolicyParams p) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const HeadParams& hp = p.head;
+  if (b >= hp.B) return;
+  const int t = hp.task[b];
+  float acc[HD];
+  head_dot<HD>(hp.h + (long long)b * hp.W, hp.Wh + (long long)t * hp.W * HD, hp.W, acc);
+  const int A = p.A;
+  float term = 0.f;
+  if (lane < A) {
+    // lane j owns action dimension j; pick acc[j], acc[A+j] with a static unroll
+    float mu = 0.f, ls = 0.f;
+#pragma unroll
+    for (int o = 0; o < HD; ++o) {
+      if (o == lane) mu = acc[o];
+      if (o == lane + A) ls = acc[o];
+    }
+    mu += hp.bh[t * HD + lane];
+    ls += hp.bh[t * HD + A + lane];
+    float eps;
+    if (p.eps != nullptr) {
+      eps = p.eps[(long long)b * A + lane];
+    } else {
+      float nz[4];
+      normal4(p.seed, p.stream_id + 16u * (uint32_t)(lane >> 2), *p.counter, (uint32_t)b, nz);
+      eps = nz[lane & 3];
+    }
+    const float lsc = fminf(fmaxf(ls, p.ls_min), p.ls_max);
+    const float sigma = expf(lsc);
+    const float x = mu + sigma * eps;
+    const float a = tanhf(x);
+    // MVNDiag base log-prob (eps form) minus the Tanh forward log-det (distrax Tanh)
+    term = -0.5f * eps * eps - HALF_LOG_2PI - logf(sigma) - 2.0f * (LOG2F - x - softplusf(-2.0f * x));
+    p.a_out[(long long)b * p.ld_a_out + lane] = a;
+    if (p.a_out2) p.a_out2[(long long)b * p.ld_a_out2 + lane] = a;
+    if (p.cache) {
+      float* c = p.cache + (long long)b * 5 * A;
+      c[lane] = mu;
+      c[A + lane] = ls;
+      c[2 * A + lane] = x;
+      c[3 * A + lane] = a;
+      c[4 * A + lane] = eps;
+    }
+  }
+  term = wsum(term);
+  if (lane == 0) p.logpi[b] = term;
+}
+
+// ------------------------------------------------------------------ critic heads + losses
+__global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
+  const int lane = threadIdx.x & 63;
+  const HeadParams& hp = p.head;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= hp.B) return;
+  const int t = hp.task[b];
+  float q[4];
+  const int E = hp.E;
+  for (int e = 0; e < E; ++e) {
+    float acc[1];
+    head_dot<1>(hp.h + e * hp.sh + (long long)b * hp.W, hp.Wh + e * hp.sWh + (long long)t * hp.W, hp.W, acc);
+    q[e] = acc[0] + hp.bh[e * hp.sbh + t];
+  }
+  if (lane != 0) return;
+  const float alpha = expf(p.log_alpha[p.task_begin + t]);  // exp(onehot . log_alpha), mtsac.py:60-63
+  float w = 1.f;
+  if (p.tw != nullptr) w = p.tw[b];  // T * softmax(-log_alpha)[t] (mtsac.py:103-113)
+  if (p.mode == CH_TARGET) {
+    float mn = q[0];
+    for (int e = 1; e < E; ++e) mn = fminf(mn, q[e]);
+    const float mnext = mn - alpha * p.logpi[b];
+    float y = p.rew[b] + (1.0f - p.done[b]) * p.gamma * mnext;  // mtsac.py:547-553
+    if (p.clip) y = fminf(fmaxf(y, -5000.f), 5000.f);
+    p.y_out[b] = y;
+  } else if (p.mode == CH_CRITIC) {
+    const float y = p.y[b];
+    float sq = 0.f, qs = 0.f;
+    for (int e = 0; e < E; ++e) {
+      float qc = q[e], dcl = 1.f;
+      if (p.clip) {
+        dcl = clip_grad(qc, -5000.f, 5000.f);
+        qc = fminf(fmaxf(qc, -5000.f), 5000.f);
+      }
+      const float diff = qc - y;
+      sq += w * diff * diff;
+      qs += qc;
+      p.dq[e * hp.B + b] = w * 2.0f * diff * p.inv_norm * dcl;
+    }
+    p.row_a[b] = sq;
+    p.row_b[b] = qs;
+  } else {  // CH_ACTOR: loss = mean(w * (alpha*logpi - min_k Q_k))   mtsac.py:659-666
+    float mn = q[0];
+    for (int e = 1; e < E; ++e) mn = fminf(mn, q[e]);
+    int cnt = 0;
+    for (int e = 0; e < E; ++e) cnt += (q[e] == mn) ? 1 : 0;
+    for (int e = 0; e < E; ++e) p.dq[e * hp.B + b] = (q[e] == mn) ? (-w * p.inv_norm / (float)cnt) : 0.f;
+    p.row_a[b] = w * (alpha * p.logpi[b] - mn);
+    p.alpha_w[b] = w * alpha * p.inv_norm;
+  }
+}
+
+// ------------------------------------------------------------------ head backward (data)
+template <int HD>
+__global__ __launch_bounds__(256) void head_bwd_data_kernel(HeadParams hp, const float* __restrict__ dout,
+                                                            long long s_dout, float* __restrict__ dz) {
+  const int W4 = hp.W >> 2;
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long per = (long long)hp.B * W4;
+  if (gid >= per * hp.E) return;
+  const int e = (int)(gid / per);
+  const long long r = gid - e * per;
+  const int b = (int)(r / W4);
+  const int w = (int)(r - (long long)b * W4) * 4;
+  const int t = hp.task[b];
+  const float* Wt = hp.Wh + e * hp.sWh + ((long long)t * hp.W + w) * HD;
+  const float* d = dout + e * s_dout + (long long)b * HD;
+  float g[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float s = 0.f;
+#pragma unroll
+    for (int o = 0; o < HD; ++o) s += d[o] * Wt[k * HD + o];
+    g[k] = s;
+  }
+  const long long off = e * hp.sh + (long long)b * hp.W + w;
+  const float4 h = *reinterpret_cast<const float4*>(hp.h + off);
+  float4 out;
+  out.x = h.x > 0.f ? g[0] : 0.f;
+  out.y = h.y > 0.f ? g[1] : 0.f;
+  out.z = h.z > 0.f ? g[2] : 0.f;
+  out.w = h.w > 0.f ? g[3] : 0.f;
+  *reinterpret_cast<float4*>(dz + off) = out;
+}
+
+// ------------------------------------------------------------------ head backward (weights)
+template <int HD>
+__global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, const float* __restrict__ dout,
+                                                              long long s_dout, const int* __restrict__ counts,
+                                                              const int* __restrict__ rows, int max_rows,
+                                                              float* __restrict__ dWh, float* __restrict__ dbh) {
+  __shared__ float red[4][64][HD];
+  const int t = blockIdx.x;
+  const int w0 = blockIdx.y * 64;
+  const int e = blockIdx.z;
+  const int wl = threadIdx.x & 63;
+  const int rg = threadIdx.x >> 6;
+  const int w = w0 + wl;
+  const int n = counts[t];
+  const int* rl = rows + (long long)t * max_rows;
+  const float* h = hp.h + e * hp.sh;
+  const float* d = dout + e * s_dout;
+  float acc[HD];
+#pragma unroll
+  for (int o = 0; o < HD; ++o) acc[o] = 0.f;
+  if (w < hp.W) {
+    for (int j = rg; j < n; j += 4) {
+      const int row = rl[j];
+      const float hv = h[(long long)row * hp.W + w];
+#pragma unroll
+      for (int o = 0; o < HD; ++o) acc[o] += hv * d[(long long)row * HD + o];
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < HD; ++o) red[rg][wl][o] = acc[o];
+  __syncthreads();
+  if (rg == 0 && w < hp.W) {
+    float* out = dWh + e * hp.sWh + ((long long)t * hp.W + w) * HD;
+#pragma unroll
+    for (int o = 0; o < HD; ++o) out[o] = red[0][wl][o] + red[1][wl][o] + red[2][wl][o] + red[3][wl][o];
+  }
+  if (blockIdx.y == 0 && threadIdx.x < HD) {
+    const int o = threadIdx.x;
+    float s = 0.f;
+    for (int j = 0; j < n; ++j) s += d[(long long)rl[j] * HD + o];
+    dbh[e * hp.sbh + t * HD + o] = s;
+  }
+}
+
+// ------------------------------------------------------------------ critic -> action grad -> policy grad
+__global__ __launch_bounds__(256) void action_grad_kernel(ActionGradParams p) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= p.B) return;
+  const int A = p.A;
+  float ga[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ga[j] = 0.f;
+  for (int e = 0; e < p.E; ++e) {
+    const float* dz = p.dz1 + e * p.s_dz + (long long)b * p.Wc;
+    const float* W0 = p.W0 + e * p.s_W0;
+    for (int w = lane; w < p.Wc; w += 64) {
+      const float g = dz[w];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j < A) ga[j] += g * W0[(long long)j * p.Wc + w];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ga[j] = wsum(ga[j]);
+  if (lane < A) {
+    float g_a = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j == lane) g_a = ga[j];
+    const float* c = p.cache + (long long)b * 5 * A;
+    const float ls = c[A + lane], a = c[3 * A + lane], eps = c[4 * A + lane];
+    const float g_logpi = p.alpha_w[b];
+    const float sigma = expf(fminf(fmaxf(ls, p.ls_min), p.ls_max));
+    const float g_x = g_a * (1.0f - a * a) + g_logpi * 2.0f * a;  // d logpi/dx = 2 tanh(x)
+    const float g_ls = (g_x * sigma * eps - g_logpi) * clip_grad(ls, p.ls_min, p.ls_max);
+    p.dout[(long long)b * 2 * A + lane] = g_x;
+    p.dout[(long long)b * 2 * A + A + lane] = g_ls;
+  }
+}
+
+// ------------------------------------------------------------------ per-row alpha / task weights
+__global__ __launch_bounds__(256) void row_alpha_kernel(const int* __restrict__ task, int task_begin,
+                                                        const float* __restrict__ log_alpha, int T_glob, int B,
+                                                        int use_tw, float* __restrict__ alpha_row,
+                                                        float* __restrict__ tw_row) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int tg = task_begin + task[b];
+  alpha_row[b] = expf(log_alpha[tg]);
+  if (use_tw) {  // T * softmax(-log_alpha)[t]  (mtsac.py:103-113)
+    float mx = -log_alpha[0];
+    for (int i = 1; i < T_glob; ++i) mx = fmaxf(mx, -log_alpha[i]);
+    float s = 0.f;
+    for (int i = 0; i < T_glob; ++i) s += expf(-log_alpha[i] - mx);
+    tw_row[b] = (expf(-log_alpha[tg] - mx) / s) * (float)T_glob;
+  }
+}
+
+}  // namespace
+
+void policy_head(const PolicyParams& p, hipStream_t st) {
+  dim3 grid((p.head.B + 3) / 4);
+  if (p.head.hd == 8)
+    hipLaunchKernelGGL(policy_head_kernel<8>, grid, dim3(256), 0, st, p);
+  else if (p.head.hd == 6)
+    hipLaunchKernelGGL(policy_head_kernel<6>, grid, dim3(256), 0, st, p);
+  else if (p.head.hd == 4)
+    hipLaunchKernelGGL(policy_head_kernel<4>, grid, dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL(policy_head_kernel<2>, grid, dim3(256), 0, st, p);
+}
+
+void critic_head(const CriticHeadParams& p, hipStream_t st) {
+  hipLaunchKernelGGL(critic_head_kernel, dim3((p.head.B + 3) / 4), dim3(256), 0, st, p);
+}
+
+void head_backward_data(const HeadParams& hp, const float* dout, long long s_dout, float* dz, hipStream_t st) {
+  const long long n = (long long)hp.E * hp.B * (hp.W / 4);
+  dim3 grid((unsigned)((n + 255) / 256));
+  switch (hp.hd) {
+    case 1: hipLaunchKernelGGL(head_bwd_data_kernel<1>, grid, dim3(256), 0, st, hp, dout, s_dout, dz); break;
+    case 2: hipLaunchKernelGGL(head_bwd_data_kernel<2>, grid, dim3(256), 0, st, hp, dout, s_dout, dz); break;
+    case 4: hipLaunchKernelGGL(head_bwd_data_kernel<4>, grid, dim3(256), 0, st, hp, dout, s_dout, dz); break;
+    case 6: hipLaunchKernelGGL(head_bwd_data_kernel<6>, grid, dim3(256), 0, st, hp, dout, s_dout, dz); break;
+    default: hipLaunchKernelGGL(head_bwd_data_kernel<8>, grid, dim3(256), 0, st, hp, dout, s_dout, dz); break;
+  }
+}
+
+void head_backward_weight(const HeadParams& hp, const float* dout, long long s_dout, const int* counts,
+                          const int* rows, int max_rows, float* dWh, float* dbh, hipStream_t st) {
+  dim3 grid(0, (hp.W + 63) / 64, hp.E);
+  grid.x = (unsigned)(hp.sbh / hp.hd);  // T_l (bias stride per member = T_l * hd)
+  switch (hp.hd) {
+    case 1: hipLaunchKernelGGL(head_bwd_weight_kernel<1>, grid, dim3(256), 0, st, hp, dout, s_dout, counts, rows, max_rows, dWh, dbh); break;
+    case 2: hipLaunchKernelGGL(head_bwd_weight_kernel<2>, grid, dim3(256), 0, st, hp, dout, s_dout, counts, rows, max_rows, dWh, dbh); break;
+    case 4: hipLaunchKernelGGL(head_bwd_weight_kernel<4>, grid, dim3(256), 0, st, hp, dout, s_dout, counts, rows, max_rows, dWh, dbh); break;
+    case 6: hipLaunchKernelGGL(head_bwd_weight_kernel<6>, grid, dim3(256), 0, st, hp, dout, s_dout, counts, rows, max_rows, dWh, dbh); break;
+    default: hipLaunchKernelGGL(head_bwd_weight_kernel<8>, grid, dim3(256), 0, st, hp, dout, s_dout, counts, rows, max_rows, dWh, dbh); break;
+  }
+}
+
+void action_grad(const ActionGradParams& p, hipStream_t st) {
+  hipLaunchKernelGGL(action_grad_kernel, dim3((p.B + 3) / 4), dim3(256), 0, st, p);
+}
+
+void row_alpha(const int* task, int task_begin, const float* log_alpha, int T_glob, int B, int use_task_weights,
+               float* alpha_row, float* tw_row, hipStream_t st) {
+  hipLaunchKernelGGL(row_alpha_kernel, dim3((B + 255) / 256), dim3(256), 0, st, task, task_begin, log_alpha, T_glob,
+                     B, use_task_weights, alpha_row, tw_row);
+}
+
+}  // namespace mtsac

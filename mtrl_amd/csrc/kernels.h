@@ -1,0 +1,204 @@
+// kernels.h -- launch wrappers of the MTSAC device kernels (internal to libmtsac.so).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mtsac {
+
+// ------------------------------------------------------------------ GEMM
+// C[z] = op(A[z]) . op(B[z]) with a fused epilogue, fp32 in / fp32 accumulate on
+// v_mfma_f32_32x32x2_f32.  TA: A stored [K][M] (else [M][K]); TB: B stored [N][K]
+// (else [K][N]).  Leading dims and base pointers must be multiples of 4 floats.
+enum GemmEpi {
+  EPI_STORE = 0,      // C = acc                       (weight grads; + optional db column sums)
+  EPI_BIAS_RELU = 1,  // C = max(acc + bias[n], 0)     (trunk forward)
+  EPI_RELU_MASK = 2,  // C = acc * (mask[m][n] > 0)    (data grad through the previous ReLU)
+};
+
+struct GemmParams {
+  const float* A;
+  const float* B;
+  float* C;
+  const float* bias;  // EPI_BIAS_RELU
+  const float* mask;  // EPI_RELU_MASK
+  float* db;          // EPI_STORE + TB==false: column sums of B (bias gradient), may be null
+  int M, N, K;
+  int lda, ldb, ldc, ldm;
+  long long sA, sB, sC, sBias, sMask, sDb;  // per-batch strides (elements)
+};
+
+enum GemmKind { GEMM_NN = 0, GEMM_NT = 1, GEMM_TN = 2 };
+void gemm_f32(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_t st);
+
+// ------------------------------------------------------------------ replay
+struct PcgDev {  // device-resident numpy PCG64 state (buffers.py:260)
+  unsigned long long state_hi, state_lo, inc_hi, inc_lo;
+  int has_uint32;
+  unsigned int uinteger;
+};
+// n indices in [0, max(size, n)) with numpy's Generator.integers stream; size read from *buf_size
+void replay_indices(PcgDev* rng, const unsigned long long* jump /*65 x (A_hi,A_lo,C_hi,C_lo)*/,
+                    const long long* buf_size, int n, int* idx_out, hipStream_t st);
+
+struct GatherParams {
+  const float* store;   // [cap][T_l][R] transition records
+  const int* idx;       // [n]
+  int n, T_l, R, obs_dim, act_dim, T_glob, task_begin;
+  int ld_a, ld_c;       // padded widths of actor / critic inputs
+  float* xa;            // [B][ld_a]  obs
+  float* xa_next;       // [B][ld_a]  next_obs
+  float* xc;            // [B][ld_c]  (action | obs)
+  float* xc_next;       // [B][ld_c]  (a' | next_obs), a' columns written later
+  float* xc_pi;         // [B][ld_c]  (a | obs), a columns written later
+  float* rew;           // [B]
+  float* done;          // [B]
+  int* task;            // [B] local task id
+  const double* rmin;   // per-task reward min/max (normalize_rewards) or null
+  const double* rmax;
+  double norm_eps;
+  int* err;             // error flag (one-hot violation)
+};
+void replay_gather(const GatherParams& p, hipStream_t st);
+// a user batch (ReplayBufferSamples layout) into the same input buffers
+void batch_scatter(const GatherParams& p, const float* obs, const float* act, const float* nobs,
+                   const float* done, const float* rew, int B, hipStream_t st);
+void fill_synthetic(float* store, long long cap, int T_l, int R, int obs_dim, int act_dim, int T_glob,
+                    int task_begin, unsigned long long seed, hipStream_t st);
+// stable per-task row lists: rows_of[t*max_rows + j], counts[t]
+void task_rows(const int* task, int B, int T_l, int* counts, int* rows, int max_rows, hipStream_t st);
+
+// ------------------------------------------------------------------ heads / policy / losses
+struct HeadParams {
+  const float* h;       // [E][B][W] last trunk activation
+  const float* Wh;      // [E][T_l][W][hd]
+  const float* bh;      // [E][T_l][hd]
+  const int* task;      // [B]
+  int B, W, hd, E;
+  long long sWh, sbh, sh;
+};
+
+// actor head + tanh-normal sample (networks.py:28-45, distributions.py:6-16)
+struct PolicyParams {
+  HeadParams head;
+  const float* eps;     // [B][A] injected noise or null (device stream)
+  unsigned long long seed;
+  const unsigned long long* counter;  // device step counter (noise stream position)
+  unsigned int stream_id;
+  int A;
+  float ls_min, ls_max;
+  float* a_out;         // written at [b*ld_a_out + j]
+  int ld_a_out;
+  float* a_out2;        // optional second copy
+  int ld_a_out2;
+  float* logpi;         // [B]
+  float* cache;         // optional [B][5A]: mu, ls, x, a, eps
+};
+void policy_head(const PolicyParams& p, hipStream_t st);
+
+enum CriticHeadMode { CH_TARGET = 0, CH_CRITIC = 1, CH_ACTOR = 2 };
+struct CriticHeadParams {
+  HeadParams head;      // E = num_critics, hd = 1
+  int mode;
+  const float* rew;
+  const float* done;
+  const float* logpi;   // target: logpi(a'|s'); actor: logpi(a|s)
+  const float* log_alpha;  // [T_glob]
+  const int* task;
+  int task_begin;
+  const float* y;       // critic mode input
+  float* y_out;         // target mode output
+  float* dq;            // [E][B] dL/dq (critic, actor modes)
+  float* row_a;         // per-row reduction inputs [B]
+  float* row_b;         // [B]
+  const float* tw;      // per-row task weights or null
+  float* alpha_w;       // CH_ACTOR: per-row dL/dlogpi = w * alpha / B
+  float gamma;
+  int clip;
+  int use_task_weights;
+  int T_glob;
+  float inv_norm;       // 1/(E*B) critic, 1/B actor (global B)
+};
+void critic_head(const CriticHeadParams& p, hipStream_t st);
+
+// dz[e][b][w] = (sum_o dout[e][b][o] * Wh[e][t_b][w][o]) * (h[e][b][w] > 0)
+void head_backward_data(const HeadParams& hp, const float* dout, long long s_dout, float* dz,
+                        hipStream_t st);
+// dWh[e][t][w][o] = sum_{b in t} h[e][b][w] dout[e][b][o];  dbh[e][t][o] = sum dout
+void head_backward_weight(const HeadParams& hp, const float* dout, long long s_dout, const int* counts,
+                          const int* rows, int max_rows, float* dWh, float* dbh, hipStream_t st);
+
+// critic data grad into the action columns + tanh-normal backward -> actor head grad
+struct ActionGradParams {
+  const float* dz1;     // [E][B][Wc]  grad at critic layer-0 pre-activation
+  const float* W0;      // [E][Ic][Wc] critic layer-0 kernel (rows 0..A-1 = action)
+  long long s_dz, s_W0;
+  int E, B, Wc, A;
+  const float* cache;   // [B][5A] from policy_head
+  const float* alpha_w; // [B] per-row dL/dlogpi (alpha * w / B)
+  float ls_min, ls_max;
+  float* dout;          // [B][2A]
+};
+void action_grad(const ActionGradParams& p, hipStream_t st);
+
+// per-row alpha (and task weights) from log_alpha (mtsac.py:60-63,103-113)
+void row_alpha(const int* task, int task_begin, const float* log_alpha, int T_glob, int B,
+               int use_task_weights, float* alpha_row, float* tw_row, hipStream_t st);
+
+// ------------------------------------------------------------------ reductions / optimizer
+// out[i] = sum over rows of in_i (deterministic single-block tree)
+void reduce_rows(const float* const* ins, int n_in, int B, float* out, hipStream_t st);
+// partial sums of squares of x[0..n) into partials[grid]; returns grid size used
+int sumsq_partials(const float* x, long long n, float* partials, int max_blocks, hipStream_t st);
+// optimizer scalars: sums partials, computes norm and clip scale
+struct OptScalars {
+  float gnorm;          // pre-clip global norm
+  float scale;          // clip factor applied to the gradient
+  float pnorm;          // post-update parameter norm
+  int count;            // adam step count (after increment)
+};
+void grad_norm_finalize(const float* partials, int nparts, const float* extra_sq /*nullable*/,
+                        float max_norm, OptScalars* sc, hipStream_t st);
+struct AdamParams {
+  float* p; float* m; float* v; const float* g;
+  float* target;        // polyak target (critic) or null
+  long long n;
+  float lr, b1, b2, eps, tau;
+  OptScalars* sc;
+  float* p_partials;    // sum of squares of new params per block
+};
+int adam_update(const AdamParams& a, float max_norm, int max_blocks, hipStream_t st);
+void param_norm_finalize(const float* partials, int nparts, OptScalars* sc, hipStream_t st);
+// *out = sum(partials)  (one block, double accumulation)
+void sum_partials(const float* partials, int nparts, float* out, hipStream_t st);
+void adam_count_incr(OptScalars* sc, hipStream_t st);
+
+struct AlphaParams {
+  const float* logpi;   // [B] (actor pass)
+  const int* counts;    // per local task
+  const int* rows;
+  int max_rows;
+  int T_l, task_begin, T_glob, B_glob;
+  float target_entropy;
+  float* log_alpha;     // [T_glob] replicated
+  float* m; float* v;
+  float* grad;          // [T_glob] scratch (allreduced in multi-GPU)
+  float* loss_part;     // scalar scratch: sum over rows of -(log_alpha_t)(logpi + H)
+  OptScalars* sc;
+};
+void alpha_grad(const AlphaParams& a, hipStream_t st);
+void alpha_adam(const AlphaParams& a, float lr, float b1, float b2, float eps, float max_norm,
+                hipStream_t st);
+
+struct LogParams {
+  const float* critic_sums;  // [0] sum w (q - y)^2 over members, [1] sum q
+  const float* actor_sums;   // [0] sum of actor loss terms
+  const OptScalars* critic; const OptScalars* actor;
+  const float* alpha_loss_sum;
+  const float* log_alpha; int T_glob;
+  float inv_critic; float inv_actor; float inv_b;
+  float* logs;
+};
+void write_logs(const LogParams& p, hipStream_t st);
+void bump_counter(unsigned long long* c, hipStream_t st);
+
+}  // namespace mtsac

@@ -1,0 +1,295 @@
+// optim.hip -- clip_by_global_norm + Adam (+ Polyak target) + temperature update.
+//
+// Reference: OptimizerConfig.spawn (mtrl/config/optim.py:26-43) = optax.chain(
+// clip_by_global_norm(max_grad_norm), adam(lr, eps=1e-5)); TrainState.apply_gradients
+// (mtrl/rl/algorithms/utils.py:11-46); optax.incremental_update Polyak
+// (mtsac.py:607-613); update_alpha (mtsac.py:713-731).
+//
+// Every network's parameters, gradients and moments live in ONE flat, 256-B aligned
+// buffer each, so the whole optimizer is three streaming passes: sum of squares of
+// the gradient (fixed grid -> deterministic partials), a one-block finalize, and the
+// fused clip / Adam / Polyak / param-norm pass (7 x 4 B per parameter, +8 B for the
+// target).  All reductions have a fixed shape, so results are run-to-run bitwise
+// reproducible.
+#include "kernels.h"
+
+namespace mtsac {
+
+namespace {
+
+__device__ inline float wsumf(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ inline double wsumd(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// block-wide sum for 256 threads, result valid in thread 0
+__device__ inline float block_sum256(float v) {
+  __shared__ float s[4];
+  v = wsumf(v);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = 0.f;
+  if (threadIdx.x == 0) r = (s[0] + s[1]) + (s[2] + s[3]);
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long long n4,
+                                                    float* __restrict__ partials) {
+  float acc = 0.f;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const float4 v = x4[i];
+    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  acc = block_sum256(acc);
+  if (threadIdx.x == 0) partials[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(256) void grad_norm_finalize_kernel(const float* __restrict__ partials, int nparts,
+                                                                 const float* __restrict__ extra_sq,
+                                                                 OptScalars* sc) {
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) acc += (double)partials[i];
+  acc = wsumd(acc);
+  __shared__ double s[4];
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot = (s[0] + s[1]) + (s[2] + s[3]);
+    if (extra_sq) tot += (double)(*extra_sq);
+    sc->gnorm = (float)sqrt(tot);
+    sc->count += 1;  // optax safe_increment of the adam count
+  }
+}
+
+__global__ __launch_bounds__(256) void param_norm_finalize_kernel(const float* __restrict__ partials, int nparts,
+                                                                  OptScalars* sc) {
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) acc += (double)partials[i];
+  acc = wsumd(acc);
+  __shared__ double s[4];
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) sc->pnorm = (float)sqrt((s[0] + s[1]) + (s[2] + s[3]));
+}
+
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ partials, int nparts,
+                                                           float* __restrict__ out) {
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) acc += (double)partials[i];
+  acc = wsumd(acc);
+  __shared__ double s[4];
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = (float)((s[0] + s[1]) + (s[2] + s[3]));
+}
+
+// clip (t / ||g||) * max when !(||g|| < max); Adam: mu = (1-b1) g + b1 mu,
+// nu = (1-b2) g^2 + b2 nu, mu_hat = mu / (1 - b1^k), nu_hat = nu / (1 - b2^k),
+// p += -lr * mu_hat / (sqrt(nu_hat) + eps); then target = tau p + (1 - tau) target.
+template <bool POLYAK>
+__global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm) {
+  const OptScalars sc = *a.sc;
+  const bool clip = (max_norm > 0.f) && !(sc.gnorm < max_norm);
+  const float gn = sc.gnorm;
+  const float bc1 = 1.0f - powf(a.b1, (float)sc.count);
+  const float bc2 = 1.0f - powf(a.b2, (float)sc.count);
+  const float omb1 = 1.0f - a.b1, omb2 = 1.0f - a.b2, neg_lr = -a.lr;
+  const float omtau = 1.0f - a.tau;
+  const long long n4 = a.n >> 2;
+  float acc = 0.f;
+  float4* p4 = reinterpret_cast<float4*>(a.p);
+  float4* m4 = reinterpret_cast<float4*>(a.m);
+  float4* v4 = reinterpret_cast<float4*>(a.v);
+  const float4* g4 = reinterpret_cast<const float4*>(a.g);
+  float4* t4 = reinterpret_cast<float4*>(a.target);
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float4 g = g4[i], p = p4[i], m = m4[i], v = v4[i];
+    float* gp = &g.x;
+    float* pp = &p.x;
+    float* mp = &m.x;
+    float* vp = &v.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gk = gp[k];
+      if (clip) gk = (gk / gn) * max_norm;
+      mp[k] = omb1 * gk + a.b1 * mp[k];
+      vp[k] = omb2 * (gk * gk) + a.b2 * vp[k];
+      const float mh = mp[k] / bc1;
+      const float vh = vp[k] / bc2;
+      const float u = mh / (sqrtf(vh) + a.eps);
+      pp[k] = pp[k] + u * neg_lr;
+      acc += pp[k] * pp[k];
+    }
+    p4[i] = p;
+    m4[i] = m;
+    v4[i] = v;
+    if (POLYAK) {
+      float4 t = t4[i];
+      t.x = a.tau * p.x + omtau * t.x;
+      t.y = a.tau * p.y + omtau * t.y;
+      t.z = a.tau * p.z + omtau * t.z;
+      t.w = a.tau * p.w + omtau * t.w;
+      t4[i] = t;
+    }
+  }
+  acc = block_sum256(acc);
+  if (threadIdx.x == 0) a.p_partials[blockIdx.x] = acc;
+}
+
+struct RowPtrs {
+  const float* p[4];
+};
+
+__global__ __launch_bounds__(1024) void reduce_rows_kernel(RowPtrs in, int n_in, int B, float* __restrict__ out) {
+  __shared__ double s[16];
+  for (int k = 0; k < n_in; ++k) {
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < B; i += 1024) acc += (double)in.p[k][i];
+    acc = wsumd(acc);
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int w = 0; w < 16; ++w) t += s[w];
+      out[k] = (float)t;
+    }
+    __syncthreads();
+  }
+}
+
+// temperature gradient: d/dlogalpha_t mean_b(-(x_b . logalpha)(logpi_b + H))
+//   = -(1/B) sum_{b in t}(logpi_b + H)    (x one-hot, validated by the gather)
+__global__ __launch_bounds__(256) void alpha_grad_kernel(AlphaParams a) {
+  __shared__ float red[4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < a.T_glob; i += 256) a.grad[i] = 0.f;
+  __syncthreads();
+  float loss_acc = 0.f;  // lane-0 accumulators per wave
+  for (int t = wave; t < a.T_l; t += 4) {
+    const int n = a.counts[t];
+    const int* rl = a.rows + (long long)t * a.max_rows;
+    float s = 0.f;
+    for (int j = lane; j < n; j += 64) s += a.logpi[rl[j]] + a.target_entropy;
+    s = wsumf(s);
+    const int tg = a.task_begin + t;
+    if (lane == 0) {
+      a.grad[tg] = -s / (float)a.B_glob;
+      loss_acc += -a.log_alpha[tg] * s;
+    }
+  }
+  if (lane == 0) red[wave] = loss_acc;
+  __syncthreads();
+  if (threadIdx.x == 0) *a.loss_part = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(64) void alpha_adam_kernel(AlphaParams a, float lr, float b1, float b2, float eps,
+                                                        float max_norm) {
+  const int lane = threadIdx.x;
+  float sq = 0.f;
+  for (int i = lane; i < a.T_glob; i += 64) sq += a.grad[i] * a.grad[i];
+  const float gn = sqrtf(wsumf(sq));
+  const bool clip = (max_norm > 0.f) && !(gn < max_norm);
+  const int count = a.sc->count + 1;
+  const float bc1 = 1.0f - powf(b1, (float)count), bc2 = 1.0f - powf(b2, (float)count);
+  float es = 0.f;
+  for (int i = lane; i < a.T_glob; i += 64) {
+    float g = a.grad[i];
+    if (clip) g = (g / gn) * max_norm;
+    const float m = (1.0f - b1) * g + b1 * a.m[i];
+    const float v = (1.0f - b2) * (g * g) + b2 * a.v[i];
+    a.m[i] = m;
+    a.v[i] = v;
+    const float u = (m / bc1) / (sqrtf(v / bc2) + eps);
+    const float p = a.log_alpha[i] + u * (-lr);
+    a.log_alpha[i] = p;
+    es += expf(p);
+  }
+  es = wsumf(es);
+  if (lane == 0) {
+    a.sc->count = count;
+    a.sc->gnorm = gn;
+    a.sc->pnorm = es;  // alpha log: sum(exp(log_alpha))  (mtsac.py:730)
+  }
+}
+
+__global__ void write_logs_kernel(LogParams p) {
+  p.logs[0] = p.critic_sums[1] * p.inv_critic;  // losses/qf_values
+  p.logs[1] = p.critic_sums[0] * p.inv_critic;  // losses/qf_loss
+  p.logs[2] = p.critic->gnorm;              // metrics/critic_grad_magnitude
+  p.logs[3] = p.critic->pnorm;              // metrics/critic_params_norm
+  p.logs[4] = p.actor_sums[0] * p.inv_actor;    // losses/actor_loss
+  p.logs[5] = p.actor->gnorm;               // metrics/actor_grad_magnitude
+  p.logs[6] = p.actor->pnorm;               // metrics/actor_params_norm
+  p.logs[7] = 0.0f;                         // metrics/explore_loss (explore=False, mtsac.py:277)
+  p.logs[8] = *p.alpha_loss_sum * p.inv_b;  // losses/alpha_loss
+  float s = 0.f;
+  for (int i = 0; i < p.T_glob; ++i) s += expf(p.log_alpha[i]);
+  p.logs[9] = s;                            // alpha
+}
+
+__global__ void bump_kernel(unsigned long long* c) { *c += 1ull; }
+
+}  // namespace
+
+void reduce_rows(const float* const* ins, int n_in, int B, float* out, hipStream_t st) {
+  RowPtrs r{};
+  for (int i = 0; i < n_in && i < 4; ++i) r.p[i] = ins[i];
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(1), dim3(1024), 0, st, r, n_in, B, out);
+}
+
+int sumsq_partials(const float* x, long long n, float* partials, int max_blocks, hipStream_t st) {
+  const long long n4 = n >> 2;
+  long long g = (n4 + 255) / 256;
+  if (g > max_blocks) g = max_blocks;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)g), dim3(256), 0, st, x, n4, partials);
+  return (int)g;
+}
+
+void grad_norm_finalize(const float* partials, int nparts, const float* extra_sq, float max_norm, OptScalars* sc,
+                        hipStream_t st) {
+  (void)max_norm;
+  hipLaunchKernelGGL(grad_norm_finalize_kernel, dim3(1), dim3(256), 0, st, partials, nparts, extra_sq, sc);
+}
+
+int adam_update(const AdamParams& a, float max_norm, int max_blocks, hipStream_t st) {
+  const long long n4 = a.n >> 2;
+  long long g = (n4 + 255) / 256;
+  if (g > max_blocks) g = max_blocks;
+  if (g < 1) g = 1;
+  if (a.target)
+    hipLaunchKernelGGL(adam_kernel<true>, dim3((unsigned)g), dim3(256), 0, st, a, max_norm);
+  else
+    hipLaunchKernelGGL(adam_kernel<false>, dim3((unsigned)g), dim3(256), 0, st, a, max_norm);
+  return (int)g;
+}
+
+void param_norm_finalize(const float* partials, int nparts, OptScalars* sc, hipStream_t st) {
+  hipLaunchKernelGGL(param_norm_finalize_kernel, dim3(1), dim3(256), 0, st, partials, nparts, sc);
+}
+
+void sum_partials(const float* partials, int nparts, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, st, partials, nparts, out);
+}
+
+void alpha_grad(const AlphaParams& a, hipStream_t st) {
+  hipLaunchKernelGGL(alpha_grad_kernel, dim3(1), dim3(256), 0, st, a);
+}
+
+void alpha_adam(const AlphaParams& a, float lr, float b1, float b2, float eps, float max_norm, hipStream_t st) {
+  hipLaunchKernelGGL(alpha_adam_kernel, dim3(1), dim3(64), 0, st, a, lr, b1, b2, eps, max_norm);
+}
+
+void write_logs(const LogParams& p, hipStream_t st) { hipLaunchKernelGGL(write_logs_kernel, dim3(1), dim3(1), 0, st, p); }
+
+void bump_counter(unsigned long long* c, hipStream_t st) { hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(1), 0, st, c); }
+
+}  // namespace mtsac

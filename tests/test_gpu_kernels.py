@@ -1,0 +1,184 @@
+"""GPU parity of the individual device kernels (fp32 MFMA GEMM, index stream, gather).
+
+All calls go through libmtsac.so.  GEMMs are checked against a float64 numpy
+product of the same fp32 inputs (the "plain fp32 reference of the same op");
+the index stream and the gather are checked BIT-EXACT against the oracle, whose
+PCG64 restatement is itself pinned to ``numpy.random.default_rng`` (the
+reference's dependency; tests/test_oracle_pcg64.py).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from oracle.buffer import MultiTaskReplayBufferOracle
+from oracle.pcg64 import PCG64State
+
+pytestmark = pytest.mark.gpu
+
+NN, NT, TN = 0, 1, 2
+STORE, BIAS_RELU, MASK = 0, 1, 2
+
+
+def _ref(kind, A, B, M, N, K):
+    A64, B64 = A.astype(np.float64), B.astype(np.float64)
+    if kind == NN:
+        return A64[:M, :K] @ B64[:K, :N], np.abs(A64[:M, :K]) @ np.abs(B64[:K, :N])
+    if kind == NT:
+        return A64[:M, :K] @ B64[:N, :K].T, np.abs(A64[:M, :K]) @ np.abs(B64[:N, :K]).T
+    return A64[:K, :M].T @ B64[:K, :N], np.abs(A64[:K, :M]).T @ np.abs(B64[:K, :N])
+
+
+@pytest.mark.parametrize("kind", [NN, NT, TN])
+@pytest.mark.parametrize("shape", [(200, 136, 93), (128, 128, 32), (64, 400, 400), (257, 132, 260), (8, 4, 4)])
+def test_gemm_store(kind, shape):
+    from mtrl_amd.engine import debug_gemm
+
+    M, N, K = shape
+    rng = np.random.default_rng(0)
+    Kp = (K + 3) // 4 * 4
+    if kind == NN:
+        A = np.zeros((M, Kp), np.float32); A[:, :K] = rng.standard_normal((M, K))
+        B = rng.standard_normal((K, N)).astype(np.float32)
+    elif kind == NT:
+        A = np.zeros((M, Kp), np.float32); A[:, :K] = rng.standard_normal((M, K))
+        B = np.zeros((N, Kp), np.float32); B[:, :K] = rng.standard_normal((N, K))
+    else:
+        Mp = (M + 3) // 4 * 4
+        A = np.zeros((K, Mp), np.float32); A[:, :M] = rng.standard_normal((K, M))
+        B = rng.standard_normal((K, N)).astype(np.float32)
+    C0 = np.full((M, N), 7.0, np.float32)
+    C, db = debug_gemm(kind, STORE, A, B, C0, M, N, K, want_db=(kind == TN))
+    ref, mag = _ref(kind, A, B, M, N, K)
+    err = np.abs(C - ref)
+    assert np.all(err <= 2e-6 * mag + 1e-30), float((err / mag).max())
+    if kind == TN:
+        np.testing.assert_allclose(db[0], B[:K, :N].astype(np.float64).sum(0), rtol=1e-5, atol=1e-4)
+
+
+def test_gemm_epilogues_batched():
+    from mtrl_amd.engine import debug_gemm
+
+    rng = np.random.default_rng(1)
+    M, N, K, E = 300, 200, 96, 2
+    A = rng.standard_normal((M, K)).astype(np.float32)
+    B = rng.standard_normal((E, K, N)).astype(np.float32)
+    bias = rng.standard_normal((E, N)).astype(np.float32)
+    C, _ = debug_gemm(NN, BIAS_RELU, A, B, np.zeros((E, M, N), np.float32), M, N, K, batch=E, a_shared=True,
+                      bias=bias)
+    for e in range(E):
+        ref = np.maximum(A.astype(np.float64) @ B[e] + bias[e], 0)
+        np.testing.assert_allclose(C[e], ref, rtol=1e-5, atol=1e-4)
+    # relu-mask epilogue on NT: C = (dY W^T) * (H > 0)
+    dY = rng.standard_normal((E, M, N)).astype(np.float32)
+    W = rng.standard_normal((E, K, N)).astype(np.float32)  # stored [N=K][K=N] for the NT product
+    H = rng.standard_normal((E, M, K)).astype(np.float32)
+    C, _ = debug_gemm(NT, MASK, dY, W, np.zeros((E, M, K), np.float32), M, K, N, batch=E, mask=H)
+    for e in range(E):
+        ref = (dY[e].astype(np.float64) @ W[e].T.astype(np.float64)) * (H[e] > 0)
+        np.testing.assert_allclose(C[e], ref, rtol=1e-5, atol=1e-4)
+
+
+def _small_engine(T=3, n=4, cap=50, D=None, normalize=False, **kw):
+    from mtrl_amd.engine import MTSACEngine, make_config
+
+    D = D if D is not None else 39 + T
+    cfg = make_config(num_tasks=T, task_count=T, obs_dim=D, batch_per_task=n, capacity=cap, actor_width=16,
+                      critic_width=16, normalize_rewards=1 if normalize else 0, **kw)
+    return MTSACEngine(cfg)
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 128])
+@pytest.mark.parametrize("seed", [0, 1, 42])
+def test_index_stream_bit_exact(n, seed):
+    cap = 100_000 if n == 128 else 5000
+    eng = _small_engine(T=2, n=n, cap=cap)
+    eng.seed_rng(seed)
+    ref = PCG64State.from_seed(seed)
+    # sizes before full (pos < n gives high = n), mid-fill, and full
+    for pos, full in [(0, False), (1, False), (n, False), (777 % cap, False), (0, True), (0, True), (13, True)]:
+        eng.set_buffer_state(pos, full)
+        high = max(cap if full else pos, n)
+        idx, _ = eng.sample()
+        want = ref.integers(high, n)
+        np.testing.assert_array_equal(idx, want)
+        assert eng.get_rng_state() == ref.to_numpy_state()
+    eng.close()
+
+
+def _fill(eng_or_oracle_pairs, cap, T, D, A, seed=5, slots=None):
+    rng = np.random.default_rng(seed)
+    slots = cap if slots is None else slots
+    F = D - T
+    obs = np.zeros((slots, T, D), np.float32)
+    obs[:, :, :F] = rng.standard_normal((slots, T, F))
+    obs[:, np.arange(T), F + np.arange(T)] = 1.0
+    nobs = obs.copy()
+    nobs[:, :, :F] = rng.standard_normal((slots, T, F))
+    act = rng.uniform(-1, 1, (slots, T, A)).astype(np.float32)
+    rew = rng.uniform(0, 10, (slots, T)).astype(np.float32)
+    done = (rng.uniform(size=(slots, T)) < 0.1).astype(np.float32)
+    return obs, nobs, act, rew, done
+
+
+@pytest.mark.parametrize("normalize", [False, True])
+def test_gather_bit_exact(normalize):
+    T, n, cap, A = 3, 8, 64, 4
+    D = 39 + T
+    eng = _small_engine(T=T, n=n, cap=cap, normalize=normalize)
+    orc = MultiTaskReplayBufferOracle(cap * T, T, D, A, seed=7, normalize_rewards=normalize)
+    eng.seed_rng(7)
+    obs, nobs, act, rew, done = _fill(None, cap, T, D, A, slots=40)
+    for s in range(40):  # buffer_add path (advances pos, tracks reward stats)
+        eng.buffer_add(obs[s], nobs[s], act[s], rew[s], done[s])
+        orc.add(obs[s], nobs[s], act[s], rew[s], done[s])
+    assert eng.buffer_state() == (orc.pos, orc.full)
+    for _ in range(3):
+        idx, got = eng.sample()
+        want_idx = orc.sample_indices(n * T)
+        np.testing.assert_array_equal(idx, want_idx)
+        want = orc.gather(want_idx)
+        for g, w in zip(got, want):
+            np.testing.assert_array_equal(g.reshape(w.shape), w.astype(np.float32))
+    # bulk write path + wrap-around semantics (buffers.py:337-343)
+    eng.buffer_write(0, obs[:32].reshape(-1, D), nobs[:32].reshape(-1, D), act[:32].reshape(-1, A),
+                     rew[:32].reshape(-1), done[:32].reshape(-1))
+    o2, n2, a2, r2, d2 = eng.buffer_read(0, 32)
+    np.testing.assert_array_equal(o2, obs[:32]); np.testing.assert_array_equal(n2, nobs[:32])
+    np.testing.assert_array_equal(a2, act[:32]); np.testing.assert_array_equal(r2, rew[:32])
+    np.testing.assert_array_equal(d2, done[:32])
+    eng.close()
+
+
+def test_buffer_add_wraps_like_reference():
+    """tests/test_rl_buffers.py:21-35 semantics, on the multi-task device buffer."""
+    T, cap, A = 2, 4, 4
+    D = 39 + T
+    eng = _small_engine(T=T, n=1, cap=cap)
+    obs, nobs, act, rew, done = _fill(None, cap, T, D, A, slots=cap + 2)
+    for s in range(cap):
+        eng.buffer_add(obs[s], nobs[s], act[s], rew[s], done[s])
+    assert eng.buffer_state() == (0, True)
+    for s in range(2):
+        eng.buffer_add(obs[cap + s], nobs[cap + s], act[cap + s], rew[cap + s], done[cap + s])
+    assert eng.buffer_state() == (2, True)
+    o, _, _, _, _ = eng.buffer_read(0, 2)
+    np.testing.assert_array_equal(o, obs[cap:cap + 2])
+    eng.close()
+
+
+def test_bad_one_hot_is_reported():
+    from mtrl_amd._lib import MTSACError
+
+    T, n, cap, A = 2, 2, 8, 4
+    D = 39 + T
+    eng = _small_engine(T=T, n=n, cap=cap)
+    obs, nobs, act, rew, done = _fill(None, cap, T, D, A)
+    obs[:, 0, D - T:] = 0.0  # task 0 rows lose their one-hot
+    eng.buffer_write(0, obs.reshape(-1, D), nobs.reshape(-1, D), act.reshape(-1, A), rew.reshape(-1),
+                     done.reshape(-1))
+    eng.set_buffer_state(0, True)
+    with pytest.raises(MTSACError):
+        eng.sample()
+    eng.close()
