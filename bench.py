@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""bench.py -- SAC gradient-steps/sec of the MI355X MTSAC engine (BASELINE.json metric).
+
+One "step" = one complete MTSAC gradient step (reference MTSAC.update,
+mtrl/rl/algorithms/mtsac.py:1173-1251) on one batch of 128 rows per task drawn
+from the device-resident replay buffer: index stream + gather, actor forward on s',
+target critic, critic forward/backward + clip/Adam/Polyak, actor forward, critic
+with the updated params, actor backward + clip/Adam, temperature update.  Nothing
+is skipped inside the timed region; inputs are resident in HBM.
+
+Default workload (N=1): MT50 MTMHSAC-v2 at width 2048 (experiments/width_scaling/
+mt50_mtmhsac_v2_2048.py): T=50, B=6400, fp32.  With --gpus N (torchrun, one rank per
+GPU) the 50 tasks are sharded contiguously over the ranks and the trunk gradients
+are all-reduced over RCCL; the problem size is fixed, so scaling is "strong".
+
+Prints ONE JSON line on rank 0 (keys per the driver contract, plus roofline and
+cpu_baseline).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+WORKLOADS = {
+    # name: (T, width, clip, description)
+    "mt50_w2048": (50, 2048, False, "MT50 MTMHSAC-v2 width=2048 (experiments/width_scaling/mt50_mtmhsac_v2_2048.py)"),
+    "mt10_w2048": (10, 2048, True, "MT10 MTMHSAC width=2048 clip (experiments/width_scaling/mt10_mtmhsac_v2_2048.py)"),
+    "mt10_w400": (10, 400, False, "MT10 MTMHSAC width=400 (experiments/mt10_mtmhsac.py)"),
+    "mt50_w400": (50, 400, False, "MT50 MTMHSAC-v2 width=400 (experiments/mt50_mtmhsac_v2.py)"),
+}
+FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+HBM_PEAK_GBS = 8000.0
+GEMM_FAMILIES = {0: "gemm_f32_kernel<NN> (trunk forward)", 1: "gemm_f32_kernel<NT> (data grad)",
+                 2: "gemm_f32_kernel<TN> (weight grad)"}
+
+
+def algorithmic_flops(T, W, n=128, A=4):
+    """GEMM flops of one step counting only each row's own head."""
+    B = n * T
+    Ia, Ic = 39 + T, 39 + T + A
+    Af = 2 * B * (Ia * W + 2 * W * W + 8 * W)
+    Cf = 2 * B * (Ic * W + 2 * W * W + W)
+    return (Af + 2 * Cf + 2 * (3 * Cf - 2 * B * Ic * W) + (3 * Af - 2 * B * Ia * W)
+            + 2 * (2 * Cf - 2 * B * Ic * W + 2 * B * 4 * W))
+
+
+def shard(T, world, rank):
+    base, rem = divmod(T, world)
+    begin = rank * base + min(rank, rem)
+    return begin, base + (1 if rank < rem else 0)
+
+
+def cpu_baseline(T, W, clip, steps):
+    import torch
+    from oracle.cpu_baseline import CPUMTSAC
+
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    m = CPUMTSAC(T, 39 + T, W, 128, 100_000, clip=clip)
+    m.step()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m.step()
+    dt = time.perf_counter() - t0
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
+    except OSError:
+        pass
+    return {"value": steps / dt, "unit": "SAC gradient-steps/sec", "cores": threads, "kind": "port",
+            "sample": f"{steps} full steps (B={128 * T}, W={W}, fp32 PyTorch-CPU autograd restatement, "
+                      f"oracle/cpu_baseline.py) after 1 warm-up step, {dt:.1f}s, {model}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="mt50_w2048", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")  # host-side control plane only; gradients go over RCCL
+
+    from mtrl_amd import _lib as L
+    from mtrl_amd.engine import MTSACEngine, make_config
+    from mtrl_amd.init import init_mtsac
+
+    T, W, clip, desc = WORKLOADS[args.workload]
+    tb, tc = shard(T, world, rank)
+    cfg = make_config(num_tasks=T, task_begin=tb, task_count=tc, obs_dim=39 + T, actor_width=W, critic_width=W,
+                      batch_per_task=128, capacity=100_000, clip=int(clip))
+    eng = MTSACEngine(cfg, device=local_rank)
+    actor, critic = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=1, task_begin=tb, task_count=tc)
+    eng.set_params(L.ACTOR, actor)
+    eng.set_params(L.CRITIC, critic)
+    eng.set_params(L.CRITIC_TARGET, critic)
+    eng.buffer_fill_synthetic(1234)
+    eng.seed_rng(1)  # every rank draws the same index vector (buffers.py:523-527)
+    eng.enable_graph(not args.no_graph)
+    if world > 1:
+        uid = [MTSACEngine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(uid[0], world, rank)
+
+    import torch
+
+    eng.update_many(args.warmup)
+    eng.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(local_rank)
+    t0 = time.perf_counter()
+    eng.update_many(args.steps)
+    eng.synchronize()
+    torch.cuda.synchronize(local_rank)
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    logs = eng.logs()
+    assert all(math.isfinite(v) for v in logs.values()), logs
+
+    # dominant-kernel roofline: HIP events around every GEMM launch of one captured step
+    eng.set_timing(True)
+    eng.update_many(1)
+    eng.synchronize()
+    fam = {f: eng.timing(f) for f in GEMM_FAMILIES}
+    eng.set_timing(False)
+    dom = max(fam, key=lambda f: fam[f][0])
+    ms, nl, fl = fam[dom]
+    gemm_ms = sum(v[0] for v in fam.values())
+    gemm_fl = sum(v[2] for v in fam.values())
+    achieved = (fl / nl) / (ms / nl * 1e-3) / 1e12 if nl else 0.0
+
+    flops = algorithmic_flops(T, W)
+    sps = args.steps / elapsed
+    out = {
+        "metric": "SAC gradient-steps/sec, MT50 width-2048 batch=128/task",
+        "value": sps,
+        "unit": "SAC gradient-steps/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (SURVEY.md §8d recipe, device-filled full buffer, cap=100000/task; random-init weights)",
+        "config": {"workload": desc, "num_tasks": T, "width": W, "batch_per_task": 128, "global_batch": 128 * T,
+                   "parallelism": f"task-shard{world}" if world > 1 else "single", "graph": not args.no_graph},
+        "roofline": {"bound": "mfma", "kernel": GEMM_FAMILIES[dom], "achieved": achieved,
+                     "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TF,
+                     "traffic": None, "launches": nl, "avg_launch_us": 1e3 * ms / max(nl, 1),
+                     "algorithmic_flops_per_launch": fl / max(nl, 1)},
+        "step_flops": flops,
+        "step_tflops_per_s": flops * sps / world / 1e12,
+        "gemm_share_of_step": gemm_ms / (1e3 * elapsed / args.steps),
+        "gemm_tflops_per_s": gemm_fl / (gemm_ms * 1e-3) / 1e12 if gemm_ms else 0.0,
+        "logs": logs,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(T, W, clip, args.cpu_steps)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    eng.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

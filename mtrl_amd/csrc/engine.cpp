@@ -971,7 +971,7 @@ int mtsac_update(mtsac_engine* h, const mtsac_batch* b, const float* eps_next, c
 int mtsac_update_many(mtsac_engine* h, int32_t steps) {
   if (!h) return fail(-22, "null engine");
   if (steps <= 0) return 0;
-  if (!h->use_graph) {
+  if (!h->use_graph || h->timing) {  // event pairs around launches need eager issue
     for (int s = 0; s < steps; ++s) {
       h->tl_next = 0;
       h->step(true, true);

@@ -104,7 +104,7 @@ class MTSACEngine:
         check(self.lib.mtsac_buffer_add(self._h, *[a[0] for a in args]))
 
     def buffer_write(self, slot_begin: int, obs, next_obs, actions, rewards, dones) -> None:
-        n = int(np.asarray(rewards).shape[0])
+        n = int(np.asarray(rewards).size) // self.T_l  # slots (rows are slot-major, T_l per slot)
         args = [_ptr(x) for x in (obs, next_obs, actions, rewards, dones)]
         check(self.lib.mtsac_buffer_write(self._h, slot_begin, n, *[a[0] for a in args]))
 

@@ -94,6 +94,7 @@ def _small_engine(T=3, n=4, cap=50, D=None, normalize=False, **kw):
 def test_index_stream_bit_exact(n, seed):
     cap = 100_000 if n == 128 else 5000
     eng = _small_engine(T=2, n=n, cap=cap)
+    eng.buffer_fill_synthetic(3)  # valid one-hot rows everywhere
     eng.seed_rng(seed)
     ref = PCG64State.from_seed(seed)
     # sizes before full (pos < n gives high = n), mid-fill, and full
