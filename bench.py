@@ -54,12 +54,6 @@ def algorithmic_flops(T, W, n=128, A=4):
             + 2 * (2 * Cf - 2 * B * Ic * W + 2 * B * 4 * W))
 
 
-def shard(T, world, rank):
-    base, rem = divmod(T, world)
-    begin = rank * base + min(rank, rem)
-    return begin, base + (1 if rank < rem else 0)
-
-
 def cpu_baseline(T, W, clip, steps):
     import torch
     from oracle.cpu_baseline import CPUMTSAC
@@ -106,9 +100,10 @@ def main():
     from mtrl_amd import _lib as L
     from mtrl_amd.engine import MTSACEngine, make_config
     from mtrl_amd.init import init_mtsac
+    from mtrl_amd.shard import shard_tasks
 
     T, W, clip, desc = WORKLOADS[args.workload]
-    tb, tc = shard(T, world, rank)
+    tb, tc = shard_tasks(T, world, rank)
     cfg = make_config(num_tasks=T, task_begin=tb, task_count=tc, obs_dim=39 + T, actor_width=W, critic_width=W,
                       batch_per_task=128, capacity=100_000, clip=int(clip))
     eng = MTSACEngine(cfg, device=local_rank)

@@ -174,6 +174,14 @@ int mtsac_sample_action(mtsac_engine* h, const float* obs, int32_t n, const floa
 int mtsac_comm_unique_id_size(void);
 int mtsac_comm_get_unique_id(void* id_out);
 int mtsac_comm_init(mtsac_engine* h, const void* unique_id, int32_t nranks, int32_t rank);
+/* Bring-your-own collective: when no RCCL communicator is set, the engine calls
+ * fn(user, device_buffer, count) at each all-reduce point (after synchronising its
+ * stream); fn must leave the element-wise SUM over all shards in the buffer before
+ * returning.  Disables hipGraph replay for this engine.  fn == NULL removes it. */
+typedef int (*mtsac_allreduce_fn)(void* user, float* device_buffer, int64_t count);
+int mtsac_set_allreduce_hook(mtsac_engine* h, mtsac_allreduce_fn fn, void* user);
+/* plain device/host copy helper for hooks written in a host language (hipMemcpyDefault) */
+int mtsac_memcpy(void* dst, const void* src, int64_t bytes);
 
 /* measurement: per-kernel-family HIP event timing of the last update_many call */
 int mtsac_set_timing(mtsac_engine* h, int32_t enable);

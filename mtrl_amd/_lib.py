@@ -124,6 +124,8 @@ SIGNATURES = {
     "mtsac_comm_unique_id_size": (ctypes.c_int, []),
     "mtsac_comm_get_unique_id": (ctypes.c_int, [P]),
     "mtsac_comm_init": (ctypes.c_int, [P, P, I32, I32]),
+    "mtsac_set_allreduce_hook": (ctypes.c_int, [P, ctypes.c_void_p, P]),
+    "mtsac_memcpy": (ctypes.c_int, [P, P, I64]),
     "mtsac_set_timing": (ctypes.c_int, [P, I32]),
     "mtsac_get_timing": (ctypes.c_int, [P, I32, PD, PI32, PD]),
     "mtsac_debug_gemm": (
@@ -132,6 +134,8 @@ SIGNATURES = {
          ctypes.c_int, P, ctypes.c_int, P, ctypes.c_int, P, P, ctypes.c_int, P],
     ),
 }
+
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
 
 _lib = None
 

@@ -136,6 +136,9 @@ struct mtsac_engine {
   // comm
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  mtsac_allreduce_fn hook = nullptr;
+  void* hook_user = nullptr;
+  std::string comm_error;
   // timing
   bool timing = false;
   struct TimedLaunch {
@@ -288,8 +291,18 @@ struct mtsac_engine {
   }
 
   void allreduce(float* buf, size_t count) {
-    if (comm == nullptr || nranks <= 1) return;
-    ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm, st);
+    if (comm != nullptr && nranks > 1) {
+      ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm, st);
+      if (r != ncclSuccess) comm_error = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
+      return;
+    }
+    if (hook) {
+      if (hipStreamSynchronize(st) != hipSuccess) {
+        comm_error = "stream sync before all-reduce hook failed";
+        return;
+      }
+      if (hook(hook_user, buf, (int64_t)count) != 0) comm_error = "all-reduce hook failed";
+    }
   }
 
   // clip + Adam (+ Polyak) over one network; gradient already complete (and reduced)
@@ -509,6 +522,11 @@ struct mtsac_engine {
   }
 
   int check_err() {
+    if (!comm_error.empty()) {
+      std::string m = comm_error;
+      comm_error.clear();
+      return fail(-5, m);
+    }
     int e = 0;
     HIP_TRY(hipMemcpyAsync(&e, err, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -971,7 +989,7 @@ int mtsac_update(mtsac_engine* h, const mtsac_batch* b, const float* eps_next, c
 int mtsac_update_many(mtsac_engine* h, int32_t steps) {
   if (!h) return fail(-22, "null engine");
   if (steps <= 0) return 0;
-  if (!h->use_graph || h->timing) {  // event pairs around launches need eager issue
+  if (!h->use_graph || h->timing || h->hook) {  // events / host hooks need eager issue
     for (int s = 0; s < steps; ++s) {
       h->tl_next = 0;
       h->step(true, true);
@@ -1097,6 +1115,19 @@ int mtsac_comm_init(mtsac_engine* h, const void* unique_id, int32_t nranks, int3
     h->gexec = nullptr;
     h->graph = nullptr;
   }
+  return 0;
+}
+
+int mtsac_set_allreduce_hook(mtsac_engine* h, mtsac_allreduce_fn fn, void* user) {
+  if (!h) return fail(-22, "null engine");
+  h->hook = fn;
+  h->hook_user = user;
+  return 0;
+}
+
+int mtsac_memcpy(void* dst, const void* src, int64_t bytes) {
+  if (!dst || !src || bytes < 0) return fail(-22, "bad copy arguments");
+  HIP_TRY(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDefault));
   return 0;
 }
 

@@ -223,6 +223,26 @@ class MTSACEngine:
         buf = ctypes.create_string_buffer(bytes(unique_id), len(unique_id))
         check(self.lib.mtsac_comm_init(self._h, buf, nranks, rank))
 
+    def set_allreduce_hook(self, fn) -> None:
+        """``fn(device_ptr: int, count: int)`` must leave the SUM over shards in the buffer."""
+        if fn is None:
+            self._hook = None
+            check(self.lib.mtsac_set_allreduce_hook(self._h, None, None))
+            return
+
+        def tramp(_user, ptr, count):
+            try:
+                fn(ptr, count)
+                return 0
+            except Exception:  # pragma: no cover - reported through the engine
+                import traceback
+
+                traceback.print_exc()
+                return -1
+
+        self._hook = _lib.ALLREDUCE_FN(tramp)
+        check(self.lib.mtsac_set_allreduce_hook(self._h, ctypes.cast(self._hook, ctypes.c_void_p), None))
+
     # ------------------------------------------------------------------ measurement
     def set_timing(self, on: bool) -> None:
         check(self.lib.mtsac_set_timing(self._h, 1 if on else 0))
