@@ -117,6 +117,7 @@ struct mtsac_engine {
   float *logpi_n = nullptr, *logpi = nullptr, *y = nullptr, *dq = nullptr, *row_a = nullptr, *row_b = nullptr,
         *row_c = nullptr, *alpha_w = nullptr, *cache = nullptr, *dout_a = nullptr;
   float* partials = nullptr;
+  float* pn = nullptr;  // [critic trunk |p|^2, actor trunk, critic heads, actor heads]
   float* log_alpha = nullptr;
   float *la_m = nullptr, *la_v = nullptr;
   OptScalars* sc_alpha = nullptr;
@@ -291,7 +292,7 @@ struct mtsac_engine {
   }
 
   void allreduce(float* buf, size_t count) {
-    if (comm != nullptr && nranks > 1) {
+    if (comm != nullptr) {
       ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm, st);
       if (r != ncclSuccess) comm_error = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
       return;
@@ -305,8 +306,9 @@ struct mtsac_engine {
     }
   }
 
-  // clip + Adam (+ Polyak) over one network; gradient already complete (and reduced)
-  void optimize(Net& net, float lr, float max_norm, bool polyak) {
+  // clip + Adam (+ Polyak) over one network; gradient already complete (and reduced).
+  // |p|^2 lands in pn[slot] (trunk, replicated) and pn[2 + slot] (local heads, summed later).
+  void optimize(Net& net, float lr, float max_norm, bool polyak, int slot) {
     float* extra = net.g + net.n_flat;
     int np = sumsq_partials(net.g + net.trunk_off, net.n_flat - net.trunk_off, partials, PART, st);
     grad_norm_finalize(partials, np, extra + 0, max_norm, net.sc, st);
@@ -324,8 +326,19 @@ struct mtsac_engine {
     a.tau = cfg.tau;
     a.sc = net.sc;
     a.p_partials = partials;
-    int na = adam_update(a, max_norm, PART, st);
-    param_norm_finalize(partials, na, net.sc, st);
+    // heads and trunk as two launches so the trunk's reduction tree does not depend on the
+    // shard's head count (bitwise-identical replicated trunks and norms on every rank)
+    a.n = net.trunk_off;
+    int nh = adam_update(a, max_norm, 0, PART, st);
+    sum_partials(partials, nh, pn + 2 + slot, st);
+    a.p += net.trunk_off;
+    a.m += net.trunk_off;
+    a.v += net.trunk_off;
+    a.g += net.trunk_off;
+    if (a.target) a.target += net.trunk_off;
+    a.n = net.n_flat - net.trunk_off;
+    int na = adam_update(a, max_norm, 0, PART, st);
+    sum_partials(partials, na, pn + slot, st);
   }
 
   void head_sq(Net& net) {  // local |g_head|^2 into the scalar tail
@@ -400,7 +413,7 @@ struct mtsac_engine {
     }
     head_sq(critic);
     allreduce(critic.g + critic.trunk_off, (size_t)(critic.n_flat - critic.trunk_off + EXTRA));
-    optimize(critic, cfg.critic_lr, cfg.critic_max_grad_norm, true);
+    optimize(critic, cfg.critic_lr, cfg.critic_max_grad_norm, true, 0);
 
     // ---- actor update (mtsac.py:623-711), critic params already updated
     trunk_forward(actor, actor.p, xa, ld_a, ha, Bl);
@@ -452,10 +465,13 @@ struct mtsac_engine {
     alpha_grad(al, st);
     head_sq(actor);
     allreduce(actor.g + actor.trunk_off, (size_t)(actor.n_flat - actor.trunk_off + EXTRA));
-    optimize(actor, cfg.actor_lr, cfg.actor_max_grad_norm, false);
+    optimize(actor, cfg.actor_lr, cfg.actor_max_grad_norm, false, 1);
 
     // ---- temperature (mtsac.py:713-731)
     alpha_adam(al, cfg.alpha_lr, cfg.adam_b1, cfg.adam_b2, cfg.adam_eps, cfg.alpha_max_grad_norm, st);
+    // post-update parameter norms (logs): trunk |p|^2 is replicated, head |p|^2 is summed over shards
+    allreduce(pn + 2, 2);
+    pnorm_finalize(pn, pn + 2, critic.sc, actor.sc, st);
 
     LogParams lp{};
     lp.critic_sums = critic.g + critic.n_flat + 1;
@@ -682,6 +698,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   if ((rc = e->alloc(&e->cache, (size_t)B * 5 * e->A))) return bad(rc);
   if ((rc = e->alloc(&e->dout_a, (size_t)B * 2 * e->A))) return bad(rc);
   if ((rc = e->alloc(&e->partials, PART))) return bad(rc);
+  if ((rc = e->alloc(&e->pn, 4))) return bad(rc);
   if ((rc = e->alloc(&e->log_alpha, e->T_g))) return bad(rc);
   if ((rc = e->alloc(&e->la_m, e->T_g))) return bad(rc);
   if ((rc = e->alloc(&e->la_v, e->T_g))) return bad(rc);
@@ -1101,7 +1118,8 @@ int mtsac_comm_get_unique_id(void* id_out) {
 }
 int mtsac_comm_init(mtsac_engine* h, const void* unique_id, int32_t nranks, int32_t rank) {
   if (!h || !unique_id) return fail(-22, "null argument");
-  if (nranks <= 1) return 0;
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(-22, "bad rank / nranks");
+  if (h->comm) return fail(-16, "communicator already initialised");
   ncclUniqueId id;
   std::memcpy(&id, unique_id, sizeof(id));
   HIP_TRY(hipSetDevice(h->device));

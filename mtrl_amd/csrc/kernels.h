@@ -166,8 +166,10 @@ struct AdamParams {
   OptScalars* sc;
   float* p_partials;    // sum of squares of new params per block
 };
-int adam_update(const AdamParams& a, float max_norm, int max_blocks, hipStream_t st);
-void param_norm_finalize(const float* partials, int nparts, OptScalars* sc, hipStream_t st);
+// p_partials accumulate |p_new|^2 over [norm_from, n) only (the replicated trunk range)
+int adam_update(const AdamParams& a, float max_norm, long long norm_from, int max_blocks, hipStream_t st);
+// s0->pnorm = sqrt(trunk_sq[0] + head_sq[0]); s1 likewise with index 1
+void pnorm_finalize(const float* trunk_sq, const float* head_sq, OptScalars* s0, OptScalars* s1, hipStream_t st);
 // *out = sum(partials)  (one block, double accumulation)
 void sum_partials(const float* partials, int nparts, float* out, hipStream_t st);
 void adam_count_incr(OptScalars* sc, hipStream_t st);

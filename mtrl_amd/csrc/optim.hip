@@ -69,17 +69,6 @@ __global__ __launch_bounds__(256) void grad_norm_finalize_kernel(const float* __
   }
 }
 
-__global__ __launch_bounds__(256) void param_norm_finalize_kernel(const float* __restrict__ partials, int nparts,
-                                                                  OptScalars* sc) {
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < nparts; i += 256) acc += (double)partials[i];
-  acc = wsumd(acc);
-  __shared__ double s[4];
-  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) sc->pnorm = (float)sqrt((s[0] + s[1]) + (s[2] + s[3]));
-}
-
 __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ partials, int nparts,
                                                            float* __restrict__ out) {
   double acc = 0.0;
@@ -95,7 +84,7 @@ __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restri
 // nu = (1-b2) g^2 + b2 nu, mu_hat = mu / (1 - b1^k), nu_hat = nu / (1 - b2^k),
 // p += -lr * mu_hat / (sqrt(nu_hat) + eps); then target = tau p + (1 - tau) target.
 template <bool POLYAK>
-__global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm) {
+__global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm, long long norm_from4) {
   const OptScalars sc = *a.sc;
   const bool clip = (max_norm > 0.f) && !(sc.gnorm < max_norm);
   const float gn = sc.gnorm;
@@ -116,6 +105,7 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm)
     float* pp = &p.x;
     float* mp = &m.x;
     float* vp = &v.x;
+    float sq = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float gk = gp[k];
@@ -126,8 +116,9 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm)
       const float vh = vp[k] / bc2;
       const float u = mh / (sqrtf(vh) + a.eps);
       pp[k] = pp[k] + u * neg_lr;
-      acc += pp[k] * pp[k];
+      sq += pp[k] * pp[k];
     }
+    if (i >= norm_from4) acc += sq;  // |p|^2 of the replicated (trunk) range only
     p4[i] = p;
     m4[i] = m;
     v4[i] = v;
@@ -260,20 +251,26 @@ void grad_norm_finalize(const float* partials, int nparts, const float* extra_sq
   hipLaunchKernelGGL(grad_norm_finalize_kernel, dim3(1), dim3(256), 0, st, partials, nparts, extra_sq, sc);
 }
 
-int adam_update(const AdamParams& a, float max_norm, int max_blocks, hipStream_t st) {
+int adam_update(const AdamParams& a, float max_norm, long long norm_from, int max_blocks, hipStream_t st) {
   const long long n4 = a.n >> 2;
   long long g = (n4 + 255) / 256;
   if (g > max_blocks) g = max_blocks;
   if (g < 1) g = 1;
   if (a.target)
-    hipLaunchKernelGGL(adam_kernel<true>, dim3((unsigned)g), dim3(256), 0, st, a, max_norm);
+    hipLaunchKernelGGL(adam_kernel<true>, dim3((unsigned)g), dim3(256), 0, st, a, max_norm, norm_from >> 2);
   else
-    hipLaunchKernelGGL(adam_kernel<false>, dim3((unsigned)g), dim3(256), 0, st, a, max_norm);
+    hipLaunchKernelGGL(adam_kernel<false>, dim3((unsigned)g), dim3(256), 0, st, a, max_norm, norm_from >> 2);
   return (int)g;
 }
 
-void param_norm_finalize(const float* partials, int nparts, OptScalars* sc, hipStream_t st) {
-  hipLaunchKernelGGL(param_norm_finalize_kernel, dim3(1), dim3(256), 0, st, partials, nparts, sc);
+__global__ void pnorm_finalize_kernel(const float* __restrict__ trunk_sq, const float* __restrict__ head_sq,
+                                      OptScalars* s0, OptScalars* s1) {
+  s0->pnorm = sqrtf(trunk_sq[0] + head_sq[0]);
+  s1->pnorm = sqrtf(trunk_sq[1] + head_sq[1]);
+}
+
+void pnorm_finalize(const float* trunk_sq, const float* head_sq, OptScalars* s0, OptScalars* s1, hipStream_t st) {
+  hipLaunchKernelGGL(pnorm_finalize_kernel, dim3(1), dim3(1), 0, st, trunk_sq, head_sq, s0, s1);
 }
 
 void sum_partials(const float* partials, int nparts, float* out, hipStream_t st) {

@@ -188,3 +188,28 @@ def test_rollout_actions_match_oracle():
                                om.sample_action(cfg, st.actor, obs.astype(np.float64), eps.astype(np.float64)),
                                rtol=1e-5, atol=1e-6)
     eng.close()
+
+
+def test_rccl_single_rank_graph_path():
+    """The RCCL all-reduce points captured in the hipGraph (1-rank communicator):
+    same results as the communicator-free engine."""
+    from mtrl_amd import _lib as L
+    from mtrl_amd.engine import MTSACEngine
+
+    T, W, n = 3, 32, 4
+    cfg = om.OracleConfig(num_tasks=T, obs_dim=39 + T, actor_width=W, critic_width=W)
+    BATCH_PER_TASK[0] = n
+    st = _f32_state(cfg, seed=4)
+    outs = []
+    for use_comm in (False, True):
+        eng = _engine_for(cfg, capacity=64, graph=True)
+        _load_state(eng, st)
+        if use_comm:
+            eng.comm_init(MTSACEngine.comm_unique_id(), 1, 0)
+        eng.buffer_fill_synthetic(5)
+        eng.seed_rng(2)
+        eng.update_many(3)
+        outs.append((eng.logs(), eng.get_params(L.ACTOR)))
+        eng.close()
+    assert outs[0][0] == outs[1][0]
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
