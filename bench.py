@@ -39,6 +39,8 @@ WORKLOADS = {
     "mt50_w400": (50, 400, False, "MT50 MTMHSAC-v2 width=400 (experiments/mt50_mtmhsac_v2.py)"),
 }
 FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
+PRECISIONS = {"fp32": 0, "split3": 1}
 HBM_PEAK_GBS = 8000.0
 GEMM_FAMILIES = {0: "gemm_f32_kernel<NN> (trunk forward)", 1: "gemm_f32_kernel<NT> (data grad)",
                  2: "gemm_f32_kernel<TN> (weight grad)"}
@@ -83,7 +85,11 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="mt50_w2048", choices=sorted(WORKLOADS))
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="same as --exec eager")
+    ap.add_argument("--exec", default="auto", choices=["auto", "graph", "eager"],
+                    help="hipGraph replay (serial DAG) or eager 4-stream DAG; auto = faster of the two")
+    ap.add_argument("--precision", default="split3", choices=sorted(PRECISIONS),
+                    help="fp32: f32-input MFMA; split3: fp32-accurate 3-way bf16 split on bf16 MFMA")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -105,7 +111,7 @@ def main():
     T, W, clip, desc = WORKLOADS[args.workload]
     tb, tc = shard_tasks(T, world, rank)
     cfg = make_config(num_tasks=T, task_begin=tb, task_count=tc, obs_dim=39 + T, actor_width=W, critic_width=W,
-                      batch_per_task=128, capacity=100_000, clip=int(clip))
+                      batch_per_task=128, capacity=100_000, clip=int(clip), precision=PRECISIONS[args.precision])
     eng = MTSACEngine(cfg, device=local_rank)
     actor, critic = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=1, task_begin=tb, task_count=tc)
     eng.set_params(L.ACTOR, actor)
@@ -113,7 +119,6 @@ def main():
     eng.set_params(L.CRITIC_TARGET, critic)
     eng.buffer_fill_synthetic(1234)
     eng.seed_rng(1)  # every rank draws the same index vector (buffers.py:523-527)
-    eng.enable_graph(not args.no_graph)
     if world > 1:
         uid = [MTSACEngine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -121,8 +126,29 @@ def main():
 
     import torch
 
+    mode = "eager" if args.no_graph else args.exec
+    eng.enable_graph(mode != "eager")
     eng.update_many(args.warmup)
     eng.synchronize()
+    if mode == "auto":  # pick the faster execution mode on rank 0, same choice everywhere
+        trial = {}
+        for m in ("graph", "eager"):
+            eng.enable_graph(m == "graph")
+            eng.update_many(1)
+            eng.synchronize()
+            if dist:
+                dist.barrier()
+            a = time.perf_counter()
+            eng.update_many(3)
+            eng.synchronize()
+            trial[m] = time.perf_counter() - a
+        choice = [min(trial, key=trial.get)]
+        if dist:
+            dist.broadcast_object_list(choice, src=0)
+        mode = choice[0]
+        eng.enable_graph(mode == "graph")
+        eng.update_many(1)
+        eng.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize(local_rank)
@@ -152,6 +178,10 @@ def main():
     gemm_ms = sum(v[0] for v in fam.values())
     gemm_fl = sum(v[2] for v in fam.values())
     achieved = (fl / nl) / (ms / nl * 1e-3) / 1e12 if nl else 0.0
+    if args.precision == "split3":  # 6 bf16 MFMA products per fp32 multiply-add
+        peak, basis = BF16_MFMA_PEAK_TF / 6.0, "bf16 dense MFMA peak / 6 products (fp32-accurate split)"
+    else:
+        peak, basis = FP32_MFMA_PEAK_TF, "f32-input MFMA dense peak"
 
     flops = algorithmic_flops(T, W)
     sps = args.steps / elapsed
@@ -166,18 +196,22 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "fp32" if args.precision == "fp32" else "fp32 (3xbf16 split MFMA, fp32-accurate)",
         "data": "synthetic (SURVEY.md §8d recipe, device-filled full buffer, cap=100000/task; random-init weights)",
         "config": {"workload": desc, "num_tasks": T, "width": W, "batch_per_task": 128, "global_batch": 128 * T,
-                   "parallelism": f"task-shard{world}" if world > 1 else "single", "graph": not args.no_graph},
+                   "parallelism": f"task-shard{world}" if world > 1 else "single", "exec": mode,
+                   "precision": args.precision},
         "roofline": {"bound": "mfma", "kernel": GEMM_FAMILIES[dom], "achieved": achieved,
-                     "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TF,
+                     "peak": peak, "peak_basis": basis, "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": None, "launches": nl, "avg_launch_us": 1e3 * ms / max(nl, 1),
                      "algorithmic_flops_per_launch": fl / max(nl, 1)},
         "step_flops": flops,
         "step_tflops_per_s": flops * sps / world / 1e12,
         "gemm_share_of_step": gemm_ms / (1e3 * elapsed / args.steps),
         "gemm_tflops_per_s": gemm_fl / (gemm_ms * 1e-3) / 1e12 if gemm_ms else 0.0,
+        "gemm_families": {GEMM_FAMILIES[f]: {"ms_per_step": v[0], "launches": v[1],
+                                             "tflops": v[2] / (v[0] * 1e-3) / 1e12 if v[0] else 0.0}
+                          for f, v in fam.items()},
         "logs": logs,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -78,7 +78,10 @@ enum mtsac_tensor {
 };
 
 enum mtsac_precision {
-  MTSAC_FP32 = 0 /* exact-f32 MFMA (v_mfma_f32_32x32x2_f32), fp32 everywhere */
+  MTSAC_FP32 = 0,       /* f32-input MFMA (v_mfma_f32_32x32x2_f32), fp32 everywhere          */
+  MTSAC_FP32_SPLIT3 = 1 /* fp32-accurate trunk GEMMs on bf16 MFMA: each fp32 operand split
+                           exactly into 3 bf16 terms, 6 cross products accumulated in fp32
+                           (dropped terms <= 2^-23 relative); everything else fp32           */
 };
 
 /* Hyper-parameters: MTSACConfig (mtsac.py:116-127) + AlgorithmConfig

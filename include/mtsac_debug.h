@@ -19,7 +19,7 @@ extern "C" {
  *   epi 1 relu(acc + bias[n]), epi 2 acc * (mask[m][n] > 0).
  * Every operand is dense with the given leading dimension; batch strides are the
  * dense matrix sizes (A shared across the batch when a_shared != 0). */
-int mtsac_debug_gemm(int kind, int epi, int batch, int M, int N, int K, const float* A, int lda, int a_shared,
+int mtsac_debug_gemm(int precision, int kind, int epi, int batch, int M, int N, int K, const float* A, int lda, int a_shared,
                      const float* B, int ldb, float* C, int ldc, const float* bias, const float* mask, int ldm,
                      float* db);
 

@@ -130,8 +130,8 @@ SIGNATURES = {
     "mtsac_get_timing": (ctypes.c_int, [P, I32, PD, PI32, PD]),
     "mtsac_debug_gemm": (
         ctypes.c_int,
-        [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int,
-         ctypes.c_int, P, ctypes.c_int, P, ctypes.c_int, P, P, ctypes.c_int, P],
+        # precision, kind, epi, batch, M, N, K, A, lda, a_shared, B, ldb, C, ldc, bias, mask, ldm, db
+        [ctypes.c_int] * 7 + [P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int, P, ctypes.c_int, P, P, ctypes.c_int, P],
     ),
 }
 
@@ -153,10 +153,11 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     # torch ships its own ROCm runtime (torch/lib/libamdhip64.so, librccl.so, libhsa-runtime64.so)
     # with the same SONAMEs as /opt/rocm.  Import it first so our DT_NEEDED entries bind to the
     # copies already in the process: one HIP/HSA runtime per process, shared with torch.
-    try:
-        import torch  # noqa: F401
-    except ImportError:  # pragma: no cover
-        pass
+    if os.environ.get("MTSAC_NO_TORCH_RUNTIME") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:  # pragma: no cover
+            pass
     try:
         lib = ctypes.CDLL(str(p), mode=ctypes.RTLD_GLOBAL)
     except OSError as e:  # pragma: no cover - depends on the runtime

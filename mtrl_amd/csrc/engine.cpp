@@ -89,7 +89,10 @@ struct Net {
 struct mtsac_engine {
   mtsac_config cfg{};
   int device = 0;
-  hipStream_t st = nullptr;
+  hipStream_t st = nullptr, s1 = nullptr, s2 = nullptr, s3 = nullptr;
+  hipStream_t cur = nullptr;
+  std::vector<hipEvent_t> evpool;
+  size_t ev_next = 0;
   int T_l = 0, T_g = 0, A = 0, D = 0, B = 0, n = 0, R = 0, ld_a = 0, ld_c = 0, B_glob = 0;
   Net actor, critic;
   // replay
@@ -112,8 +115,11 @@ struct mtsac_engine {
   float *eps_n = nullptr, *eps_c = nullptr;
   // activations / grads
   float* ha[MAXD] = {};
+  float* han[MAXD] = {};  // actor(s') activations (concurrent with ha)
   float* hc[MAXD] = {};
-  float *dza[2] = {}, *dzc[2] = {};
+  float* hct[MAXD] = {};  // target-critic activations (concurrent with hc)
+  float* dza[MAXD] = {};  // per-layer pre-activation grads
+  float* dzc[MAXD] = {};
   float *logpi_n = nullptr, *logpi = nullptr, *y = nullptr, *dq = nullptr, *row_a = nullptr, *row_b = nullptr,
         *row_c = nullptr, *alpha_w = nullptr, *cache = nullptr, *dout_a = nullptr;
   float* partials = nullptr;
@@ -160,7 +166,9 @@ struct mtsac_engine {
     }
     if (comm) ncclCommDestroy(comm);
     for (void* p : allocs) (void)hipFree(p);
-    if (st) (void)hipStreamDestroy(st);
+    for (hipEvent_t e : evpool) (void)hipEventDestroy(e);
+    for (hipStream_t x : {st, s1, s2, s3})
+      if (x) (void)hipStreamDestroy(x);
   }
 
   template <typename T>
@@ -177,7 +185,25 @@ struct mtsac_engine {
     return 0;
   }
 
-  // ------------------------------------------------------------ timing hooks
+  // ------------------------------------------------------------ streams / timing hooks
+  // Work is issued on `cur`; fork/join between the engine's streams goes through a pool of
+  // timing-free events (captured into the graph as dependencies).
+  void dep(hipStream_t from, hipStream_t to) {
+    if (from == to) return;
+    if (ev_next >= evpool.size()) {  // pool is pre-created (no event creation inside a capture)
+      comm_error = "event pool exhausted";
+      return;
+    }
+    hipEvent_t e = evpool[ev_next++];
+    static const bool trace = getenv("MTSAC_TRACE") != nullptr;
+    if (trace) fprintf(stderr, "[mtsac] dep %zu %p -> %p\n", ev_next, (void*)from, (void*)to), fflush(stderr);
+    hipError_t r = hipEventRecord(e, from);
+    if (trace) fprintf(stderr, "[mtsac]   record rc=%d\n", (int)r), fflush(stderr);
+    if (r == hipSuccess) r = hipStreamWaitEvent(to, e, 0);
+    if (trace) fprintf(stderr, "[mtsac]   wait rc=%d\n", (int)r), fflush(stderr);
+    if (r != hipSuccess) comm_error = std::string("stream fork/join: ") + hipGetErrorString(r);
+  }
+
   void t_begin(int family, double flops) {
     if (!timing) return;
     if (tl_next >= tl.size()) {
@@ -188,17 +214,20 @@ struct mtsac_engine {
     }
     tl[tl_next].family = family;
     tl[tl_next].flops = flops;
-    (void)hipEventRecord(tl[tl_next].a, st);
+    (void)hipEventRecord(tl[tl_next].a, cur);
   }
   void t_end() {
     if (!timing) return;
-    (void)hipEventRecord(tl[tl_next].b, st);
+    (void)hipEventRecord(tl[tl_next].b, cur);
     ++tl_next;
   }
 
   void gemm(const GemmParams& p, GemmKind kind, int epi, int batch) {
     t_begin((int)kind, 2.0 * (double)p.M * p.N * p.K * batch);
-    gemm_f32(p, kind, epi, batch, st);
+    if (cfg.precision == MTSAC_FP32_SPLIT3)
+      gemm_x3(p, kind, epi, batch, cur);
+    else
+      gemm_f32(p, kind, epi, batch, cur);
     t_end();
   }
 
@@ -225,54 +254,46 @@ struct mtsac_engine {
     }
   }
 
-  // dz_top: grad at the last trunk layer's pre-activation.  Walks down computing weight
-  // grads (if wgrad) and dz of lower layers; returns the buffer holding dz of layer 0.
-  float* trunk_backward(Net& net, const float* params, const float* X, int ldx, float** acts, float* dz_top,
-                        float** dzbuf, bool wgrad, int M) {
-    float* dz = dz_top;
-    int which = (dz_top == dzbuf[0]) ? 1 : 0;
-    for (int i = net.depth - 1; i >= 0; --i) {
-      if (wgrad) {
-        GemmParams g{};
-        g.A = (i == 0) ? X : acts[i - 1];  // [K=rows][M=fan_in] storage -> TA
-        g.lda = (i == 0) ? ldx : net.width;
-        g.sA = (i == 0) ? 0 : (long long)M * net.width;
-        g.B = dz;
-        g.ldb = net.width;
-        g.sB = (long long)M * net.width;
-        g.C = net.g + net.off_W[i];
-        g.ldc = net.width;
-        g.sC = net.ms_W[i];
-        g.db = net.g + net.off_b[i];
-        g.sDb = net.ms_b;
-        g.M = (i == 0) ? net.in_dim : net.width;
-        g.N = net.width;
-        g.K = M;
-        gemm(g, GEMM_TN, EPI_STORE, net.E);
-      }
-      if (i > 0) {
-        GemmParams g{};
-        g.A = dz;
-        g.lda = net.width;
-        g.sA = (long long)M * net.width;
-        g.B = params + net.off_W[i];  // W_i (fan_in x W) == [N=fan_in][K=W]
-        g.ldb = net.width;
-        g.sB = net.ms_W[i];
-        g.C = dzbuf[which];
-        g.ldc = net.width;
-        g.sC = (long long)M * net.width;
-        g.mask = acts[i - 1];
-        g.ldm = net.width;
-        g.sMask = (long long)M * net.width;
-        g.M = M;
-        g.N = net.width;
-        g.K = net.width;
-        gemm(g, GEMM_NT, EPI_RELU_MASK, net.E);
-        dz = dzbuf[which];
-        which ^= 1;
-      }
-    }
-    return dz;
+  // Backward through trunk layer i, split so the two halves can run concurrently:
+  //   wgrad_layer: dW_i = in_i^T dz[i] (+ db_i fused into the GEMM's m-tile-0 blocks)
+  //   dgrad_layer: dz[i-1] = (dz[i] W_i^T) * [acts[i-1] > 0]
+  void wgrad_layer(Net& net, const float* X, int ldx, float** acts, float** dz, int i, int M) {
+    GemmParams g{};
+    g.A = (i == 0) ? X : acts[i - 1];  // [K=rows][M=fan_in] storage -> TA
+    g.lda = (i == 0) ? ldx : net.width;
+    g.sA = (i == 0) ? 0 : (long long)M * net.width;
+    g.B = dz[i];
+    g.ldb = net.width;
+    g.sB = (long long)M * net.width;
+    g.C = net.g + net.off_W[i];
+    g.ldc = net.width;
+    g.sC = net.ms_W[i];
+    g.db = net.g + net.off_b[i];
+    g.sDb = net.ms_b;
+    g.M = (i == 0) ? net.in_dim : net.width;
+    g.N = net.width;
+    g.K = M;
+    gemm(g, GEMM_TN, EPI_STORE, net.E);
+  }
+
+  void dgrad_layer(Net& net, const float* params, float** acts, float** dz, int i, int M) {
+    GemmParams g{};
+    g.A = dz[i];
+    g.lda = net.width;
+    g.sA = (long long)M * net.width;
+    g.B = params + net.off_W[i];  // W_i (fan_in x W) == [N=fan_in][K=W]
+    g.ldb = net.width;
+    g.sB = net.ms_W[i];
+    g.C = dz[i - 1];
+    g.ldc = net.width;
+    g.sC = (long long)M * net.width;
+    g.mask = acts[i - 1];
+    g.ldm = net.width;
+    g.sMask = (long long)M * net.width;
+    g.M = M;
+    g.N = net.width;
+    g.K = net.width;
+    gemm(g, GEMM_NT, EPI_RELU_MASK, net.E);
   }
 
   HeadParams head(Net& net, const float* params, const float* h, int M, const int* tsk) {
@@ -293,12 +314,12 @@ struct mtsac_engine {
 
   void allreduce(float* buf, size_t count) {
     if (comm != nullptr) {
-      ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm, st);
+      ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm, cur);
       if (r != ncclSuccess) comm_error = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
       return;
     }
     if (hook) {
-      if (hipStreamSynchronize(st) != hipSuccess) {
+      if (hipStreamSynchronize(cur) != hipSuccess) {
         comm_error = "stream sync before all-reduce hook failed";
         return;
       }
@@ -310,15 +331,14 @@ struct mtsac_engine {
   // |p|^2 lands in pn[slot] (trunk, replicated) and pn[2 + slot] (local heads, summed later).
   void optimize(Net& net, float lr, float max_norm, bool polyak, int slot) {
     float* extra = net.g + net.n_flat;
-    int np = sumsq_partials(net.g + net.trunk_off, net.n_flat - net.trunk_off, partials, PART, st);
-    grad_norm_finalize(partials, np, extra + 0, max_norm, net.sc, st);
+    int np = sumsq_partials(net.g + net.trunk_off, net.n_flat - net.trunk_off, partials, PART, cur);
+    grad_norm_finalize(partials, np, extra + 0, max_norm, net.sc, cur);
     AdamParams a{};
     a.p = net.p;
     a.m = net.m;
     a.v = net.v;
     a.g = net.g;
     a.target = polyak ? net.tgt : nullptr;
-    a.n = net.n_flat;
     a.lr = lr;
     a.b1 = cfg.adam_b1;
     a.b2 = cfg.adam_b2;
@@ -329,164 +349,253 @@ struct mtsac_engine {
     // heads and trunk as two launches so the trunk's reduction tree does not depend on the
     // shard's head count (bitwise-identical replicated trunks and norms on every rank)
     a.n = net.trunk_off;
-    int nh = adam_update(a, max_norm, 0, PART, st);
-    sum_partials(partials, nh, pn + 2 + slot, st);
+    int nh = adam_update(a, max_norm, 0, PART, cur);
+    sum_partials(partials, nh, pn + 2 + slot, cur);
     a.p += net.trunk_off;
     a.m += net.trunk_off;
     a.v += net.trunk_off;
     a.g += net.trunk_off;
     if (a.target) a.target += net.trunk_off;
     a.n = net.n_flat - net.trunk_off;
-    int na = adam_update(a, max_norm, 0, PART, st);
-    sum_partials(partials, na, pn + slot, st);
+    int na = adam_update(a, max_norm, 0, PART, cur);
+    sum_partials(partials, na, pn + slot, cur);
   }
 
   void head_sq(Net& net) {  // local |g_head|^2 into the scalar tail
-    int np = sumsq_partials(net.g, net.trunk_off, partials, PART, st);
-    sum_partials(partials, np, net.g + net.n_flat + 0, st);
+    int np = sumsq_partials(net.g, net.trunk_off, partials, PART, cur);
+    sum_partials(partials, np, net.g + net.n_flat + 0, cur);
+  }
+
+  // ------------------------------------------------------------ step DAG
+  // One step = a DAG of segments; a segment is a short single-stream kernel sequence.
+  //  * eager: each segment runs on one of 4 lanes (streams); cross-lane edges are events.
+  //  * graph build: each segment is captured ALONE (single-stream capture) into a child graph
+  //    and added to the step graph with explicit dependency edges.  No multi-stream capture:
+  //    the ROCm 7.0 HIP runtime bundled with torch segfaults in hipStreamEndCapture on nested
+  //    stream forks (tools/capture_probe.cpp), while child-graph composition works.
+  struct Seg {
+    hipStream_t lane;
+    hipEvent_t ev;
+    hipGraphNode_t node;
+  };
+  std::vector<Seg> segs;
+  hipGraph_t build = nullptr;  // non-null while building the step graph
+
+  template <class F>
+  int seg(std::initializer_list<int> deps, int lane, F&& body) {
+    Seg s{};
+    if (build) {
+      std::vector<hipGraphNode_t> dn;
+      for (int d : deps) dn.push_back(segs[d].node);
+      hipGraph_t g = nullptr;
+      hipError_t r = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+      cur = st;
+      body();
+      hipError_t r2 = hipStreamEndCapture(st, &g);
+      if (r == hipSuccess) r = r2;
+      if (r == hipSuccess) r = hipGraphAddChildGraphNode(&s.node, build, dn.data(), dn.size(), g);
+      if (g) (void)hipGraphDestroy(g);
+      if (r != hipSuccess) comm_error = std::string("step graph build: ") + hipGetErrorString(r);
+    } else {
+      hipStream_t L = timing ? st : (lane == 0 ? st : lane == 1 ? s1 : lane == 2 ? s2 : s3);
+      for (int d : deps)
+        if (segs[d].lane != L) (void)hipStreamWaitEvent(L, segs[d].ev, 0);
+      cur = L;
+      body();
+      s.lane = L;
+      if (ev_next < evpool.size()) {
+        s.ev = evpool[ev_next++];
+        (void)hipEventRecord(s.ev, L);
+      } else {
+        comm_error = "event pool exhausted";
+      }
+    }
+    segs.push_back(s);
+    cur = st;
+    return (int)segs.size() - 1;
+  }
+
+  // trunk backward as segments: data chain on lane 1, weight grads on lane 3
+  int backward_segs(Net& net, const float* params, const float* X, int ldx, float** acts, float** dz, int d_top,
+                    int w_prev, int M) {
+    int dprev = d_top, wprev = w_prev;
+    for (int i = net.depth - 1; i >= 0; --i) {
+      wprev = seg({dprev, wprev}, 3, [&, i] { wgrad_layer(net, X, ldx, acts, dz, i, M); });
+      if (i > 0) dprev = seg({dprev}, 1, [&, i] { dgrad_layer(net, params, acts, dz, i, M); });
+    }
+    return seg({dprev, wprev}, 1, [] {});  // join point
   }
 
   // ------------------------------------------------------------ one gradient step
+  // Segments of _update_inner (mtsac.py:1173-1247):
+  //   inputs -> { critic(s,a) fwd | actor(s) fwd + pi | actor(s') + target critic -> y }
+  //   -> critic loss -> { data-grad chain | weight grads } -> all-reduce, clip/Adam/Polyak
+  //   -> critic(s, a~pi) with the UPDATED critic -> action grad -> actor backward
+  //   -> all-reduce, clip/Adam, temperature, logs.
+  // Independent GEMM chains fill each other's tail waves.  With timing on, everything runs
+  // serialised on the main stream so per-launch events measure solo kernels.
   void step(bool device_batch, bool device_noise) {
     const int Bl = B;
-    GatherParams gp = gather_params();
-    if (device_batch) {
-      replay_indices(rng, jump, buf_size, n, idx, st);
-      replay_gather(gp, st);
-    } else {
-      batch_scatter(gp, u_obs, u_act, u_nobs, u_done, u_rew, Bl, st);
-    }
-    task_rows(task, Bl, T_l, counts, rows, Bl, st);
-    if (cfg.use_task_weights) row_alpha(task, cfg.task_begin, log_alpha, T_g, Bl, 1, row_c, tw, st);
+    ev_next = 0;
+    segs.clear();
     const float* twp = cfg.use_task_weights ? tw : nullptr;
-
-    // ---- critic update (mtsac.py:513-621)
-    trunk_forward(actor, actor.p, xan, ld_a, ha, Bl);
     PolicyParams pp{};
-    pp.head = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
-    pp.eps = device_noise ? nullptr : eps_n;
     pp.seed = cfg.noise_seed;
     pp.counter = counter;
-    pp.stream_id = 1;
     pp.A = A;
     pp.ls_min = cfg.log_std_min;
     pp.ls_max = cfg.log_std_max;
-    pp.a_out = xcn;
     pp.ld_a_out = ld_c;
-    pp.logpi = logpi_n;
-    policy_head(pp, st);
-
-    trunk_forward(critic, critic.tgt, xcn, ld_c, hc, Bl);
     CriticHeadParams ch{};
-    ch.head = head(critic, critic.tgt, hc[critic.depth - 1], Bl, task);
-    ch.mode = CH_TARGET;
     ch.rew = rew;
     ch.done = done;
-    ch.logpi = logpi_n;
     ch.log_alpha = log_alpha;
     ch.task = task;
     ch.task_begin = cfg.task_begin;
-    ch.y_out = y;
     ch.tw = twp;
     ch.gamma = cfg.gamma;
     ch.clip = cfg.clip;
     ch.T_glob = T_g;
-    critic_head(ch, st);
 
-    trunk_forward(critic, critic.p, xc, ld_c, hc, Bl);
-    ch.head = head(critic, critic.p, hc[critic.depth - 1], Bl, task);
-    ch.mode = CH_CRITIC;
-    ch.y = y;
-    ch.dq = dq;
-    ch.row_a = row_a;
-    ch.row_b = row_b;
-    ch.inv_norm = 1.0f / ((float)critic.E * (float)B_glob);
-    critic_head(ch, st);
-
-    HeadParams chp = head(critic, critic.p, hc[critic.depth - 1], Bl, task);
-    head_backward_weight(chp, dq, Bl, counts, rows, Bl, critic.g + critic.off_hW, critic.g + critic.off_hb, st);
-    head_backward_data(chp, dq, Bl, dzc[0], st);
-    trunk_backward(critic, critic.p, xc, ld_c, hc, dzc[0], dzc, true, Bl);
-    {
+    const int s_in = seg({}, 0, [&] {
+      GatherParams gp = gather_params();
+      if (device_batch) {
+        replay_indices(rng, jump, buf_size, n, idx, cur);
+        replay_gather(gp, cur);
+      } else {
+        batch_scatter(gp, u_obs, u_act, u_nobs, u_done, u_rew, Bl, cur);
+      }
+      task_rows(task, Bl, T_l, counts, rows, Bl, cur);
+      if (cfg.use_task_weights) row_alpha(task, cfg.task_begin, log_alpha, T_g, Bl, 1, row_c, tw, cur);
+    });
+    // critic forward on (s, a) with the current critic (mtsac.py:555)
+    const int s_cf = seg({s_in}, 1, [&] { trunk_forward(critic, critic.p, xc, ld_c, hc, Bl); });
+    // actor forward on s with the pre-update actor (mtsac.py:640-642)
+    const int s_af = seg({s_in}, 2, [&] {
+      trunk_forward(actor, actor.p, xa, ld_a, ha, Bl);
+      PolicyParams q = pp;
+      q.head = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
+      q.eps = device_noise ? nullptr : eps_c;
+      q.stream_id = 2;
+      q.a_out = xcp;
+      q.logpi = logpi;
+      q.cache = cache;
+      policy_head(q, cur);
+    });
+    // a' ~ pi(.|s'), target critic, TD target (mtsac.py:525-553)
+    const int s_tg = seg({s_in}, 0, [&] {
+      trunk_forward(actor, actor.p, xan, ld_a, han, Bl);
+      PolicyParams q = pp;
+      q.head = head(actor, actor.p, han[actor.depth - 1], Bl, task);
+      q.eps = device_noise ? nullptr : eps_n;
+      q.stream_id = 1;
+      q.a_out = xcn;
+      q.logpi = logpi_n;
+      policy_head(q, cur);
+      trunk_forward(critic, critic.tgt, xcn, ld_c, hct, Bl);
+      CriticHeadParams c = ch;
+      c.head = head(critic, critic.tgt, hct[critic.depth - 1], Bl, task);
+      c.mode = CH_TARGET;
+      c.logpi = logpi_n;
+      c.y_out = y;
+      critic_head(c, cur);
+    });
+    // critic loss (mtsac.py:538-566) and head backward
+    const HeadParams chp = head(critic, critic.p, hc[critic.depth - 1], Bl, task);
+    const int s_cl = seg({s_cf, s_tg}, 1, [&] {
+      CriticHeadParams c = ch;
+      c.head = chp;
+      c.mode = CH_CRITIC;
+      c.y = y;
+      c.dq = dq;
+      c.row_a = row_a;
+      c.row_b = row_b;
+      c.inv_norm = 1.0f / ((float)critic.E * (float)B_glob);
+      critic_head(c, cur);
+      head_backward_data(chp, dq, Bl, dzc[critic.depth - 1], cur);
       const float* ins[2] = {row_a, row_b};
-      reduce_rows(ins, 2, Bl, critic.g + critic.n_flat + 1, st);
-    }
-    head_sq(critic);
-    allreduce(critic.g + critic.trunk_off, (size_t)(critic.n_flat - critic.trunk_off + EXTRA));
-    optimize(critic, cfg.critic_lr, cfg.critic_max_grad_norm, true, 0);
-
-    // ---- actor update (mtsac.py:623-711), critic params already updated
-    trunk_forward(actor, actor.p, xa, ld_a, ha, Bl);
-    pp.head = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
-    pp.eps = device_noise ? nullptr : eps_c;
-    pp.stream_id = 2;
-    pp.a_out = xcp;
-    pp.logpi = logpi;
-    pp.cache = cache;
-    policy_head(pp, st);
-
-    trunk_forward(critic, critic.p, xcp, ld_c, hc, Bl);
-    ch.head = head(critic, critic.p, hc[critic.depth - 1], Bl, task);
-    ch.mode = CH_ACTOR;
-    ch.logpi = logpi;
-    ch.dq = dq;
-    ch.row_a = row_c;
-    ch.alpha_w = alpha_w;
-    ch.inv_norm = 1.0f / (float)B_glob;
-    critic_head(ch, st);
-    head_backward_data(ch.head, dq, Bl, dzc[0], st);
-    float* dz0 = trunk_backward(critic, critic.p, xcp, ld_c, hc, dzc[0], dzc, false, Bl);
-    ActionGradParams ag{};
-    ag.dz1 = dz0;
-    ag.W0 = critic.p + critic.off_W[0];
-    ag.s_dz = (long long)Bl * critic.width;
-    ag.s_W0 = critic.ms_W[0];
-    ag.E = critic.E;
-    ag.B = Bl;
-    ag.Wc = critic.width;
-    ag.A = A;
-    ag.cache = cache;
-    ag.alpha_w = alpha_w;
-    ag.ls_min = cfg.log_std_min;
-    ag.ls_max = cfg.log_std_max;
-    ag.dout = dout_a;
-    action_grad(ag, st);
-
-    HeadParams ahp = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
-    head_backward_weight(ahp, dout_a, 0, counts, rows, Bl, actor.g + actor.off_hW, actor.g + actor.off_hb, st);
-    head_backward_data(ahp, dout_a, 0, dza[0], st);
-    trunk_backward(actor, actor.p, xa, ld_a, ha, dza[0], dza, true, Bl);
-    {
+      reduce_rows(ins, 2, Bl, critic.g + critic.n_flat + 1, cur);
+    });
+    const int s_chw = seg({s_cl}, 3, [&] {
+      head_backward_weight(chp, dq, Bl, counts, rows, Bl, critic.g + critic.off_hW, critic.g + critic.off_hb, cur);
+    });
+    const int s_cb = backward_segs(critic, critic.p, xc, ld_c, hc, dzc, s_cl, s_chw, Bl);
+    // reduce over shards, clip + Adam + Polyak (mtsac.py:599-613)
+    const int s_co = seg({s_cb}, 1, [&] {
+      head_sq(critic);
+      allreduce(critic.g + critic.trunk_off, (size_t)(critic.n_flat - critic.trunk_off + EXTRA));
+      optimize(critic, cfg.critic_lr, cfg.critic_max_grad_norm, true, 0);
+    });
+    // actor loss through the UPDATED critic (mtsac.py:659-691)
+    const int s_ap = seg({s_co, s_af}, 1, [&] {
+      trunk_forward(critic, critic.p, xcp, ld_c, hc, Bl);
+      CriticHeadParams c = ch;
+      c.head = head(critic, critic.p, hc[critic.depth - 1], Bl, task);
+      c.mode = CH_ACTOR;
+      c.logpi = logpi;
+      c.dq = dq;
+      c.row_a = row_c;
+      c.alpha_w = alpha_w;
+      c.inv_norm = 1.0f / (float)B_glob;
+      critic_head(c, cur);
+      head_backward_data(c.head, dq, Bl, dzc[critic.depth - 1], cur);
+      for (int i = critic.depth - 1; i > 0; --i) dgrad_layer(critic, critic.p, hc, dzc, i, Bl);
+      ActionGradParams ag{};
+      ag.dz1 = dzc[0];
+      ag.W0 = critic.p + critic.off_W[0];
+      ag.s_dz = (long long)Bl * critic.width;
+      ag.s_W0 = critic.ms_W[0];
+      ag.E = critic.E;
+      ag.B = Bl;
+      ag.Wc = critic.width;
+      ag.A = A;
+      ag.cache = cache;
+      ag.alpha_w = alpha_w;
+      ag.ls_min = cfg.log_std_min;
+      ag.ls_max = cfg.log_std_max;
+      ag.dout = dout_a;
+      action_grad(ag, cur);
       const float* ins[1] = {row_c};
-      reduce_rows(ins, 1, Bl, actor.g + actor.n_flat + 1, st);
+      reduce_rows(ins, 1, Bl, actor.g + actor.n_flat + 1, cur);
+    });
+    const HeadParams ahp = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
+    const int s_ahw = seg({s_ap}, 3, [&] {
+      head_backward_weight(ahp, dout_a, 0, counts, rows, Bl, actor.g + actor.off_hW, actor.g + actor.off_hb, cur);
+    });
+    const int s_ad = seg({s_ap}, 1, [&] { head_backward_data(ahp, dout_a, 0, dza[actor.depth - 1], cur); });
+    const int s_ab = backward_segs(actor, actor.p, xa, ld_a, ha, dza, s_ad, s_ahw, Bl);
+    seg({s_ab}, 1, [&] {
+      // temperature gradient rides in the actor's scalar tail: [2] loss part, [3..] grad
+      AlphaParams al = alpha_params();
+      alpha_grad(al, cur);
+      head_sq(actor);
+      allreduce(actor.g + actor.trunk_off, (size_t)(actor.n_flat - actor.trunk_off + EXTRA));
+      optimize(actor, cfg.actor_lr, cfg.actor_max_grad_norm, false, 1);
+      // temperature (mtsac.py:713-731)
+      alpha_adam(al, cfg.alpha_lr, cfg.adam_b1, cfg.adam_b2, cfg.adam_eps, cfg.alpha_max_grad_norm, cur);
+      // post-update parameter norms: trunk |p|^2 replicated, head |p|^2 summed over shards
+      allreduce(pn + 2, 2);
+      pnorm_finalize(pn, pn + 2, critic.sc, actor.sc, cur);
+      LogParams lp{};
+      lp.critic_sums = critic.g + critic.n_flat + 1;
+      lp.actor_sums = actor.g + actor.n_flat + 1;
+      lp.critic = critic.sc;
+      lp.actor = actor.sc;
+      lp.alpha_loss_sum = actor.g + actor.n_flat + 2;
+      lp.log_alpha = log_alpha;
+      lp.T_glob = T_g;
+      lp.inv_critic = 1.0f / ((float)critic.E * (float)B_glob);
+      lp.inv_actor = 1.0f / (float)B_glob;
+      lp.inv_b = 1.0f / (float)B_glob;
+      lp.logs = logs;
+      write_logs(lp, cur);
+      bump_counter(counter, cur);
+    });
+    if (!build) {  // eager: the main stream waits for every lane
+      for (const Seg& s : segs)
+        if (s.lane != st && s.ev) (void)hipStreamWaitEvent(st, s.ev, 0);
     }
-    // temperature gradient rides in the actor's scalar tail: [2] loss part, [3..] grad
-    AlphaParams al = alpha_params();
-    alpha_grad(al, st);
-    head_sq(actor);
-    allreduce(actor.g + actor.trunk_off, (size_t)(actor.n_flat - actor.trunk_off + EXTRA));
-    optimize(actor, cfg.actor_lr, cfg.actor_max_grad_norm, false, 1);
-
-    // ---- temperature (mtsac.py:713-731)
-    alpha_adam(al, cfg.alpha_lr, cfg.adam_b1, cfg.adam_b2, cfg.adam_eps, cfg.alpha_max_grad_norm, st);
-    // post-update parameter norms (logs): trunk |p|^2 is replicated, head |p|^2 is summed over shards
-    allreduce(pn + 2, 2);
-    pnorm_finalize(pn, pn + 2, critic.sc, actor.sc, st);
-
-    LogParams lp{};
-    lp.critic_sums = critic.g + critic.n_flat + 1;
-    lp.actor_sums = actor.g + actor.n_flat + 1;
-    lp.critic = critic.sc;
-    lp.actor = actor.sc;
-    lp.alpha_loss_sum = actor.g + actor.n_flat + 2;
-    lp.log_alpha = log_alpha;
-    lp.T_glob = T_g;
-    lp.inv_critic = 1.0f / ((float)critic.E * (float)B_glob);
-    lp.inv_actor = 1.0f / (float)B_glob;
-    lp.inv_b = 1.0f / (float)B_glob;
-    lp.logs = logs;
-    write_logs(lp, st);
-    bump_counter(counter, st);
+    cur = st;
   }
 
   AlphaParams alpha_params() {
@@ -626,7 +735,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   if (c.batch_per_task < 1) return fail(-22, "batch_per_task must be positive");
   if (c.capacity < c.batch_per_task || c.capacity >= (1ll << 31))
     return fail(-22, "capacity must be in [batch_per_task, 2^31)");
-  if (c.precision != MTSAC_FP32) return fail(-22, "unsupported precision");
+  if (c.precision != MTSAC_FP32 && c.precision != MTSAC_FP32_SPLIT3) return fail(-22, "unsupported precision");
   hipError_t he = hipSetDevice(hip_device);
   if (he != hipSuccess) return fail(-19, std::string("hipSetDevice: ") + hipGetErrorString(he));
 
@@ -649,7 +758,14 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     delete e;
     return r;
   };
-  if (hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) != hipSuccess) return bad(fail(-5, "stream"));
+  for (hipStream_t* x : {&e->st, &e->s1, &e->s2, &e->s3})
+    if (hipStreamCreateWithFlags(x, hipStreamNonBlocking) != hipSuccess) return bad(fail(-5, "stream"));
+  e->cur = e->st;
+  for (int i = 0; i < 128; ++i) {
+    hipEvent_t ev;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return bad(fail(-5, "event"));
+    e->evpool.push_back(ev);
+  }
 
   e->actor.layout(e->D, e->ld_a, c.actor_width, c.actor_depth, e->T_l, 2 * e->A, 1);
   e->critic.layout(e->D + e->A, e->ld_c, c.critic_width, c.critic_depth, e->T_l, 1, c.num_critics);
@@ -687,13 +803,11 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   if ((rc = e->alloc(&e->eps_n, (size_t)B * e->A))) return bad(rc);
   if ((rc = e->alloc(&e->eps_c, (size_t)B * e->A))) return bad(rc);
   for (int i = 0; i < c.actor_depth; ++i)
-    if ((rc = e->alloc(&e->ha[i], (size_t)B * c.actor_width))) return bad(rc);
+    for (float** p : {&e->ha[i], &e->han[i], &e->dza[i]})
+      if ((rc = e->alloc(p, (size_t)B * c.actor_width))) return bad(rc);
   for (int i = 0; i < c.critic_depth; ++i)
-    if ((rc = e->alloc(&e->hc[i], (size_t)c.num_critics * B * c.critic_width))) return bad(rc);
-  for (int i = 0; i < 2; ++i) {
-    if ((rc = e->alloc(&e->dza[i], (size_t)B * c.actor_width))) return bad(rc);
-    if ((rc = e->alloc(&e->dzc[i], (size_t)c.num_critics * B * c.critic_width))) return bad(rc);
-  }
+    for (float** p : {&e->hc[i], &e->hct[i], &e->dzc[i]})
+      if ((rc = e->alloc(p, (size_t)c.num_critics * B * c.critic_width))) return bad(rc);
   if ((rc = e->alloc(&e->dq, (size_t)c.num_critics * B))) return bad(rc);
   if ((rc = e->alloc(&e->cache, (size_t)B * 5 * e->A))) return bad(rc);
   if ((rc = e->alloc(&e->dout_a, (size_t)B * 2 * e->A))) return bad(rc);
@@ -1022,10 +1136,15 @@ int mtsac_update_many(mtsac_engine* h, int32_t steps) {
   }
   if (!h->gexec) {
     h->tl_next = 0;
-    HIP_TRY(hipStreamBeginCapture(h->st, hipStreamCaptureModeThreadLocal));
+    HIP_TRY(hipGraphCreate(&h->graph, 0));
+    h->build = h->graph;
     h->step(true, true);
-    hipError_t ce = hipStreamEndCapture(h->st, &h->graph);
-    if (ce != hipSuccess) return fail(-5, std::string("graph capture: ") + hipGetErrorString(ce));
+    h->build = nullptr;
+    if (!h->comm_error.empty()) {
+      (void)hipGraphDestroy(h->graph);
+      h->graph = nullptr;
+      return h->check_err();
+    }
     HIP_TRY(hipGraphInstantiate(&h->gexec, h->graph, nullptr, nullptr, 0));
     h->graph_timed = h->timing;
   }
@@ -1175,7 +1294,7 @@ int mtsac_get_timing(mtsac_engine* h, int32_t family, double* total_ms, int32_t*
 }
 
 // ---------------------------------------------------------------- debug (include/mtsac_debug.h)
-int mtsac_debug_gemm(int kind, int epi, int batch, int M, int N, int K, const float* A, int lda, int a_shared,
+int mtsac_debug_gemm(int precision, int kind, int epi, int batch, int M, int N, int K, const float* A, int lda, int a_shared,
                      const float* B, int ldb, float* C, int ldc, const float* bias, const float* mask, int ldm,
                      float* db) {
   if (kind < 0 || kind > 2 || batch < 1 || M < 1 || N < 1 || K < 1) return fail(-22, "bad gemm arguments");
@@ -1210,7 +1329,10 @@ int mtsac_debug_gemm(int kind, int epi, int batch, int M, int N, int K, const fl
   g.mask = dmask; g.ldm = ldm; g.sMask = (long long)M * ldm;
   g.db = ddb; g.sDb = N;
   g.M = M; g.N = N; g.K = K;
-  gemm_f32(g, (GemmKind)kind, epi, batch, nullptr);
+  if (precision == MTSAC_FP32_SPLIT3)
+    gemm_x3(g, (GemmKind)kind, epi, batch, nullptr);
+  else
+    gemm_f32(g, (GemmKind)kind, epi, batch, nullptr);
   hipError_t e = hipDeviceSynchronize();
   if (e == hipSuccess) e = hipMemcpy(C, dC, sizeof(float) * sC * batch, hipMemcpyDeviceToHost);
   if (e == hipSuccess && db) e = hipMemcpy(db, ddb, sizeof(float) * N * batch, hipMemcpyDeviceToHost);

@@ -29,6 +29,8 @@ struct GemmParams {
 
 enum GemmKind { GEMM_NN = 0, GEMM_NT = 1, GEMM_TN = 2 };
 void gemm_f32(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_t st);
+// same contract, fp32-accurate via 3-way bf16 operand split on bf16 MFMA (gemm_x3.hip)
+void gemm_x3(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_t st);
 
 // ------------------------------------------------------------------ replay
 struct PcgDev {  // device-resident numpy PCG64 state (buffers.py:260)

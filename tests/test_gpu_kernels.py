@@ -30,9 +30,12 @@ def _ref(kind, A, B, M, N, K):
     return A64[:K, :M].T @ B64[:K, :N], np.abs(A64[:K, :M]).T @ np.abs(B64[:K, :N])
 
 
+@pytest.mark.parametrize("precision", [0, 1])
 @pytest.mark.parametrize("kind", [NN, NT, TN])
 @pytest.mark.parametrize("shape", [(200, 136, 93), (128, 128, 32), (64, 400, 400), (257, 132, 260), (8, 4, 4)])
-def test_gemm_store(kind, shape):
+def test_gemm_store(kind, shape, precision):
+    """precision 0: f32-input MFMA; 1: 3-way bf16 split (fp32-accurate).  Error bound vs a
+    float64 product of the same fp32 inputs: |err| <= 2e-6 (f32) / 4e-6 (split) x sum|a*b|."""
     from mtrl_amd.engine import debug_gemm
 
     M, N, K = shape
@@ -49,16 +52,22 @@ def test_gemm_store(kind, shape):
         A = np.zeros((K, Mp), np.float32); A[:, :M] = rng.standard_normal((K, M))
         B = rng.standard_normal((K, N)).astype(np.float32)
     C0 = np.full((M, N), 7.0, np.float32)
-    C, db = debug_gemm(kind, STORE, A, B, C0, M, N, K, want_db=(kind == TN))
+    C, db = debug_gemm(kind, STORE, A, B, C0, M, N, K, want_db=(kind == TN), precision=precision)
     ref, mag = _ref(kind, A, B, M, N, K)
     err = np.abs(C - ref)
-    assert np.all(err <= 2e-6 * mag + 1e-30), float((err / mag).max())
+    tol = 2e-6 if precision == 0 else 4e-6
+    assert np.all(err <= tol * mag + 1e-30), float((err / mag).max())
     if kind == TN:
         np.testing.assert_allclose(db[0], B[:K, :N].astype(np.float64).sum(0), rtol=1e-5, atol=1e-4)
 
 
-def test_gemm_epilogues_batched():
-    from mtrl_amd.engine import debug_gemm
+@pytest.mark.parametrize("precision", [0, 1])
+def test_gemm_epilogues_batched(precision):
+    from functools import partial
+
+    from mtrl_amd.engine import debug_gemm as _dg
+
+    debug_gemm = partial(_dg, precision=precision)
 
     rng = np.random.default_rng(1)
     M, N, K, E = 300, 200, 96, 2

@@ -19,10 +19,11 @@ pytestmark = pytest.mark.gpu
 LOSS_RTOL = 1e-5
 
 
-def _engine_for(cfg: om.OracleConfig, capacity=256, graph=False):
+def _engine_for(cfg: om.OracleConfig, capacity=256, graph=False, precision=0):
     from mtrl_amd.engine import MTSACEngine, make_config
 
     c = make_config(
+        precision=precision,
         num_tasks=cfg.num_tasks, task_count=cfg.num_tasks, obs_dim=cfg.obs_dim, action_dim=cfg.action_dim,
         actor_width=cfg.actor_width, actor_depth=cfg.actor_depth, critic_width=cfg.critic_width,
         critic_depth=cfg.critic_depth, num_critics=cfg.num_critics, batch_per_task=BATCH_PER_TASK[0],
@@ -67,8 +68,9 @@ CONFIGS = {
 }
 
 
+@pytest.mark.parametrize("precision", [0, 1])
 @pytest.mark.parametrize("name", list(CONFIGS))
-def test_update_matches_oracle(name):
+def test_update_matches_oracle(name, precision):
     from mtrl_amd import _lib as L
 
     spec = CONFIGS[name]
@@ -79,7 +81,7 @@ def test_update_matches_oracle(name):
     BATCH_PER_TASK[0] = n
     B = n * T
     st = _f32_state(cfg, seed=11)
-    eng = _engine_for(cfg)
+    eng = _engine_for(cfg, precision=precision)
     _load_state(eng, st)
     for step in range(3):
         batch = synthetic_batch(T, B, seed=100 + step, dtype=np.float32)
