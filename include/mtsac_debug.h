@@ -18,10 +18,34 @@ extern "C" {
  *   epi 0 store (+ db = column sums of B when kind 2 and db != NULL),
  *   epi 1 relu(acc + bias[n]), epi 2 acc * (mask[m][n] > 0).
  * Every operand is dense with the given leading dimension; batch strides are the
- * dense matrix sizes (A shared across the batch when a_shared != 0). */
+ * dense matrix sizes (A shared across the batch when a_shared != 0).
+ * precision: low byte = enum mtsac_precision; bits 8-15 = split-K slices for epi 0
+ * (0 or 1: no split). */
 int mtsac_debug_gemm(int precision, int kind, int epi, int batch, int M, int N, int K, const float* A, int lda, int a_shared,
                      const float* B, int ldb, float* C, int ldc, const float* bias, const float* mask, int ldm,
                      float* db);
+
+/* Time `iters` back-to-back launches of one GEMM on device-resident random operands
+ * (allocated once, dense, lda = K or M as the kind requires); writes the mean
+ * milliseconds per launch (HIP events on the launch stream). */
+int mtsac_debug_gemm_bench(int precision, int kind, int epi, int batch, int M, int N, int K, int iters,
+                           double* ms_per_launch);
+
+/* Pre-split-plane GEMM (gemm_x3p.hip): C[M][N] = op(A) . op(B) from host fp32 arrays.
+ * a_kmajor: A given as [K][M] (else [M][K]); b_kmajor: B given as [K][N] (else [N][K]).
+ * The operands are split into bf16 planes on the device (transposing as needed), then
+ * multiplied; epi as in mtsac_debug_gemm (bias / mask may be NULL for other epilogues). */
+int mtsac_debug_gemm_x3p(int epi, int M, int N, int K, const float* A, int a_kmajor, const float* B, int b_kmajor,
+                         float* C, const float* bias, const float* mask);
+/* Time iters launches of the plane GEMM on device-resident random planes (NT form). */
+int mtsac_debug_gemm_x3p_bench(int epi, int batch, int M, int N, int K, int iters, double* ms_per_launch);
+/* Select the plane GEMM tile geometry (0: 128x128 / 4 waves, 1: 256x128 / 8 waves); returns the old one. */
+int mtsac_debug_x3p_geo(int geo);
+
+/* Per-launch record of the last timed step (mtsac_set_timing): i < 0 returns the number of
+ * records; else dims = {family = GEMM kind, M, N, K, batch} and *ms its duration. */
+struct mtsac_engine;
+int mtsac_debug_timed_launch(struct mtsac_engine* engine, int32_t i, int32_t* dims, double* ms);
 
 #ifdef __cplusplus
 }

@@ -128,6 +128,11 @@ SIGNATURES = {
     "mtsac_memcpy": (ctypes.c_int, [P, P, I64]),
     "mtsac_set_timing": (ctypes.c_int, [P, I32]),
     "mtsac_get_timing": (ctypes.c_int, [P, I32, PD, PI32, PD]),
+    "mtsac_debug_gemm_bench": (ctypes.c_int, [ctypes.c_int] * 8 + [PD]),
+    "mtsac_debug_gemm_x3p": (ctypes.c_int, [ctypes.c_int] * 4 + [P, ctypes.c_int, P, ctypes.c_int, P, P, P]),
+    "mtsac_debug_gemm_x3p_bench": (ctypes.c_int, [ctypes.c_int] * 6 + [PD]),
+    "mtsac_debug_x3p_geo": (ctypes.c_int, [ctypes.c_int]),
+    "mtsac_debug_timed_launch": (ctypes.c_int, [P, I32, PI32, PD]),
     "mtsac_debug_gemm": (
         ctypes.c_int,
         # precision, kind, epi, batch, M, N, K, A, lda, a_shared, B, ldb, C, ldc, bias, mask, ldm, db

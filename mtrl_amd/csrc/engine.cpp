@@ -59,6 +59,9 @@ struct Net {
   long long n_flat = 0, trunk_off = 0, n_params = 0;
   std::vector<std::pair<long long, long long>> leaves;  // (offset, count) in flax order
   float *p = nullptr, *g = nullptr, *m = nullptr, *v = nullptr, *tgt = nullptr;
+  // transposed hidden kernels W_i^T ([E][out][in], i >= 1) of p (wt[0]) and tgt (wt[1]): the
+  // trunk forward runs as an NT product against them (k-contiguous operands on both sides)
+  float* wt[2][MAXD] = {};
   OptScalars* sc = nullptr;
 
   void layout(int in, int in_ld_, int W, int D, int T, int hd_, int E_) {
@@ -123,6 +126,7 @@ struct mtsac_engine {
   float *logpi_n = nullptr, *logpi = nullptr, *y = nullptr, *dq = nullptr, *row_a = nullptr, *row_b = nullptr,
         *row_c = nullptr, *alpha_w = nullptr, *cache = nullptr, *dout_a = nullptr;
   float* partials = nullptr;
+  float* splitk_ws = nullptr;
   float* pn = nullptr;  // [critic trunk |p|^2, actor trunk, critic heads, actor heads]
   float* log_alpha = nullptr;
   float *la_m = nullptr, *la_v = nullptr;
@@ -151,6 +155,7 @@ struct mtsac_engine {
   struct TimedLaunch {
     int family;
     double flops;
+    int M, N, K, batch;
     hipEvent_t a, b;
   };
   std::vector<TimedLaunch> tl;
@@ -214,6 +219,7 @@ struct mtsac_engine {
     }
     tl[tl_next].family = family;
     tl[tl_next].flops = flops;
+    tl[tl_next].M = tl[tl_next].N = tl[tl_next].K = tl[tl_next].batch = 0;
     (void)hipEventRecord(tl[tl_next].a, cur);
   }
   void t_end() {
@@ -224,6 +230,12 @@ struct mtsac_engine {
 
   void gemm(const GemmParams& p, GemmKind kind, int epi, int batch) {
     t_begin((int)kind, 2.0 * (double)p.M * p.N * p.K * batch);
+    if (timing) {
+      tl[tl_next].M = p.M;
+      tl[tl_next].N = p.N;
+      tl[tl_next].K = p.K;
+      tl[tl_next].batch = batch;
+    }
     if (cfg.precision == MTSAC_FP32_SPLIT3)
       gemm_x3(p, kind, epi, batch, cur);
     else
@@ -233,13 +245,15 @@ struct mtsac_engine {
 
   // ------------------------------------------------------------ trunk passes
   // acts[i] = relu(in_i @ W_i + b_i) for every member (batched over the ensemble)
-  void trunk_forward(Net& net, const float* params, const float* X, int ldx, float** acts, int M) {
+  // wt: the transposed kernels of `params` (Net::wt) or null for the NN form throughout
+  void trunk_forward(Net& net, const float* params, float* const* wt, const float* X, int ldx, float** acts, int M) {
     for (int i = 0; i < net.depth; ++i) {
       GemmParams g{};
       g.A = (i == 0) ? X : acts[i - 1];
       g.lda = (i == 0) ? ldx : net.width;
       g.sA = (i == 0) ? 0 : (long long)M * net.width;
-      g.B = params + net.off_W[i];
+      const bool nt = wt != nullptr && i > 0;
+      g.B = nt ? wt[i] : params + net.off_W[i];
       g.ldb = net.width;
       g.sB = net.ms_W[i];
       g.C = acts[i];
@@ -250,8 +264,14 @@ struct mtsac_engine {
       g.M = M;
       g.N = net.width;
       g.K = (i == 0) ? net.in_dim : net.width;
-      gemm(g, GEMM_NN, EPI_BIAS_RELU, net.E);
+      gemm(g, nt ? GEMM_NT : GEMM_NN, EPI_BIAS_RELU, net.E);
     }
+  }
+
+  // Net::wt[which] = transposed hidden kernels of `params` (after every write of params)
+  void refresh_wt(Net& net, const float* params, int which, hipStream_t s) {
+    for (int i = 1; i < net.depth; ++i)
+      transpose_f32(params + net.off_W[i], net.ms_W[i], net.wt[which][i], net.ms_W[i], net.width, net.width, net.E, s);
   }
 
   // Backward through trunk layer i, split so the two halves can run concurrently:
@@ -273,6 +293,8 @@ struct mtsac_engine {
     g.M = (i == 0) ? net.in_dim : net.width;
     g.N = net.width;
     g.K = M;
+    g.splits = gemm_splits(g.M, g.N, g.K, net.E);
+    g.ws = splitk_ws;  // one workspace: weight-grad GEMMs are serialised (lane 3 chain, actor after critic)
     gemm(g, GEMM_TN, EPI_STORE, net.E);
   }
 
@@ -469,10 +491,10 @@ struct mtsac_engine {
       if (cfg.use_task_weights) row_alpha(task, cfg.task_begin, log_alpha, T_g, Bl, 1, row_c, tw, cur);
     });
     // critic forward on (s, a) with the current critic (mtsac.py:555)
-    const int s_cf = seg({s_in}, 1, [&] { trunk_forward(critic, critic.p, xc, ld_c, hc, Bl); });
+    const int s_cf = seg({s_in}, 1, [&] { trunk_forward(critic, critic.p, critic.wt[0], xc, ld_c, hc, Bl); });
     // actor forward on s with the pre-update actor (mtsac.py:640-642)
     const int s_af = seg({s_in}, 2, [&] {
-      trunk_forward(actor, actor.p, xa, ld_a, ha, Bl);
+      trunk_forward(actor, actor.p, actor.wt[0], xa, ld_a, ha, Bl);
       PolicyParams q = pp;
       q.head = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
       q.eps = device_noise ? nullptr : eps_c;
@@ -484,7 +506,7 @@ struct mtsac_engine {
     });
     // a' ~ pi(.|s'), target critic, TD target (mtsac.py:525-553)
     const int s_tg = seg({s_in}, 0, [&] {
-      trunk_forward(actor, actor.p, xan, ld_a, han, Bl);
+      trunk_forward(actor, actor.p, actor.wt[0], xan, ld_a, han, Bl);
       PolicyParams q = pp;
       q.head = head(actor, actor.p, han[actor.depth - 1], Bl, task);
       q.eps = device_noise ? nullptr : eps_n;
@@ -492,7 +514,7 @@ struct mtsac_engine {
       q.a_out = xcn;
       q.logpi = logpi_n;
       policy_head(q, cur);
-      trunk_forward(critic, critic.tgt, xcn, ld_c, hct, Bl);
+      trunk_forward(critic, critic.tgt, critic.wt[1], xcn, ld_c, hct, Bl);
       CriticHeadParams c = ch;
       c.head = head(critic, critic.tgt, hct[critic.depth - 1], Bl, task);
       c.mode = CH_TARGET;
@@ -525,10 +547,12 @@ struct mtsac_engine {
       head_sq(critic);
       allreduce(critic.g + critic.trunk_off, (size_t)(critic.n_flat - critic.trunk_off + EXTRA));
       optimize(critic, cfg.critic_lr, cfg.critic_max_grad_norm, true, 0);
+      refresh_wt(critic, critic.p, 0, cur);
+      refresh_wt(critic, critic.tgt, 1, cur);
     });
     // actor loss through the UPDATED critic (mtsac.py:659-691)
     const int s_ap = seg({s_co, s_af}, 1, [&] {
-      trunk_forward(critic, critic.p, xcp, ld_c, hc, Bl);
+      trunk_forward(critic, critic.p, critic.wt[0], xcp, ld_c, hc, Bl);
       CriticHeadParams c = ch;
       c.head = head(critic, critic.p, hc[critic.depth - 1], Bl, task);
       c.mode = CH_ACTOR;
@@ -571,6 +595,7 @@ struct mtsac_engine {
       head_sq(actor);
       allreduce(actor.g + actor.trunk_off, (size_t)(actor.n_flat - actor.trunk_off + EXTRA));
       optimize(actor, cfg.actor_lr, cfg.actor_max_grad_norm, false, 1);
+      refresh_wt(actor, actor.p, 0, cur);
       // temperature (mtsac.py:713-731)
       alpha_adam(al, cfg.alpha_lr, cfg.adam_b1, cfg.adam_b2, cfg.adam_eps, cfg.alpha_max_grad_norm, cur);
       // post-update parameter norms: trunk |p|^2 replicated, head |p|^2 summed over shards
@@ -777,6 +802,19 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     if ((rc = e->alloc(&net->sc, 1))) return bad(rc);
   }
   if ((rc = e->alloc(&e->critic.tgt, e->critic.n_flat))) return bad(rc);
+  for (Net* net : {&e->actor, &e->critic})
+    for (int w = 0; w < (net == &e->critic ? 2 : 1); ++w)
+      for (int i = 1; i < net->depth; ++i)
+        if ((rc = e->alloc(&net->wt[w][i], (size_t)net->ms_W[i] * net->E))) return bad(rc);
+  {  // split-K workspace: the largest weight-gradient GEMM that splits
+    long long ws = 0;
+    for (Net* net : {&e->actor, &e->critic})
+      for (int i = 0; i < net->depth; ++i) {
+        const int M = i == 0 ? net->in_dim : net->width;
+        ws = std::max(ws, gemm_ws_floats(M, net->width, net->E, gemm_splits(M, net->width, e->B, net->E)));
+      }
+    if ((rc = e->alloc(&e->splitk_ws, (size_t)std::max(ws, 1LL)))) return bad(rc);
+  }
 
   const int B = e->B;
   if ((rc = e->alloc(&e->store, (size_t)c.capacity * e->T_l * e->R))) return bad(rc);
@@ -899,6 +937,11 @@ static int copy_params(mtsac_engine* h, int which, float* host, int64_t n, bool 
     else
       HIP_TRY(hipMemcpy(host + o, buf + lf.first, sizeof(float) * lf.second, hipMemcpyDefault));
     o += lf.second;
+  }
+  if (to_device && (buf == net->p || buf == net->tgt)) {
+    h->refresh_wt(*net, buf, buf == net->p ? 0 : 1, h->st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(h->st));
   }
   return 0;
 }
@@ -1200,7 +1243,7 @@ static int act(mtsac_engine* h, const float* obs, int n, const float* eps, float
   gp.err = h->err;
   // obs doubles as next_obs; the action / reward / done inputs are ignored scratch
   batch_scatter(gp, h->r_obs, h->r_eps, h->r_obs, h->r_lp, h->r_lp, n, h->st);
-  h->trunk_forward(h->actor, h->actor.p, h->r_x, h->ld_a, h->r_h, n);
+  h->trunk_forward(h->actor, h->actor.p, h->actor.wt[0], h->r_x, h->ld_a, h->r_h, n);
   PolicyParams pp{};
   pp.head = h->head(h->actor, h->actor.p, h->r_h[h->actor.depth - 1], n, h->r_task);
   pp.eps = h->r_eps;
@@ -1294,16 +1337,35 @@ int mtsac_get_timing(mtsac_engine* h, int32_t family, double* total_ms, int32_t*
 }
 
 // ---------------------------------------------------------------- debug (include/mtsac_debug.h)
+int mtsac_debug_timed_launch(mtsac_engine* h, int32_t i, int32_t* dims, double* ms) {
+  if (!h) return fail(-22, "null engine");
+  if (i < 0) return (int)std::min(h->tl_next, h->tl.size());
+  if ((size_t)i >= std::min(h->tl_next, h->tl.size()) || !dims || !ms) return fail(-22, "bad launch index");
+  HIP_TRY(hipStreamSynchronize(h->st));
+  const auto& t = h->tl[i];
+  dims[0] = t.family;
+  dims[1] = t.M;
+  dims[2] = t.N;
+  dims[3] = t.K;
+  dims[4] = t.batch;
+  float v = 0.f;
+  HIP_TRY(hipEventElapsedTime(&v, t.a, t.b));
+  *ms = v;
+  return 0;
+}
+
 int mtsac_debug_gemm(int precision, int kind, int epi, int batch, int M, int N, int K, const float* A, int lda, int a_shared,
                      const float* B, int ldb, float* C, int ldc, const float* bias, const float* mask, int ldm,
                      float* db) {
+  const int splits = (precision >> 8) & 255;
+  precision &= 255;
   if (kind < 0 || kind > 2 || batch < 1 || M < 1 || N < 1 || K < 1) return fail(-22, "bad gemm arguments");
   const bool ta = kind == 2, tb = kind == 1;
   const long long a_rows = ta ? K : M, b_rows = tb ? N : K;
   const long long sA = a_rows * lda, sB = b_rows * ldb, sC = (long long)M * ldc;
-  float *dA = nullptr, *dB = nullptr, *dC = nullptr, *dbias = nullptr, *dmask = nullptr, *ddb = nullptr;
+  float *dA = nullptr, *dB = nullptr, *dC = nullptr, *dbias = nullptr, *dmask = nullptr, *ddb = nullptr, *dws = nullptr;
   auto cleanup = [&]() {
-    for (float* p : {dA, dB, dC, dbias, dmask, ddb})
+    for (float* p : {dA, dB, dC, dbias, dmask, ddb, dws})
       if (p) (void)hipFree(p);
   };
   const long long nA = a_shared ? sA : sA * batch;
@@ -1312,6 +1374,7 @@ int mtsac_debug_gemm(int precision, int kind, int epi, int batch, int M, int N, 
   if (ok && bias) ok = hipMalloc(&dbias, sizeof(float) * N * batch) == hipSuccess;
   if (ok && mask) ok = hipMalloc(&dmask, sizeof(float) * (long long)M * ldm * batch) == hipSuccess;
   if (ok && db) ok = hipMalloc(&ddb, sizeof(float) * N * batch) == hipSuccess;
+  if (ok && splits > 1) ok = hipMalloc(&dws, sizeof(float) * gemm_ws_floats(M, N, batch, splits)) == hipSuccess;
   if (!ok) {
     cleanup();
     return fail(-12, "hipMalloc failed");
@@ -1329,6 +1392,8 @@ int mtsac_debug_gemm(int precision, int kind, int epi, int batch, int M, int N, 
   g.mask = dmask; g.ldm = ldm; g.sMask = (long long)M * ldm;
   g.db = ddb; g.sDb = N;
   g.M = M; g.N = N; g.K = K;
+  g.splits = splits;
+  g.ws = dws;
   if (precision == MTSAC_FP32_SPLIT3)
     gemm_x3(g, (GemmKind)kind, epi, batch, nullptr);
   else
@@ -1338,6 +1403,68 @@ int mtsac_debug_gemm(int precision, int kind, int epi, int batch, int M, int N, 
   if (e == hipSuccess && db) e = hipMemcpy(db, ddb, sizeof(float) * N * batch, hipMemcpyDeviceToHost);
   cleanup();
   if (e != hipSuccess) return fail(-5, std::string("debug gemm: ") + hipGetErrorString(e));
+  return 0;
+}
+
+__global__ void fill_rand_kernel(float* p, long long n, unsigned seed) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  unsigned x = (unsigned)i * 2654435761u ^ seed;
+  x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+  p[i] = ((float)(x & 0xFFFFFF) / 8388608.0f) - 1.0f;
+}
+
+int mtsac_debug_gemm_bench(int precision, int kind, int epi, int batch, int M, int N, int K, int iters,
+                           double* ms_per_launch) {
+  const int splits = (precision >> 8) & 255;
+  precision &= 255;
+  if (kind < 0 || kind > 2 || batch < 1 || M < 1 || N < 1 || K < 1 || iters < 1 || !ms_per_launch)
+    return fail(-22, "bad gemm bench arguments");
+  const bool ta = kind == 2, tb = kind == 1;
+  const int lda = ta ? M : K, ldb = tb ? K : N;
+  const long long sA = (long long)(ta ? K : M) * lda, sB = (long long)(tb ? N : K) * ldb, sC = (long long)M * N;
+  float *A = nullptr, *B = nullptr, *C = nullptr, *bias = nullptr, *db = nullptr, *ws = nullptr;
+  if (splits > 1) HIP_TRY(hipMalloc(&ws, sizeof(float) * gemm_ws_floats(M, N, batch, splits)));
+  HIP_TRY(hipMalloc(&A, sizeof(float) * sA * batch));
+  HIP_TRY(hipMalloc(&B, sizeof(float) * sB * batch));
+  HIP_TRY(hipMalloc(&C, sizeof(float) * sC * batch));
+  HIP_TRY(hipMalloc(&bias, sizeof(float) * N * batch));
+  HIP_TRY(hipMalloc(&db, sizeof(float) * N * batch));
+  for (auto pr : {std::make_pair(A, sA * batch), std::make_pair(B, sB * batch), std::make_pair(C, sC * batch),
+                  std::make_pair(bias, (long long)N * batch)})
+    hipLaunchKernelGGL(fill_rand_kernel, dim3((unsigned)((pr.second + 255) / 256)), dim3(256), 0, nullptr,
+                       pr.first, pr.second, 17u);
+  GemmParams g{};
+  g.A = A; g.lda = lda; g.sA = sA;
+  g.B = B; g.ldb = ldb; g.sB = sB;
+  g.C = C; g.ldc = N; g.sC = sC;
+  g.bias = bias; g.sBias = N;
+  g.mask = C; g.ldm = N; g.sMask = sC;  // any sign pattern will do
+  g.db = (kind == 2) ? db : nullptr; g.sDb = N;
+  g.M = M; g.N = N; g.K = K;
+  g.splits = splits;
+  g.ws = ws;
+  auto launch = [&]() {
+    if (precision == MTSAC_FP32_SPLIT3)
+      gemm_x3(g, (GemmKind)kind, epi, batch, nullptr);
+    else
+      gemm_f32(g, (GemmKind)kind, epi, batch, nullptr);
+  };
+  launch();
+  hipEvent_t e0, e1;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  HIP_TRY(hipEventRecord(e0, nullptr));
+  for (int i = 0; i < iters; ++i) launch();
+  HIP_TRY(hipEventRecord(e1, nullptr));
+  HIP_TRY(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+  *ms_per_launch = ms / iters;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  for (float* p : {A, B, C, bias, db, ws})
+    if (p) (void)hipFree(p);
   return 0;
 }
 

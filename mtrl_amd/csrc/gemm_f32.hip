@@ -10,7 +10,7 @@
 // staging with the next K-tile's loads in flight during the MFMAs; operands are
 // stored k-major in LDS ([k][m], [k][n]) so each MFMA operand is one conflict-free
 // ds_read_b32 per lane (lanes 0-31 consecutive m/n, lanes 32-63 the next k row).
-#include "kernels.h"
+#include "gemm_common.h"
 
 namespace mtsac {
 
@@ -82,10 +82,12 @@ __global__ __launch_bounds__(NTH, 2) void gemm_f32_kernel(GemmParams p) {
   __shared__ float As[BK * LA::LD];
   __shared__ float Bs[BK * LB::LD];
 
-  const int z = blockIdx.z;
-  const float* __restrict__ A = p.A + z * p.sA;
-  const float* __restrict__ B = p.B + z * p.sB;
-  float* __restrict__ C = p.C + z * p.sC;
+  const GemmSlice sl = gemm_slice<TA, TB>(p);
+  const int z = sl.z;
+  const float* __restrict__ A = sl.A;
+  const float* __restrict__ B = sl.B;
+  float* __restrict__ C = sl.C;
+  const int K = sl.K;
 
   const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
@@ -98,15 +100,15 @@ __global__ __launch_bounds__(NTH, 2) void gemm_f32_kernel(GemmParams p) {
   const int lk = lane >> 5;
 
   // fused bias-gradient (column sums of B) for weight-grad GEMMs: m-tile 0 only
-  const bool do_db = (EPI == EPI_STORE) && !TB && p.db != nullptr && blockIdx.x == 0;
+  const bool do_db = (EPI == EPI_STORE) && !TB && sl.db != nullptr && blockIdx.x == 0;
   float dbacc = 0.f;
 
   f32x16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
 
   float4 ra[4], rb[4];
-  const int nk = (p.K + BK - 1) / BK;
-  LA::load(A, p.lda, m0, p.M, 0, p.K, ra);
-  LB::load(B, p.ldb, n0, p.N, 0, p.K, rb);
+  const int nk = (K + BK - 1) / BK;
+  LA::load(A, p.lda, m0, p.M, 0, K, ra);
+  LB::load(B, p.ldb, n0, p.N, 0, K, rb);
   LA::store(As, ra);
   LB::store(Bs, rb);
   __syncthreads();
@@ -114,8 +116,8 @@ __global__ __launch_bounds__(NTH, 2) void gemm_f32_kernel(GemmParams p) {
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = (kt + 1) < nk;
     if (more) {
-      LA::load(A, p.lda, m0, p.M, (kt + 1) * BK, p.K, ra);
-      LB::load(B, p.ldb, n0, p.N, (kt + 1) * BK, p.K, rb);
+      LA::load(A, p.lda, m0, p.M, (kt + 1) * BK, K, ra);
+      LB::load(B, p.ldb, n0, p.N, (kt + 1) * BK, K, rb);
     }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
@@ -146,7 +148,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_f32_kernel(GemmParams p) {
     const int col = t & 127, half = t >> 7;
     if (half == 1) As[col] = dbacc;
     __syncthreads();
-    if (half == 0 && n0 + col < p.N) p.db[z * p.sDb + n0 + col] = dbacc + As[col];
+    if (half == 0 && n0 + col < p.N) sl.db[n0 + col] = dbacc + As[col];
   }
 
   // epilogue: acc[i][j] element r -> row = (r&3) + 8(r>>2) + 4*lk, col = lr (32x32 C/D map)
@@ -167,7 +169,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_f32_kernel(GemmParams p) {
           float v = acc[r];
           if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
           if (EPI == EPI_RELU_MASK) v = (mask[(long long)row * p.ldm + col] > 0.f) ? v : 0.f;
-          C[(long long)row * p.ldc + col] = v;
+          C[(long long)row * sl.ldc + col] = v;
         }
       }
     }
@@ -176,10 +178,19 @@ __global__ __launch_bounds__(NTH, 2) void gemm_f32_kernel(GemmParams p) {
 
 }  // namespace
 
-void gemm_f32(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_t st) {
-  dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, batch);
+void gemm_f32(const GemmParams& p0, GemmKind kind, int epi, int batch, hipStream_t st) {
+  if (p0.M <= 0 || p0.N <= 0) return;
+  GemmParams p = p0;
+  int S = 1;
+  if (p.splits > 1 && epi == EPI_STORE && p.ws != nullptr && p.K > 0) {
+    const int kt = (p.K + BK - 1) / BK;
+    p.kchunk = (kt + p.splits - 1) / p.splits * BK;
+    S = (p.K + p.kchunk - 1) / p.kchunk;
+  }
+  p.splits = S;
+  if (S == 1) p.kchunk = p.K;
+  dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, batch * S);
   dim3 block(NTH);
-  if (p.M <= 0 || p.N <= 0) return;
   switch (kind) {
     case GEMM_NN:
       if (epi == EPI_BIAS_RELU)
@@ -190,6 +201,8 @@ void gemm_f32(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_
     case GEMM_NT:
       if (epi == EPI_RELU_MASK)
         hipLaunchKernelGGL((gemm_f32_kernel<false, true, EPI_RELU_MASK>), grid, block, 0, st, p);
+      else if (epi == EPI_BIAS_RELU)
+        hipLaunchKernelGGL((gemm_f32_kernel<false, true, EPI_BIAS_RELU>), grid, block, 0, st, p);
       else
         hipLaunchKernelGGL((gemm_f32_kernel<false, true, EPI_STORE>), grid, block, 0, st, p);
       break;
@@ -197,6 +210,7 @@ void gemm_f32(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_
       hipLaunchKernelGGL((gemm_f32_kernel<true, false, EPI_STORE>), grid, block, 0, st, p);
       break;
   }
+  if (S > 1) splitk_reduce(p, batch, S, st);
 }
 
 }  // namespace mtsac

@@ -14,7 +14,7 @@
 // accumulators.  fp32 tiles are loaded to registers with the next K-tile in flight, split
 // into three bf16 planes and stored k-contiguous in LDS ([plane][row][k], rows padded to
 // 80 B so the MFMA operand reads -- one ds_read_b128 per lane -- are bank-conflict free).
-#include "kernels.h"
+#include "gemm_common.h"
 
 namespace mtsac {
 
@@ -110,10 +110,12 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3_kernel(GemmParams p) {
   __bf16* As = smem;
   __bf16* Bs = smem + OPER;
 
-  const int z = blockIdx.z;
-  const float* __restrict__ A = p.A + z * p.sA;
-  const float* __restrict__ B = p.B + z * p.sB;
-  float* __restrict__ C = p.C + z * p.sC;
+  const GemmSlice sl = gemm_slice<TA, TB>(p);
+  const int z = sl.z;
+  const float* __restrict__ A = sl.A;
+  const float* __restrict__ B = sl.B;
+  float* __restrict__ C = sl.C;
+  const int K = sl.K;
   const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
   const int t = threadIdx.x;
@@ -121,14 +123,14 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3_kernel(GemmParams p) {
   const int wm = (wave & 1) * 64, wn = (wave >> 1) * 64;
   const int lr = lane & 31, lh = lane >> 5;
 
-  const bool do_db = (EPI == EPI_STORE) && !TB && p.db != nullptr && blockIdx.x == 0;
+  const bool do_db = (EPI == EPI_STORE) && !TB && sl.db != nullptr && blockIdx.x == 0;
   float dbacc = 0.f;
   f32x16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
 
   float4 ra[4], rb[4];
-  const int nk = (p.K + BK - 1) / BK;
-  LA::load(A, p.lda, m0, p.M, 0, p.K, ra);
-  LB::load(B, p.ldb, n0, p.N, 0, p.K, rb);
+  const int nk = (K + BK - 1) / BK;
+  LA::load(A, p.lda, m0, p.M, 0, K, ra);
+  LB::load(B, p.ldb, n0, p.N, 0, K, rb);
   LA::store(As, ra);
   LB::store(Bs, rb);
   __syncthreads();
@@ -136,8 +138,8 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3_kernel(GemmParams p) {
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = (kt + 1) < nk;
     if (more) {
-      LA::load(A, p.lda, m0, p.M, (kt + 1) * BK, p.K, ra);
-      LB::load(B, p.ldb, n0, p.N, (kt + 1) * BK, p.K, rb);
+      LA::load(A, p.lda, m0, p.M, (kt + 1) * BK, K, ra);
+      LB::load(B, p.ldb, n0, p.N, (kt + 1) * BK, K, rb);
     }
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
@@ -184,7 +186,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3_kernel(GemmParams p) {
     const int col = t & 127, half = t >> 7;
     if (half == 1) red[col] = dbacc;
     __syncthreads();
-    if (half == 0 && n0 + col < p.N) p.db[z * p.sDb + n0 + col] = dbacc + red[col];
+    if (half == 0 && n0 + col < p.N) sl.db[n0 + col] = dbacc + red[col];
   }
 
   const float* __restrict__ bias = (EPI == EPI_BIAS_RELU) ? p.bias + z * p.sBias : nullptr;
@@ -204,7 +206,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3_kernel(GemmParams p) {
           float v = acc[r];
           if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
           if (EPI == EPI_RELU_MASK) v = (mask[(long long)row * p.ldm + col] > 0.f) ? v : 0.f;
-          C[(long long)row * p.ldc + col] = v;
+          C[(long long)row * sl.ldc + col] = v;
         }
       }
     }
@@ -213,10 +215,19 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3_kernel(GemmParams p) {
 
 }  // namespace
 
-void gemm_x3(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_t st) {
-  dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, batch);
+void gemm_x3(const GemmParams& p0, GemmKind kind, int epi, int batch, hipStream_t st) {
+  if (p0.M <= 0 || p0.N <= 0) return;
+  GemmParams p = p0;
+  int S = 1;
+  if (p.splits > 1 && epi == EPI_STORE && p.ws != nullptr && p.K > 0) {
+    const int kt = (p.K + BK - 1) / BK;
+    p.kchunk = (kt + p.splits - 1) / p.splits * BK;
+    S = (p.K + p.kchunk - 1) / p.kchunk;
+  }
+  p.splits = S;
+  if (S == 1) p.kchunk = p.K;
+  dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, batch * S);
   dim3 block(NTH);
-  if (p.M <= 0 || p.N <= 0) return;
   switch (kind) {
     case GEMM_NN:
       if (epi == EPI_BIAS_RELU)
@@ -227,6 +238,8 @@ void gemm_x3(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_t
     case GEMM_NT:
       if (epi == EPI_RELU_MASK)
         hipLaunchKernelGGL((gemm_x3_kernel<false, true, EPI_RELU_MASK>), grid, block, 0, st, p);
+      else if (epi == EPI_BIAS_RELU)
+        hipLaunchKernelGGL((gemm_x3_kernel<false, true, EPI_BIAS_RELU>), grid, block, 0, st, p);
       else
         hipLaunchKernelGGL((gemm_x3_kernel<false, true, EPI_STORE>), grid, block, 0, st, p);
       break;
@@ -234,6 +247,7 @@ void gemm_x3(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_t
       hipLaunchKernelGGL((gemm_x3_kernel<true, false, EPI_STORE>), grid, block, 0, st, p);
       break;
   }
+  if (S > 1) splitk_reduce(p, batch, S, st);
 }
 
 }  // namespace mtsac

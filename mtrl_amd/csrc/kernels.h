@@ -25,12 +25,65 @@ struct GemmParams {
   int M, N, K;
   int lda, ldb, ldc, ldm;
   long long sA, sB, sC, sBias, sMask, sDb;  // per-batch strides (elements)
+  // split-K (EPI_STORE only): `splits` slices of K write dense partials (and db partials) into
+  // ws, then a fixed-order reduction writes C / db.  ws needs gemm_ws_floats() floats.
+  int splits;
+  int kchunk;                               // set by the launcher
+  float* ws;
 };
 
 enum GemmKind { GEMM_NN = 0, GEMM_NT = 1, GEMM_TN = 2 };
+// K slices that fill the chip for an EPI_STORE GEMM with few output tiles (1 = no split)
+int gemm_splits(int M, int N, int K, int batch);
+long long gemm_ws_floats(int M, int N, int batch, int splits);
+// C[z] = sum_s ws[z*S + s] (+ db likewise), fixed order: deterministic
+void splitk_reduce(const GemmParams& p, int batch, int splits, hipStream_t st);
+// out[z][c][r] = in[z][r][c]  (rows x cols per batch entry, dense)
+void transpose_f32(const float* in, long long s_in, float* out, long long s_out, int rows, int cols, int batch,
+                   hipStream_t st);
 void gemm_f32(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_t st);
 // same contract, fp32-accurate via 3-way bf16 operand split on bf16 MFMA (gemm_x3.hip)
 void gemm_x3(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_t st);
+
+// ------------------------------------------------------------------ pre-split plane GEMM
+// C[z] = A[z] . B[z]^T with A planes [3][M][lda], B planes [3][N][ldb] (bf16, k contiguous,
+// K a multiple of 32 with zero padding) -- gemm_x3p.hip.
+struct SplitGemmParams {
+  const __bf16* A;
+  long long lda, pA, sA;  // row stride, plane stride, batch stride (elements)
+  const __bf16* B;
+  long long ldb, pB, sB;
+  float* C;               // fp32 output (may be null when only planes are wanted)
+  int ldc;
+  long long sC;
+  const float* bias;
+  long long sBias;
+  const float* mask;
+  int ldm;
+  long long sMask;
+  __bf16* Cp;             // optional split planes of C: [3][M][ldcp]
+  long long ldcp, pC, sCp;
+  int M, N, K;
+  int dbg;                // experiments only: bit0 skip steady-state loads, bit1 skip MFMA
+};
+void gemm_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
+extern int g_x3p_geo;
+extern int g_x3p_dbg;  // tile geometry of gemm_x3p (0: 128x128/4 waves, 1: 256x128/8 waves)
+
+// fp32 x[z][rows][ldx] -> bf16 planes out[z][3][out_rows][ldo] (plane stride po); TRANSPOSE
+// writes out[q][col][row].  Elements past rows/cols inside [out_rows, out_cols) become 0.
+struct SplitParams {
+  const float* x;
+  long long ldx, sx;
+  int rows, cols;
+  __bf16* out;
+  long long ldo, po, so;
+  int out_rows, out_cols;
+};
+void split_planes(const SplitParams& s, bool transpose, int batch, hipStream_t st);
+// db[z][c] = sum_r x[z][r][c] (deterministic two-pass; part holds batch*16*cols floats)
+void colsum(const float* x, int rows, int cols, int ld, long long sx, int batch, float* part, float* db,
+            long long sdb, hipStream_t st);
 
 // ------------------------------------------------------------------ replay
 struct PcgDev {  // device-resident numpy PCG64 state (buffers.py:260)

@@ -254,7 +254,7 @@ class MTSACEngine:
 
 
 def debug_gemm(kind: int, epi: int, A, B, C, M: int, N: int, K: int, batch: int = 1, a_shared: bool = False,
-               bias=None, mask=None, want_db: bool = False, precision: int = 0):
+               bias=None, mask=None, want_db: bool = False, precision: int = 0, splits: int = 1):
     """Run one device GEMM (include/mtsac_debug.h) on host arrays; returns (C, db)."""
     lib = _lib.load()
     A = np.ascontiguousarray(A, np.float32)
@@ -264,7 +264,7 @@ def debug_gemm(kind: int, epi: int, A, B, C, M: int, N: int, K: int, batch: int 
     bias_a = None if bias is None else np.ascontiguousarray(bias, np.float32)
     mask_a = None if mask is None else np.ascontiguousarray(mask, np.float32)
     db = np.zeros((batch, N), np.float32) if want_db else None
-    check(lib.mtsac_debug_gemm(precision, kind, epi, batch, M, N, K, A.ctypes.data, lda, 1 if a_shared else 0, B.ctypes.data,
+    check(lib.mtsac_debug_gemm(precision | (splits << 8), kind, epi, batch, M, N, K, A.ctypes.data, lda, 1 if a_shared else 0, B.ctypes.data,
                                ldb, C.ctypes.data, ldc, None if bias_a is None else bias_a.ctypes.data,
                                None if mask_a is None else mask_a.ctypes.data,
                                0 if mask_a is None else mask_a.shape[-1], None if db is None else db.ctypes.data))

@@ -89,6 +89,47 @@ def test_gemm_epilogues_batched(precision):
         np.testing.assert_allclose(C[e], ref, rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("splits", [2, 5, 16])
+@pytest.mark.parametrize("shape", [(93, 300, 6400, 2), (64, 130, 1000, 1), (7, 8, 33, 1)])
+def test_gemm_splitk_weight_grad(shape, splits, precision):
+    """Split-K TN (weight gradient of a narrow layer over a long batch): partial slabs reduced in
+    slice order, db column sums from the same slices; same bound as the unsplit GEMM."""
+    from mtrl_amd.engine import debug_gemm
+
+    M, N, K, E = shape
+    rng = np.random.default_rng(3)
+    Mp = (M + 3) // 4 * 4
+    A = np.zeros((E, K, Mp), np.float32)
+    A[..., :M] = rng.standard_normal((E, K, M))
+    B = rng.standard_normal((E, K, N)).astype(np.float32)
+    C, db = debug_gemm(TN, STORE, A, B, np.zeros((E, M, N), np.float32), M, N, K, batch=E, want_db=True,
+                       precision=precision, splits=splits)
+    tol = 2e-6 if precision == 0 else 4e-6
+    for e in range(E):
+        ref, mag = _ref(TN, A[e], B[e], M, N, K)
+        err = np.abs(C[e] - ref)
+        assert np.all(err <= tol * mag + 1e-30), float((err / mag).max())
+        np.testing.assert_allclose(db[e], B[e].astype(np.float64).sum(0), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+def test_gemm_nt_bias_relu(precision):
+    """Trunk forward against a pre-transposed weight: relu(A W^T_stored^T + b) on the NT kernel."""
+    from mtrl_amd.engine import debug_gemm
+
+    rng = np.random.default_rng(4)
+    M, N, K, E = 300, 200, 96, 2
+    A = rng.standard_normal((E, M, K)).astype(np.float32)
+    Wt = rng.standard_normal((E, N, K)).astype(np.float32)
+    bias = rng.standard_normal((E, N)).astype(np.float32)
+    C, _ = debug_gemm(NT, BIAS_RELU, A, Wt, np.zeros((E, M, N), np.float32), M, N, K, batch=E, bias=bias,
+                      precision=precision)
+    for e in range(E):
+        ref = np.maximum(A[e].astype(np.float64) @ Wt[e].T.astype(np.float64) + bias[e], 0)
+        np.testing.assert_allclose(C[e], ref, rtol=1e-5, atol=1e-4)
+
+
 def _small_engine(T=3, n=4, cap=50, D=None, normalize=False, **kw):
     from mtrl_amd.engine import MTSACEngine, make_config
 
