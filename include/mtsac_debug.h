@@ -33,13 +33,18 @@ int mtsac_debug_gemm_bench(int precision, int kind, int epi, int batch, int M, i
 
 /* Pre-split-plane GEMM (gemm_x3p.hip): C[M][N] = op(A) . op(B) from host fp32 arrays.
  * a_kmajor: A given as [K][M] (else [M][K]); b_kmajor: B given as [K][N] (else [N][K]).
- * The operands are split into bf16 planes on the device (transposing as needed), then
- * multiplied; epi as in mtsac_debug_gemm (bias / mask may be NULL for other epilogues). */
+ * The operands are split into bf16 planes on the device in their stored orientation and
+ * multiplied (k-major operands through the transposed LDS read); epi as in mtsac_debug_gemm
+ * (bits 8-15: split-K slices for epi 0).  Csum (nullable): the GEMM also writes C's split
+ * planes and Csum receives their sum h + m + l. */
 int mtsac_debug_gemm_x3p(int epi, int M, int N, int K, const float* A, int a_kmajor, const float* B, int b_kmajor,
-                         float* C, const float* bias, const float* mask);
+                         float* C, const float* bias, const float* mask, float* Csum);
 /* Time iters launches of the plane GEMM on device-resident random planes (NT form). */
 int mtsac_debug_gemm_x3p_bench(int epi, int batch, int M, int N, int K, int iters, double* ms_per_launch);
-/* Select the plane GEMM tile geometry (0: 128x128 / 4 waves, 1: 256x128 / 8 waves); returns the old one. */
+/* Select the plane GEMM tile geometry (bits 0-7: 0 = 128x128 k32, 1 = 256x128 k32, 2 = 256x128 k16,
+ * 3 = 256x256 k16, 255 = by operand form (default)) and
+ * ablation bits for experiments (bits 8-15: plane GEMM, bits 16-23: split GEMM; 0 = normal);
+ * returns the old geometry. */
 int mtsac_debug_x3p_geo(int geo);
 
 /* Per-launch record of the last timed step (mtsac_set_timing): i < 0 returns the number of

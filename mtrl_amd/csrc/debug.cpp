@@ -39,23 +39,36 @@ struct DevBuf {
   }
 };
 
-// planes of an operand that the GEMM reads as [rows][K]; source fp32 either [rows][K] or [K][rows]
-__bf16* make_planes(DevBuf& db, const float* dsrc, int rows, int K, bool kmajor, long long& ld, long long& ps) {
-  ld = up32(K);
-  ps = (long long)rows * ld;
-  __bf16* out = db.get<__bf16>(3 * ps);
-  if (!out) return nullptr;
+long long up8(long long x) { return (x + 7) / 8 * 8; }
+
+// planes of a fp32 operand stored [rows][K] (k contiguous) or, kmajor, [K][rows]; split in its
+// stored orientation: row-major planes [3][rows][up32(K)], k-major planes [3][up32(K)][up8(rows)]
+// (zeros in the padding)
+void plane_geom(int rows, int K, bool kmajor, long long& ld, long long& ps) {
+  ld = kmajor ? up8(rows) : up32(K);
+  ps = (kmajor ? up32(K) : (long long)rows) * ld;
+}
+
+void split_into(const float* dsrc, int rows, int K, bool kmajor, __bf16* out) {
+  long long ld, ps;
+  plane_geom(rows, K, kmajor, ld, ps);
   SplitParams s{};
   s.x = dsrc;
   s.ldx = kmajor ? rows : K;
   s.rows = kmajor ? K : rows;
   s.cols = kmajor ? rows : K;
+  s.out_rows = kmajor ? (int)up32(K) : rows;
   s.out = out;
   s.ldo = ld;
   s.po = ps;
-  s.out_rows = rows;
   s.out_cols = (int)ld;
-  split_planes(s, kmajor, 1, nullptr);
+  split_planes(s, false, 1, nullptr);
+}
+
+__bf16* make_planes(DevBuf& db, const float* dsrc, int rows, int K, bool kmajor, long long& ld, long long& ps) {
+  plane_geom(rows, K, kmajor, ld, ps);
+  __bf16* out = db.get<__bf16>(3 * ps);
+  if (out) split_into(dsrc, rows, K, kmajor, out);
   return out;
 }
 
@@ -64,7 +77,9 @@ __bf16* make_planes(DevBuf& db, const float* dsrc, int rows, int K, bool kmajor,
 extern "C" {
 
 int mtsac_debug_gemm_x3p(int epi, int M, int N, int K, const float* A, int a_kmajor, const float* B, int b_kmajor,
-                         float* C, const float* bias, const float* mask) {
+                         float* C, const float* bias, const float* mask, float* Csum) {
+  const int splits = (epi >> 8) & 255;
+  epi &= 255;
   if (M < 1 || N < 1 || K < 1 || !A || !B || !C) return -22;
   DevBuf d;
   float* dA = d.get<float>((size_t)M * K);
@@ -72,7 +87,9 @@ int mtsac_debug_gemm_x3p(int epi, int M, int N, int K, const float* A, int a_kma
   float* dC = d.get<float>((size_t)M * N);
   float* dbias = d.get<float>(N);
   float* dmask = d.get<float>((size_t)M * N);
-  if (!dA || !dB || !dC || !dbias || !dmask) return -12;
+  __bf16* dCp = d.get<__bf16>((size_t)3 * M * N);
+  float* dws = d.get<float>(splits > 1 ? (size_t)gemm_ws_floats(M, N, 1, splits) : 1);
+  if (!dA || !dB || !dC || !dbias || !dmask || !dCp || !dws) return -12;
   (void)hipMemcpy(dA, A, sizeof(float) * M * K, hipMemcpyHostToDevice);
   (void)hipMemcpy(dB, B, sizeof(float) * N * K, hipMemcpyHostToDevice);
   if (bias) (void)hipMemcpy(dbias, bias, sizeof(float) * N, hipMemcpyHostToDevice);
@@ -82,57 +99,61 @@ int mtsac_debug_gemm_x3p(int epi, int M, int N, int K, const float* A, int a_kma
   __bf16* Bp = make_planes(d, dB, N, K, b_kmajor != 0, ldb, pb);
   if (!Ap || !Bp) return -12;
   SplitGemmParams g{};
-  g.A = Ap;
-  g.lda = lda;
-  g.pA = pa;
-  g.B = Bp;
-  g.ldb = ldb;
-  g.pB = pb;
-  g.C = dC;
-  g.ldc = N;
+  g.A = Ap; g.lda = lda; g.pA = pa; g.a_kmajor = a_kmajor != 0;
+  g.B = Bp; g.ldb = ldb; g.pB = pb; g.b_kmajor = b_kmajor != 0;
+  g.C = dC; g.ldc = N;
   g.bias = dbias;
-  g.mask = dmask;
-  g.ldm = N;
-  g.M = M;
-  g.N = N;
-  g.K = (int)lda;
+  g.mask = dmask; g.ldm = N;
+  if (Csum) {
+    g.Cp = dCp; g.ldcp = N; g.pC = (long long)M * N;
+  }
+  g.M = M; g.N = N; g.K = (int)up32(K);
+  g.splits = splits;
+  g.ws = dws;
   gemm_x3p(g, epi, 1, nullptr);
   if (hipDeviceSynchronize() != hipSuccess) return -5;
   if (hipMemcpy(C, dC, sizeof(float) * M * N, hipMemcpyDeviceToHost) != hipSuccess) return -5;
+  if (Csum) {
+    std::vector<__bf16> h((size_t)3 * M * N);
+    if (hipMemcpy(h.data(), dCp, sizeof(__bf16) * h.size(), hipMemcpyDeviceToHost) != hipSuccess) return -5;
+    const size_t n = (size_t)M * N;
+    for (size_t i = 0; i < n; ++i) Csum[i] = ((float)h[i] + (float)h[n + i]) + (float)h[2 * n + i];
+  }
   return 0;
 }
 
 int mtsac_debug_gemm_x3p_bench(int epi, int batch, int M, int N, int K, int iters, double* ms_per_launch) {
+  const int layout = (epi >> 8) & 3;  // bit 0: A k-major, bit 1: B k-major
+  epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || iters < 1 || !ms_per_launch) return -22;
   DevBuf d;
-  const long long ld = up32(K);
-  const long long pa = (long long)M * ld, pb = (long long)N * ld;
   float* fa = d.get<float>((size_t)M * K);
   float* fb = d.get<float>((size_t)N * K);
-  __bf16* Ap = d.get<__bf16>((size_t)3 * pa * batch);
-  __bf16* Bp = d.get<__bf16>((size_t)3 * pb * batch);
   float* C = d.get<float>((size_t)M * N * batch);
   float* bias = d.get<float>((size_t)N * batch);
-  if (!fa || !fb || !Ap || !Bp || !C || !bias) return -12;
+  if (!fa || !fb || !C || !bias) return -12;
   hipLaunchKernelGGL(fill_rand_f32, dim3((unsigned)(((long long)M * K + 255) / 256)), dim3(256), 0, nullptr, fa,
                      (long long)M * K, 3u);
   hipLaunchKernelGGL(fill_rand_f32, dim3((unsigned)(((long long)N * K + 255) / 256)), dim3(256), 0, nullptr, fb,
                      (long long)N * K, 5u);
+  // one plane set per batch entry (distinct memory, same values)
+  long long lda, pa, ldb, pb;
+  plane_geom(M, K, layout & 1, lda, pa);
+  plane_geom(N, K, layout & 2, ldb, pb);
+  __bf16* Ap = d.get<__bf16>((size_t)3 * pa * batch);
+  __bf16* Bp = d.get<__bf16>((size_t)3 * pb * batch);
+  if (!Ap || !Bp) return -12;
   for (int z = 0; z < batch; ++z) {
-    SplitParams s{};
-    s.x = fa; s.ldx = K; s.rows = M; s.cols = K; s.out = Ap + z * 3 * pa; s.ldo = ld; s.po = pa;
-    s.out_rows = M; s.out_cols = (int)ld;
-    split_planes(s, false, 1, nullptr);
-    s.x = fb; s.rows = N; s.out = Bp + z * 3 * pb; s.po = pb; s.out_rows = N;
-    split_planes(s, false, 1, nullptr);
+    split_into(fa, M, K, layout & 1, Ap + 3 * pa * z);
+    split_into(fb, N, K, layout & 2, Bp + 3 * pb * z);
   }
   SplitGemmParams g{};
-  g.A = Ap; g.lda = ld; g.pA = pa; g.sA = 3 * pa;
-  g.B = Bp; g.ldb = ld; g.pB = pb; g.sB = 3 * pb;
+  g.A = Ap; g.lda = lda; g.pA = pa; g.sA = 3 * pa; g.a_kmajor = layout & 1;
+  g.B = Bp; g.ldb = ldb; g.pB = pb; g.sB = 3 * pb; g.b_kmajor = (layout >> 1) & 1;
   g.C = C; g.ldc = N; g.sC = (long long)M * N;
   g.bias = bias; g.sBias = N;
   g.mask = C; g.ldm = N; g.sMask = (long long)M * N;
-  g.M = M; g.N = N; g.K = (int)ld;
+  g.M = M; g.N = N; g.K = (int)up32(K);
   gemm_x3p(g, epi, batch, nullptr);
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return -5;
@@ -150,8 +171,15 @@ int mtsac_debug_gemm_x3p_bench(int epi, int batch, int M, int N, int K, int iter
 
 int mtsac_debug_x3p_geo(int geo) {
   const int old = g_x3p_geo;
-  if ((geo & 255) <= 1) g_x3p_geo = geo & 255;
-  g_x3p_dbg = geo >> 8;
+  if (geo < 0) {  // restore the default (e.g. the value this function returned)
+    g_x3p_geo = -1;
+    g_x3p_dbg = g_x3_dbg = 0;
+    return old;
+  }
+  const int g = geo & 255;
+  g_x3p_geo = g <= 3 ? g : -1;
+  g_x3p_dbg = (geo >> 8) & 255;
+  g_x3_dbg = (geo >> 16) & 255;
   return old;
 }
 

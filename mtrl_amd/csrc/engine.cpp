@@ -62,6 +62,13 @@ struct Net {
   // transposed hidden kernels W_i^T ([E][out][in], i >= 1) of p (wt[0]) and tgt (wt[1]): the
   // trunk forward runs as an NT product against them (k-contiguous operands on both sides)
   float* wt[2][MAXD] = {};
+  // split3: bf16 planes of W_i ([E][3][in][wld], data grads) and of W_i^T ([E][3][out][wld],
+  // forward) for i >= 1, of p ([0]) and tgt ([1]); activation / data-grad planes of this net are
+  // [E][3][arows][ald] (arows = B rounded up to 32 with zero rows, ald = width rounded up to 32)
+  __bf16* wp[2][MAXD] = {};
+  __bf16* wtp[2][MAXD] = {};
+  long long wld = 0, arows = 0, ald = 0;
+  long long aps() const { return arows * ald; }  // plane stride of activation planes
   OptScalars* sc = nullptr;
 
   void layout(int in, int in_ld_, int W, int D, int T, int hd_, int E_) {
@@ -123,6 +130,15 @@ struct mtsac_engine {
   float* hct[MAXD] = {};  // target-critic activations (concurrent with hc)
   float* dza[MAXD] = {};  // per-layer pre-activation grads
   float* dzc[MAXD] = {};
+  // split3 planes of the GEMM operands among them (layers 0..D-2 of activations, 1..D-1 of grads)
+  bool planes = false;
+  __bf16* hap[MAXD] = {};
+  __bf16* hanp[MAXD] = {};
+  __bf16* hcp[MAXD] = {};
+  __bf16* hctp[MAXD] = {};
+  __bf16* dzap[MAXD] = {};
+  __bf16* dzcp[MAXD] = {};
+  float* cs_part = nullptr;  // column-sum partials (bias grads beside the plane weight-grad GEMM)
   float *logpi_n = nullptr, *logpi = nullptr, *y = nullptr, *dq = nullptr, *row_a = nullptr, *row_b = nullptr,
         *row_c = nullptr, *alpha_w = nullptr, *cache = nullptr, *dout_a = nullptr;
   float* partials = nullptr;
@@ -243,17 +259,73 @@ struct mtsac_engine {
     t_end();
   }
 
+  void gemmp(const SplitGemmParams& p, int epi, int batch, GemmKind family) {
+    t_begin((int)family, 2.0 * (double)p.M * p.N * p.K * batch);
+    if (timing) {
+      tl[tl_next].M = p.M;
+      tl[tl_next].N = p.N;
+      tl[tl_next].K = p.K;
+      tl[tl_next].batch = batch;
+    }
+    gemm_x3p(p, epi, batch, cur);
+    t_end();
+  }
+
+  // planes of the top layer's data grad (written by the head backward), when the trunk has
+  // hidden layers that read them
+  PlaneOut top_planes(Net& net, __bf16** dzp) {
+    PlaneOut po{};
+    if (planes && net.depth > 1) {
+      po.p = dzp[net.depth - 1];
+      po.ld = net.ald;
+      po.ps = net.aps();
+      po.sm = 3 * net.aps();
+    }
+    return po;
+  }
+
   // ------------------------------------------------------------ trunk passes
   // acts[i] = relu(in_i @ W_i + b_i) for every member (batched over the ensemble)
-  // wt: the transposed kernels of `params` (Net::wt) or null for the NN form throughout
-  void trunk_forward(Net& net, const float* params, float* const* wt, const float* X, int ldx, float** acts, int M) {
+  // which: 0 / 1 = params is Net::p / Net::tgt (their transposed copies or planes are current),
+  // -1 = plain NN form.  actp (split3): planes of acts[0..D-2] to produce, or null.
+  void trunk_forward(Net& net, const float* params, int which, const float* X, int ldx, float** acts, __bf16** actp,
+                     int M) {
+    const bool pl = planes && which >= 0 && actp != nullptr;
     for (int i = 0; i < net.depth; ++i) {
+      const bool last = i == net.depth - 1;
+      if (pl && i > 0) {  // NT on planes: acts[i-1] . (W_i^T)^T
+        SplitGemmParams g{};
+        g.A = actp[i - 1];
+        g.lda = net.ald;
+        g.pA = net.aps();
+        g.sA = 3 * net.aps();
+        g.B = net.wtp[which][i];
+        g.ldb = net.wld;
+        g.pB = (long long)net.width * net.wld;
+        g.sB = 3 * g.pB;
+        g.C = acts[i];
+        g.ldc = net.width;
+        g.sC = (long long)M * net.width;
+        g.bias = params + net.off_b[i];
+        g.sBias = net.ms_b;
+        if (!last) {
+          g.Cp = actp[i];
+          g.ldcp = net.ald;
+          g.pC = net.aps();
+          g.sCp = 3 * net.aps();
+        }
+        g.M = M;
+        g.N = net.width;
+        g.K = (int)net.ald;
+        gemmp(g, EPI_BIAS_RELU, net.E, GEMM_NT);
+        continue;
+      }
       GemmParams g{};
       g.A = (i == 0) ? X : acts[i - 1];
       g.lda = (i == 0) ? ldx : net.width;
       g.sA = (i == 0) ? 0 : (long long)M * net.width;
-      const bool nt = wt != nullptr && i > 0;
-      g.B = nt ? wt[i] : params + net.off_W[i];
+      const bool nt = !planes && which >= 0 && i > 0;
+      g.B = nt ? net.wt[which][i] : params + net.off_W[i];
       g.ldb = net.width;
       g.sB = net.ms_W[i];
       g.C = acts[i];
@@ -264,20 +336,72 @@ struct mtsac_engine {
       g.M = M;
       g.N = net.width;
       g.K = (i == 0) ? net.in_dim : net.width;
+      if (pl && !last) {
+        g.Cp = actp[i];
+        g.ldcp = net.ald;
+        g.pC = net.aps();
+        g.sCp = 3 * net.aps();
+      }
       gemm(g, nt ? GEMM_NT : GEMM_NN, EPI_BIAS_RELU, net.E);
     }
   }
 
-  // Net::wt[which] = transposed hidden kernels of `params` (after every write of params)
+  // after every write of params: Net::wt[which] (fp32) or the planes wp / wtp[which] (split3)
   void refresh_wt(Net& net, const float* params, int which, hipStream_t s) {
-    for (int i = 1; i < net.depth; ++i)
-      transpose_f32(params + net.off_W[i], net.ms_W[i], net.wt[which][i], net.ms_W[i], net.width, net.width, net.E, s);
+    for (int i = 1; i < net.depth; ++i) {
+      if (!planes) {
+        transpose_f32(params + net.off_W[i], net.ms_W[i], net.wt[which][i], net.ms_W[i], net.width, net.width, net.E,
+                      s);
+        continue;
+      }
+      SplitParams sp{};
+      sp.x = params + net.off_W[i];
+      sp.ldx = net.width;
+      sp.sx = net.ms_W[i];
+      sp.rows = net.width;
+      sp.cols = net.width;
+      sp.out = net.wp[which][i];
+      sp.ldo = net.wld;
+      sp.po = (long long)net.width * net.wld;
+      sp.so = 3 * sp.po;
+      sp.out_rows = net.width;
+      sp.out_cols = (int)net.wld;
+      split_planes(sp, false, net.E, s);
+      sp.out = net.wtp[which][i];
+      split_planes(sp, true, net.E, s);
+    }
   }
 
   // Backward through trunk layer i, split so the two halves can run concurrently:
   //   wgrad_layer: dW_i = in_i^T dz[i] (+ db_i fused into the GEMM's m-tile-0 blocks)
   //   dgrad_layer: dz[i-1] = (dz[i] W_i^T) * [acts[i-1] > 0]
-  void wgrad_layer(Net& net, const float* X, int ldx, float** acts, float** dz, int i, int M) {
+  void wgrad_layer(Net& net, const float* X, int ldx, float** acts, __bf16** actp, float** dz, __bf16** dzp, int i,
+                   int M) {
+    if (planes && i > 0 && actp && dzp) {  // TN on k-major planes; bias grad by column sums
+      SplitGemmParams g{};
+      g.A = actp[i - 1];
+      g.lda = net.ald;
+      g.pA = net.aps();
+      g.sA = 3 * net.aps();
+      g.a_kmajor = 1;
+      g.B = dzp[i];
+      g.ldb = net.ald;
+      g.pB = net.aps();
+      g.sB = 3 * net.aps();
+      g.b_kmajor = 1;
+      g.C = net.g + net.off_W[i];
+      g.ldc = net.width;
+      g.sC = net.ms_W[i];
+      g.M = net.width;
+      g.N = net.width;
+      g.K = (int)net.arows;
+      g.splits = gemm_x3p_splits(g.M, g.N, g.K, net.E);
+      g.ws = splitk_ws;
+      gemmp(g, EPI_STORE, net.E, GEMM_TN);
+      colsum(dz[i], M, net.width, net.width, (long long)M * net.width, net.E, cs_part, net.g + net.off_b[i], net.ms_b,
+             cur);
+      return;
+    }
     GemmParams g{};
     g.A = (i == 0) ? X : acts[i - 1];  // [K=rows][M=fan_in] storage -> TA
     g.lda = (i == 0) ? ldx : net.width;
@@ -298,7 +422,35 @@ struct mtsac_engine {
     gemm(g, GEMM_TN, EPI_STORE, net.E);
   }
 
-  void dgrad_layer(Net& net, const float* params, float** acts, float** dz, int i, int M) {
+  void dgrad_layer(Net& net, const float* params, float** acts, float** dz, __bf16** dzp, int i, int M) {
+    if (planes && dzp) {  // NT on planes: dz[i] . W_i^T, W_i planes read as [N = in][K = out]
+      SplitGemmParams g{};
+      g.A = dzp[i];
+      g.lda = net.ald;
+      g.pA = net.aps();
+      g.sA = 3 * net.aps();
+      g.B = net.wp[0][i];
+      g.ldb = net.wld;
+      g.pB = (long long)net.width * net.wld;
+      g.sB = 3 * g.pB;
+      g.C = dz[i - 1];
+      g.ldc = net.width;
+      g.sC = (long long)M * net.width;
+      g.mask = acts[i - 1];
+      g.ldm = net.width;
+      g.sMask = (long long)M * net.width;
+      if (i - 1 >= 1) {
+        g.Cp = dzp[i - 1];
+        g.ldcp = net.ald;
+        g.pC = net.aps();
+        g.sCp = 3 * net.aps();
+      }
+      g.M = M;
+      g.N = net.width;
+      g.K = (int)net.ald;
+      gemmp(g, EPI_RELU_MASK, net.E, GEMM_NT);
+      return;
+    }
     GemmParams g{};
     g.A = dz[i];
     g.lda = net.width;
@@ -438,12 +590,12 @@ struct mtsac_engine {
   }
 
   // trunk backward as segments: data chain on lane 1, weight grads on lane 3
-  int backward_segs(Net& net, const float* params, const float* X, int ldx, float** acts, float** dz, int d_top,
-                    int w_prev, int M) {
+  int backward_segs(Net& net, const float* params, const float* X, int ldx, float** acts, __bf16** actp, float** dz,
+                    __bf16** dzp, int d_top, int w_prev, int M) {
     int dprev = d_top, wprev = w_prev;
     for (int i = net.depth - 1; i >= 0; --i) {
-      wprev = seg({dprev, wprev}, 3, [&, i] { wgrad_layer(net, X, ldx, acts, dz, i, M); });
-      if (i > 0) dprev = seg({dprev}, 1, [&, i] { dgrad_layer(net, params, acts, dz, i, M); });
+      wprev = seg({dprev, wprev}, 3, [&, i] { wgrad_layer(net, X, ldx, acts, actp, dz, dzp, i, M); });
+      if (i > 0) dprev = seg({dprev}, 1, [&, i] { dgrad_layer(net, params, acts, dz, dzp, i, M); });
     }
     return seg({dprev, wprev}, 1, [] {});  // join point
   }
@@ -491,10 +643,10 @@ struct mtsac_engine {
       if (cfg.use_task_weights) row_alpha(task, cfg.task_begin, log_alpha, T_g, Bl, 1, row_c, tw, cur);
     });
     // critic forward on (s, a) with the current critic (mtsac.py:555)
-    const int s_cf = seg({s_in}, 1, [&] { trunk_forward(critic, critic.p, critic.wt[0], xc, ld_c, hc, Bl); });
+    const int s_cf = seg({s_in}, 1, [&] { trunk_forward(critic, critic.p, 0, xc, ld_c, hc, hcp, Bl); });
     // actor forward on s with the pre-update actor (mtsac.py:640-642)
     const int s_af = seg({s_in}, 2, [&] {
-      trunk_forward(actor, actor.p, actor.wt[0], xa, ld_a, ha, Bl);
+      trunk_forward(actor, actor.p, 0, xa, ld_a, ha, hap, Bl);
       PolicyParams q = pp;
       q.head = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
       q.eps = device_noise ? nullptr : eps_c;
@@ -506,7 +658,7 @@ struct mtsac_engine {
     });
     // a' ~ pi(.|s'), target critic, TD target (mtsac.py:525-553)
     const int s_tg = seg({s_in}, 0, [&] {
-      trunk_forward(actor, actor.p, actor.wt[0], xan, ld_a, han, Bl);
+      trunk_forward(actor, actor.p, 0, xan, ld_a, han, hanp, Bl);
       PolicyParams q = pp;
       q.head = head(actor, actor.p, han[actor.depth - 1], Bl, task);
       q.eps = device_noise ? nullptr : eps_n;
@@ -514,7 +666,7 @@ struct mtsac_engine {
       q.a_out = xcn;
       q.logpi = logpi_n;
       policy_head(q, cur);
-      trunk_forward(critic, critic.tgt, critic.wt[1], xcn, ld_c, hct, Bl);
+      trunk_forward(critic, critic.tgt, 1, xcn, ld_c, hct, hctp, Bl);
       CriticHeadParams c = ch;
       c.head = head(critic, critic.tgt, hct[critic.depth - 1], Bl, task);
       c.mode = CH_TARGET;
@@ -534,14 +686,14 @@ struct mtsac_engine {
       c.row_b = row_b;
       c.inv_norm = 1.0f / ((float)critic.E * (float)B_glob);
       critic_head(c, cur);
-      head_backward_data(chp, dq, Bl, dzc[critic.depth - 1], cur);
+      head_backward_data(chp, dq, Bl, dzc[critic.depth - 1], cur, top_planes(critic, dzcp));
       const float* ins[2] = {row_a, row_b};
       reduce_rows(ins, 2, Bl, critic.g + critic.n_flat + 1, cur);
     });
     const int s_chw = seg({s_cl}, 3, [&] {
       head_backward_weight(chp, dq, Bl, counts, rows, Bl, critic.g + critic.off_hW, critic.g + critic.off_hb, cur);
     });
-    const int s_cb = backward_segs(critic, critic.p, xc, ld_c, hc, dzc, s_cl, s_chw, Bl);
+    const int s_cb = backward_segs(critic, critic.p, xc, ld_c, hc, hcp, dzc, dzcp, s_cl, s_chw, Bl);
     // reduce over shards, clip + Adam + Polyak (mtsac.py:599-613)
     const int s_co = seg({s_cb}, 1, [&] {
       head_sq(critic);
@@ -552,7 +704,7 @@ struct mtsac_engine {
     });
     // actor loss through the UPDATED critic (mtsac.py:659-691)
     const int s_ap = seg({s_co, s_af}, 1, [&] {
-      trunk_forward(critic, critic.p, critic.wt[0], xcp, ld_c, hc, Bl);
+      trunk_forward(critic, critic.p, 0, xcp, ld_c, hc, hcp, Bl);
       CriticHeadParams c = ch;
       c.head = head(critic, critic.p, hc[critic.depth - 1], Bl, task);
       c.mode = CH_ACTOR;
@@ -562,8 +714,8 @@ struct mtsac_engine {
       c.alpha_w = alpha_w;
       c.inv_norm = 1.0f / (float)B_glob;
       critic_head(c, cur);
-      head_backward_data(c.head, dq, Bl, dzc[critic.depth - 1], cur);
-      for (int i = critic.depth - 1; i > 0; --i) dgrad_layer(critic, critic.p, hc, dzc, i, Bl);
+      head_backward_data(c.head, dq, Bl, dzc[critic.depth - 1], cur, top_planes(critic, dzcp));
+      for (int i = critic.depth - 1; i > 0; --i) dgrad_layer(critic, critic.p, hc, dzc, dzcp, i, Bl);
       ActionGradParams ag{};
       ag.dz1 = dzc[0];
       ag.W0 = critic.p + critic.off_W[0];
@@ -586,8 +738,10 @@ struct mtsac_engine {
     const int s_ahw = seg({s_ap}, 3, [&] {
       head_backward_weight(ahp, dout_a, 0, counts, rows, Bl, actor.g + actor.off_hW, actor.g + actor.off_hb, cur);
     });
-    const int s_ad = seg({s_ap}, 1, [&] { head_backward_data(ahp, dout_a, 0, dza[actor.depth - 1], cur); });
-    const int s_ab = backward_segs(actor, actor.p, xa, ld_a, ha, dza, s_ad, s_ahw, Bl);
+    const int s_ad = seg({s_ap}, 1, [&] {
+      head_backward_data(ahp, dout_a, 0, dza[actor.depth - 1], cur, top_planes(actor, dzap));
+    });
+    const int s_ab = backward_segs(actor, actor.p, xa, ld_a, ha, hap, dza, dzap, s_ad, s_ahw, Bl);
     seg({s_ab}, 1, [&] {
       // temperature gradient rides in the actor's scalar tail: [2] loss part, [3..] grad
       AlphaParams al = alpha_params();
@@ -802,16 +956,31 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     if ((rc = e->alloc(&net->sc, 1))) return bad(rc);
   }
   if ((rc = e->alloc(&e->critic.tgt, e->critic.n_flat))) return bad(rc);
-  for (Net* net : {&e->actor, &e->critic})
+  e->planes = c.precision == MTSAC_FP32_SPLIT3;
+  for (Net* net : {&e->actor, &e->critic}) {
+    net->wld = align_up(net->width, 32);
+    net->ald = align_up(net->width, 32);
+    net->arows = align_up(e->B, 32);
     for (int w = 0; w < (net == &e->critic ? 2 : 1); ++w)
-      for (int i = 1; i < net->depth; ++i)
-        if ((rc = e->alloc(&net->wt[w][i], (size_t)net->ms_W[i] * net->E))) return bad(rc);
+      for (int i = 1; i < net->depth; ++i) {
+        if (!e->planes) {
+          if ((rc = e->alloc(&net->wt[w][i], (size_t)net->ms_W[i] * net->E))) return bad(rc);
+          continue;
+        }
+        const size_t np = (size_t)net->E * 3 * net->width * net->wld;
+        if ((rc = e->alloc(&net->wp[w][i], np))) return bad(rc);
+        if ((rc = e->alloc(&net->wtp[w][i], np))) return bad(rc);
+      }
+  }
   {  // split-K workspace: the largest weight-gradient GEMM that splits
     long long ws = 0;
     for (Net* net : {&e->actor, &e->critic})
       for (int i = 0; i < net->depth; ++i) {
         const int M = i == 0 ? net->in_dim : net->width;
         ws = std::max(ws, gemm_ws_floats(M, net->width, net->E, gemm_splits(M, net->width, e->B, net->E)));
+        if (e->planes && i > 0)
+          ws = std::max(ws, gemm_ws_floats(M, net->width, net->E,
+                                           gemm_x3p_splits(M, net->width, (int)net->arows, net->E)));
       }
     if ((rc = e->alloc(&e->splitk_ws, (size_t)std::max(ws, 1LL)))) return bad(rc);
   }
@@ -846,6 +1015,19 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   for (int i = 0; i < c.critic_depth; ++i)
     for (float** p : {&e->hc[i], &e->hct[i], &e->dzc[i]})
       if ((rc = e->alloc(p, (size_t)c.num_critics * B * c.critic_width))) return bad(rc);
+  if (e->planes) {
+    for (Net* net : {&e->actor, &e->critic}) {
+      const bool cr = net == &e->critic;
+      const size_t np = (size_t)net->E * 3 * net->aps();
+      for (int i = 0; i + 1 < net->depth; ++i)
+        for (__bf16** p : {cr ? &e->hcp[i] : &e->hap[i], cr ? &e->hctp[i] : &e->hanp[i]})
+          if ((rc = e->alloc(p, np))) return bad(rc);
+      for (int i = 1; i < net->depth; ++i)
+        if ((rc = e->alloc(cr ? &e->dzcp[i] : &e->dzap[i], np))) return bad(rc);
+    }
+    const int wmax = std::max(c.actor_width, c.critic_width);
+    if ((rc = e->alloc(&e->cs_part, (size_t)std::max(1, c.num_critics) * COLSUM_CHUNKS * wmax))) return bad(rc);
+  }
   if ((rc = e->alloc(&e->dq, (size_t)c.num_critics * B))) return bad(rc);
   if ((rc = e->alloc(&e->cache, (size_t)B * 5 * e->A))) return bad(rc);
   if ((rc = e->alloc(&e->dout_a, (size_t)B * 2 * e->A))) return bad(rc);
@@ -1243,7 +1425,7 @@ static int act(mtsac_engine* h, const float* obs, int n, const float* eps, float
   gp.err = h->err;
   // obs doubles as next_obs; the action / reward / done inputs are ignored scratch
   batch_scatter(gp, h->r_obs, h->r_eps, h->r_obs, h->r_lp, h->r_lp, n, h->st);
-  h->trunk_forward(h->actor, h->actor.p, h->actor.wt[0], h->r_x, h->ld_a, h->r_h, n);
+  h->trunk_forward(h->actor, h->actor.p, -1, h->r_x, h->ld_a, h->r_h, nullptr, n);
   PolicyParams pp{};
   pp.head = h->head(h->actor, h->actor.p, h->r_h[h->actor.depth - 1], n, h->r_task);
   pp.eps = h->r_eps;

@@ -37,4 +37,98 @@ __device__ inline GemmSlice gemm_slice(const GemmParams& p) {
   return s;
 }
 
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+// Where one 32x32 accumulator tile goes: pointers already offset to the batch entry.
+struct TileOut {
+  float* C;             // fp32 output or null
+  long long ldc;
+  const float* bias;    // EPI_BIAS_RELU
+  const float* mask;    // EPI_RELU_MASK
+  long long ldm;
+  __bf16* Cp;           // split planes of the output or null
+  long long ldcp, pC;
+  int M, N;
+  bool vec;             // every row start 16-B aligned (N, ldc, ldm, ldcp multiples of 4)
+};
+
+__device__ inline void split3_dev(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)x;
+  const float r1 = x - (float)h;
+  m = (__bf16)r1;
+  l = (__bf16)(r1 - (float)m);
+}
+
+// Epilogue of one 32x32 MFMA accumulator (col = lane & 31, row = (r&3) + 8(r>>2) + 4(lane>>5))
+// at (row0, col0): restaged through a wave-private 32 x 36-float LDS scratch so every lane
+// stores 16 B of fp32 (and 8 B of each bf16 plane) -- whole 128-B row segments per 8 lanes.
+template <int EPI>
+__device__ inline void store_tile32(const f32x16_t& acc, float* scr, int lane, int row0, int col0, const TileOut& o) {
+  const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) scr[((r & 3) + 8 * (r >> 2) + 4 * lh) * 36 + lr] = acc[r];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int c4 = 4 * (lane & 7);
+  const int col = col0 + c4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int rr = (lane >> 3) + 8 * q;
+    const int row = row0 + rr;
+    if (row >= o.M) continue;
+    float4 v = *reinterpret_cast<const float4*>(scr + rr * 36 + c4);
+    float e[4] = {v.x, v.y, v.z, v.w};
+    if (o.vec && col + 3 < o.N) {
+      if (EPI == EPI_BIAS_RELU) {
+        const float4 b = *reinterpret_cast<const float4*>(o.bias + col);
+        e[0] = fmaxf(e[0] + b.x, 0.f); e[1] = fmaxf(e[1] + b.y, 0.f);
+        e[2] = fmaxf(e[2] + b.z, 0.f); e[3] = fmaxf(e[3] + b.w, 0.f);
+      }
+      if (EPI == EPI_RELU_MASK) {
+        const float4 mk = *reinterpret_cast<const float4*>(o.mask + (long long)row * o.ldm + col);
+        e[0] = mk.x > 0.f ? e[0] : 0.f; e[1] = mk.y > 0.f ? e[1] : 0.f;
+        e[2] = mk.z > 0.f ? e[2] : 0.f; e[3] = mk.w > 0.f ? e[3] : 0.f;
+      }
+      if (o.C) *reinterpret_cast<float4*>(o.C + (long long)row * o.ldc + col) = make_float4(e[0], e[1], e[2], e[3]);
+      if (o.Cp) {
+        bf16x4_t h, m, l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          __bf16 a, b, c;
+          split3_dev(e[j], a, b, c);
+          h[j] = a; m[j] = b; l[j] = c;
+        }
+        __bf16* cp = o.Cp + (long long)row * o.ldcp + col;
+        *reinterpret_cast<bf16x4_t*>(cp) = h;
+        *reinterpret_cast<bf16x4_t*>(cp + o.pC) = m;
+        *reinterpret_cast<bf16x4_t*>(cp + 2 * o.pC) = l;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cc = col + j;
+        if (cc >= o.N) continue;
+        float x = e[j];
+        if (EPI == EPI_BIAS_RELU) x = fmaxf(x + o.bias[cc], 0.f);
+        if (EPI == EPI_RELU_MASK) x = o.mask[(long long)row * o.ldm + cc] > 0.f ? x : 0.f;
+        if (o.C) o.C[(long long)row * o.ldc + cc] = x;
+        if (o.Cp) {
+          __bf16 a, b, c;
+          split3_dev(x, a, b, c);
+          __bf16* cp = o.Cp + (long long)row * o.ldcp + cc;
+          cp[0] = a;
+          cp[o.pC] = b;
+          cp[2 * o.pC] = c;
+        }
+      }
+    }
+  }
+  // the next tile's scratch writes must not pass this tile's reads (LDS is in order per wave)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 }  // namespace mtsac

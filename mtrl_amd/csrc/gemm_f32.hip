@@ -182,7 +182,7 @@ void gemm_f32(const GemmParams& p0, GemmKind kind, int epi, int batch, hipStream
   if (p0.M <= 0 || p0.N <= 0) return;
   GemmParams p = p0;
   int S = 1;
-  if (p.splits > 1 && epi == EPI_STORE && p.ws != nullptr && p.K > 0) {
+  if (p.splits > 1 && epi == EPI_STORE && p.ws != nullptr && p.K > 0 && p.Cp == nullptr) {
     const int kt = (p.K + BK - 1) / BK;
     p.kchunk = (kt + p.splits - 1) / p.splits * BK;
     S = (p.K + p.kchunk - 1) / p.kchunk;

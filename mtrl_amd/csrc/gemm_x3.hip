@@ -65,7 +65,7 @@ struct Loader {
     }
   }
 
-  __device__ static inline void store(__bf16* __restrict__ lds, const float4 (&v)[4]) {
+  __device__ static inline void store(__bf16* __restrict__ lds, const float4 (&v)[4], int dbg) {
     const int t = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -85,13 +85,18 @@ struct Loader {
         e[0] = c0[i]; e[1] = c1[i]; e[2] = c2[i]; e[3] = c3[i];
       }
       bf16x4 h, m, l;
+      if (dbg & 4) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        __bf16 a, b, c;
-        split3(e[j], a, b, c);
-        h[j] = a;
-        m[j] = b;
-        l[j] = c;
+        for (int j = 0; j < 4; ++j) h[j] = m[j] = l[j] = (__bf16)e[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          __bf16 a, b, c;
+          split3(e[j], a, b, c);
+          h[j] = a;
+          m[j] = b;
+          l[j] = c;
+        }
       }
       __bf16* p = lds + row * RS + kc;
       *reinterpret_cast<bf16x4*>(p) = h;
@@ -102,11 +107,11 @@ struct Loader {
 };
 
 template <bool TA, bool TB, int EPI>
-__global__ __launch_bounds__(NTH, 2) void gemm_x3_kernel(GemmParams p) {
+__global__ __launch_bounds__(NTH, 2) void gemm_x3_kernel(GemmParams p, int dbg) {
   // A: TA ? [K][M] : [M][K] (k contiguous);  B: TB ? [N][K] (k contiguous) : [K][N]
   using LA = Loader<!TA>;
   using LB = Loader<TB>;
-  __shared__ __bf16 smem[2 * OPER];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * OPER];
   __bf16* As = smem;
   __bf16* Bs = smem + OPER;
 
@@ -131,13 +136,13 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3_kernel(GemmParams p) {
   const int nk = (K + BK - 1) / BK;
   LA::load(A, p.lda, m0, p.M, 0, K, ra);
   LB::load(B, p.ldb, n0, p.N, 0, K, rb);
-  LA::store(As, ra);
-  LB::store(Bs, rb);
+  LA::store(As, ra, 0);
+  LB::store(Bs, rb, 0);
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = (kt + 1) < nk;
-    if (more) {
+    if (more && !(dbg & 1)) {
       LA::load(A, p.lda, m0, p.M, (kt + 1) * BK, K, ra);
       LB::load(B, p.ldb, n0, p.N, (kt + 1) * BK, K, rb);
     }
@@ -160,6 +165,13 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3_kernel(GemmParams p) {
   ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[I][0], b[J][1], ACC, 0, 0, 0);           \
   ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[I][1], b[J][0], ACC, 0, 0, 0);           \
   ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[I][0], b[J][0], ACC, 0, 0, 0);
+      if (dbg & 2) {
+        acc00[0] += (float)a[0][0][0] + (float)a[1][1][1] + (float)a[0][2][2];
+        acc01[0] += (float)b[0][0][0] + (float)b[1][1][1] + (float)b[0][2][2];
+        acc10[0] += (float)a[1][0][0] + (float)a[0][1][1] + (float)a[1][2][2];
+        acc11[0] += (float)b[1][0][0] + (float)b[0][1][1] + (float)b[1][2][2];
+        continue;
+      }
       X3_TILE(acc00, 0, 0)
       X3_TILE(acc01, 0, 1)
       X3_TILE(acc10, 1, 0)
@@ -175,8 +187,8 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3_kernel(GemmParams p) {
     }
     __syncthreads();
     if (more) {
-      LA::store(As, ra);
-      LB::store(Bs, rb);
+      LA::store(As, ra, dbg);
+      LB::store(Bs, rb, dbg);
       __syncthreads();
     }
   }
@@ -189,37 +201,36 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3_kernel(GemmParams p) {
     if (half == 0 && n0 + col < p.N) sl.db[n0 + col] = dbacc + red[col];
   }
 
-  const float* __restrict__ bias = (EPI == EPI_BIAS_RELU) ? p.bias + z * p.sBias : nullptr;
-  const float* __restrict__ mask = (EPI == EPI_RELU_MASK) ? p.mask + z * p.sMask : nullptr;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = n0 + wn + 32 * j + lr;
-    const bool colok = col < p.N;
-    const float bv = (EPI == EPI_BIAS_RELU && colok) ? bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const f32x16 acc = (i == 0) ? (j == 0 ? acc00 : acc01) : (j == 0 ? acc10 : acc11);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row < p.M && colok) {
-          float v = acc[r];
-          if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
-          if (EPI == EPI_RELU_MASK) v = (mask[(long long)row * p.ldm + col] > 0.f) ? v : 0.f;
-          C[(long long)row * sl.ldc + col] = v;
-        }
-      }
-    }
-  }
+  TileOut o{};
+  o.C = C;
+  o.ldc = sl.ldc;
+  o.bias = (EPI == EPI_BIAS_RELU) ? p.bias + z * p.sBias : nullptr;
+  o.mask = (EPI == EPI_RELU_MASK) ? p.mask + z * p.sMask : nullptr;
+  o.ldm = p.ldm;
+  o.Cp = p.Cp ? p.Cp + z * p.sCp : nullptr;
+  o.ldcp = p.ldcp;
+  o.pC = p.pC;
+  o.M = p.M;
+  o.N = p.N;
+  o.vec = (p.N % 4 == 0) && (sl.ldc % 4 == 0) && (EPI != EPI_RELU_MASK || p.ldm % 4 == 0) &&
+          (!p.Cp || p.ldcp % 4 == 0);
+  __syncthreads();  // operand tiles (and the db scratch) are dead: reuse LDS as store scratch
+  float* scr = reinterpret_cast<float*>(smem) + wave * (32 * 36);
+  store_tile32<EPI>(acc00, scr, lane, m0 + wm, n0 + wn, o);
+  store_tile32<EPI>(acc01, scr, lane, m0 + wm, n0 + wn + 32, o);
+  store_tile32<EPI>(acc10, scr, lane, m0 + wm + 32, n0 + wn, o);
+  store_tile32<EPI>(acc11, scr, lane, m0 + wm + 32, n0 + wn + 32, o);
 }
 
 }  // namespace
+
+int g_x3_dbg = 0;
 
 void gemm_x3(const GemmParams& p0, GemmKind kind, int epi, int batch, hipStream_t st) {
   if (p0.M <= 0 || p0.N <= 0) return;
   GemmParams p = p0;
   int S = 1;
-  if (p.splits > 1 && epi == EPI_STORE && p.ws != nullptr && p.K > 0) {
+  if (p.splits > 1 && epi == EPI_STORE && p.ws != nullptr && p.K > 0 && p.Cp == nullptr) {
     const int kt = (p.K + BK - 1) / BK;
     p.kchunk = (kt + p.splits - 1) / p.splits * BK;
     S = (p.K + p.kchunk - 1) / p.kchunk;
@@ -231,20 +242,20 @@ void gemm_x3(const GemmParams& p0, GemmKind kind, int epi, int batch, hipStream_
   switch (kind) {
     case GEMM_NN:
       if (epi == EPI_BIAS_RELU)
-        hipLaunchKernelGGL((gemm_x3_kernel<false, false, EPI_BIAS_RELU>), grid, block, 0, st, p);
+        hipLaunchKernelGGL((gemm_x3_kernel<false, false, EPI_BIAS_RELU>), grid, block, 0, st, p, g_x3_dbg);
       else
-        hipLaunchKernelGGL((gemm_x3_kernel<false, false, EPI_STORE>), grid, block, 0, st, p);
+        hipLaunchKernelGGL((gemm_x3_kernel<false, false, EPI_STORE>), grid, block, 0, st, p, g_x3_dbg);
       break;
     case GEMM_NT:
       if (epi == EPI_RELU_MASK)
-        hipLaunchKernelGGL((gemm_x3_kernel<false, true, EPI_RELU_MASK>), grid, block, 0, st, p);
+        hipLaunchKernelGGL((gemm_x3_kernel<false, true, EPI_RELU_MASK>), grid, block, 0, st, p, g_x3_dbg);
       else if (epi == EPI_BIAS_RELU)
-        hipLaunchKernelGGL((gemm_x3_kernel<false, true, EPI_BIAS_RELU>), grid, block, 0, st, p);
+        hipLaunchKernelGGL((gemm_x3_kernel<false, true, EPI_BIAS_RELU>), grid, block, 0, st, p, g_x3_dbg);
       else
-        hipLaunchKernelGGL((gemm_x3_kernel<false, true, EPI_STORE>), grid, block, 0, st, p);
+        hipLaunchKernelGGL((gemm_x3_kernel<false, true, EPI_STORE>), grid, block, 0, st, p, g_x3_dbg);
       break;
     case GEMM_TN:
-      hipLaunchKernelGGL((gemm_x3_kernel<true, false, EPI_STORE>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((gemm_x3_kernel<true, false, EPI_STORE>), grid, block, 0, st, p, g_x3_dbg);
       break;
   }
   if (S > 1) splitk_reduce(p, batch, S, st);

@@ -1,93 +1,160 @@
 // gemm_x3p.hip -- fp32-accurate GEMM on PRE-SPLIT bf16 planes (gfx950).
 //
-// Operands arrive as three bf16 planes each (x = x_h + x_m + x_l exactly, see gemm_x3.hip),
-// k-contiguous: A planes [3][M][lda], B planes [3][N][ldb] (C = A . B^T), K padded with
-// zeros to a multiple of 32 in both.  So the main loop has no VALU at all:
-//   * global -> LDS by LDS-DMA (global_load_lds_dwordx4, 16 B per lane), 3-stage ring,
-//     counted vmcnt + raw s_barrier (one barrier per 32-deep K-step, loads for step k+2
-//     in flight while step k computes);
-//   * LDS image [row][4 x 16 B] per plane, chunk XOR-swizzled by (row >> 2) & 3 -- done on
-//     the SOURCE address because the DMA writes lane-linearly -- so the MFMA operand
-//     reads (one ds_read_b128 per lane) are bank-conflict free;
+// Operands arrive as three bf16 planes each (x = x_h + x_m + x_l exactly, see gemm_x3.hip), so
+// the main loop has no VALU at all:
+//   C[M][N] = sum_k A(m, k) B(n, k), A given either row-major [3][M][lda] (k contiguous) or
+//   k-major [3][K][lda] (m contiguous), B likewise with N.  K is a multiple of 32; the planes
+//   of row-major operands carry zeros in k >= K up to the next multiple of 32.
+//   * global -> LDS by LDS-DMA (global_load_lds_dwordx4, 16 B per lane) into a ring of
+//     STAGES K-steps, counted vmcnt + one raw s_barrier per 32-deep K-step;
+//   * row-major image [rows][4 x 16 B] per plane, chunk XOR (row >> 2) & 3, read with one
+//     ds_read_b128 per lane; k-major image [32 k][rows] per plane, chunk XOR 4 * (k & 3),
+//     read with two ds_read_b64_tr_b16 per lane (hardware transpose).  The swizzles are
+//     applied on the SOURCE address (the DMA writes lane-linearly); both reads are
+//     bank-conflict free;
 //   * 6 x v_mfma_f32_32x32x16_bf16 per 32x32 tile and 16-deep k-slice (m*m, h*l, l*h, h*m,
-//     m*h, h*h; small terms first), fp32 accumulation.
-// Tile 128x128 per 256-thread workgroup (2x2 waves of 64x64), 144 KiB LDS, one block per CU.
-// Epilogue: fp32 C with bias+ReLU / ReLU-mask / plain, optionally also the split planes of
-// C (natural layout) for the next GEMM.
-#include "kernels.h"
+//     m*h, h*h; small terms first), fp32 accumulation;
+//   * optional split-K: slices of K write dense partial slabs, reduced in slice order.
+// Epilogue: fp32 C with bias+ReLU / ReLU-mask / plain, and optionally the split planes of C
+// (natural layout) for the next GEMM.
+#include <algorithm>
+
+#include "gemm_common.h"
 
 namespace mtsac {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef f32x16_t f32x16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
-constexpr int BK = 32;
-constexpr int ROWB = BK * 2;  // 64 B per row per plane
+constexpr int BK = 32;  // K granule of the operands (split-K slices, padding); K-steps are 16 or 32
 
-__device__ inline int swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+typedef __attribute__((address_space(3))) void lds_void;
 
-// Tile geometry: BM x BN per workgroup, WM x WN waves, each wave (BM/WM) x (BN/WN) made of
-// 32x32 MFMA tiles; STAGES-deep LDS ring of [3 planes][rows][64 B] images.
-template <int BM_, int BN_, int WM_, int WN_, int STAGES_>
-struct Geo {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, STAGES = STAGES_;
-  static constexpr int NW = WM * WN, NTH = 64 * NW;
-  static constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
-  static constexpr int PLANE_A = BM * ROWB, PLANE_B = BN * ROWB;
-  static constexpr int OPER_A = 3 * PLANE_A, OPER_B = 3 * PLANE_B;
-  static constexpr int STAGE = OPER_A + OPER_B;
-  static constexpr int LDS = STAGES * STAGE;
-  static constexpr int DMA_A = 3 * BM / 16, DMA_B = 3 * BN / 16;  // 1 KiB wave-instructions
-  static constexpr int DMA_PER_WAVE = (DMA_A + DMA_B) / NW;
-  static_assert((DMA_A + DMA_B) % NW == 0, "DMA split");
-  static_assert(LDS <= 160 * 1024, "LDS");
+__device__ inline void glds16(const void* src, char* dst) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void*)dst, 16, 0, 0);
+}
+
+// One operand's image of a K-step: R rows (M or N) x KS k, three planes.
+template <int R, bool KM, int KS>
+struct Oper {
+  static constexpr int PLANE = R * KS * 2;  // bytes per plane
+  static constexpr int BYTES = 3 * PLANE;
+  static constexpr int NJ = 3 * PLANE / 1024;  // 1-KiB wave-instructions per stage
+  static constexpr int ROWB = KM ? 2 * R : 2 * KS;
+  static constexpr int RPI = 1024 / ROWB;   // image rows per wave-instruction
+  static constexpr int LPR = ROWB / 16;     // lanes per image row
+  static constexpr int PER_PLANE = NJ / 3;
+  static_assert(!KM || LPR >= 16, "k-major swizzle needs >= 16 chunks per row");
+
+  // physical 16-B chunk of logical chunk c in image row irow (conflict-free reads, see header)
+  __device__ static inline int pchunk(int irow, int c) {
+    if (KM) return c ^ (4 * (irow & 3));
+    return KS == 32 ? (c ^ ((irow >> 2) & 3)) : (c ^ ((irow >> 3) & 1));
+  }
+
+  // issue wave-instructions first, first + stride, ... (< NJ) of the stage at k0
+  __device__ static inline void dma(const __bf16* __restrict__ base, long long ld, long long ps, int r0, int nrows,
+                                    int k0, char* lds, int first, int stride) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = first; j < NJ; j += stride) {
+      const int q = j / PER_PLANE;
+      const int ib = (j % PER_PLANE) * RPI;  // first image row of the instruction
+      const int irow = ib + lane / LPR;
+      const int c = pchunk(irow, lane % LPR);  // logical chunk this lane fetches (XOR is an involution)
+      const __bf16* src;
+      if (KM) {  // image row = k, chunk = 8 columns
+        int col = r0 + 8 * c;
+        const int last = ((nrows + 7) & ~7) - 8;
+        col = col < last ? col : last;  // columns past the edge feed discarded outputs
+        src = base + q * ps + (long long)(k0 + irow) * ld + col;
+      } else {   // image row = row, chunk = 8 k
+        int row = r0 + irow;
+        row = row < nrows ? row : nrows - 1;
+        src = base + q * ps + (long long)row * ld + k0 + 8 * c;
+      }
+      glds16(src, lds + q * PLANE + ib * ROWB);
+    }
+  }
+
+  // MFMA fragment of plane q: 8 bf16 = k 16ks + 8h .. +7 of row rb + (lane & 31)
+  __device__ static inline bf16x8 frag(const char* lds, int q, int rb, int ks, int lane) {
+    const char* pl = lds + q * PLANE;
+    if (!KM) {
+      const int r = rb + (lane & 31);
+      const int o = r * ROWB + 16 * pchunk(r, (KS / 8 == 4 ? 2 * ks : 0) + (lane >> 5));
+      return *reinterpret_cast<const bf16x8*>(pl + o);
+    } else {
+      // ds_read_b64_tr_b16: 16-lane group G reads a 4 k x 16 column block; lane 4qq+p gives the
+      // address of k-row qq, columns 4p..4p+3; lane i receives column i (= its MFMA row).
+      const int G = lane >> 4, i = lane & 15, qq = i >> 2, p = i & 3;
+      const int m = rb + 16 * (G & 1) + 4 * p;
+      const int c = m >> 3, inb = 8 * (p & 1);
+      const int k0 = 16 * ks + 8 * (G >> 1) + qq;
+      const int o0 = k0 * ROWB + 16 * pchunk(k0, c) + inb;
+      const int o1 = (k0 + 4) * ROWB + 16 * pchunk(k0 + 4, c) + inb;
+      const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(pl + o0));
+      const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(pl + o1));
+      const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      return __builtin_bit_cast(bf16x8, v);
+    }
+  }
 };
 
-// Issue the LDS-DMA loads of one operand tile (3 planes x ROWS x 32 k) into `lds`: the
-// wave-instructions j = first, first + stride, ... of the 3*ROWS/16 needed.
-template <int ROWS>
-__device__ inline void dma_tile(const __bf16* __restrict__ base, long long ld, long long plane_stride, int r0,
-                                int nrows, int k0, char* lds, int first, int stride) {
-  constexpr int NJ = 3 * ROWS / 16, PER_PLANE = ROWS / 16;
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int j = first; j < NJ; j += stride) {
-    const int q = j / PER_PLANE;              // plane
-    const int rb = (j % PER_PLANE) * 16;      // first row of this instruction
-    const int row = rb + (lane >> 2);         // physical row written by this lane
-    const int logical = swz(row, lane & 3);   // chunk to fetch so the image comes out swizzled
-    int grow = r0 + row;
-    grow = grow < nrows ? grow : nrows - 1;   // clamp: rows past the edge feed discarded outputs
-    const __bf16* src = base + q * plane_stride + (long long)grow * ld + k0 + 8 * logical;
-    char* dst = lds + q * (ROWS * ROWB) + rb * ROWB;
-    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-  }
-}
+// Tile geometry: BM x BN per workgroup, WM x WN waves, each wave (BM/WM) x (BN/WN) made of
+// 32x32 MFMA tiles; STAGES-deep LDS ring.
+template <int BM_, int BN_, int WM_, int WN_, int STAGES_, int KS_>
+struct Geo {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, STAGES = STAGES_, KS = KS_;
+  static constexpr int NW = WM * WN, NTH = 64 * NW;
+  static constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
+};
 
-template <class G>
-__device__ inline void dma_stage(const SplitGemmParams& p, const __bf16* A, const __bf16* B, int m0, int n0, int k0,
-                                 char* st, int wave) {
-  // A's and B's wave-instructions are dealt round-robin over all waves
-  dma_tile<G::BM>(A, p.lda, p.pA, m0, p.M, k0, st, wave, G::NW);
-  const int fb = (G::NW - (G::DMA_A % G::NW) + wave) % G::NW;
-  dma_tile<G::BN>(B, p.ldb, p.pB, n0, p.N, k0, st + G::OPER_A, fb, G::NW);
-}
-
-template <class G, int EPI, bool PLANES_OUT>
+template <class G, bool AKM, bool BKM, int EPI, bool PLANES_OUT>
 __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+  using OA = Oper<G::BM, AKM, G::KS>;
+  using OB = Oper<G::BN, BKM, G::KS>;
+  constexpr int STAGE = OA::BYTES + OB::BYTES;
+  // the stage's wave-instructions are dealt round robin: waves < DMA_X issue one more
+  constexpr int DMA_LO = (OA::NJ + OB::NJ) / G::NW, DMA_X = (OA::NJ + OB::NJ) % G::NW;
+  static_assert(G::STAGES * STAGE <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[G::STAGES * STAGE];
   char* lds = smem;
-  const int z = blockIdx.z;
-  const __bf16* __restrict__ A = p.A + z * p.sA;
-  const __bf16* __restrict__ B = p.B + z * p.sB;
-  const int m0 = blockIdx.x * G::BM, n0 = blockIdx.y * G::BN;
+
+  // XCD-aware tile order: the grid is 1-D; consecutive workgroups land on different XCDs
+  // (round robin), so hand each XCD a contiguous run of tiles, N-tile fastest -- the
+  // workgroups resident on one XCD then share a few A row-blocks and every B column-block
+  // through its L2.
+  const int ny = (p.N + G::BN - 1) / G::BN, nx = (p.M + G::BM - 1) / G::BM;
+  int tile = blockIdx.x;
+  if (!(p.dbg & 4)) {
+    const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = tile % 8;
+    tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + tile / 8;
+  }
+  const int by = tile % ny, bx = (tile / ny) % nx;
+  const int S = p.splits > 1 ? p.splits : 1;
+  const int zz = tile / (ny * nx), z = zz / S, sp = zz - z * S;
+  const int kbeg = sp * p.kchunk;
+  const int Kl = S > 1 ? min(p.kchunk, p.K - kbeg) : p.K;
+  const __bf16* __restrict__ A = p.A + z * p.sA + (AKM ? (long long)kbeg * p.lda : (long long)kbeg);
+  const __bf16* __restrict__ B = p.B + z * p.sB + (BKM ? (long long)kbeg * p.ldb : (long long)kbeg);
+  const int m0 = bx * G::BM, n0 = by * G::BN;
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = (wave % G::WM) * (G::BM / G::WM), wn = (wave / G::WM) * (G::BN / G::WN);
   const int lr = lane & 31, lh = lane >> 5;
-  const int nk = p.K / BK;  // K is padded to a multiple of BK
+  const int nk = Kl / G::KS;
+  const int fb = (G::NW - (OA::NJ % G::NW) + wave) % G::NW;  // B's instructions continue the round robin
+
+  auto stage = [&](int s, int k0) {
+    char* st = lds + s * STAGE;
+    OA::dma(A, p.lda, p.pA, m0, p.M, k0, st, wave, G::NW);
+    OB::dma(B, p.ldb, p.pB, n0, p.N, k0, st + OA::BYTES, fb, G::NW);
+  };
 
   f32x16 acc[G::TI][G::TJ];
 #pragma unroll
@@ -95,46 +162,43 @@ __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) 
 #pragma unroll
     for (int j = 0; j < G::TJ; ++j) acc[i][j] = f32x16{0};
 
-  // prologue: the first STAGES-1 stages in flight
 #pragma unroll
   for (int s = 0; s < G::STAGES - 1; ++s)
-    if (s < nk) dma_stage<G>(p, A, B, m0, n0, s * BK, lds + s * G::STAGE, wave);
+    if (s < nk) stage(s, s * G::KS);
 
   for (int kt = 0; kt < nk; ++kt) {
     // retire stage kt (younger stages may stay in flight), then one barrier: every wave's
     // stage-kt data has landed and every wave is done reading the buffer about to be refilled
     const int younger = min(G::STAGES - 2, nk - 1 - kt);
-    if (younger >= 2)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G::DMA_PER_WAVE) : "memory");
-    else if (younger == 1)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::DMA_PER_WAVE) : "memory");
-    else
+    const bool more = DMA_X != 0 && wave < DMA_X;
+    if (younger >= 3) {
+      if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DMA_LO + 1)) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * DMA_LO) : "memory");
+    } else if (younger == 2) {
+      if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (DMA_LO + 1)) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DMA_LO) : "memory");
+    } else if (younger == 1) {
+      if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_LO + 1) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_LO) : "memory");
+    } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (kt + G::STAGES - 1 < nk && !(p.dbg & 1))
-      dma_stage<G>(p, A, B, m0, n0, (kt + G::STAGES - 1) * BK, lds + ((kt + G::STAGES - 1) % G::STAGES) * G::STAGE,
-                   wave);
-    const char* cur = lds + (kt % G::STAGES) * G::STAGE;
+      stage((kt + G::STAGES - 1) % G::STAGES, (kt + G::STAGES - 1) * G::KS);
+    const char* cur = lds + (kt % G::STAGES) * STAGE;
 #pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      const int chunk = 2 * ks + lh;
+    for (int ks = 0; ks < G::KS / 16; ++ks) {
       bf16x8 a[G::TI][3], b[G::TJ][3];
 #pragma unroll
-      for (int i = 0; i < G::TI; ++i) {
-        const int r = wm + 32 * i + lr;
-        const int o = r * ROWB + 16 * swz(r, chunk);
+      for (int i = 0; i < G::TI; ++i)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) a[i][q] = *reinterpret_cast<const bf16x8*>(cur + q * G::PLANE_A + o);
-      }
+        for (int q = 0; q < 3; ++q) a[i][q] = OA::frag(cur, q, wm + 32 * i, ks, lane);
 #pragma unroll
-      for (int j = 0; j < G::TJ; ++j) {
-        const int r = wn + 32 * j + lr;
-        const int o = r * ROWB + 16 * swz(r, chunk);
+      for (int j = 0; j < G::TJ; ++j)
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-          b[j][q] = *reinterpret_cast<const bf16x8*>(cur + G::OPER_A + q * G::PLANE_B + o);
-      }
+        for (int q = 0; q < 3; ++q) b[j][q] = OB::frag(cur + OA::BYTES, q, wn + 32 * j, ks, lane);
       if (p.dbg & 2) {
 #pragma unroll
         for (int i = 0; i < G::TI; ++i)
@@ -158,41 +222,36 @@ __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) 
     }
   }
 
-  float* __restrict__ C = p.C ? p.C + z * p.sC : nullptr;
-  const float* __restrict__ bias = (EPI == EPI_BIAS_RELU) ? p.bias + z * p.sBias : nullptr;
-  const float* __restrict__ mask = (EPI == EPI_RELU_MASK) ? p.mask + z * p.sMask : nullptr;
-#pragma unroll
-  for (int j = 0; j < G::TJ; ++j) {
-    const int col = n0 + wn + 32 * j + lr;
-    const bool colok = col < p.N;
-    const float bv = (EPI == EPI_BIAS_RELU && colok) ? bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < G::TI; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row < p.M && colok) {
-          float v = acc[i][j][r];
-          if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
-          if (EPI == EPI_RELU_MASK) v = (mask[(long long)row * p.ldm + col] > 0.f) ? v : 0.f;
-          if (C) C[(long long)row * p.ldc + col] = v;
-          if (PLANES_OUT) {
-            __bf16* cp = p.Cp + z * p.sCp + (long long)row * p.ldcp + col;
-            const __bf16 h = (__bf16)v;
-            const float r1 = v - (float)h;
-            const __bf16 m = (__bf16)r1;
-            cp[0] = h;
-            cp[p.pC] = m;
-            cp[2 * p.pC] = (__bf16)(r1 - (float)m);
-          }
-        }
-      }
-    }
+  TileOut o{};
+  if (S > 1) {
+    o.C = p.ws + (long long)zz * p.M * p.N;
+    o.ldc = p.N;
+  } else {
+    o.C = p.C ? p.C + z * p.sC : nullptr;
+    o.ldc = p.ldc;
   }
+  o.bias = (EPI == EPI_BIAS_RELU) ? p.bias + z * p.sBias : nullptr;
+  o.mask = (EPI == EPI_RELU_MASK) ? p.mask + z * p.sMask : nullptr;
+  o.ldm = p.ldm;
+  o.Cp = PLANES_OUT ? p.Cp + z * p.sCp : nullptr;
+  o.ldcp = p.ldcp;
+  o.pC = p.pC;
+  o.M = p.M;
+  o.N = p.N;
+  o.vec = (p.N % 4 == 0) && (o.ldc % 4 == 0) && (EPI != EPI_RELU_MASK || p.ldm % 4 == 0) &&
+          (!PLANES_OUT || p.ldcp % 4 == 0);
+  __builtin_amdgcn_s_barrier();  // every wave is done with the ring: reuse it as scratch
+  float* scr = reinterpret_cast<float*>(smem) + wave * (32 * 36);
+#pragma unroll
+  for (int i = 0; i < G::TI; ++i)
+#pragma unroll
+    for (int j = 0; j < G::TJ; ++j) store_tile32<EPI>(acc[i][j], scr, lane, m0 + wm + 32 * i, n0 + wn + 32 * j, o);
 }
 
-using GeoSmall = Geo<128, 128, 2, 2, 3>;  // 4 waves, 144 KiB
-using GeoWide = Geo<256, 128, 4, 2, 2>;   // 8 waves, 144 KiB
+using GeoSmall = Geo<128, 128, 2, 2, 3, 32>;   // 4 waves, 3 x 48 KiB
+using GeoWide = Geo<256, 128, 4, 2, 2, 32>;    // 8 waves, 2 x 72 KiB
+using GeoWide16 = Geo<256, 128, 4, 2, 4, 16>;  // 8 waves, 4 x 36 KiB
+using GeoBig16 = Geo<256, 256, 2, 4, 3, 16>;   // 8 waves of 128 x 64, 3 x 48 KiB
 
 // fp32 [rows][ld] -> planes.  TRANS: out[q][col][row] (k = row contiguous), else out[q][row][col].
 // 64x64 tiles staged through LDS so both the fp32 reads and the bf16 writes are coalesced.
@@ -235,17 +294,25 @@ __global__ __launch_bounds__(256) void split_kernel(SplitParams s) {
   }
 }
 
-// db[z][n] = sum over rows of x[z][rows][n] in two deterministic passes
+// db[z][n] = sum over rows of x[z][rows][n] in two deterministic passes (COLSUM_CHUNKS row
+// chunks per column, then the chunks in order)
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ x, int rows, int cols, int ld,
                                                              long long sx, int chunks, float* __restrict__ part) {
   const int z = blockIdx.z, c = blockIdx.x * 256 + threadIdx.x, ch = blockIdx.y;
   if (c >= cols) return;
   const int per = (rows + chunks - 1) / chunks;
   const int r0 = ch * per, r1 = min(rows, r0 + per);
-  const float* xp = x + z * sx;
-  float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += xp[(long long)r * ld + c];
-  part[((long long)z * chunks + ch) * cols + c] = s;
+  const float* xp = x + z * sx + c;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int r = r0;
+  for (; r + 4 <= r1; r += 4) {
+    s0 += xp[(long long)r * ld];
+    s1 += xp[(long long)(r + 1) * ld];
+    s2 += xp[(long long)(r + 2) * ld];
+    s3 += xp[(long long)(r + 3) * ld];
+  }
+  for (; r < r1; ++r) s0 += xp[(long long)r * ld];
+  part[((long long)z * chunks + ch) * cols + c] = (s0 + s1) + (s2 + s3);
 }
 
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int cols, int chunks,
@@ -259,33 +326,79 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
 
 }  // namespace
 
-template <class G>
-static void launch_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st) {
-  dim3 grid((p.M + G::BM - 1) / G::BM, (p.N + G::BN - 1) / G::BN, batch);
+template <class G, bool AKM, bool BKM>
+static void launch_x3p(const SplitGemmParams& p, int epi, dim3 grid, hipStream_t st) {
   const bool planes = p.Cp != nullptr;
+  const dim3 block(G::NTH);
   if (epi == EPI_BIAS_RELU) {
-    if (planes) hipLaunchKernelGGL((gemm_x3p_kernel<G, EPI_BIAS_RELU, true>), grid, dim3(G::NTH), 0, st, p);
-    else hipLaunchKernelGGL((gemm_x3p_kernel<G, EPI_BIAS_RELU, false>), grid, dim3(G::NTH), 0, st, p);
+    if (planes) hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_BIAS_RELU, true>), grid, block, 0, st, p);
+    else hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_BIAS_RELU, false>), grid, block, 0, st, p);
   } else if (epi == EPI_RELU_MASK) {
-    if (planes) hipLaunchKernelGGL((gemm_x3p_kernel<G, EPI_RELU_MASK, true>), grid, dim3(G::NTH), 0, st, p);
-    else hipLaunchKernelGGL((gemm_x3p_kernel<G, EPI_RELU_MASK, false>), grid, dim3(G::NTH), 0, st, p);
+    if (planes) hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_RELU_MASK, true>), grid, block, 0, st, p);
+    else hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_RELU_MASK, false>), grid, block, 0, st, p);
   } else {
-    if (planes) hipLaunchKernelGGL((gemm_x3p_kernel<G, EPI_STORE, true>), grid, dim3(G::NTH), 0, st, p);
-    else hipLaunchKernelGGL((gemm_x3p_kernel<G, EPI_STORE, false>), grid, dim3(G::NTH), 0, st, p);
+    if (planes) hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_STORE, true>), grid, block, 0, st, p);
+    else hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_STORE, false>), grid, block, 0, st, p);
   }
 }
 
-int g_x3p_geo = 1;
-int g_x3p_dbg = 0;  // 0: 128x128 / 4 waves, 1: 256x128 / 8 waves
-
-void gemm_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st) {
-  if (p.M <= 0 || p.N <= 0 || p.K <= 0) return;
-  SplitGemmParams q = p;
-  q.dbg |= g_x3p_dbg;
-  if (g_x3p_geo == 0)
-    launch_x3p<GeoSmall>(q, epi, batch, st);
+template <class G>
+static void launch_geo(const SplitGemmParams& p, int epi, int batch, hipStream_t st) {
+  dim3 grid(((p.M + G::BM - 1) / G::BM) * ((p.N + G::BN - 1) / G::BN) * batch * (p.splits > 1 ? p.splits : 1));
+  if (!p.a_kmajor && !p.b_kmajor)
+    launch_x3p<G, false, false>(p, epi, grid, st);
+  else if (p.a_kmajor && p.b_kmajor)
+    launch_x3p<G, true, true>(p, epi, grid, st);
+  else if (p.a_kmajor)
+    launch_x3p<G, true, false>(p, epi, grid, st);
   else
-    launch_x3p<GeoWide>(q, epi, batch, st);
+    launch_x3p<G, false, true>(p, epi, grid, st);
+}
+
+int g_x3p_geo = -1;  // -1: by operand form; 0: 128x128 k32, 1: 256x128 k32, 2: 256x128 k16, 3: 256x256 k16
+int g_x3p_dbg = 0;
+
+int gemm_x3p_splits(int M, int N, int K, int batch) {
+  const long long tiles = (long long)((M + 255) / 256) * ((N + 127) / 128) * batch;
+  if (tiles >= 256) return 1;
+  int s = (int)((256 + tiles - 1) / tiles);
+  s = std::min(s, 16);
+  s = std::min(s, std::max(1, K / BK / 4));
+  return std::max(s, 1);
+}
+
+void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
+  if (p0.M <= 0 || p0.N <= 0 || p0.K <= 0) return;
+  SplitGemmParams p = p0;
+  p.dbg |= g_x3p_dbg;
+  int S = 1;
+  if (p.splits > 1 && epi == EPI_STORE && p.ws != nullptr && !p.Cp) {
+    const int kt = p.K / BK;
+    p.kchunk = (kt + p.splits - 1) / p.splits * BK;
+    S = (p.K + p.kchunk - 1) / p.kchunk;
+  }
+  p.splits = S;
+  if (S == 1) p.kchunk = p.K;
+  // default: 256x256 tiles (least operand traffic per MFMA) for the NT forms, 256x128 for the
+  // k-major weight-gradient form (2048^2 outputs: 256 tiles per member, split-K below that)
+  int geo = g_x3p_geo;
+  if (geo < 0) geo = (p.a_kmajor && p.b_kmajor) ? 1 : 3;
+  switch (geo) {
+    case 0: launch_geo<GeoSmall>(p, epi, batch, st); break;
+    case 2: launch_geo<GeoWide16>(p, epi, batch, st); break;
+    case 3: launch_geo<GeoBig16>(p, epi, batch, st); break;
+    default: launch_geo<GeoWide>(p, epi, batch, st); break;
+  }
+  if (S > 1) {
+    GemmParams r{};
+    r.M = p.M;
+    r.N = p.N;
+    r.C = p.C;
+    r.ldc = p.ldc;
+    r.sC = p.sC;
+    r.ws = p.ws;
+    splitk_reduce(r, batch, S, st);
+  }
 }
 
 void split_planes(const SplitParams& s, bool transpose, int batch, hipStream_t st) {
@@ -298,7 +411,7 @@ void split_planes(const SplitParams& s, bool transpose, int batch, hipStream_t s
 
 void colsum(const float* x, int rows, int cols, int ld, long long sx, int batch, float* part, float* db,
             long long sdb, hipStream_t st) {
-  const int chunks = 16;
+  const int chunks = std::max(1, std::min(COLSUM_CHUNKS, rows));
   hipLaunchKernelGGL(colsum_partial_kernel, dim3((cols + 255) / 256, chunks, batch), dim3(256), 0, st, x, rows, cols,
                      ld, sx, chunks, part);
   hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256, 1, batch), dim3(256), 0, st, part, cols, chunks, db,

@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
 // ------------------------------------------------------------------ head backward (data)
 template <int HD>
 __global__ __launch_bounds__(256) void head_bwd_data_kernel(HeadParams hp, const float* __restrict__ dout,
-                                                            long long s_dout, float* __restrict__ dz) {
+                                                            long long s_dout, float* __restrict__ dz, PlaneOut po) {
   const int W4 = hp.W >> 2;
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long per = (long long)hp.B * W4;
@@ -190,6 +190,24 @@ __global__ __launch_bounds__(256) void head_bwd_data_kernel(HeadParams hp, const
   out.z = h.z > 0.f ? g[2] : 0.f;
   out.w = h.w > 0.f ? g[3] : 0.f;
   *reinterpret_cast<float4*>(dz + off) = out;
+  if (po.p) {  // the bf16 split planes the next GEMMs read
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    const float v[4] = {out.x, out.y, out.z, out.w};
+    bf16x4 ph, pm, pl;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const __bf16 hh = (__bf16)v[k];
+      const float r1 = v[k] - (float)hh;
+      const __bf16 mm = (__bf16)r1;
+      ph[k] = hh;
+      pm[k] = mm;
+      pl[k] = (__bf16)(r1 - (float)mm);
+    }
+    __bf16* q = po.p + e * po.sm + (long long)b * po.ld + w;
+    *reinterpret_cast<bf16x4*>(q) = ph;
+    *reinterpret_cast<bf16x4*>(q + po.ps) = pm;
+    *reinterpret_cast<bf16x4*>(q + 2 * po.ps) = pl;
+  }
 }
 
 // ------------------------------------------------------------------ head backward (weights)
@@ -228,11 +246,23 @@ __global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, con
 #pragma unroll
     for (int o = 0; o < HD; ++o) out[o] = red[0][wl][o] + red[1][wl][o] + red[2][wl][o] + red[3][wl][o];
   }
-  if (blockIdx.y == 0 && threadIdx.x < HD) {
-    const int o = threadIdx.x;
-    float s = 0.f;
-    for (int j = 0; j < n; ++j) s += d[(long long)rl[j] * HD + o];
-    dbh[e * hp.sbh + t * HD + o] = s;
+  if (blockIdx.y == 0) {  // bias grad: 256 strided partial sums, then a fixed-order tree
+    __syncthreads();
+    float* part = &red[0][0][0];  // 256 * HD floats
+#pragma unroll
+    for (int o = 0; o < HD; ++o) {
+      float s = 0.f;
+      for (int j = threadIdx.x; j < n; j += 256) s += d[(long long)rl[j] * HD + o];
+      part[o * 256 + threadIdx.x] = s;
+    }
+    __syncthreads();
+    for (int half = 128; half > 0; half >>= 1) {
+      if (threadIdx.x < half)
+#pragma unroll
+        for (int o = 0; o < HD; ++o) part[o * 256 + threadIdx.x] += part[o * 256 + threadIdx.x + half];
+      __syncthreads();
+    }
+    if (threadIdx.x < HD) dbh[e * hp.sbh + t * HD + threadIdx.x] = part[threadIdx.x * 256];
   }
 }
 
@@ -309,15 +339,16 @@ void critic_head(const CriticHeadParams& p, hipStream_t st) {
   hipLaunchKernelGGL(critic_head_kernel, dim3((p.head.B + 3) / 4), dim3(256), 0, st, p);
 }
 
-void head_backward_data(const HeadParams& hp, const float* dout, long long s_dout, float* dz, hipStream_t st) {
+void head_backward_data(const HeadParams& hp, const float* dout, long long s_dout, float* dz, hipStream_t st,
+                        PlaneOut po) {
   const long long n = (long long)hp.E * hp.B * (hp.W / 4);
   dim3 grid((unsigned)((n + 255) / 256));
   switch (hp.hd) {
-    case 1: hipLaunchKernelGGL(head_bwd_data_kernel<1>, grid, dim3(256), 0, st, hp, dout, s_dout, dz); break;
-    case 2: hipLaunchKernelGGL(head_bwd_data_kernel<2>, grid, dim3(256), 0, st, hp, dout, s_dout, dz); break;
-    case 4: hipLaunchKernelGGL(head_bwd_data_kernel<4>, grid, dim3(256), 0, st, hp, dout, s_dout, dz); break;
-    case 6: hipLaunchKernelGGL(head_bwd_data_kernel<6>, grid, dim3(256), 0, st, hp, dout, s_dout, dz); break;
-    default: hipLaunchKernelGGL(head_bwd_data_kernel<8>, grid, dim3(256), 0, st, hp, dout, s_dout, dz); break;
+    case 1: hipLaunchKernelGGL(head_bwd_data_kernel<1>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po); break;
+    case 2: hipLaunchKernelGGL(head_bwd_data_kernel<2>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po); break;
+    case 4: hipLaunchKernelGGL(head_bwd_data_kernel<4>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po); break;
+    case 6: hipLaunchKernelGGL(head_bwd_data_kernel<6>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po); break;
+    default: hipLaunchKernelGGL(head_bwd_data_kernel<8>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po); break;
   }
 }
 

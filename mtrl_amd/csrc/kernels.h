@@ -30,6 +30,9 @@ struct GemmParams {
   int splits;
   int kchunk;                               // set by the launcher
   float* ws;
+  // gemm_x3 only: also write the bf16 split planes of C ([3][M][ldcp] per batch entry)
+  __bf16* Cp;
+  long long ldcp, pC, sCp;
 };
 
 enum GemmKind { GEMM_NN = 0, GEMM_NT = 1, GEMM_TN = 2 };
@@ -46,13 +49,15 @@ void gemm_f32(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_
 void gemm_x3(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_t st);
 
 // ------------------------------------------------------------------ pre-split plane GEMM
-// C[z] = A[z] . B[z]^T with A planes [3][M][lda], B planes [3][N][ldb] (bf16, k contiguous,
-// K a multiple of 32 with zero padding) -- gemm_x3p.hip.
+// C[z][m][n] = sum_k A(m,k) B(n,k) on bf16 planes (gemm_x3p.hip).  A planes [3][M][lda]
+// (k contiguous) or, with a_kmajor, [3][K][lda] (m contiguous); B likewise with N.  K is a
+// multiple of 32 (row-major planes zero-padded to it); lda/ldb multiples of 8.
 struct SplitGemmParams {
   const __bf16* A;
   long long lda, pA, sA;  // row stride, plane stride, batch stride (elements)
   const __bf16* B;
   long long ldb, pB, sB;
+  int a_kmajor, b_kmajor;
   float* C;               // fp32 output (may be null when only planes are wanted)
   int ldc;
   long long sC;
@@ -64,11 +69,15 @@ struct SplitGemmParams {
   __bf16* Cp;             // optional split planes of C: [3][M][ldcp]
   long long ldcp, pC, sCp;
   int M, N, K;
+  int splits, kchunk;     // split-K (EPI_STORE, no Cp): partial slabs in ws (gemm_ws_floats)
+  float* ws;
   int dbg;                // experiments only: bit0 skip steady-state loads, bit1 skip MFMA
 };
 void gemm_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
-extern int g_x3p_geo;
-extern int g_x3p_dbg;  // tile geometry of gemm_x3p (0: 128x128/4 waves, 1: 256x128/8 waves)
+int gemm_x3p_splits(int M, int N, int K, int batch);
+extern int g_x3p_geo;  // tile geometry of gemm_x3p (-1: by operand form, 0..3: forced; see gemm_x3p.hip)
+extern int g_x3p_dbg;  // experiment bits OR-ed into SplitGemmParams::dbg
+extern int g_x3_dbg;   // experiments on gemm_x3: bit0 skip loads after the first tile, bit1 skip MFMA, bit2 skip split
 
 // fp32 x[z][rows][ldx] -> bf16 planes out[z][3][out_rows][ldo] (plane stride po); TRANSPOSE
 // writes out[q][col][row].  Elements past rows/cols inside [out_rows, out_cols) become 0.
@@ -81,7 +90,8 @@ struct SplitParams {
   int out_rows, out_cols;
 };
 void split_planes(const SplitParams& s, bool transpose, int batch, hipStream_t st);
-// db[z][c] = sum_r x[z][r][c] (deterministic two-pass; part holds batch*16*cols floats)
+// db[z][c] = sum_r x[z][r][c] (deterministic two-pass; part holds batch*COLSUM_CHUNKS*cols floats)
+constexpr int COLSUM_CHUNKS = 64;
 void colsum(const float* x, int rows, int cols, int ld, long long sx, int batch, float* part, float* db,
             long long sdb, hipStream_t st);
 
@@ -175,9 +185,14 @@ struct CriticHeadParams {
 };
 void critic_head(const CriticHeadParams& p, hipStream_t st);
 
-// dz[e][b][w] = (sum_o dout[e][b][o] * Wh[e][t_b][w][o]) * (h[e][b][w] > 0)
-void head_backward_data(const HeadParams& hp, const float* dout, long long s_dout, float* dz,
-                        hipStream_t st);
+// optional bf16 split planes of an output: [E][3][rows][ld], plane stride ps, member stride sm
+struct PlaneOut {
+  __bf16* p;
+  long long ld, ps, sm;
+};
+// dz[e][b][w] = (sum_o dout[e][b][o] * Wh[e][t_b][w][o]) * (h[e][b][w] > 0)  (+ its planes)
+void head_backward_data(const HeadParams& hp, const float* dout, long long s_dout, float* dz, hipStream_t st,
+                        PlaneOut po = PlaneOut{});
 // dWh[e][t][w][o] = sum_{b in t} h[e][b][w] dout[e][b][o];  dbh[e][t][o] = sum dout
 void head_backward_weight(const HeadParams& hp, const float* dout, long long s_dout, const int* counts,
                           const int* rows, int max_rows, float* dWh, float* dbh, hipStream_t st);
