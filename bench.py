@@ -42,8 +42,41 @@ FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense p
 BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
 PRECISIONS = {"fp32": 0, "split3": 1}
 HBM_PEAK_GBS = 8000.0
-GEMM_FAMILIES = {0: "gemm_f32_kernel<NN> (trunk forward)", 1: "gemm_f32_kernel<NT> (data grad)",
-                 2: "gemm_f32_kernel<TN> (weight grad)"}
+# enum mtsac_gemm_family (include/mtsac.h) -> the rocprof kernel(s) of that family, per precision
+GEMM_FAMILIES = {
+    "split3": {
+        0: "gemm_x3p_kernel<Geo<256, 256, 2, 4, 3, 16>, false, false, 1, *> (hidden-layer forward, NT on planes, bias+ReLU)",
+        1: "gemm_x3p_kernel<Geo<256, 256, 2, 4, 3, 16>, false, false, 2, *> (hidden-layer data grad, NT on planes, ReLU mask)",
+        2: "gemm_x3p_kernel<Geo<256, 256, 2, 4, 3, 16>, true, true, 0, false> (hidden-layer weight grad, k-major planes, split-K)",
+        3: "gemm_x3_kernel<false, false, 1> (input-layer forward, on-the-fly split)",
+        4: "gemm_x3_kernel<true, false, 0> (input-layer weight grad, split-K)",
+    },
+    "fp32": {
+        0: "gemm_f32_kernel<false, true, 1> (hidden-layer forward, NT vs transposed kernel)",
+        1: "gemm_f32_kernel<false, true, 2> (hidden-layer data grad)",
+        2: "gemm_f32_kernel<true, false, 0> (hidden-layer weight grad)",
+        3: "gemm_f32_kernel<false, false, 1> (input-layer forward)",
+        4: "gemm_f32_kernel<true, false, 0> (input-layer weight grad, split-K)",
+    },
+}
+METRIC = "SAC gradient-steps/sec, MT50 width-2048 batch=128/task, 1/2/4/8 MI355X"
+
+
+def pmc_traffic(precision, family):
+    """HBM bytes per launch of a GEMM family from the committed rocprofv3 PMC summary
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py), or None."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            v = d.get(precision, {}).get(str(family))
+            if v is not None:
+                return v["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+        except (OSError, ValueError, KeyError):
+            continue
+    return None, None
 
 
 def algorithmic_flops(T, W, n=128, A=4):
@@ -149,6 +182,11 @@ def main():
         eng.enable_graph(mode == "graph")
         eng.update_many(1)
         eng.synchronize()
+    # Eager issue: HIP events around every GEMM launch on the stream it runs on, live over the
+    # timed steps (the step keeps its concurrent streams).  A graph replay cannot carry events:
+    # then the kernel timing comes from one extra eager step after the timed region.
+    live = mode == "eager"
+    eng.set_timing(live)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(local_rank)
@@ -167,17 +205,27 @@ def main():
     logs = eng.logs()
     assert all(math.isfinite(v) for v in logs.values()), logs
 
-    # dominant-kernel roofline: HIP events around every GEMM launch of one captured step
-    eng.set_timing(True)
+    # dominant-kernel roofline from the per-launch HIP events
+    if not live:
+        eng.set_timing(True)
+        eng.update_many(1)
+        eng.synchronize()
+    names = GEMM_FAMILIES[args.precision]
+    fam = {f: eng.timing(f) for f in names}
+    # the same kernels solo: one extra step serialised on one stream (context for the roofline
+    # fraction: under the step's concurrency a launch shares the CUs with its neighbours)
+    eng.set_timing(True, serial=True)
     eng.update_many(1)
     eng.synchronize()
-    fam = {f: eng.timing(f) for f in GEMM_FAMILIES}
+    solo = {f: eng.timing(f) for f in names}
     eng.set_timing(False)
+    timed_steps = args.steps if live else 1
     dom = max(fam, key=lambda f: fam[f][0])
     ms, nl, fl = fam[dom]
-    gemm_ms = sum(v[0] for v in fam.values())
-    gemm_fl = sum(v[2] for v in fam.values())
+    gemm_ms = sum(v[0] for v in fam.values()) / timed_steps
+    gemm_fl = sum(v[2] for v in fam.values()) / timed_steps
     achieved = (fl / nl) / (ms / nl * 1e-3) / 1e12 if nl else 0.0
+    traffic, traffic_src = pmc_traffic(args.precision, dom)
     if args.precision == "split3":  # 6 bf16 MFMA products per fp32 multiply-add
         peak, basis = BF16_MFMA_PEAK_TF / 6.0, "bf16 dense MFMA peak / 6 products (fp32-accurate split)"
     else:
@@ -186,7 +234,7 @@ def main():
     flops = algorithmic_flops(T, W)
     sps = args.steps / elapsed
     out = {
-        "metric": "SAC gradient-steps/sec, MT50 width-2048 batch=128/task",
+        "metric": METRIC,
         "value": sps,
         "unit": "SAC gradient-steps/sec",
         "n_gpus": world,
@@ -201,16 +249,25 @@ def main():
         "config": {"workload": desc, "num_tasks": T, "width": W, "batch_per_task": 128, "global_batch": 128 * T,
                    "parallelism": f"task-shard{world}" if world > 1 else "single", "exec": mode,
                    "precision": args.precision},
-        "roofline": {"bound": "mfma", "kernel": GEMM_FAMILIES[dom], "achieved": achieved,
+        "roofline": {"bound": "mfma", "kernel": names[dom], "achieved": achieved,
                      "peak": peak, "peak_basis": basis, "unit": "TFLOP/s", "frac": achieved / peak,
-                     "traffic": None, "launches": nl, "avg_launch_us": 1e3 * ms / max(nl, 1),
-                     "algorithmic_flops_per_launch": fl / max(nl, 1)},
+                     "traffic": traffic, "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, gfx950-corrected)",
+                     "traffic_source": traffic_src, "launches": nl, "avg_launch_us": 1e3 * ms / max(nl, 1),
+                     "algorithmic_flops_per_launch": fl / max(nl, 1),
+                     "timing": "HIP events per launch over the timed steps (concurrent streams)" if live
+                     else "HIP events per launch, one eager step after the timed graph replays",
+                     "solo": {"achieved": (solo[dom][2] / max(solo[dom][1], 1)) / (solo[dom][0] / max(solo[dom][1], 1) * 1e-3) / 1e12
+                              if solo[dom][0] else None,
+                              "avg_launch_us": 1e3 * solo[dom][0] / max(solo[dom][1], 1),
+                              "frac": ((solo[dom][2] / (solo[dom][0] * 1e-3) / 1e12) / peak) if solo[dom][0] else None,
+                              "timing": "one extra step with every kernel serialised on one stream"}},
         "step_flops": flops,
         "step_tflops_per_s": flops * sps / world / 1e12,
-        "gemm_share_of_step": gemm_ms / (1e3 * elapsed / args.steps),
+        "gemm_kernel_ms_per_step": gemm_ms,  # sum of GEMM launch durations (they overlap across streams)
         "gemm_tflops_per_s": gemm_fl / (gemm_ms * 1e-3) / 1e12 if gemm_ms else 0.0,
-        "gemm_families": {GEMM_FAMILIES[f]: {"ms_per_step": v[0], "launches": v[1],
-                                             "tflops": v[2] / (v[0] * 1e-3) / 1e12 if v[0] else 0.0}
+        "gemm_families": {names[f]: {"ms_per_step": v[0] / timed_steps, "launches_per_step": v[1] / timed_steps,
+                                     "avg_launch_us": 1e3 * v[0] / max(v[1], 1),
+                                     "tflops": v[2] / (v[0] * 1e-3) / 1e12 if v[0] else 0.0}
                           for f, v in fam.items()},
         "logs": logs,
     }

@@ -186,7 +186,19 @@ int mtsac_set_allreduce_hook(mtsac_engine* h, mtsac_allreduce_fn fn, void* user)
 /* plain device/host copy helper for hooks written in a host language (hipMemcpyDefault) */
 int mtsac_memcpy(void* dst, const void* src, int64_t bytes);
 
-/* measurement: per-kernel-family HIP event timing of the last update_many call */
+/* measurement: per-kernel-family HIP event timing (events on each launch's own stream) over all
+ * steps of the last update / update_many call.  enable: 0 off, 1 on (the step keeps its
+ * concurrent streams; forces eager issue), 2 on with every kernel serialised on one stream (solo
+ * kernel durations).  Families (enum mtsac_gemm_family):
+ * hidden-layer forward, hidden-layer data grad, hidden-layer weight grad, input-layer forward,
+ * input-layer weight grad. */
+enum mtsac_gemm_family {
+  MTSAC_FAM_FORWARD = 0,
+  MTSAC_FAM_DATA_GRAD = 1,
+  MTSAC_FAM_WEIGHT_GRAD = 2,
+  MTSAC_FAM_INPUT_FORWARD = 3,
+  MTSAC_FAM_INPUT_WEIGHT_GRAD = 4
+};
 int mtsac_set_timing(mtsac_engine* h, int32_t enable);
 int mtsac_get_timing(mtsac_engine* h, int32_t family, double* total_ms, int32_t* launches,
                      double* flops);

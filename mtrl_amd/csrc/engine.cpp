@@ -168,6 +168,7 @@ struct mtsac_engine {
   std::string comm_error;
   // timing
   bool timing = false;
+  bool timing_serial = false;  // timing with every segment on the main stream (solo kernels)
   struct TimedLaunch {
     int family;
     double flops;
@@ -244,8 +245,9 @@ struct mtsac_engine {
     ++tl_next;
   }
 
-  void gemm(const GemmParams& p, GemmKind kind, int epi, int batch) {
-    t_begin((int)kind, 2.0 * (double)p.M * p.N * p.K * batch);
+  // family: enum mtsac_gemm_family (timing only)
+  void gemm(const GemmParams& p, GemmKind kind, int epi, int batch, int family) {
+    t_begin(family, 2.0 * (double)p.M * p.N * p.K * batch);
     if (timing) {
       tl[tl_next].M = p.M;
       tl[tl_next].N = p.N;
@@ -259,8 +261,8 @@ struct mtsac_engine {
     t_end();
   }
 
-  void gemmp(const SplitGemmParams& p, int epi, int batch, GemmKind family) {
-    t_begin((int)family, 2.0 * (double)p.M * p.N * p.K * batch);
+  void gemmp(const SplitGemmParams& p, int epi, int batch, int family) {
+    t_begin(family, 2.0 * (double)p.M * p.N * p.K * batch);
     if (timing) {
       tl[tl_next].M = p.M;
       tl[tl_next].N = p.N;
@@ -317,7 +319,7 @@ struct mtsac_engine {
         g.M = M;
         g.N = net.width;
         g.K = (int)net.ald;
-        gemmp(g, EPI_BIAS_RELU, net.E, GEMM_NT);
+        gemmp(g, EPI_BIAS_RELU, net.E, MTSAC_FAM_FORWARD);
         continue;
       }
       GemmParams g{};
@@ -342,7 +344,7 @@ struct mtsac_engine {
         g.pC = net.aps();
         g.sCp = 3 * net.aps();
       }
-      gemm(g, nt ? GEMM_NT : GEMM_NN, EPI_BIAS_RELU, net.E);
+      gemm(g, nt ? GEMM_NT : GEMM_NN, EPI_BIAS_RELU, net.E, i == 0 ? MTSAC_FAM_INPUT_FORWARD : MTSAC_FAM_FORWARD);
     }
   }
 
@@ -395,9 +397,9 @@ struct mtsac_engine {
       g.M = net.width;
       g.N = net.width;
       g.K = (int)net.arows;
-      g.splits = gemm_x3p_splits(g.M, g.N, g.K, net.E);
+      g.splits = -1;  // by tile count (gemm_x3p_splits); splitk_ws is sized for it
       g.ws = splitk_ws;
-      gemmp(g, EPI_STORE, net.E, GEMM_TN);
+      gemmp(g, EPI_STORE, net.E, MTSAC_FAM_WEIGHT_GRAD);
       colsum(dz[i], M, net.width, net.width, (long long)M * net.width, net.E, cs_part, net.g + net.off_b[i], net.ms_b,
              cur);
       return;
@@ -419,7 +421,7 @@ struct mtsac_engine {
     g.K = M;
     g.splits = gemm_splits(g.M, g.N, g.K, net.E);
     g.ws = splitk_ws;  // one workspace: weight-grad GEMMs are serialised (lane 3 chain, actor after critic)
-    gemm(g, GEMM_TN, EPI_STORE, net.E);
+    gemm(g, GEMM_TN, EPI_STORE, net.E, i == 0 ? MTSAC_FAM_INPUT_WEIGHT_GRAD : MTSAC_FAM_WEIGHT_GRAD);
   }
 
   void dgrad_layer(Net& net, const float* params, float** acts, float** dz, __bf16** dzp, int i, int M) {
@@ -448,7 +450,7 @@ struct mtsac_engine {
       g.M = M;
       g.N = net.width;
       g.K = (int)net.ald;
-      gemmp(g, EPI_RELU_MASK, net.E, GEMM_NT);
+      gemmp(g, EPI_RELU_MASK, net.E, MTSAC_FAM_DATA_GRAD);
       return;
     }
     GemmParams g{};
@@ -467,7 +469,7 @@ struct mtsac_engine {
     g.M = M;
     g.N = net.width;
     g.K = net.width;
-    gemm(g, GEMM_NT, EPI_RELU_MASK, net.E);
+    gemm(g, GEMM_NT, EPI_RELU_MASK, net.E, MTSAC_FAM_DATA_GRAD);
   }
 
   HeadParams head(Net& net, const float* params, const float* h, int M, const int* tsk) {
@@ -571,7 +573,7 @@ struct mtsac_engine {
       if (g) (void)hipGraphDestroy(g);
       if (r != hipSuccess) comm_error = std::string("step graph build: ") + hipGetErrorString(r);
     } else {
-      hipStream_t L = timing ? st : (lane == 0 ? st : lane == 1 ? s1 : lane == 2 ? s2 : s3);
+      hipStream_t L = timing_serial ? st : (lane == 0 ? st : lane == 1 ? s1 : lane == 2 ? s2 : s3);
       for (int d : deps)
         if (segs[d].lane != L) (void)hipStreamWaitEvent(L, segs[d].ev, 0);
       cur = L;
@@ -620,6 +622,11 @@ struct mtsac_engine {
     pp.ls_min = cfg.log_std_min;
     pp.ls_max = cfg.log_std_max;
     pp.ld_a_out = ld_c;
+    pp.counts = counts;
+    pp.rows = rows;
+    pp.max_rows = Bl;
+    pp.T_l = T_l;
+    pp.max_count = device_batch ? n : Bl;  // replay batches hold exactly n rows per task
     CriticHeadParams ch{};
     ch.rew = rew;
     ch.done = done;
@@ -1346,10 +1353,8 @@ int mtsac_update_many(mtsac_engine* h, int32_t steps) {
   if (!h) return fail(-22, "null engine");
   if (steps <= 0) return 0;
   if (!h->use_graph || h->timing || h->hook) {  // events / host hooks need eager issue
-    for (int s = 0; s < steps; ++s) {
-      h->tl_next = 0;
-      h->step(true, true);
-    }
+    h->tl_next = 0;  // timing records every launch of this call
+    for (int s = 0; s < steps; ++s) h->step(true, true);
     HIP_TRY(hipGetLastError());
     return 0;
   }
@@ -1497,6 +1502,7 @@ int mtsac_memcpy(void* dst, const void* src, int64_t bytes) {
 int mtsac_set_timing(mtsac_engine* h, int32_t enable) {
   if (!h) return fail(-22, "null engine");
   h->timing = enable != 0;
+  h->timing_serial = enable == 2;
   return 0;
 }
 int mtsac_get_timing(mtsac_engine* h, int32_t family, double* total_ms, int32_t* launches, double* flops) {

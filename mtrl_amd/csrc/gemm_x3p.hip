@@ -59,9 +59,15 @@ struct Oper {
   // issue wave-instructions first, first + stride, ... (< NJ) of the stage at k0
   __device__ static inline void dma(const __bf16* __restrict__ base, long long ld, long long ps, int r0, int nrows,
                                     int k0, char* lds, int first, int stride) {
-    const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int j = first; j < NJ; j += stride) {
+    for (int j = first; j < NJ; j += stride) dma_one(base, ld, ps, r0, nrows, k0, lds, j);
+  }
+
+  // wave-instruction j (< NJ) of the stage at k0
+  __device__ static inline void dma_one(const __bf16* __restrict__ base, long long ld, long long ps, int r0, int nrows,
+                                        int k0, char* lds, int j) {
+    const int lane = threadIdx.x & 63;
+    {
       const int q = j / PER_PLANE;
       const int ib = (j % PER_PLANE) * RPI;  // first image row of the instruction
       const int irow = ib + lane / LPR;
@@ -155,6 +161,19 @@ __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) 
     OA::dma(A, p.lda, p.pA, m0, p.M, k0, st, wave, G::NW);
     OB::dma(B, p.ldb, p.pB, n0, p.N, k0, st + OA::BYTES, fb, G::NW);
   };
+  // the wave's q-th wave-instruction of a stage (same dealing as stage(): global index
+  // wave + q * NW, A's instructions first)
+  auto piece = [&](int s, int k0, int q) {
+    char* st = lds + s * STAGE;
+    const int jg = wave + q * G::NW;
+    if (jg < OA::NJ)
+      OA::dma_one(A, p.lda, p.pA, m0, p.M, k0, st, jg);
+    else if (jg - OA::NJ < OB::NJ)
+      OB::dma_one(B, p.ldb, p.pB, n0, p.N, k0, st + OA::BYTES, jg - OA::NJ);
+  };
+  (void)fb;
+  constexpr int PIECES = DMA_LO + (DMA_X ? 1 : 0);          // per wave and stage (the last maybe empty)
+  constexpr int SLOTS = (G::KS / 16) * G::TI * G::TJ;        // MFMA groups per K-step
 
   f32x16 acc[G::TI][G::TJ];
 #pragma unroll
@@ -185,8 +204,12 @@ __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) 
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (kt + G::STAGES - 1 < nk && !(p.dbg & 1))
-      stage((kt + G::STAGES - 1) % G::STAGES, (kt + G::STAGES - 1) * G::KS);
+    // the refill of the slot read at kt-1 is spread over this K-step's MFMA groups (p.dbg & 8:
+    // all issued up front)
+    const bool refill = kt + G::STAGES - 1 < nk && !(p.dbg & 1);
+    const int rs = (kt + G::STAGES - 1) % G::STAGES, rk = (kt + G::STAGES - 1) * G::KS;
+    if (refill && (p.dbg & 8)) stage(rs, rk);
+    const bool spread = refill && !(p.dbg & 8);
     const char* cur = lds + (kt % G::STAGES) * STAGE;
 #pragma unroll
     for (int ks = 0; ks < G::KS / 16; ++ks) {
@@ -204,12 +227,20 @@ __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) 
         for (int i = 0; i < G::TI; ++i)
 #pragma unroll
           for (int j = 0; j < G::TJ; ++j) acc[i][j][0] += (float)a[i][0][0] + (float)b[j][2][7];
+        if (spread && ks == 0)
+#pragma unroll
+          for (int q = 0; q < PIECES; ++q) piece(rs, rk, q);
         continue;
       }
 #pragma unroll
       for (int i = 0; i < G::TI; ++i)
 #pragma unroll
         for (int j = 0; j < G::TJ; ++j) {
+          const int slot = (ks * G::TI + i) * G::TJ + j;
+          if (spread) {
+#pragma unroll
+            for (int q = slot * PIECES / SLOTS; q < (slot + 1) * PIECES / SLOTS; ++q) piece(rs, rk, q);
+          }
           f32x16 c = acc[i][j];
           c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], c, 0, 0, 0);  // m*m
           c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], c, 0, 0, 0);  // h*l
@@ -358,8 +389,20 @@ static void launch_geo(const SplitGemmParams& p, int epi, int batch, hipStream_t
 int g_x3p_geo = -1;  // -1: by operand form; 0: 128x128 k32, 1: 256x128 k32, 2: 256x128 k16, 3: 256x256 k16
 int g_x3p_dbg = 0;
 
+// tile shape of a geometry id (see Geo aliases above)
+static void geo_tile(int geo, int& bm, int& bn) {
+  bm = geo == 0 ? 128 : 256;
+  bn = geo == 3 ? 256 : 128;
+}
+
+// auto geometry: 256x256 tiles (least operand traffic per MFMA, LDS-DMA spread over the MFMA
+// groups) for every form; g_x3p_geo forces one (experiments)
+static int pick_geo() { return g_x3p_geo >= 0 ? g_x3p_geo : 3; }
+
 int gemm_x3p_splits(int M, int N, int K, int batch) {
-  const long long tiles = (long long)((M + 255) / 256) * ((N + 127) / 128) * batch;
+  int bm, bn;
+  geo_tile(pick_geo(), bm, bn);
+  const long long tiles = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch;
   if (tiles >= 256) return 1;
   int s = (int)((256 + tiles - 1) / tiles);
   s = std::min(s, 16);
@@ -371,6 +414,7 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
   if (p0.M <= 0 || p0.N <= 0 || p0.K <= 0) return;
   SplitGemmParams p = p0;
   p.dbg |= g_x3p_dbg;
+  if (p.splits < 0) p.splits = gemm_x3p_splits(p.M, p.N, p.K, batch);  // auto
   int S = 1;
   if (p.splits > 1 && epi == EPI_STORE && p.ws != nullptr && !p.Cp) {
     const int kt = p.K / BK;
@@ -379,10 +423,7 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
   }
   p.splits = S;
   if (S == 1) p.kchunk = p.K;
-  // default: 256x256 tiles (least operand traffic per MFMA) for the NT forms, 256x128 for the
-  // k-major weight-gradient form (2048^2 outputs: 256 tiles per member, split-K below that)
-  int geo = g_x3p_geo;
-  if (geo < 0) geo = (p.a_kmajor && p.b_kmajor) ? 1 : 3;
+  const int geo = pick_geo();
   switch (geo) {
     case 0: launch_geo<GeoSmall>(p, epi, batch, st); break;
     case 2: launch_geo<GeoWide16>(p, epi, batch, st); break;

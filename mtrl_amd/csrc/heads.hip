@@ -57,19 +57,15 @@ __device__ inline void head_dot(const float* __restrict__ h, const float* __rest
 }
 
 // ------------------------------------------------------------------ actor head + policy
+// Given the head outputs acc (mu | log_std) of row b (task t), sample the tanh-Gaussian action and
+// its log-probability; lane j < A owns action dimension j.
 template <int HD>
-__global__ __launch_bounds__(256) void policy_head_kernel(PolicyParams p) {
-  const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+__device__ inline void policy_finish(const PolicyParams& p, int b, int t, const float (&acc)[HD], int lane) {
   const HeadParams& hp = p.head;
-  if (b >= hp.B) return;
-  const int t = hp.task[b];
-  float acc[HD];
-  head_dot<HD>(hp.h + (long long)b * hp.W, hp.Wh + (long long)t * hp.W * HD, hp.W, acc);
   const int A = p.A;
   float term = 0.f;
   if (lane < A) {
-    // lane j owns action dimension j; pick acc[j], acc[A+j] with a static unroll
+    // pick acc[j], acc[A+j] with a static unroll
     float mu = 0.f, ls = 0.f;
 #pragma unroll
     for (int o = 0; o < HD; ++o) {
@@ -105,6 +101,80 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyParams p) {
   }
   term = wsum(term);
   if (lane == 0) p.logpi[b] = term;
+}
+
+// one wavefront per row (rollout: rows without task lists)
+template <int HD>
+__global__ __launch_bounds__(256) void policy_head_kernel(PolicyParams p) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const HeadParams& hp = p.head;
+  if (b >= hp.B) return;
+  const int t = hp.task[b];
+  float acc[HD];
+  head_dot<HD>(hp.h + (long long)b * hp.W, hp.Wh + (long long)t * hp.W * HD, hp.W, acc);
+  policy_finish<HD>(p, b, t, acc, lane);
+}
+
+// Rows grouped by task (task_rows lists): a workgroup takes PH_ROWS rows of one task and stages
+// that task's head kernel through LDS in PH_CHUNK-row slices, so the kernel is read once per
+// group instead of once per row.  Each lane accumulates w = lane, lane + 64, ... in the same
+// order as head_dot: bitwise the same sums.
+constexpr int PH_RW = 4;               // rows per wave
+constexpr int PH_ROWS = 4 * PH_RW;     // rows per workgroup
+constexpr int PH_CHUNK = 512;          // head-kernel rows (w) per LDS slice
+
+template <int HD>
+__global__ __launch_bounds__(256) void policy_head_grouped_kernel(PolicyParams p) {
+  __shared__ __attribute__((aligned(16))) float wl[PH_CHUNK * HD];
+  const HeadParams& hp = p.head;
+  const int t = blockIdx.x;
+  const int n = p.counts[t];
+  const int j0 = blockIdx.y * PH_ROWS;
+  if (j0 >= n) return;  // uniform over the workgroup
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int* rl = p.rows + (long long)t * p.max_rows;
+  int row[PH_RW];
+#pragma unroll
+  for (int r = 0; r < PH_RW; ++r) {
+    const int jj = j0 + wave * PH_RW + r;
+    row[r] = rl[jj < n ? jj : j0];
+  }
+  float acc[PH_RW][HD];
+#pragma unroll
+  for (int r = 0; r < PH_RW; ++r)
+#pragma unroll
+    for (int o = 0; o < HD; ++o) acc[r][o] = 0.f;
+  const float* Wt = hp.Wh + (long long)t * hp.W * HD;
+  const bool vec = ((hp.W * HD) % 4 == 0);
+  for (int w0 = 0; w0 < hp.W; w0 += PH_CHUNK) {
+    const int cw = min(PH_CHUNK, hp.W - w0);
+    __syncthreads();
+    if (vec) {
+      for (int i = threadIdx.x; i < cw * HD / 4; i += 256)
+        reinterpret_cast<float4*>(wl)[i] = reinterpret_cast<const float4*>(Wt + (long long)w0 * HD)[i];
+    } else {
+      for (int i = threadIdx.x; i < cw * HD; i += 256) wl[i] = Wt[(long long)w0 * HD + i];
+    }
+    __syncthreads();
+    for (int w = lane; w < cw; w += 64) {
+      float wv[HD];
+#pragma unroll
+      for (int o = 0; o < HD; ++o) wv[o] = wl[w * HD + o];
+#pragma unroll
+      for (int r = 0; r < PH_RW; ++r) {
+        const float hv = hp.h[(long long)row[r] * hp.W + w0 + w];
+#pragma unroll
+        for (int o = 0; o < HD; ++o) acc[r][o] += hv * wv[o];
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < PH_RW; ++r) {
+#pragma unroll
+    for (int o = 0; o < HD; ++o) acc[r][o] = wsum(acc[r][o]);
+    if (j0 + wave * PH_RW + r < n) policy_finish<HD>(p, row[r], t, acc[r], lane);
+  }
 }
 
 // ------------------------------------------------------------------ critic heads + losses
@@ -211,8 +281,10 @@ __global__ __launch_bounds__(256) void head_bwd_data_kernel(HeadParams hp, const
 }
 
 // ------------------------------------------------------------------ head backward (weights)
+// dWh[t][w][o] = sum over the task's rows of h[row][w] dout[row][o]; wave g sums rows j = g mod 4
+// in order, then the four waves are added in order (same association in both kernels).
 template <int HD>
-__global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, const float* __restrict__ dout,
+__global__ __launch_bounds__(256) void head_bwd_weight_scalar_kernel(HeadParams hp, const float* __restrict__ dout,
                                                               long long s_dout, const int* __restrict__ counts,
                                                               const int* __restrict__ rows, int max_rows,
                                                               float* __restrict__ dWh, float* __restrict__ dbh) {
@@ -249,6 +321,76 @@ __global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, con
   if (blockIdx.y == 0) {  // bias grad: 256 strided partial sums, then a fixed-order tree
     __syncthreads();
     float* part = &red[0][0][0];  // 256 * HD floats
+#pragma unroll
+    for (int o = 0; o < HD; ++o) {
+      float s = 0.f;
+      for (int j = threadIdx.x; j < n; j += 256) s += d[(long long)rl[j] * HD + o];
+      part[o * 256 + threadIdx.x] = s;
+    }
+    __syncthreads();
+    for (int half = 128; half > 0; half >>= 1) {
+      if (threadIdx.x < half)
+#pragma unroll
+        for (int o = 0; o < HD; ++o) part[o * 256 + threadIdx.x] += part[o * 256 + threadIdx.x + half];
+      __syncthreads();
+    }
+    if (threadIdx.x < HD) dbh[e * hp.sbh + t * HD + threadIdx.x] = part[threadIdx.x * 256];
+  }
+}
+
+// W % 4 == 0: each lane owns 4 consecutive w (16-B loads), a workgroup 256 w
+template <int HD>
+__global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, const float* __restrict__ dout,
+                                                              long long s_dout, const int* __restrict__ counts,
+                                                              const int* __restrict__ rows, int max_rows,
+                                                              float* __restrict__ dWh, float* __restrict__ dbh) {
+  __shared__ float4 red[4][64][HD];
+  const int t = blockIdx.x, e = blockIdx.z;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int w = blockIdx.y * 256 + 4 * lane;
+  const int n = counts[t];
+  const int* rl = rows + (long long)t * max_rows;
+  const float* h = hp.h + e * hp.sh;
+  const float* d = dout + e * s_dout;
+  float4 acc[HD];
+#pragma unroll
+  for (int o = 0; o < HD; ++o) acc[o] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (w < hp.W) {
+    for (int j = wave; j < n; j += 4) {
+      const int row = rl[j];
+      const float4 hv = *reinterpret_cast<const float4*>(h + (long long)row * hp.W + w);
+#pragma unroll
+      for (int o = 0; o < HD; ++o) {
+        const float dv = d[(long long)row * HD + o];
+        acc[o].x += hv.x * dv;
+        acc[o].y += hv.y * dv;
+        acc[o].z += hv.z * dv;
+        acc[o].w += hv.w * dv;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < HD; ++o) red[wave][lane][o] = acc[o];
+  __syncthreads();
+  if (wave == 0 && w < hp.W) {
+    float v[4][HD];
+#pragma unroll
+    for (int o = 0; o < HD; ++o) {
+      const float4 a0 = red[0][lane][o], a1 = red[1][lane][o], a2 = red[2][lane][o], a3 = red[3][lane][o];
+      v[0][o] = a0.x + a1.x + a2.x + a3.x;
+      v[1][o] = a0.y + a1.y + a2.y + a3.y;
+      v[2][o] = a0.z + a1.z + a2.z + a3.z;
+      v[3][o] = a0.w + a1.w + a2.w + a3.w;
+    }
+    float* out = dWh + e * hp.sWh + ((long long)t * hp.W + w) * HD;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int o = 0; o < HD; ++o) out[k * HD + o] = v[k][o];
+  }
+  if (blockIdx.y == 0) {  // bias grad: 256 strided partial sums, then a fixed-order tree
+    __syncthreads();
+    float* part = reinterpret_cast<float*>(&red[0][0][0]);  // >= 256 * HD floats
 #pragma unroll
     for (int o = 0; o < HD; ++o) {
       float s = 0.f;
@@ -324,12 +466,25 @@ __global__ __launch_bounds__(256) void row_alpha_kernel(const int* __restrict__ 
 }  // namespace
 
 void policy_head(const PolicyParams& p, hipStream_t st) {
+  const int hd = p.head.hd;
+  if (p.counts != nullptr) {
+    dim3 grid((unsigned)p.T_l, (unsigned)((p.max_count + PH_ROWS - 1) / PH_ROWS));
+    if (hd == 8)
+      hipLaunchKernelGGL(policy_head_grouped_kernel<8>, grid, dim3(256), 0, st, p);
+    else if (hd == 6)
+      hipLaunchKernelGGL(policy_head_grouped_kernel<6>, grid, dim3(256), 0, st, p);
+    else if (hd == 4)
+      hipLaunchKernelGGL(policy_head_grouped_kernel<4>, grid, dim3(256), 0, st, p);
+    else
+      hipLaunchKernelGGL(policy_head_grouped_kernel<2>, grid, dim3(256), 0, st, p);
+    return;
+  }
   dim3 grid((p.head.B + 3) / 4);
-  if (p.head.hd == 8)
+  if (hd == 8)
     hipLaunchKernelGGL(policy_head_kernel<8>, grid, dim3(256), 0, st, p);
-  else if (p.head.hd == 6)
+  else if (hd == 6)
     hipLaunchKernelGGL(policy_head_kernel<6>, grid, dim3(256), 0, st, p);
-  else if (p.head.hd == 4)
+  else if (hd == 4)
     hipLaunchKernelGGL(policy_head_kernel<4>, grid, dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL(policy_head_kernel<2>, grid, dim3(256), 0, st, p);
@@ -354,15 +509,19 @@ void head_backward_data(const HeadParams& hp, const float* dout, long long s_dou
 
 void head_backward_weight(const HeadParams& hp, const float* dout, long long s_dout, const int* counts,
                           const int* rows, int max_rows, float* dWh, float* dbh, hipStream_t st) {
-  dim3 grid(0, (hp.W + 63) / 64, hp.E);
-  grid.x = (unsigned)(hp.sbh / hp.hd);  // T_l (bias stride per member = T_l * hd)
+  const unsigned T_l = (unsigned)(hp.sbh / hp.hd);  // bias stride per member = T_l * hd
+#define HBW_LAUNCH(K, HDV, WPB)                                                                             \
+  hipLaunchKernelGGL(K<HDV>, dim3(T_l, (hp.W + WPB - 1) / WPB, hp.E), dim3(256), 0, st, hp, dout, s_dout, counts, \
+                     rows, max_rows, dWh, dbh)
+  const bool vec = hp.W % 4 == 0;
   switch (hp.hd) {
-    case 1: hipLaunchKernelGGL(head_bwd_weight_kernel<1>, grid, dim3(256), 0, st, hp, dout, s_dout, counts, rows, max_rows, dWh, dbh); break;
-    case 2: hipLaunchKernelGGL(head_bwd_weight_kernel<2>, grid, dim3(256), 0, st, hp, dout, s_dout, counts, rows, max_rows, dWh, dbh); break;
-    case 4: hipLaunchKernelGGL(head_bwd_weight_kernel<4>, grid, dim3(256), 0, st, hp, dout, s_dout, counts, rows, max_rows, dWh, dbh); break;
-    case 6: hipLaunchKernelGGL(head_bwd_weight_kernel<6>, grid, dim3(256), 0, st, hp, dout, s_dout, counts, rows, max_rows, dWh, dbh); break;
-    default: hipLaunchKernelGGL(head_bwd_weight_kernel<8>, grid, dim3(256), 0, st, hp, dout, s_dout, counts, rows, max_rows, dWh, dbh); break;
+    case 1: if (vec) HBW_LAUNCH(head_bwd_weight_kernel, 1, 256); else HBW_LAUNCH(head_bwd_weight_scalar_kernel, 1, 64); break;
+    case 2: if (vec) HBW_LAUNCH(head_bwd_weight_kernel, 2, 256); else HBW_LAUNCH(head_bwd_weight_scalar_kernel, 2, 64); break;
+    case 4: if (vec) HBW_LAUNCH(head_bwd_weight_kernel, 4, 256); else HBW_LAUNCH(head_bwd_weight_scalar_kernel, 4, 64); break;
+    case 6: if (vec) HBW_LAUNCH(head_bwd_weight_kernel, 6, 256); else HBW_LAUNCH(head_bwd_weight_scalar_kernel, 6, 64); break;
+    default: if (vec) HBW_LAUNCH(head_bwd_weight_kernel, 8, 256); else HBW_LAUNCH(head_bwd_weight_scalar_kernel, 8, 64); break;
   }
+#undef HBW_LAUNCH
 }
 
 void action_grad(const ActionGradParams& p, hipStream_t st) {

@@ -69,7 +69,7 @@ struct SplitGemmParams {
   __bf16* Cp;             // optional split planes of C: [3][M][ldcp]
   long long ldcp, pC, sCp;
   int M, N, K;
-  int splits, kchunk;     // split-K (EPI_STORE, no Cp): partial slabs in ws (gemm_ws_floats)
+  int splits, kchunk;     // split-K (EPI_STORE, no Cp): partial slabs in ws (gemm_ws_floats); -1 = auto
   float* ws;
   int dbg;                // experiments only: bit0 skip steady-state loads, bit1 skip MFMA
 };
@@ -157,6 +157,11 @@ struct PolicyParams {
   int ld_a_out2;
   float* logpi;         // [B]
   float* cache;         // optional [B][5A]: mu, ls, x, a, eps
+  // optional per-task row lists (task_rows): rows grouped by task share head-kernel reads
+  const int* counts;
+  const int* rows;
+  int max_rows, T_l;    // row-list stride, local tasks
+  int max_count;        // bound on counts[] (sizes the grid)
 };
 void policy_head(const PolicyParams& p, hipStream_t st);
 

@@ -244,8 +244,10 @@ class MTSACEngine:
         check(self.lib.mtsac_set_allreduce_hook(self._h, ctypes.cast(self._hook, ctypes.c_void_p), None))
 
     # ------------------------------------------------------------------ measurement
-    def set_timing(self, on: bool) -> None:
-        check(self.lib.mtsac_set_timing(self._h, 1 if on else 0))
+    def set_timing(self, on: bool, serial: bool = False) -> None:
+        """HIP-event timing of every GEMM launch of the next update call(s); serial=True runs
+        the step on one stream (solo kernel durations), else the step keeps its streams."""
+        check(self.lib.mtsac_set_timing(self._h, (2 if serial else 1) if on else 0))
 
     def timing(self, family: int) -> tuple[float, int, float]:
         ms, n, fl = ctypes.c_double(), ctypes.c_int32(), ctypes.c_double()

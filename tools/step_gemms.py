@@ -21,7 +21,7 @@ eng.seed_rng(1)
 eng.enable_graph(False)
 eng.update_many(3)
 eng.synchronize()
-eng.set_timing(True)
+eng.set_timing(True, serial=True)
 eng.update_many(1)
 eng.synchronize()
 lib = L.load()
@@ -29,11 +29,11 @@ n = lib.mtsac_debug_timed_launch(eng._h, -1, None, None)
 dims = (ctypes.c_int32 * 5)()
 ms = ctypes.c_double()
 tot = 0.0
-kinds = ["NN", "NT", "TN"]
+kinds = ["fwd", "dgrad", "wgrad", "in-fwd", "in-wgrad"]
 for i in range(n):
     L.check(lib.mtsac_debug_timed_launch(eng._h, i, dims, ctypes.byref(ms)))
     f, M, N, K, E = list(dims)
     fl = 2.0 * M * N * K * E
     tot += ms.value
-    print(f"{i:3d} {kinds[f]} M={M:5d} N={N:5d} K={K:5d} E={E} {ms.value * 1e3:8.1f} us {fl / (ms.value * 1e-3) / 1e12:7.1f} TF/s")
+    print(f"{i:3d} {kinds[f]:8s} M={M:5d} N={N:5d} K={K:5d} E={E} {ms.value * 1e3:8.1f} us {fl / (ms.value * 1e-3) / 1e12:7.1f} TF/s")
 print(f"total GEMM {tot:.3f} ms")
