@@ -142,7 +142,10 @@ struct mtsac_engine {
   float *logpi_n = nullptr, *logpi = nullptr, *y = nullptr, *dq = nullptr, *row_a = nullptr, *row_b = nullptr,
         *row_c = nullptr, *alpha_w = nullptr, *cache = nullptr, *dout_a = nullptr;
   float* partials = nullptr;
-  float* splitk_ws = nullptr;
+  // split-K workspaces, one per lane: segments on different lanes may run concurrently, the
+  // segments of one lane are ordered by the step DAG (see seg())
+  float* ws_lane[4] = {};
+  int cur_lane = 0;
   float* pn = nullptr;  // [critic trunk |p|^2, actor trunk, critic heads, actor heads]
   float* log_alpha = nullptr;
   float *la_m = nullptr, *la_v = nullptr;
@@ -319,6 +322,8 @@ struct mtsac_engine {
         g.M = M;
         g.N = net.width;
         g.K = (int)net.ald;
+        g.splits = -1;
+        g.ws = ws_lane[cur_lane];
         gemmp(g, EPI_BIAS_RELU, net.E, MTSAC_FAM_FORWARD);
         continue;
       }
@@ -397,8 +402,8 @@ struct mtsac_engine {
       g.M = net.width;
       g.N = net.width;
       g.K = (int)net.arows;
-      g.splits = -1;  // by tile count (gemm_x3p_splits); splitk_ws is sized for it
-      g.ws = splitk_ws;
+      g.splits = -1;  // by tile count (gemm_x3p_splits); the lane workspace is sized for it
+      g.ws = ws_lane[cur_lane];
       gemmp(g, EPI_STORE, net.E, MTSAC_FAM_WEIGHT_GRAD);
       colsum(dz[i], M, net.width, net.width, (long long)M * net.width, net.E, cs_part, net.g + net.off_b[i], net.ms_b,
              cur);
@@ -420,7 +425,7 @@ struct mtsac_engine {
     g.N = net.width;
     g.K = M;
     g.splits = gemm_splits(g.M, g.N, g.K, net.E);
-    g.ws = splitk_ws;  // one workspace: weight-grad GEMMs are serialised (lane 3 chain, actor after critic)
+    g.ws = ws_lane[cur_lane];
     gemm(g, GEMM_TN, EPI_STORE, net.E, i == 0 ? MTSAC_FAM_INPUT_WEIGHT_GRAD : MTSAC_FAM_WEIGHT_GRAD);
   }
 
@@ -450,6 +455,8 @@ struct mtsac_engine {
       g.M = M;
       g.N = net.width;
       g.K = (int)net.ald;
+      g.splits = -1;
+      g.ws = ws_lane[cur_lane];
       gemmp(g, EPI_RELU_MASK, net.E, MTSAC_FAM_DATA_GRAD);
       return;
     }
@@ -560,6 +567,7 @@ struct mtsac_engine {
   template <class F>
   int seg(std::initializer_list<int> deps, int lane, F&& body) {
     Seg s{};
+    cur_lane = lane;
     if (build) {
       std::vector<hipGraphNode_t> dn;
       for (int d : deps) dn.push_back(segs[d].node);
@@ -979,17 +987,19 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
         if ((rc = e->alloc(&net->wtp[w][i], np))) return bad(rc);
       }
   }
-  {  // split-K workspace: the largest weight-gradient GEMM that splits
+  {  // split-K workspaces: the largest GEMM that splits, per lane
     long long ws = 0;
     for (Net* net : {&e->actor, &e->critic})
       for (int i = 0; i < net->depth; ++i) {
         const int M = i == 0 ? net->in_dim : net->width;
         ws = std::max(ws, gemm_ws_floats(M, net->width, net->E, gemm_splits(M, net->width, e->B, net->E)));
-        if (e->planes && i > 0)
-          ws = std::max(ws, gemm_ws_floats(M, net->width, net->E,
-                                           gemm_x3p_splits(M, net->width, (int)net->arows, net->E)));
+        if (e->planes && i > 0) {
+          ws = std::max(ws, gemm_x3p_ws_floats(M, net->width, (int)net->arows, net->E, true));      // weight grad
+          ws = std::max(ws, gemm_x3p_ws_floats(e->B, net->width, (int)net->ald, net->E, false));   // fwd / data grad
+        }
       }
-    if ((rc = e->alloc(&e->splitk_ws, (size_t)std::max(ws, 1LL)))) return bad(rc);
+    for (float*& w : e->ws_lane)
+      if ((rc = e->alloc(&w, (size_t)std::max(ws, 1LL)))) return bad(rc);
   }
 
   const int B = e->B;

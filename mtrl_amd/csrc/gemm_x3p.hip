@@ -283,6 +283,7 @@ using GeoSmall = Geo<128, 128, 2, 2, 3, 32>;   // 4 waves, 3 x 48 KiB
 using GeoWide = Geo<256, 128, 4, 2, 2, 32>;    // 8 waves, 2 x 72 KiB
 using GeoWide16 = Geo<256, 128, 4, 2, 4, 16>;  // 8 waves, 4 x 36 KiB
 using GeoBig16 = Geo<256, 256, 2, 4, 3, 16>;   // 8 waves of 128 x 64, 3 x 48 KiB
+using GeoSmall16 = Geo<128, 128, 2, 2, 3, 16>;  // 4 waves, 3 x 24 KiB: two workgroups per CU
 
 // fp32 [rows][ld] -> planes.  TRANS: out[q][col][row] (k = row contiguous), else out[q][row][col].
 // 64x64 tiles staged through LDS so both the fp32 reads and the bf16 writes are coalesced.
@@ -391,46 +392,116 @@ int g_x3p_dbg = 0;
 
 // tile shape of a geometry id (see Geo aliases above)
 static void geo_tile(int geo, int& bm, int& bn) {
-  bm = geo == 0 ? 128 : 256;
+  bm = (geo == 0 || geo == 4) ? 128 : 256;
   bn = geo == 3 ? 256 : 128;
 }
 
-// auto geometry: 256x256 tiles (least operand traffic per MFMA, LDS-DMA spread over the MFMA
-// groups) for every form; g_x3p_geo forces one (experiments)
-static int pick_geo() { return g_x3p_geo >= 0 ? g_x3p_geo : 3; }
+// Auto geometry by size (measured, tools/x3p_bench.py): 256x256 tiles (least operand traffic
+// per MFMA) when they give >= 192 workgroups or the form is the k-major weight gradient (split-K
+// fills the chip there); else 256x128.  g_x3p_geo forces one (experiments).
+static int pick_geo(int M, int N, int batch, bool kmajor) {
+  if (g_x3p_geo >= 0) return g_x3p_geo;
+  if (kmajor) return 3;
+  const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256) * batch;
+  return big >= 192 ? 3 : 1;
+}
 
-int gemm_x3p_splits(int M, int N, int K, int batch) {
+int gemm_x3p_splits(int M, int N, int K, int batch, bool kmajor) {
   int bm, bn;
-  geo_tile(pick_geo(), bm, bn);
+  geo_tile(pick_geo(M, N, batch, kmajor), bm, bn);
   const long long tiles = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch;
-  if (tiles >= 256) return 1;
+  if (tiles >= 192) return 1;
   int s = (int)((256 + tiles - 1) / tiles);
-  s = std::min(s, 16);
-  s = std::min(s, std::max(1, K / BK / 4));
+  s = std::min(s, kmajor ? 16 : 4);
+  s = std::min(s, std::max(1, K / BK / 8));  // >= 8 K-granules per slice
   return std::max(s, 1);
 }
+
+long long gemm_x3p_ws_floats(int M, int N, int K, int batch, bool kmajor) {
+  return gemm_ws_floats(M, N, batch, gemm_x3p_splits(M, N, K, batch, kmajor));
+}
+
+namespace {
+
+// split-K finish: C = epi(sum_s ws[z*S+s]) (+ its planes), slices added in order
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(SplitGemmParams p, int S, int batch) {
+  const long long slab = (long long)p.M * p.N;
+  const int n4 = p.N / 4;
+  const long long per = (long long)p.M * n4;
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= per * batch) return;
+  const int z = (int)(gid / per);
+  const long long r = gid - z * per;
+  const int row = (int)(r / n4), col = (int)(r - (long long)row * n4) * 4;
+  const float* w = p.ws + (long long)z * S * slab + (long long)row * p.N + col;
+  float4 v = *reinterpret_cast<const float4*>(w);
+  for (int s = 1; s < S; ++s) {
+    const float4 u = *reinterpret_cast<const float4*>(w + s * slab);
+    v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+  }
+  float e[4] = {v.x, v.y, v.z, v.w};
+  if (EPI == EPI_BIAS_RELU) {
+    const float4 b = *reinterpret_cast<const float4*>(p.bias + z * p.sBias + col);
+    e[0] = fmaxf(e[0] + b.x, 0.f); e[1] = fmaxf(e[1] + b.y, 0.f);
+    e[2] = fmaxf(e[2] + b.z, 0.f); e[3] = fmaxf(e[3] + b.w, 0.f);
+  }
+  if (EPI == EPI_RELU_MASK) {
+    const float4 mk = *reinterpret_cast<const float4*>(p.mask + z * p.sMask + (long long)row * p.ldm + col);
+    e[0] = mk.x > 0.f ? e[0] : 0.f; e[1] = mk.y > 0.f ? e[1] : 0.f;
+    e[2] = mk.z > 0.f ? e[2] : 0.f; e[3] = mk.w > 0.f ? e[3] : 0.f;
+  }
+  if (p.C) *reinterpret_cast<float4*>(p.C + z * p.sC + (long long)row * p.ldc + col) = make_float4(e[0], e[1], e[2], e[3]);
+  if (p.Cp) {
+    bf16x4_t h, m, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      __bf16 a, b, c;
+      split3_dev(e[j], a, b, c);
+      h[j] = a; m[j] = b; l[j] = c;
+    }
+    __bf16* cp = p.Cp + z * p.sCp + (long long)row * p.ldcp + col;
+    *reinterpret_cast<bf16x4_t*>(cp) = h;
+    *reinterpret_cast<bf16x4_t*>(cp + p.pC) = m;
+    *reinterpret_cast<bf16x4_t*>(cp + 2 * p.pC) = l;
+  }
+}
+
+}  // namespace
 
 void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
   if (p0.M <= 0 || p0.N <= 0 || p0.K <= 0) return;
   SplitGemmParams p = p0;
   p.dbg |= g_x3p_dbg;
-  if (p.splits < 0) p.splits = gemm_x3p_splits(p.M, p.N, p.K, batch);  // auto
+  const bool kmajor = p.a_kmajor && p.b_kmajor;
+  if (p.splits < 0) p.splits = gemm_x3p_splits(p.M, p.N, p.K, batch, kmajor);  // auto
+  // split-K: every epilogue works (the finishing pass applies it); the vector finish needs
+  // N, ldc, ldm, ldcp multiples of 4
+  const bool vec = p.N % 4 == 0 && (!p.C || p.ldc % 4 == 0) && (epi != EPI_RELU_MASK || p.ldm % 4 == 0) &&
+                   (!p.Cp || p.ldcp % 4 == 0);
   int S = 1;
-  if (p.splits > 1 && epi == EPI_STORE && p.ws != nullptr && !p.Cp) {
+  if (p.splits > 1 && p.ws != nullptr && (epi == EPI_STORE && !p.Cp ? true : vec)) {
     const int kt = p.K / BK;
     p.kchunk = (kt + p.splits - 1) / p.splits * BK;
     S = (p.K + p.kchunk - 1) / p.kchunk;
   }
   p.splits = S;
   if (S == 1) p.kchunk = p.K;
-  const int geo = pick_geo();
-  switch (geo) {
-    case 0: launch_geo<GeoSmall>(p, epi, batch, st); break;
-    case 2: launch_geo<GeoWide16>(p, epi, batch, st); break;
-    case 3: launch_geo<GeoBig16>(p, epi, batch, st); break;
-    default: launch_geo<GeoWide>(p, epi, batch, st); break;
+  SplitGemmParams q = p;
+  int kepi = epi;
+  if (S > 1) {  // the GEMM writes raw partial slabs
+    q.Cp = nullptr;
+    kepi = EPI_STORE;
   }
-  if (S > 1) {
+  switch (pick_geo(p.M, p.N, batch, kmajor)) {
+    case 0: launch_geo<GeoSmall>(q, kepi, batch, st); break;
+    case 2: launch_geo<GeoWide16>(q, kepi, batch, st); break;
+    case 3: launch_geo<GeoBig16>(q, kepi, batch, st); break;
+    case 4: launch_geo<GeoSmall16>(q, kepi, batch, st); break;
+    default: launch_geo<GeoWide>(q, kepi, batch, st); break;
+  }
+  if (S == 1) return;
+  if (epi == EPI_STORE && !p.Cp) {
     GemmParams r{};
     r.M = p.M;
     r.N = p.N;
@@ -439,7 +510,16 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
     r.sC = p.sC;
     r.ws = p.ws;
     splitk_reduce(r, batch, S, st);
+    return;
   }
+  const long long n = (long long)batch * p.M * (p.N / 4);
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (epi == EPI_BIAS_RELU)
+    hipLaunchKernelGGL(splitk_epilogue_kernel<EPI_BIAS_RELU>, grid, dim3(256), 0, st, p, S, batch);
+  else if (epi == EPI_RELU_MASK)
+    hipLaunchKernelGGL(splitk_epilogue_kernel<EPI_RELU_MASK>, grid, dim3(256), 0, st, p, S, batch);
+  else
+    hipLaunchKernelGGL(splitk_epilogue_kernel<EPI_STORE>, grid, dim3(256), 0, st, p, S, batch);
 }
 
 void split_planes(const SplitParams& s, bool transpose, int batch, hipStream_t st) {

@@ -69,12 +69,14 @@ struct SplitGemmParams {
   __bf16* Cp;             // optional split planes of C: [3][M][ldcp]
   long long ldcp, pC, sCp;
   int M, N, K;
-  int splits, kchunk;     // split-K (EPI_STORE, no Cp): partial slabs in ws (gemm_ws_floats); -1 = auto
+  int splits, kchunk;     // split-K: partial slabs in ws (gemm_x3p_ws_floats), then a finishing pass; -1 = auto
   float* ws;
   int dbg;                // experiments only: bit0 skip steady-state loads, bit1 skip MFMA
 };
 void gemm_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
-int gemm_x3p_splits(int M, int N, int K, int batch);
+// auto split-K slices (1 = none) for a plane GEMM; kmajor = the k-major x k-major form
+int gemm_x3p_splits(int M, int N, int K, int batch, bool kmajor);
+long long gemm_x3p_ws_floats(int M, int N, int K, int batch, bool kmajor);
 extern int g_x3p_geo;  // tile geometry of gemm_x3p (-1: by operand form, 0..3: forced; see gemm_x3p.hip)
 extern int g_x3p_dbg;  // experiment bits OR-ed into SplitGemmParams::dbg
 extern int g_x3_dbg;   // experiments on gemm_x3: bit0 skip loads after the first tile, bit1 skip MFMA, bit2 skip split

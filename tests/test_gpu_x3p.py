@@ -8,7 +8,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=["geo128x128k32", "geo256x128k32", "geo256x128k16", "geo256x256k16"])
+@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["geo128x128k32", "geo256x128k32", "geo256x128k16", "geo256x256k16",
+                                          "geo128x128k16"])
 def geo(request):
     from mtrl_amd import _lib as L
 
@@ -84,3 +85,22 @@ def test_x3p_epilogues(geo):
     np.testing.assert_allclose(C, (A.astype(np.float64) @ Bt.T) * (H > 0), rtol=1e-5, atol=1e-4)
     np.testing.assert_allclose(S, C, rtol=1e-7, atol=1e-30)
     assert np.all(S[H <= 0] == 0)
+
+
+@pytest.mark.parametrize("splits", [2, 4])
+def test_x3p_splitk_epilogues(splits, geo):
+    """Split-K on the forward / data-grad forms: partial slabs, then the finishing pass applies
+    bias+ReLU or the ReLU mask and writes the planes."""
+    M, N, K = 300, 200, 512
+    rng = np.random.default_rng(5)
+    A = rng.standard_normal((M, K)).astype(np.float32)
+    Bt = rng.standard_normal((N, K)).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    ref = A.astype(np.float64) @ Bt.T.astype(np.float64)
+    C, S = _run(1, M, N, K, A, 0, Bt, 0, bias=bias, splits=splits, want_planes=True)
+    np.testing.assert_allclose(C, np.maximum(ref + bias, 0), rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(S, C, rtol=1e-7, atol=1e-30)
+    H = rng.standard_normal((M, N)).astype(np.float32)
+    C, S = _run(2, M, N, K, A, 0, Bt, 0, mask=H, splits=splits, want_planes=True)
+    np.testing.assert_allclose(C, ref * (H > 0), rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(S, C, rtol=1e-7, atol=1e-30)
