@@ -62,8 +62,8 @@ struct Net {
   // transposed hidden kernels W_i^T ([E][out][in], i >= 1) of p (wt[0]) and tgt (wt[1]): the
   // trunk forward runs as an NT product against them (k-contiguous operands on both sides)
   float* wt[2][MAXD] = {};
-  // split3: bf16 planes of W_i ([E][3][in][wld], data grads) and of W_i^T ([E][3][out][wld],
-  // forward) for i >= 1, of p ([0]) and tgt ([1]); activation / data-grad planes of this net are
+  // split3: bf16 planes of W_i ([E][3][in][wld], data grads; of p only) and of W_i^T
+  // ([E][3][out][wld], forward) for i >= 1, of p ([0]) and tgt ([1]); activation / data-grad planes of this net are
   // [E][3][arows][ald] (arows = B rounded up to 32 with zero rows, ald = width rounded up to 32)
   __bf16* wp[2][MAXD] = {};
   __bf16* wtp[2][MAXD] = {};
@@ -353,8 +353,9 @@ struct mtsac_engine {
     }
   }
 
-  // after every write of params: Net::wt[which] (fp32) or the planes wp / wtp[which] (split3)
-  void refresh_wt(Net& net, const float* params, int which, hipStream_t s) {
+  // after every write of params: Net::wt[which] (fp32) or the planes wp / wtp[which] (split3);
+  // natural_fused: the optimizer already wrote wp (see optimize())
+  void refresh_wt(Net& net, const float* params, int which, hipStream_t s, bool natural_fused = false) {
     for (int i = 1; i < net.depth; ++i) {
       if (!planes) {
         transpose_f32(params + net.off_W[i], net.ms_W[i], net.wt[which][i], net.ms_W[i], net.width, net.width, net.E,
@@ -367,13 +368,16 @@ struct mtsac_engine {
       sp.sx = net.ms_W[i];
       sp.rows = net.width;
       sp.cols = net.width;
-      sp.out = net.wp[which][i];
       sp.ldo = net.wld;
       sp.po = (long long)net.width * net.wld;
       sp.so = 3 * sp.po;
       sp.out_rows = net.width;
       sp.out_cols = (int)net.wld;
-      split_planes(sp, false, net.E, s);
+      // natural planes (data grads) exist for p only; the optimizer writes them itself
+      if (which == 0 && !(natural_fused && net.wld == net.width)) {
+        sp.out = net.wp[0][i];
+        split_planes(sp, false, net.E, s);
+      }
       sp.out = net.wtp[which][i];
       split_planes(sp, true, net.E, s);
     }
@@ -540,6 +544,10 @@ struct mtsac_engine {
     a.g += net.trunk_off;
     if (a.target) a.target += net.trunk_off;
     a.n = net.n_flat - net.trunk_off;
+    if (planes && net.wld == net.width)  // hidden kernels' natural planes straight from the update
+      for (int i = 1; i < net.depth && a.nseg < MAX_PLANE_SEGS; ++i)
+        a.seg[a.nseg++] = PlaneSeg{net.off_W[i] - net.trunk_off, net.ms_W[i], net.E, net.wp[0][i],
+                                   (long long)net.width * net.wld};
     int na = adam_update(a, max_norm, 0, PART, cur);
     sum_partials(partials, na, pn + slot, cur);
   }
@@ -714,8 +722,8 @@ struct mtsac_engine {
       head_sq(critic);
       allreduce(critic.g + critic.trunk_off, (size_t)(critic.n_flat - critic.trunk_off + EXTRA));
       optimize(critic, cfg.critic_lr, cfg.critic_max_grad_norm, true, 0);
-      refresh_wt(critic, critic.p, 0, cur);
-      refresh_wt(critic, critic.tgt, 1, cur);
+      refresh_wt(critic, critic.p, 0, cur, true);
+      refresh_wt(critic, critic.tgt, 1, cur, true);
     });
     // actor loss through the UPDATED critic (mtsac.py:659-691)
     const int s_ap = seg({s_co, s_af}, 1, [&] {
@@ -764,7 +772,7 @@ struct mtsac_engine {
       head_sq(actor);
       allreduce(actor.g + actor.trunk_off, (size_t)(actor.n_flat - actor.trunk_off + EXTRA));
       optimize(actor, cfg.actor_lr, cfg.actor_max_grad_norm, false, 1);
-      refresh_wt(actor, actor.p, 0, cur);
+      refresh_wt(actor, actor.p, 0, cur, true);
       // temperature (mtsac.py:713-731)
       alpha_adam(al, cfg.alpha_lr, cfg.adam_b1, cfg.adam_b2, cfg.adam_eps, cfg.alpha_max_grad_norm, cur);
       // post-update parameter norms: trunk |p|^2 replicated, head |p|^2 summed over shards
@@ -983,7 +991,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
           continue;
         }
         const size_t np = (size_t)net->E * 3 * net->width * net->wld;
-        if ((rc = e->alloc(&net->wp[w][i], np))) return bad(rc);
+        if (w == 0 && (rc = e->alloc(&net->wp[0][i], np))) return bad(rc);  // data grads use p only
         if ((rc = e->alloc(&net->wtp[w][i], np))) return bad(rc);
       }
   }

@@ -409,31 +409,49 @@ __global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, con
 }
 
 // ------------------------------------------------------------------ critic -> action grad -> policy grad
+// AG_RW rows per wavefront: the critic layer-0 kernel rows (A x Wc) are read once per AG_RW rows.
+// Per row the sums run w = lane, lane + 64, ... then over the wave: the same association as a
+// one-row-per-wave loop.
+constexpr int AG_RW = 4;
+
 __global__ __launch_bounds__(256) void action_grad_kernel(ActionGradParams p) {
   const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= p.B) return;
+  const int b0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * AG_RW;
+  if (b0 >= p.B) return;
   const int A = p.A;
-  float ga[8];
+  int rows[AG_RW];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) ga[j] = 0.f;
+  for (int r = 0; r < AG_RW; ++r) rows[r] = min(b0 + r, p.B - 1);
+  float ga[AG_RW][8];
+#pragma unroll
+  for (int r = 0; r < AG_RW; ++r)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ga[r][j] = 0.f;
   for (int e = 0; e < p.E; ++e) {
-    const float* dz = p.dz1 + e * p.s_dz + (long long)b * p.Wc;
+    const float* dz = p.dz1 + e * p.s_dz;
     const float* W0 = p.W0 + e * p.s_W0;
     for (int w = lane; w < p.Wc; w += 64) {
-      const float g = dz[w];
+      float wv[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < A) ga[j] += g * W0[(long long)j * p.Wc + w];
+      for (int j = 0; j < 8; ++j) wv[j] = j < A ? W0[(long long)j * p.Wc + w] : 0.f;
+#pragma unroll
+      for (int r = 0; r < AG_RW; ++r) {
+        const float g = dz[(long long)rows[r] * p.Wc + w];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ga[r][j] += g * wv[j];
+      }
     }
   }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) ga[j] = wsum(ga[j]);
-  if (lane < A) {
+  for (int r = 0; r < AG_RW; ++r) {
+    const int b = b0 + r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ga[r][j] = j < A ? wsum(ga[r][j]) : 0.f;
+    if (b >= p.B || lane >= A) continue;
     float g_a = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      if (j == lane) g_a = ga[j];
+      if (j == lane) g_a = ga[r][j];
     const float* c = p.cache + (long long)b * 5 * A;
     const float ls = c[A + lane], a = c[3 * A + lane], eps = c[4 * A + lane];
     const float g_logpi = p.alpha_w[b];
@@ -525,7 +543,7 @@ void head_backward_weight(const HeadParams& hp, const float* dout, long long s_d
 }
 
 void action_grad(const ActionGradParams& p, hipStream_t st) {
-  hipLaunchKernelGGL(action_grad_kernel, dim3((p.B + 3) / 4), dim3(256), 0, st, p);
+  hipLaunchKernelGGL(action_grad_kernel, dim3((p.B + 4 * AG_RW - 1) / (4 * AG_RW)), dim3(256), 0, st, p);
 }
 
 void row_alpha(const int* task, int task_begin, const float* log_alpha, int T_glob, int B, int use_task_weights,

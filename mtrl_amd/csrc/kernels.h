@@ -235,6 +235,15 @@ struct OptScalars {
 };
 void grad_norm_finalize(const float* partials, int nparts, const float* extra_sq /*nullable*/,
                         float max_norm, OptScalars* sc, hipStream_t st);
+// bf16 split planes of updated parameters: flat p[begin, begin + members * member_n) is written
+// as planes[e][q][k] (plane stride ps, member stride 3 * ps), k < member_n -- the natural-layout
+// planes of a dense kernel leaf whose row stride equals its width
+struct PlaneSeg {
+  long long begin, member_n, members;
+  __bf16* planes;
+  long long ps;
+};
+constexpr int MAX_PLANE_SEGS = 8;
 struct AdamParams {
   float* p; float* m; float* v; const float* g;
   float* target;        // polyak target (critic) or null
@@ -242,6 +251,8 @@ struct AdamParams {
   float lr, b1, b2, eps, tau;
   OptScalars* sc;
   float* p_partials;    // sum of squares of new params per block
+  int nseg;             // planes of the new params to write (offsets relative to p)
+  PlaneSeg seg[MAX_PLANE_SEGS];
 };
 // p_partials accumulate |p_new|^2 over [norm_from, n) only (the replicated trunk range)
 int adam_update(const AdamParams& a, float max_norm, long long norm_from, int max_blocks, hipStream_t st);
