@@ -100,6 +100,7 @@ struct mtsac_engine {
   mtsac_config cfg{};
   int device = 0;
   hipStream_t st = nullptr, s1 = nullptr, s2 = nullptr, s3 = nullptr;
+  hipStream_t s4 = nullptr;  // lane 4: the trunk-gradient all-reduce buckets (one collective stream)
   hipStream_t cur = nullptr;
   std::vector<hipEvent_t> evpool;
   size_t ev_next = 0;
@@ -144,7 +145,7 @@ struct mtsac_engine {
   float* partials = nullptr;
   // split-K workspaces, one per lane: segments on different lanes may run concurrently, the
   // segments of one lane are ordered by the step DAG (see seg())
-  float* ws_lane[4] = {};
+  float* ws_lane[5] = {};
   int cur_lane = 0;
   float* pn = nullptr;  // [critic trunk |p|^2, actor trunk, critic heads, actor heads]
   float* log_alpha = nullptr;
@@ -192,7 +193,7 @@ struct mtsac_engine {
     if (comm) ncclCommDestroy(comm);
     for (void* p : allocs) (void)hipFree(p);
     for (hipEvent_t e : evpool) (void)hipEventDestroy(e);
-    for (hipStream_t x : {st, s1, s2, s3})
+    for (hipStream_t x : {st, s1, s2, s3, s4})
       if (x) (void)hipStreamDestroy(x);
   }
 
@@ -589,7 +590,7 @@ struct mtsac_engine {
       if (g) (void)hipGraphDestroy(g);
       if (r != hipSuccess) comm_error = std::string("step graph build: ") + hipGetErrorString(r);
     } else {
-      hipStream_t L = timing_serial ? st : (lane == 0 ? st : lane == 1 ? s1 : lane == 2 ? s2 : s3);
+      hipStream_t L = timing_serial ? st : (lane == 0 ? st : lane == 1 ? s1 : lane == 2 ? s2 : lane == 3 ? s3 : s4);
       for (int d : deps)
         if (segs[d].lane != L) (void)hipStreamWaitEvent(L, segs[d].ev, 0);
       cur = L;
@@ -608,14 +609,36 @@ struct mtsac_engine {
   }
 
   // trunk backward as segments: data chain on lane 1, weight grads on lane 3
+  // With RCCL, each hidden layer's gradient (b_i, W_i: one contiguous trunk range) is all-reduced
+  // on lane 4 as soon as its weight grad is done, overlapping the rest of the backward; the
+  // buckets form one chain (every rank issues its collectives in the same order).  Layer 0 and
+  // the scalar tail follow in the optimizer segment (reduce_rest).
   int backward_segs(Net& net, const float* params, const float* X, int ldx, float** acts, __bf16** actp, float** dz,
                     __bf16** dzp, int d_top, int w_prev, int M) {
-    int dprev = d_top, wprev = w_prev;
+    int dprev = d_top, wprev = w_prev, rprev = -1;
+    const bool bucket = comm != nullptr && net.depth > 1;
     for (int i = net.depth - 1; i >= 0; --i) {
       wprev = seg({dprev, wprev}, 3, [&, i] { wgrad_layer(net, X, ldx, acts, actp, dz, dzp, i, M); });
+      if (bucket && i > 0) {
+        const long long b = net.off_b[i], e = (i + 1 < net.depth) ? net.off_b[i + 1] : net.n_flat;
+        rprev = rprev < 0 ? seg({wprev}, 4, [&, b, e] { allreduce(net.g + b, (size_t)(e - b)); })
+                          : seg({wprev, rprev}, 4, [&, b, e] { allreduce(net.g + b, (size_t)(e - b)); });
+      }
       if (i > 0) dprev = seg({dprev}, 1, [&, i] { dgrad_layer(net, params, acts, dz, dzp, i, M); });
     }
-    return seg({dprev, wprev}, 1, [] {});  // join point
+    if (rprev >= 0) return seg({dprev, wprev, rprev}, 1, [] {});  // join point
+    return seg({dprev, wprev}, 1, [] {});
+  }
+
+  // the trunk-gradient all-reduce left after backward_segs: everything, or (buckets) layer 0 and
+  // the scalar tail
+  void reduce_rest(Net& net) {
+    if (comm != nullptr && net.depth > 1) {
+      allreduce(net.g + net.trunk_off, (size_t)(net.off_b[1] - net.trunk_off));
+      allreduce(net.g + net.n_flat, (size_t)EXTRA);
+    } else {
+      allreduce(net.g + net.trunk_off, (size_t)(net.n_flat - net.trunk_off + EXTRA));
+    }
   }
 
   // ------------------------------------------------------------ one gradient step
@@ -720,7 +743,7 @@ struct mtsac_engine {
     // reduce over shards, clip + Adam + Polyak (mtsac.py:599-613)
     const int s_co = seg({s_cb}, 1, [&] {
       head_sq(critic);
-      allreduce(critic.g + critic.trunk_off, (size_t)(critic.n_flat - critic.trunk_off + EXTRA));
+      reduce_rest(critic);
       optimize(critic, cfg.critic_lr, cfg.critic_max_grad_norm, true, 0);
       refresh_wt(critic, critic.p, 0, cur, true);
       refresh_wt(critic, critic.tgt, 1, cur, true);
@@ -770,7 +793,7 @@ struct mtsac_engine {
       AlphaParams al = alpha_params();
       alpha_grad(al, cur);
       head_sq(actor);
-      allreduce(actor.g + actor.trunk_off, (size_t)(actor.n_flat - actor.trunk_off + EXTRA));
+      reduce_rest(actor);
       optimize(actor, cfg.actor_lr, cfg.actor_max_grad_norm, false, 1);
       refresh_wt(actor, actor.p, 0, cur, true);
       // temperature (mtsac.py:713-731)
@@ -960,7 +983,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     delete e;
     return r;
   };
-  for (hipStream_t* x : {&e->st, &e->s1, &e->s2, &e->s3})
+  for (hipStream_t* x : {&e->st, &e->s1, &e->s2, &e->s3, &e->s4})
     if (hipStreamCreateWithFlags(x, hipStreamNonBlocking) != hipSuccess) return bad(fail(-5, "stream"));
   e->cur = e->st;
   for (int i = 0; i < 128; ++i) {

@@ -114,7 +114,8 @@ def test_update_matches_oracle(name, precision):
     eng.close()
 
 
-def test_graph_replay_is_deterministic_and_matches_eager():
+@pytest.mark.parametrize("precision", [0, 1], ids=["fp32", "split3"])
+def test_graph_replay_is_deterministic_and_matches_eager(precision):
     from mtrl_amd import _lib as L
 
     T, W, n = 3, 32, 4
@@ -123,7 +124,7 @@ def test_graph_replay_is_deterministic_and_matches_eager():
     st = _f32_state(cfg, seed=3)
     outs = []
     for graph in (False, True, True):
-        eng = _engine_for(cfg, capacity=64, graph=graph)
+        eng = _engine_for(cfg, capacity=64, graph=graph, precision=precision)
         _load_state(eng, st)
         eng.buffer_fill_synthetic(99)
         eng.seed_rng(1)
@@ -192,9 +193,12 @@ def test_rollout_actions_match_oracle():
     eng.close()
 
 
-def test_rccl_single_rank_graph_path():
-    """The RCCL all-reduce points captured in the hipGraph (1-rank communicator):
-    same results as the communicator-free engine."""
+@pytest.mark.parametrize("precision", [0, 1], ids=["fp32", "split3"])
+@pytest.mark.parametrize("graph", [True, False], ids=["graph", "eager"])
+def test_rccl_single_rank_graph_path(graph, precision):
+    """The RCCL all-reduce points (per-layer buckets on their own stream, then layer 0 and the
+    scalar tail), captured in the hipGraph or issued eagerly (1-rank communicator): same
+    results as the communicator-free engine."""
     from mtrl_amd import _lib as L
     from mtrl_amd.engine import MTSACEngine
 
@@ -204,7 +208,7 @@ def test_rccl_single_rank_graph_path():
     st = _f32_state(cfg, seed=4)
     outs = []
     for use_comm in (False, True):
-        eng = _engine_for(cfg, capacity=64, graph=True)
+        eng = _engine_for(cfg, capacity=64, graph=graph, precision=precision)
         _load_state(eng, st)
         if use_comm:
             eng.comm_init(MTSACEngine.comm_unique_id(), 1, 0)
