@@ -45,7 +45,7 @@ HBM_PEAK_GBS = 8000.0
 # enum mtsac_gemm_family (include/mtsac.h) -> the rocprof kernel(s) of that family, per precision
 GEMM_FAMILIES = {
     "split3": {
-        0: "gemm_x3p_kernel<Geo<256, 256, 2, 4, 3, 16>, false, false, 1, *> (hidden-layer forward, NT on planes, bias+ReLU)",
+        0: "gemm_x3p_kernel<Geo<256, 256, 2, 4, 3, 16>, false, true, 1, *> (hidden-layer forward, planes: activations row-major x kernel k-major, bias+ReLU)",
         1: "gemm_x3p_kernel<Geo<256, 256, 2, 4, 3, 16>, false, false, 2, *> (hidden-layer data grad, NT on planes, ReLU mask)",
         2: "gemm_x3p_kernel<Geo<256, 256, 2, 4, 3, 16>, true, true, 0, false> (hidden-layer weight grad, k-major planes, split-K)",
         3: "gemm_x3_kernel<false, false, 1> (input-layer forward, on-the-fly split)",

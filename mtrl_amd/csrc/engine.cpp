@@ -62,13 +62,15 @@ struct Net {
   // transposed hidden kernels W_i^T ([E][out][in], i >= 1) of p (wt[0]) and tgt (wt[1]): the
   // trunk forward runs as an NT product against them (k-contiguous operands on both sides)
   float* wt[2][MAXD] = {};
-  // split3: bf16 planes of W_i ([E][3][in][wld], data grads; of p only) and of W_i^T
-  // ([E][3][out][wld], forward) for i >= 1, of p ([0]) and tgt ([1]); activation / data-grad planes of this net are
-  // [E][3][arows][ald] (arows = B rounded up to 32 with zero rows, ald = width rounded up to 32)
+  // split3: bf16 planes of the hidden kernels W_i ([E][3][wrows][wld], i >= 1) of p ([0]) and tgt
+  // ([1]), rows and columns rounded up to 32 with zeros.  The forward reads them k-major (its
+  // B(n, k) = W[k][n]), the data grad row-major (B(n, k) = W[n][k]).  Activation / data-grad
+  // planes of this net are [E][3][arows][ald] (arows = B rounded up to 32 with zero rows,
+  // ald = width rounded up to 32).
   __bf16* wp[2][MAXD] = {};
-  __bf16* wtp[2][MAXD] = {};
-  long long wld = 0, arows = 0, ald = 0;
+  long long wld = 0, wrows = 0, arows = 0, ald = 0;
   long long aps() const { return arows * ald; }  // plane stride of activation planes
+  long long wps() const { return wrows * wld; }  // plane stride of kernel planes
   OptScalars* sc = nullptr;
 
   void layout(int in, int in_ld_, int W, int D, int T, int hd_, int E_) {
@@ -299,16 +301,17 @@ struct mtsac_engine {
     const bool pl = planes && which >= 0 && actp != nullptr;
     for (int i = 0; i < net.depth; ++i) {
       const bool last = i == net.depth - 1;
-      if (pl && i > 0) {  // NT on planes: acts[i-1] . (W_i^T)^T
+      if (pl && i > 0) {  // on planes: acts[i-1] (row-major) . W_i (k-major)
         SplitGemmParams g{};
         g.A = actp[i - 1];
         g.lda = net.ald;
         g.pA = net.aps();
         g.sA = 3 * net.aps();
-        g.B = net.wtp[which][i];
+        g.B = net.wp[which][i];
         g.ldb = net.wld;
-        g.pB = (long long)net.width * net.wld;
-        g.sB = 3 * g.pB;
+        g.pB = net.wps();
+        g.sB = 3 * net.wps();
+        g.b_kmajor = 1;
         g.C = acts[i];
         g.ldc = net.width;
         g.sC = (long long)M * net.width;
@@ -354,9 +357,9 @@ struct mtsac_engine {
     }
   }
 
-  // after every write of params: Net::wt[which] (fp32) or the planes wp / wtp[which] (split3);
-  // natural_fused: the optimizer already wrote wp (see optimize())
-  void refresh_wt(Net& net, const float* params, int which, hipStream_t s, bool natural_fused = false) {
+  // after every write of params: Net::wt[which] (fp32) or the planes wp[which] (split3);
+  // fused: the optimizer already wrote them (see optimize())
+  void refresh_wt(Net& net, const float* params, int which, hipStream_t s, bool fused = false) {
     for (int i = 1; i < net.depth; ++i) {
       if (!planes) {
         transpose_f32(params + net.off_W[i], net.ms_W[i], net.wt[which][i], net.ms_W[i], net.width, net.width, net.E,
@@ -370,17 +373,12 @@ struct mtsac_engine {
       sp.rows = net.width;
       sp.cols = net.width;
       sp.ldo = net.wld;
-      sp.po = (long long)net.width * net.wld;
-      sp.so = 3 * sp.po;
-      sp.out_rows = net.width;
+      sp.po = net.wps();
+      sp.so = 3 * net.wps();
+      sp.out_rows = (int)net.wrows;
       sp.out_cols = (int)net.wld;
-      // natural planes (data grads) exist for p only; the optimizer writes them itself
-      if (which == 0 && !(natural_fused && net.wld == net.width)) {
-        sp.out = net.wp[0][i];
-        split_planes(sp, false, net.E, s);
-      }
-      sp.out = net.wtp[which][i];
-      split_planes(sp, true, net.E, s);
+      sp.out = net.wp[which][i];
+      if (!(fused && planes_fusable(net))) split_planes(sp, false, net.E, s);
     }
   }
 
@@ -443,8 +441,8 @@ struct mtsac_engine {
       g.sA = 3 * net.aps();
       g.B = net.wp[0][i];
       g.ldb = net.wld;
-      g.pB = (long long)net.width * net.wld;
-      g.sB = 3 * g.pB;
+      g.pB = net.wps();
+      g.sB = 3 * net.wps();
       g.C = dz[i - 1];
       g.ldc = net.width;
       g.sC = (long long)M * net.width;
@@ -545,12 +543,18 @@ struct mtsac_engine {
     a.g += net.trunk_off;
     if (a.target) a.target += net.trunk_off;
     a.n = net.n_flat - net.trunk_off;
-    if (planes && net.wld == net.width)  // hidden kernels' natural planes straight from the update
-      for (int i = 1; i < net.depth && a.nseg < MAX_PLANE_SEGS; ++i)
-        a.seg[a.nseg++] = PlaneSeg{net.off_W[i] - net.trunk_off, net.ms_W[i], net.E, net.wp[0][i],
-                                   (long long)net.width * net.wld};
+    if (planes_fusable(net))  // hidden kernels' planes (params and Polyak target) from the update
+      for (int i = 1; i < net.depth && a.nseg + 2 <= MAX_PLANE_SEGS; ++i) {
+        a.seg[a.nseg++] = PlaneSeg{net.off_W[i] - net.trunk_off, net.ms_W[i], net.E, net.wp[0][i], net.wps(), 0};
+        if (polyak) a.seg[a.nseg++] = PlaneSeg{net.off_W[i] - net.trunk_off, net.ms_W[i], net.E, net.wp[1][i], net.wps(), 1};
+      }
     int na = adam_update(a, max_norm, 0, PART, cur);
     sum_partials(partials, na, pn + slot, cur);
+  }
+
+  // the kernel planes can come straight out of the flat update when their layout is the leaf's
+  bool planes_fusable(const Net& net) const {
+    return planes && net.wld == net.width && net.wrows == net.width && net.depth - 1 <= MAX_PLANE_SEGS / 2;
   }
 
   void head_sq(Net& net) {  // local |g_head|^2 into the scalar tail
@@ -1005,6 +1009,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   e->planes = c.precision == MTSAC_FP32_SPLIT3;
   for (Net* net : {&e->actor, &e->critic}) {
     net->wld = align_up(net->width, 32);
+    net->wrows = align_up(net->width, 32);
     net->ald = align_up(net->width, 32);
     net->arows = align_up(e->B, 32);
     for (int w = 0; w < (net == &e->critic ? 2 : 1); ++w)
@@ -1013,9 +1018,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
           if ((rc = e->alloc(&net->wt[w][i], (size_t)net->ms_W[i] * net->E))) return bad(rc);
           continue;
         }
-        const size_t np = (size_t)net->E * 3 * net->width * net->wld;
-        if (w == 0 && (rc = e->alloc(&net->wp[0][i], np))) return bad(rc);  // data grads use p only
-        if ((rc = e->alloc(&net->wtp[w][i], np))) return bad(rc);
+        if ((rc = e->alloc(&net->wp[w][i], (size_t)net->E * 3 * net->wps()))) return bad(rc);
       }
   }
   {  // split-K workspaces: the largest GEMM that splits, per lane

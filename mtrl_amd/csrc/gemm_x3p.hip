@@ -326,25 +326,40 @@ __global__ __launch_bounds__(256) void split_kernel(SplitParams s) {
   }
 }
 
-// db[z][n] = sum over rows of x[z][rows][n] in two deterministic passes (COLSUM_CHUNKS row
-// chunks per column, then the chunks in order)
+// db[z][n] = sum over rows of x[z][rows][n] in two deterministic passes.  Pass 1: a workgroup
+// takes 256 columns (4 per lane, 16-B loads) of one row chunk; its 4 waves sum interleaved rows
+// (4-deep unrolled) and are added in wave order.  Pass 2: the chunks in order.
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ x, int rows, int cols, int ld,
                                                              long long sx, int chunks, float* __restrict__ part) {
-  const int z = blockIdx.z, c = blockIdx.x * 256 + threadIdx.x, ch = blockIdx.y;
-  if (c >= cols) return;
+  __shared__ float4 red[4][64];
+  const int z = blockIdx.z, ch = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + 4 * lane;
   const int per = (rows + chunks - 1) / chunks;
   const int r0 = ch * per, r1 = min(rows, r0 + per);
-  const float* xp = x + z * sx + c;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int r = r0;
-  for (; r + 4 <= r1; r += 4) {
-    s0 += xp[(long long)r * ld];
-    s1 += xp[(long long)(r + 1) * ld];
-    s2 += xp[(long long)(r + 2) * ld];
-    s3 += xp[(long long)(r + 3) * ld];
+  const float* xp = x + z * sx;
+  float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+  if (c < cols) {
+    int r = r0 + wave;
+    for (; r + 4 < r1; r += 8) {
+      const float4 a = *reinterpret_cast<const float4*>(xp + (long long)r * ld + c);
+      const float4 b = *reinterpret_cast<const float4*>(xp + (long long)(r + 4) * ld + c);
+      s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+      s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
+    }
+    for (; r < r1; r += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(xp + (long long)r * ld + c);
+      s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+    }
   }
-  for (; r < r1; ++r) s0 += xp[(long long)r * ld];
-  part[((long long)z * chunks + ch) * cols + c] = (s0 + s1) + (s2 + s3);
+  red[wave][lane] = make_float4(s0.x + s1.x, s0.y + s1.y, s0.z + s1.z, s0.w + s1.w);
+  __syncthreads();
+  if (wave == 0 && c < cols) {
+    const float4 a = red[0][lane], b = red[1][lane], d = red[2][lane], e = red[3][lane];
+    const float4 t = make_float4(((a.x + b.x) + d.x) + e.x, ((a.y + b.y) + d.y) + e.y, ((a.z + b.z) + d.z) + e.z,
+                                 ((a.w + b.w) + d.w) + e.w);
+    *reinterpret_cast<float4*>(part + ((long long)z * chunks + ch) * cols + c) = t;
+  }
 }
 
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int cols, int chunks,
@@ -354,6 +369,20 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
   float s = 0.f;
   for (int ch = 0; ch < chunks; ++ch) s += part[((long long)z * chunks + ch) * cols + c];
   db[z * sdb + c] = s;
+}
+
+// scalar fallback (cols or ld not multiples of 4)
+__global__ __launch_bounds__(256) void colsum_partial_scalar_kernel(const float* __restrict__ x, int rows, int cols,
+                                                                    int ld, long long sx, int chunks,
+                                                                    float* __restrict__ part) {
+  const int z = blockIdx.z, c = blockIdx.x * 256 + threadIdx.x, ch = blockIdx.y;
+  if (c >= cols) return;
+  const int per = (rows + chunks - 1) / chunks;
+  const int r0 = ch * per, r1 = min(rows, r0 + per);
+  const float* xp = x + z * sx + c;
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += xp[(long long)r * ld];
+  part[((long long)z * chunks + ch) * cols + c] = s;
 }
 
 }  // namespace
@@ -532,9 +561,14 @@ void split_planes(const SplitParams& s, bool transpose, int batch, hipStream_t s
 
 void colsum(const float* x, int rows, int cols, int ld, long long sx, int batch, float* part, float* db,
             long long sdb, hipStream_t st) {
-  const int chunks = std::max(1, std::min(COLSUM_CHUNKS, rows));
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3((cols + 255) / 256, chunks, batch), dim3(256), 0, st, x, rows, cols,
-                     ld, sx, chunks, part);
+  // ~256 rows per chunk keeps every lane streaming; COLSUM_CHUNKS bounds the partials
+  const int chunks = std::max(1, std::min(COLSUM_CHUNKS, (rows + 255) / 256));
+  if (cols % 4 == 0 && ld % 4 == 0 && sx % 4 == 0)
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3((cols + 255) / 256, chunks, batch), dim3(256), 0, st, x, rows, cols,
+                       ld, sx, chunks, part);
+  else
+    hipLaunchKernelGGL(colsum_partial_scalar_kernel, dim3((cols + 255) / 256, chunks, batch), dim3(256), 0, st, x,
+                       rows, cols, ld, sx, chunks, part);
   hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256, 1, batch), dim3(256), 0, st, part, cols, chunks, db,
                      sdb);
 }

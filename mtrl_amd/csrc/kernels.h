@@ -242,6 +242,7 @@ struct PlaneSeg {
   long long begin, member_n, members;
   __bf16* planes;
   long long ps;
+  int of_target;        // 1: planes of the Polyak target's new value instead of the params'
 };
 constexpr int MAX_PLANE_SEGS = 8;
 struct AdamParams {

@@ -120,17 +120,29 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm,
     }
     if (i >= norm_from4) acc += sq;  // |p|^2 of the replicated (trunk) range only
     p4[i] = p;
-    for (int sg = 0; sg < a.nseg; ++sg) {  // split planes of the new params (next GEMMs' operands)
+    m4[i] = m;
+    v4[i] = v;
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (POLYAK) {
+      t = t4[i];
+      t.x = a.tau * p.x + omtau * t.x;
+      t.y = a.tau * p.y + omtau * t.y;
+      t.z = a.tau * p.z + omtau * t.z;
+      t.w = a.tau * p.w + omtau * t.w;
+      t4[i] = t;
+    }
+    for (int sg = 0; sg < a.nseg; ++sg) {  // split planes of the new values (next GEMMs' operands)
       const PlaneSeg& ps = a.seg[sg];
       const long long f = 4 * i - ps.begin;
       if (f < 0 || f >= ps.member_n * ps.members) continue;
       const long long e = f / ps.member_n, k = f - e * ps.member_n;
+      const float* src = ps.of_target ? &t.x : pp;
       typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
       bf16x4 h, mm, l;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const __bf16 hh = (__bf16)pp[c];
-        const float r1 = pp[c] - (float)hh;
+        const __bf16 hh = (__bf16)src[c];
+        const float r1 = src[c] - (float)hh;
         const __bf16 m1 = (__bf16)r1;
         h[c] = hh;
         mm[c] = m1;
@@ -140,16 +152,6 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm,
       *reinterpret_cast<bf16x4*>(dst) = h;
       *reinterpret_cast<bf16x4*>(dst + ps.ps) = mm;
       *reinterpret_cast<bf16x4*>(dst + 2 * ps.ps) = l;
-    }
-    m4[i] = m;
-    v4[i] = v;
-    if (POLYAK) {
-      float4 t = t4[i];
-      t.x = a.tau * p.x + omtau * t.x;
-      t.y = a.tau * p.y + omtau * t.y;
-      t.z = a.tau * p.z + omtau * t.z;
-      t.w = a.tau * p.w + omtau * t.w;
-      t4[i] = t;
     }
   }
   acc = block_sum256(acc);

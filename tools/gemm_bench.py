@@ -2,7 +2,7 @@
 import ctypes
 import sys
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from mtrl_amd import _lib as L  # noqa: E402
 
 lib = L.load()

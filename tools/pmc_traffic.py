@@ -12,7 +12,7 @@ import sys
 
 FAMILY_KEYS = {
     "split3": {
-        0: "gemm_x3p_kernel<mtsac::(anonymous namespace)::Geo<256, 256, 2, 4, 3, 16>, false, false, 1,",
+        0: "gemm_x3p_kernel<mtsac::(anonymous namespace)::Geo<256, 256, 2, 4, 3, 16>, false, true, 1,",
         1: "gemm_x3p_kernel<mtsac::(anonymous namespace)::Geo<256, 256, 2, 4, 3, 16>, false, false, 2,",
         2: "gemm_x3p_kernel<mtsac::(anonymous namespace)::Geo<256, 256, 2, 4, 3, 16>, true, true, 0,",
         3: "gemm_x3_kernel<false, false, 1>",

@@ -1,0 +1,24 @@
+"""Eager steps of one small task shard (for rocprofv3 --kernel-trace --stats)."""
+import sys
+
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+from mtrl_amd import _lib as L  # noqa: E402
+from mtrl_amd.engine import MTSACEngine, make_config  # noqa: E402
+from mtrl_amd.init import init_mtsac  # noqa: E402
+
+T, W = 50, 2048
+tl = int(sys.argv[1]) if len(sys.argv) > 1 else 7
+cfg = make_config(num_tasks=T, task_begin=0, task_count=tl, obs_dim=39 + T, actor_width=W, critic_width=W,
+                  batch_per_task=128, capacity=100_000, clip=1, precision=1)
+eng = MTSACEngine(cfg, device=0)
+actor, critic = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=1, task_begin=0, task_count=tl)
+eng.set_params(L.ACTOR, actor)
+eng.set_params(L.CRITIC, critic)
+eng.set_params(L.CRITIC_TARGET, critic)
+eng.buffer_fill_synthetic(1234)
+eng.seed_rng(1)
+eng.enable_graph(False)
+eng.set_timing(True, serial=True)
+eng.update_many(10)
+eng.synchronize()
+eng.close()

@@ -1,13 +1,13 @@
 import ctypes, sys
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from mtrl_amd import _lib as L
 lib = L.load()
 # (name, epi, layout bits: 1 = A k-major, 2 = B k-major, M, N, K, E)
-cases = [("NT-E2", 1, 0, 6400, 2048, 2048, 2), ("NT-E1", 2, 0, 6400, 2048, 2048, 1),
-         ("TN-E2", 0, 3, 2048, 2048, 6400, 2), ("TN-E1", 0, 3, 2048, 2048, 6400, 1),
-         ("NT-4k", 0, 0, 4096, 4096, 4096, 1), ("TN-4k", 0, 3, 4096, 4096, 4096, 1),
-         ("NT-M3200", 1, 0, 3200, 2048, 2048, 2), ("NT-M1600", 1, 0, 1600, 2048, 2048, 2),
-         ("NT-M800", 1, 0, 800, 2048, 2048, 2), ("NT-M768E1", 1, 0, 768, 2048, 2048, 1)]
+cases = []
+for lay, nm in [(0, "rr"), (2, "rk"), (1, "kr"), (3, "kk")]:
+    cases += [(f"fwd-{nm}-E2", 1, lay, 6400, 2048, 2048, 2), (f"fwd-{nm}-E1", 1, lay, 6400, 2048, 2048, 1),
+              (f"wg-{nm}-E2", 0, lay, 2048, 2048, 6400, 2), (f"sq4k-{nm}", 0, lay, 4096, 4096, 4096, 1),
+              (f"fwd-{nm}-M896", 1, lay, 896, 2048, 2048, 2)]
 for geo in [int(g) for g in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2,3,4").split(",")]:
     lib.mtsac_debug_x3p_geo(geo)
     for name, epi, lay, M, N, K, E in cases:
