@@ -69,8 +69,11 @@ struct Net {
   // ald = width rounded up to 32).
   __bf16* wp[2][MAXD] = {};
   long long wld = 0, wrows = 0, arows = 0, ald = 0;
+  long long xld = 0;  // input planes' row stride = layer-0 kernel plane rows (in_dim rounded up to 32)
   long long aps() const { return arows * ald; }  // plane stride of activation planes
-  long long wps() const { return wrows * wld; }  // plane stride of kernel planes
+  long long wps() const { return wrows * wld; }  // plane stride of hidden kernel planes
+  long long w0ps() const { return xld * wld; }   // plane stride of the layer-0 kernel planes
+  long long kps(int i) const { return i == 0 ? w0ps() : wps(); }
   OptScalars* sc = nullptr;
 
   void layout(int in, int in_ld_, int W, int D, int T, int hd_, int E_) {
@@ -142,6 +145,17 @@ struct mtsac_engine {
   __bf16* dzap[MAXD] = {};
   __bf16* dzcp[MAXD] = {};
   float* cs_part = nullptr;  // column-sum partials (bias grads beside the plane weight-grad GEMM)
+  // planes of the GEMM-ready trunk inputs (xa, xan, xc, xcn, xcp): [3][arows][xld]
+  struct InPlanes {
+    const float* x;
+    __bf16* p;
+  };
+  InPlanes inp[5] = {};
+  __bf16* in_planes(const float* X) const {
+    for (const InPlanes& q : inp)
+      if (q.x == X) return q.p;
+    return nullptr;
+  }
   float *logpi_n = nullptr, *logpi = nullptr, *y = nullptr, *dq = nullptr, *row_a = nullptr, *row_b = nullptr,
         *row_c = nullptr, *alpha_w = nullptr, *cache = nullptr, *dout_a = nullptr;
   float* partials = nullptr;
@@ -299,18 +313,32 @@ struct mtsac_engine {
   void trunk_forward(Net& net, const float* params, int which, const float* X, int ldx, float** acts, __bf16** actp,
                      int M) {
     const bool pl = planes && which >= 0 && actp != nullptr;
+    __bf16* xp = pl ? in_planes(X) : nullptr;
+    if (xp) {  // the input's planes (rows >= M and columns >= in_dim stay zero)
+      SplitParams sp{};
+      sp.x = X;
+      sp.ldx = ldx;
+      sp.rows = M;
+      sp.cols = net.in_dim;
+      sp.out = xp;
+      sp.ldo = net.xld;
+      sp.po = net.arows * net.xld;
+      sp.out_rows = M;
+      sp.out_cols = (int)net.xld;
+      split_planes(sp, false, 1, cur);
+    }
     for (int i = 0; i < net.depth; ++i) {
       const bool last = i == net.depth - 1;
-      if (pl && i > 0) {  // on planes: acts[i-1] (row-major) . W_i (k-major)
+      if (pl && (i > 0 || xp)) {  // on planes: input (row-major) . W_i (k-major)
         SplitGemmParams g{};
-        g.A = actp[i - 1];
-        g.lda = net.ald;
-        g.pA = net.aps();
-        g.sA = 3 * net.aps();
+        g.A = i == 0 ? xp : actp[i - 1];
+        g.lda = i == 0 ? net.xld : net.ald;
+        g.pA = i == 0 ? net.arows * net.xld : net.aps();
+        g.sA = i == 0 ? 0 : 3 * net.aps();
         g.B = net.wp[which][i];
         g.ldb = net.wld;
-        g.pB = net.wps();
-        g.sB = 3 * net.wps();
+        g.pB = net.kps(i);
+        g.sB = 3 * net.kps(i);
         g.b_kmajor = 1;
         g.C = acts[i];
         g.ldc = net.width;
@@ -325,10 +353,11 @@ struct mtsac_engine {
         }
         g.M = M;
         g.N = net.width;
-        g.K = (int)net.ald;
+        g.K = (int)(i == 0 ? net.xld : net.ald);
+        g.tag = i == 0 ? 1 : 0;
         g.splits = -1;
         g.ws = ws_lane[cur_lane];
-        gemmp(g, EPI_BIAS_RELU, net.E, MTSAC_FAM_FORWARD);
+        gemmp(g, EPI_BIAS_RELU, net.E, i == 0 ? MTSAC_FAM_INPUT_FORWARD : MTSAC_FAM_FORWARD);
         continue;
       }
       GemmParams g{};
@@ -360,7 +389,7 @@ struct mtsac_engine {
   // after every write of params: Net::wt[which] (fp32) or the planes wp[which] (split3);
   // fused: the optimizer already wrote them (see optimize())
   void refresh_wt(Net& net, const float* params, int which, hipStream_t s, bool fused = false) {
-    for (int i = 1; i < net.depth; ++i) {
+    for (int i = planes ? 0 : 1; i < net.depth; ++i) {
       if (!planes) {
         transpose_f32(params + net.off_W[i], net.ms_W[i], net.wt[which][i], net.ms_W[i], net.width, net.width, net.E,
                       s);
@@ -370,12 +399,12 @@ struct mtsac_engine {
       sp.x = params + net.off_W[i];
       sp.ldx = net.width;
       sp.sx = net.ms_W[i];
-      sp.rows = net.width;
+      sp.rows = i == 0 ? net.in_dim : net.width;
       sp.cols = net.width;
       sp.ldo = net.wld;
-      sp.po = net.wps();
-      sp.so = 3 * net.wps();
-      sp.out_rows = (int)net.wrows;
+      sp.po = net.kps(i);
+      sp.so = 3 * net.kps(i);
+      sp.out_rows = (int)(i == 0 ? net.xld : net.wrows);
       sp.out_cols = (int)net.wld;
       sp.out = net.wp[which][i];
       if (!(fused && planes_fusable(net))) split_planes(sp, false, net.E, s);
@@ -387,12 +416,13 @@ struct mtsac_engine {
   //   dgrad_layer: dz[i-1] = (dz[i] W_i^T) * [acts[i-1] > 0]
   void wgrad_layer(Net& net, const float* X, int ldx, float** acts, __bf16** actp, float** dz, __bf16** dzp, int i,
                    int M) {
-    if (planes && i > 0 && actp && dzp) {  // TN on k-major planes; bias grad by column sums
+    const __bf16* xp = (planes && i == 0) ? in_planes(X) : nullptr;
+    if (planes && (i > 0 || xp) && actp && dzp && dzp[i]) {  // TN on k-major planes; bias grad by column sums
       SplitGemmParams g{};
-      g.A = actp[i - 1];
-      g.lda = net.ald;
-      g.pA = net.aps();
-      g.sA = 3 * net.aps();
+      g.A = i == 0 ? xp : actp[i - 1];
+      g.lda = i == 0 ? net.xld : net.ald;
+      g.pA = i == 0 ? net.arows * net.xld : net.aps();
+      g.sA = i == 0 ? 0 : 3 * net.aps();
       g.a_kmajor = 1;
       g.B = dzp[i];
       g.ldb = net.ald;
@@ -402,12 +432,13 @@ struct mtsac_engine {
       g.C = net.g + net.off_W[i];
       g.ldc = net.width;
       g.sC = net.ms_W[i];
-      g.M = net.width;
+      g.M = i == 0 ? net.in_dim : net.width;
       g.N = net.width;
       g.K = (int)net.arows;
+      g.tag = i == 0 ? 1 : 0;
       g.splits = -1;  // by tile count (gemm_x3p_splits); the lane workspace is sized for it
       g.ws = ws_lane[cur_lane];
-      gemmp(g, EPI_STORE, net.E, MTSAC_FAM_WEIGHT_GRAD);
+      gemmp(g, EPI_STORE, net.E, i == 0 ? MTSAC_FAM_INPUT_WEIGHT_GRAD : MTSAC_FAM_WEIGHT_GRAD);
       colsum(dz[i], M, net.width, net.width, (long long)M * net.width, net.E, cs_part, net.g + net.off_b[i], net.ms_b,
              cur);
       return;
@@ -449,7 +480,7 @@ struct mtsac_engine {
       g.mask = acts[i - 1];
       g.ldm = net.width;
       g.sMask = (long long)M * net.width;
-      if (i - 1 >= 1) {
+      if (dzp[i - 1]) {
         g.Cp = dzp[i - 1];
         g.ldcp = net.ald;
         g.pC = net.aps();
@@ -544,9 +575,10 @@ struct mtsac_engine {
     if (a.target) a.target += net.trunk_off;
     a.n = net.n_flat - net.trunk_off;
     if (planes_fusable(net))  // hidden kernels' planes (params and Polyak target) from the update
-      for (int i = 1; i < net.depth && a.nseg + 2 <= MAX_PLANE_SEGS; ++i) {
-        a.seg[a.nseg++] = PlaneSeg{net.off_W[i] - net.trunk_off, net.ms_W[i], net.E, net.wp[0][i], net.wps(), 0};
-        if (polyak) a.seg[a.nseg++] = PlaneSeg{net.off_W[i] - net.trunk_off, net.ms_W[i], net.E, net.wp[1][i], net.wps(), 1};
+      for (int i = 0; i < net.depth && a.nseg + 2 <= MAX_PLANE_SEGS; ++i) {
+        a.seg[a.nseg++] = PlaneSeg{net.off_W[i] - net.trunk_off, net.ms_W[i], net.E, net.wp[0][i], net.kps(i), 0};
+        if (polyak)
+          a.seg[a.nseg++] = PlaneSeg{net.off_W[i] - net.trunk_off, net.ms_W[i], net.E, net.wp[1][i], net.kps(i), 1};
       }
     int na = adam_update(a, max_norm, 0, PART, cur);
     sum_partials(partials, na, pn + slot, cur);
@@ -554,7 +586,7 @@ struct mtsac_engine {
 
   // the kernel planes can come straight out of the flat update when their layout is the leaf's
   bool planes_fusable(const Net& net) const {
-    return planes && net.wld == net.width && net.wrows == net.width && net.depth - 1 <= MAX_PLANE_SEGS / 2;
+    return planes && net.wld == net.width && net.wrows == net.width && net.depth <= MAX_PLANE_SEGS / 2;
   }
 
   void head_sq(Net& net) {  // local |g_head|^2 into the scalar tail
@@ -1011,14 +1043,15 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     net->wld = align_up(net->width, 32);
     net->wrows = align_up(net->width, 32);
     net->ald = align_up(net->width, 32);
+    net->xld = align_up(net->in_dim, 32);
     net->arows = align_up(e->B, 32);
     for (int w = 0; w < (net == &e->critic ? 2 : 1); ++w)
-      for (int i = 1; i < net->depth; ++i) {
+      for (int i = 0; i < net->depth; ++i) {
         if (!e->planes) {
-          if ((rc = e->alloc(&net->wt[w][i], (size_t)net->ms_W[i] * net->E))) return bad(rc);
+          if (i > 0 && (rc = e->alloc(&net->wt[w][i], (size_t)net->ms_W[i] * net->E))) return bad(rc);
           continue;
         }
-        if ((rc = e->alloc(&net->wp[w][i], (size_t)net->E * 3 * net->wps()))) return bad(rc);
+        if ((rc = e->alloc(&net->wp[w][i], (size_t)net->E * 3 * net->kps(i)))) return bad(rc);
       }
   }
   {  // split-K workspaces: the largest GEMM that splits, per lane
@@ -1027,9 +1060,10 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
       for (int i = 0; i < net->depth; ++i) {
         const int M = i == 0 ? net->in_dim : net->width;
         ws = std::max(ws, gemm_ws_floats(M, net->width, net->E, gemm_splits(M, net->width, e->B, net->E)));
-        if (e->planes && i > 0) {
-          ws = std::max(ws, gemm_x3p_ws_floats(M, net->width, (int)net->arows, net->E, true));      // weight grad
-          ws = std::max(ws, gemm_x3p_ws_floats(e->B, net->width, (int)net->ald, net->E, false));   // fwd / data grad
+        if (e->planes) {
+          ws = std::max(ws, gemm_x3p_ws_floats(M, net->width, (int)net->arows, net->E, true));  // weight grad
+          ws = std::max(ws, gemm_x3p_ws_floats(e->B, net->width, (int)(i == 0 ? net->xld : net->ald), net->E,
+                                               false));  // forward / data grad
         }
       }
     for (float*& w : e->ws_lane)
@@ -1073,8 +1107,18 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
       for (int i = 0; i + 1 < net->depth; ++i)
         for (__bf16** p : {cr ? &e->hcp[i] : &e->hap[i], cr ? &e->hctp[i] : &e->hanp[i]})
           if ((rc = e->alloc(p, np))) return bad(rc);
+      // dz[0] keeps no planes: its weight grad (K = B, M = in_dim) runs on the on-the-fly split
+      // kernel, cheaper than writing the planes in the data-grad epilogue (tools/step_gemms.py)
       for (int i = 1; i < net->depth; ++i)
         if ((rc = e->alloc(cr ? &e->dzcp[i] : &e->dzap[i], np))) return bad(rc);
+    }
+    {
+      const float* xs[5] = {e->xa, e->xan, e->xc, e->xcn, e->xcp};
+      for (int k = 0; k < 5; ++k) {
+        const Net& net = k < 2 ? e->actor : e->critic;
+        e->inp[k].x = xs[k];
+        if ((rc = e->alloc(&e->inp[k].p, (size_t)3 * net.arows * net.xld))) return bad(rc);
+      }
     }
     const int wmax = std::max(c.actor_width, c.critic_width);
     if ((rc = e->alloc(&e->cs_part, (size_t)std::max(1, c.num_critics) * COLSUM_CHUNKS * wmax))) return bad(rc);

@@ -113,7 +113,8 @@ struct Oper {
 
 // Tile geometry: BM x BN per workgroup, WM x WN waves, each wave (BM/WM) x (BN/WN) made of
 // 32x32 MFMA tiles; STAGES-deep LDS ring.
-template <int BM_, int BN_, int WM_, int WN_, int STAGES_, int KS_>
+// TAG only separates kernel symbols (e.g. input-layer launches in profiles)
+template <int BM_, int BN_, int WM_, int WN_, int STAGES_, int KS_, int TAG = 0>
 struct Geo {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, STAGES = STAGES_, KS = KS_;
   static constexpr int NW = WM * WN, NTH = 64 * NW;
@@ -284,6 +285,7 @@ using GeoWide = Geo<256, 128, 4, 2, 2, 32>;    // 8 waves, 2 x 72 KiB
 using GeoWide16 = Geo<256, 128, 4, 2, 4, 16>;  // 8 waves, 4 x 36 KiB
 using GeoBig16 = Geo<256, 256, 2, 4, 3, 16>;   // 8 waves of 128 x 64, 3 x 48 KiB
 using GeoSmall16 = Geo<128, 128, 2, 2, 3, 16>;  // 4 waves, 3 x 24 KiB: two workgroups per CU
+using GeoBig16In = Geo<256, 256, 2, 4, 3, 16, 1>;  // GeoBig16 for input-layer launches (own symbol)
 
 // fp32 [rows][ld] -> planes.  TRANS: out[q][col][row] (k = row contiguous), else out[q][row][col].
 // 64x64 tiles staged through LDS so both the fp32 reads and the bf16 writes are coalesced.
@@ -525,7 +527,12 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
   switch (pick_geo(p.M, p.N, batch, kmajor)) {
     case 0: launch_geo<GeoSmall>(q, kepi, batch, st); break;
     case 2: launch_geo<GeoWide16>(q, kepi, batch, st); break;
-    case 3: launch_geo<GeoBig16>(q, kepi, batch, st); break;
+    case 3:
+      if (p.tag == 1)
+        launch_geo<GeoBig16In>(q, kepi, batch, st);
+      else
+        launch_geo<GeoBig16>(q, kepi, batch, st);
+      break;
     case 4: launch_geo<GeoSmall16>(q, kepi, batch, st); break;
     default: launch_geo<GeoWide>(q, kepi, batch, st); break;
   }

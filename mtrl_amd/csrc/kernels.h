@@ -72,6 +72,7 @@ struct SplitGemmParams {
   int splits, kchunk;     // split-K: partial slabs in ws (gemm_x3p_ws_floats), then a finishing pass; -1 = auto
   float* ws;
   int dbg;                // experiments only: bit0 skip steady-state loads, bit1 skip MFMA
+  int tag;                // 1: input-layer launch (separate kernel symbol for profiles)
 };
 void gemm_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
 // auto split-K slices (1 = none) for a plane GEMM; kmajor = the k-major x k-major form
