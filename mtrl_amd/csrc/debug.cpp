@@ -177,7 +177,7 @@ int mtsac_debug_x3p_geo(int geo) {
     return old;
   }
   const int g = geo & 255;
-  g_x3p_geo = g <= 4 ? g : -1;
+  g_x3p_geo = g <= 5 ? g : -1;
   g_x3p_dbg = (geo >> 8) & 255;
   g_x3_dbg = (geo >> 16) & 255;
   return old;

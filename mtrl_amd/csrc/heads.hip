@@ -34,26 +34,65 @@ __device__ inline float clip_grad(float v, float lo, float hi) {
   return 0.f;
 }
 
-// out[o] = sum_w h[w] * Wt[w*HD + o], reduced over the wave (every lane gets the sums)
-template <int HD>
-__device__ inline void head_dot(const float* __restrict__ h, const float* __restrict__ Wt, int W, float (&acc)[HD]) {
+// acc[r][o] = sum_w h_r[w] * Wt[w*HD + o] for R rows of one task, reduced over the wave (every lane
+// gets the sums).  W % 4 == 0 (and 16-B aligned rows): lane l takes w = 4l + 256i .. +3 with
+// 16-B loads of h and of the head kernel (L2-resident: W*HD floats per task), several i in
+// flight; otherwise w = l + 64i.  The order is fixed per W, so every kernel that uses this
+// gets bitwise the same head outputs.
+template <int HD, int R>
+__device__ inline void rows_dot(const float* const (&h)[R], const float* __restrict__ Wt, int W, float (&acc)[R][HD]) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int o = 0; o < HD; ++o) acc[o] = 0.f;
-  for (int w = lane; w < W; w += 64) {
-    const float hv = h[w];
-    if (HD == 8) {
-      const float4 a = *reinterpret_cast<const float4*>(Wt + w * 8);
-      const float4 c = *reinterpret_cast<const float4*>(Wt + w * 8 + 4);
-      acc[0] += hv * a.x; acc[1] += hv * a.y; acc[2] += hv * a.z; acc[3] += hv * a.w;
-      acc[4 % HD] += hv * c.x; acc[5 % HD] += hv * c.y; acc[6 % HD] += hv * c.z; acc[7 % HD] += hv * c.w;
-    } else {
+  for (int r = 0; r < R; ++r)
 #pragma unroll
-      for (int o = 0; o < HD; ++o) acc[o] += hv * Wt[w * HD + o];
+    for (int o = 0; o < HD; ++o) acc[r][o] = 0.f;
+  if ((W & 3) == 0) {
+#pragma unroll 2
+    for (int w = 4 * lane; w < W; w += 256) {
+      float4 hv[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) hv[r] = *reinterpret_cast<const float4*>(h[r] + w);
+      float wv[4 * HD];  // 4 w x HD outputs, contiguous and 16-B aligned (w % 4 == 0)
+#pragma unroll
+      for (int i = 0; i < HD; ++i) {
+        const float4 v = *reinterpret_cast<const float4*>(Wt + (long long)w * HD + 4 * i);
+        wv[4 * i] = v.x; wv[4 * i + 1] = v.y; wv[4 * i + 2] = v.z; wv[4 * i + 3] = v.w;
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int o = 0; o < HD; ++o) {
+          float a = acc[r][o];
+          a += hv[r].x * wv[o];
+          a += hv[r].y * wv[HD + o];
+          a += hv[r].z * wv[2 * HD + o];
+          a += hv[r].w * wv[3 * HD + o];
+          acc[r][o] = a;
+        }
+    }
+  } else {
+    for (int w = lane; w < W; w += 64) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const float hv = h[r][w];
+#pragma unroll
+        for (int o = 0; o < HD; ++o) acc[r][o] += hv * Wt[(long long)w * HD + o];
+      }
     }
   }
 #pragma unroll
-  for (int o = 0; o < HD; ++o) acc[o] = wsum(acc[o]);
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int o = 0; o < HD; ++o) acc[r][o] = wsum(acc[r][o]);
+}
+
+template <int HD>
+__device__ inline void head_dot(const float* __restrict__ h, const float* __restrict__ Wt, int W, float (&acc)[HD]) {
+  const float* const hr[1] = {h};
+  float a[1][HD];
+  rows_dot<HD, 1>(hr, Wt, W, a);
+#pragma unroll
+  for (int o = 0; o < HD; ++o) acc[o] = a[0][o];
 }
 
 // ------------------------------------------------------------------ actor head + policy
@@ -116,17 +155,14 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyParams p) {
   policy_finish<HD>(p, b, t, acc, lane);
 }
 
-// Rows grouped by task (task_rows lists): a workgroup takes PH_ROWS rows of one task and stages
-// that task's head kernel through LDS in PH_CHUNK-row slices, so the kernel is read once per
-// group instead of once per row.  Each lane accumulates w = lane, lane + 64, ... in the same
-// order as head_dot: bitwise the same sums.
+// Rows grouped by task (task_rows lists): a workgroup takes PH_ROWS rows of one task, PH_RW per
+// wave, so the task's head kernel is fetched (from L2) once per wave for PH_RW rows; no LDS, so
+// it co-resides with the trunk GEMMs running on other streams.
 constexpr int PH_RW = 4;               // rows per wave
 constexpr int PH_ROWS = 4 * PH_RW;     // rows per workgroup
-constexpr int PH_CHUNK = 512;          // head-kernel rows (w) per LDS slice
 
 template <int HD>
 __global__ __launch_bounds__(256) void policy_head_grouped_kernel(PolicyParams p) {
-  __shared__ __attribute__((aligned(16))) float wl[PH_CHUNK * HD];
   const HeadParams& hp = p.head;
   const int t = blockIdx.x;
   const int n = p.counts[t];
@@ -135,46 +171,18 @@ __global__ __launch_bounds__(256) void policy_head_grouped_kernel(PolicyParams p
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int* rl = p.rows + (long long)t * p.max_rows;
   int row[PH_RW];
+  const float* hr[PH_RW];
 #pragma unroll
   for (int r = 0; r < PH_RW; ++r) {
     const int jj = j0 + wave * PH_RW + r;
     row[r] = rl[jj < n ? jj : j0];
+    hr[r] = hp.h + (long long)row[r] * hp.W;
   }
   float acc[PH_RW][HD];
+  rows_dot<HD, PH_RW>(hr, hp.Wh + (long long)t * hp.W * HD, hp.W, acc);
 #pragma unroll
   for (int r = 0; r < PH_RW; ++r)
-#pragma unroll
-    for (int o = 0; o < HD; ++o) acc[r][o] = 0.f;
-  const float* Wt = hp.Wh + (long long)t * hp.W * HD;
-  const bool vec = ((hp.W * HD) % 4 == 0);
-  for (int w0 = 0; w0 < hp.W; w0 += PH_CHUNK) {
-    const int cw = min(PH_CHUNK, hp.W - w0);
-    __syncthreads();
-    if (vec) {
-      for (int i = threadIdx.x; i < cw * HD / 4; i += 256)
-        reinterpret_cast<float4*>(wl)[i] = reinterpret_cast<const float4*>(Wt + (long long)w0 * HD)[i];
-    } else {
-      for (int i = threadIdx.x; i < cw * HD; i += 256) wl[i] = Wt[(long long)w0 * HD + i];
-    }
-    __syncthreads();
-    for (int w = lane; w < cw; w += 64) {
-      float wv[HD];
-#pragma unroll
-      for (int o = 0; o < HD; ++o) wv[o] = wl[w * HD + o];
-#pragma unroll
-      for (int r = 0; r < PH_RW; ++r) {
-        const float hv = hp.h[(long long)row[r] * hp.W + w0 + w];
-#pragma unroll
-        for (int o = 0; o < HD; ++o) acc[r][o] += hv * wv[o];
-      }
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < PH_RW; ++r) {
-#pragma unroll
-    for (int o = 0; o < HD; ++o) acc[r][o] = wsum(acc[r][o]);
     if (j0 + wave * PH_RW + r < n) policy_finish<HD>(p, row[r], t, acc[r], lane);
-  }
 }
 
 // ------------------------------------------------------------------ critic heads + losses
@@ -303,6 +311,7 @@ __global__ __launch_bounds__(256) void head_bwd_weight_scalar_kernel(HeadParams 
 #pragma unroll
   for (int o = 0; o < HD; ++o) acc[o] = 0.f;
   if (w < hp.W) {
+#pragma unroll 8
     for (int j = rg; j < n; j += 4) {
       const int row = rl[j];
       const float hv = h[(long long)row * hp.W + w];
@@ -356,6 +365,7 @@ __global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, con
 #pragma unroll
   for (int o = 0; o < HD; ++o) acc[o] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (w < hp.W) {
+#pragma unroll 8
     for (int j = wave; j < n; j += 4) {
       const int row = rl[j];
       const float4 hv = *reinterpret_cast<const float4*>(h + (long long)row * hp.W + w);
@@ -410,8 +420,8 @@ __global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, con
 
 // ------------------------------------------------------------------ critic -> action grad -> policy grad
 // AG_RW rows per wavefront: the critic layer-0 kernel rows (A x Wc) are read once per AG_RW rows.
-// Per row the sums run w = lane, lane + 64, ... then over the wave: the same association as a
-// one-row-per-wave loop.
+// Per row the sums run over the lane's w (16-B chunks 4l + 256i when Wc % 4 == 0, else l + 64i),
+// then over the wave.
 constexpr int AG_RW = 4;
 
 __global__ __launch_bounds__(256) void action_grad_kernel(ActionGradParams p) {
@@ -430,6 +440,29 @@ __global__ __launch_bounds__(256) void action_grad_kernel(ActionGradParams p) {
   for (int e = 0; e < p.E; ++e) {
     const float* dz = p.dz1 + e * p.s_dz;
     const float* W0 = p.W0 + e * p.s_W0;
+    if ((p.Wc & 3) == 0) {  // 16-B loads: lane l takes w = 4l + 256i .. +3
+#pragma unroll 2
+      for (int w = 4 * lane; w < p.Wc; w += 256) {
+        float4 wv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          wv[j] = j < A ? *reinterpret_cast<const float4*>(W0 + (long long)j * p.Wc + w) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int r = 0; r < AG_RW; ++r) {
+          const float4 g = *reinterpret_cast<const float4*>(dz + (long long)rows[r] * p.Wc + w);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float a = ga[r][j];
+            a += g.x * wv[j].x;
+            a += g.y * wv[j].y;
+            a += g.z * wv[j].z;
+            a += g.w * wv[j].w;
+            ga[r][j] = a;
+          }
+        }
+      }
+      continue;
+    }
     for (int w = lane; w < p.Wc; w += 64) {
       float wv[8];
 #pragma unroll

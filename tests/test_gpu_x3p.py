@@ -8,8 +8,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["geo128x128k32", "geo256x128k32", "geo256x128k16", "geo256x256k16",
-                                          "geo128x128k16"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5], ids=["geo128x128k32", "geo256x128k32", "geo256x128k16", "geo256x256k16",
+                                             "geo128x128k16", "geo224x256k16"])
 def geo(request):
     from mtrl_amd import _lib as L
 

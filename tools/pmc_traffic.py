@@ -12,10 +12,10 @@ import sys
 
 FAMILY_KEYS = {
     "split3": {
-        0: "gemm_x3p_kernel<mtsac::(anonymous namespace)::Geo<256, 256, 2, 4, 3, 16, 0>, false, true, 1,",
-        1: "gemm_x3p_kernel<mtsac::(anonymous namespace)::Geo<256, 256, 2, 4, 3, 16, 0>, false, false, 2,",
-        2: "gemm_x3p_kernel<mtsac::(anonymous namespace)::Geo<256, 256, 2, 4, 3, 16, 0>, true, true, 0,",
-        3: "gemm_x3p_kernel<mtsac::(anonymous namespace)::Geo<256, 256, 2, 4, 3, 16, 1>, false, true, 1,",
+        0: "gemm_x3p_kernel<mtsac::x3pk::Geo<224, 256, 1, 8, 3, 16, 0>, false, true, 1,",
+        1: "gemm_x3p_kernel<mtsac::x3pk::Geo<224, 256, 1, 8, 3, 16, 0>, false, false, 2,",
+        2: "gemm_x3p_kernel<mtsac::x3pk::Geo<256, 256, 2, 4, 3, 16, 0>, true, true, 0,",
+        3: "gemm_x3p_kernel<mtsac::x3pk::Geo<224, 256, 1, 8, 3, 16, 1>, false, true, 1,",
         4: "gemm_x3_kernel<true, false, 0>",
     },
     "fp32": {
