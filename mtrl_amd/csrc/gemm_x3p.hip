@@ -227,10 +227,20 @@ int gemm_x3p_splits(int M, int N, int K, int batch, bool kmajor) {
   geo_tile(pick_geo(M, N, batch, kmajor, kmajor), bm, bn);
   const long long tiles = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch;
   if (tiles >= 192) return 1;
-  int s = (int)((256 + tiles - 1) / tiles);
-  s = std::min(s, kmajor ? 16 : 4);
-  s = std::min(s, std::max(1, K / BK / 8));  // >= 8 K-granules per slice
-  return std::max(s, 1);
+  // slices: least (rounds of tiles x S workgroups on the CUs) / S, plus ~3 % of a round per extra
+  // slice for its partial slab traffic; >= 8 K-granules per slice
+  const long long ncu = cu_count();
+  const int smax = std::min(kmajor ? 16 : 8, std::max(1, K / BK / 8));
+  int best = 1;
+  double best_cost = 1e30;
+  for (int sp = 1; sp <= smax; ++sp) {
+    const double cost = (double)((tiles * sp + ncu - 1) / ncu) / sp + 0.03 * (sp - 1);
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = sp;
+    }
+  }
+  return best;
 }
 
 long long gemm_x3p_ws_floats(int M, int N, int K, int batch, bool kmajor) {

@@ -1,4 +1,5 @@
-"""Per-launch GEMM timeline of one MT50 width-2048 step (timing mode, single stream)."""
+"""Per-launch GEMM timeline of one MT50 width-2048 step (timing mode, single stream).
+usage: python tools/step_gemms.py [precision (1 = split3)] [T_local (default 50: unsharded)]"""
 import ctypes
 import sys
 
@@ -9,10 +10,11 @@ from mtrl_amd.init import init_mtsac  # noqa: E402
 
 prec = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 T, W = 50, 2048
-cfg = make_config(num_tasks=T, task_begin=0, task_count=T, obs_dim=39 + T, actor_width=W, critic_width=W,
+TL = int(sys.argv[2]) if len(sys.argv) > 2 else T
+cfg = make_config(num_tasks=T, task_begin=0, task_count=TL, obs_dim=39 + T, actor_width=W, critic_width=W,
                   batch_per_task=128, capacity=100_000, clip=1, precision=prec)
 eng = MTSACEngine(cfg, device=0)
-actor, critic = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=1)
+actor, critic = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=1, task_begin=0, task_count=TL)
 eng.set_params(L.ACTOR, actor)
 eng.set_params(L.CRITIC, critic)
 eng.set_params(L.CRITIC_TARGET, critic)
