@@ -36,10 +36,17 @@ constexpr int BK = 32;  // K granule of the operands (split-K slices, padding); 
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-__device__ inline void glds16(const void* src, char* dst) {
-  __builtin_amdgcn_global_load_lds(src, (lds_void*)dst, 16, 0, 0);
+// One LDS-DMA wave-instruction (16 B per lane to dst + 16 * lane).  Issued from inline asm: the
+// builtin makes the compiler drain every outstanding ds_read (lgkmcnt(0)) before each DMA, which
+// serialises the fragment reads against the refill spread over the MFMAs.  The ring protocol
+// (counted vmcnt + one barrier per K-step) orders the DMA against the reads instead; M0 carries
+// the wave-uniform LDS byte address (SALU write -> LDS-DMA read of M0 needs one wait state; M0 is
+// reserved, so the compiler never keeps a value of its own there across this).
+__device__ inline void glds16(const void* src, unsigned lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src),
+               "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+               : "memory");
 }
-
 // One operand's image of a K-step: R rows (M or N) x KS k, three planes.
 template <int R, bool KM, int KS>
 struct Oper {
@@ -60,14 +67,14 @@ struct Oper {
 
   // issue wave-instructions first, first + stride, ... (< NJ) of the stage at k0
   __device__ static inline void dma(const __bf16* __restrict__ base, long long ld, long long ps, int r0, int nrows,
-                                    int k0, char* lds, int first, int stride) {
+                                    int k0, unsigned lds, int first, int stride) {
 #pragma unroll
     for (int j = first; j < NJ; j += stride) dma_one(base, ld, ps, r0, nrows, k0, lds, j);
   }
 
   // wave-instruction j (< NJ) of the stage at k0
   __device__ static inline void dma_one(const __bf16* __restrict__ base, long long ld, long long ps, int r0, int nrows,
-                                        int k0, char* lds, int j) {
+                                        int k0, unsigned lds, int j) {
     const int lane = threadIdx.x & 63;
     {
       const int q = j / PER_PLANE;
@@ -133,6 +140,7 @@ __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) 
   static_assert(G::STAGES * STAGE <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[G::STAGES * STAGE];
   char* lds = smem;
+  const unsigned lds_base = (unsigned)(unsigned long long)(lds_void*)smem;  // LDS byte address
 
   const int ny = (p.N + G::BN - 1) / G::BN, nx = (p.M + G::BM - 1) / G::BM;
   const int t = threadIdx.x, lane = t & 63;
@@ -152,14 +160,14 @@ __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) 
   // tile at (m0, n0)
   auto kloop = [&](const __bf16* __restrict__ A, const __bf16* __restrict__ B, int m0, int n0, int nk) {
     auto stage = [&](int s, int k0) {
-      char* st = lds + s * STAGE;
+      const unsigned st = lds_base + s * STAGE;
       OA::dma(A, p.lda, p.pA, m0, p.M, k0, st, wave, G::NW);
       OB::dma(B, p.ldb, p.pB, n0, p.N, k0, st + OA::BYTES, fb, G::NW);
     };
     // the wave's q-th wave-instruction of a stage (same dealing as stage(): global index
     // wave + q * NW, A's instructions first)
     auto piece = [&](int s, int k0, int q) {
-      char* st = lds + s * STAGE;
+      const unsigned st = lds_base + s * STAGE;
       const int jg = wave + q * G::NW;
       if (jg < OA::NJ)
         OA::dma_one(A, p.lda, p.pA, m0, p.M, k0, st, jg);
