@@ -171,12 +171,19 @@ class MTSAC(OffPolicyAlgorithm):
 
     # ------------------------------------------------------------------ state (checkpoint)
     def state_dict(self) -> dict[str, np.ndarray]:
-        d = {f"tensor_{w}": self.engine.get_params(w) for w in range(10)}
-        d["adam_counts"] = np.array([self.engine.get_adam_count(i) for i in range(3)], np.int32)
-        return d
+        """Agent pytree keyed by flax path (compat/checkpoint.py), e.g.
+        ``critic/target_params/VmapQValueFunction_0/MultiHeadNetwork_0/layer_1/kernel``."""
+        from ...checkpoint import agent_state
+
+        return agent_state(self)
 
     def load_state_dict(self, d: Mapping) -> None:
-        for w in range(10):
-            self.engine.set_params(w, np.asarray(d[f"tensor_{w}"]))
-        for i, c in enumerate(np.asarray(d["adam_counts"])):
-            self.engine.set_adam_count(i, int(c))
+        from ...checkpoint import load_agent_state
+
+        if "tensor_0" in d:  # flat-vector layout of earlier checkpoints
+            for w in range(10):
+                self.engine.set_params(w, np.asarray(d[f"tensor_{w}"]))
+            for i, c in enumerate(np.asarray(d["adam_counts"])):
+                self.engine.set_adam_count(i, int(c))
+            return
+        load_agent_state(self, d)

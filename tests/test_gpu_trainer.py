@@ -91,3 +91,51 @@ def test_update_with_host_batch_and_actions(tmp_path):
                          "metrics/critic_params_norm", "losses/actor_loss", "metrics/actor_grad_magnitude",
                          "metrics/actor_params_norm", "metrics/explore_loss", "losses/alpha_loss", "alpha"}
     assert np.isfinite(logs["losses/qf_loss"])
+
+
+def test_flax_named_checkpoint_resumes_bitwise(tmp_path):
+    """Save the agent by flax path (compat/checkpoint.py) after 2 updates, restore into a
+    fresh engine; the next update on identical batch + noise gives identical logs and state."""
+    from mtrl.rl.algorithms import MTSAC
+    from mtrl_amd import _lib as L
+    from mtrl_amd.compat.experiment import NpzCheckpointManager
+
+    T = 10
+    exp = _experiment(tmp_path, T=T, checkpoint=False)
+    agent = MTSAC.initialize(exp.algorithm, exp.env, seed=3)
+    rng = np.random.default_rng(5)
+    B = 16 * T
+
+    def batch():
+        o = np.zeros((B, 39 + T), np.float32)
+        o[:, :39] = rng.standard_normal((B, 39))
+        o[np.arange(B), 39 + np.arange(B) % T] = 1
+        n = o.copy()
+        n[:, :39] = rng.standard_normal((B, 39))
+        return (o, rng.uniform(-1, 1, (B, 4)).astype(np.float32), n, np.zeros((B, 1), np.float32),
+                rng.uniform(0, 10, (B, 1)).astype(np.float32))
+
+    def eps():
+        return rng.standard_normal((B, 4)).astype(np.float32)
+
+    from mtrl.types import ReplayBufferSamples
+
+    agent.update(ReplayBufferSamples(*batch()))  # sizes the engine for B
+    for _ in range(2):
+        agent.engine.update(batch(), eps(), eps())
+    m = NpzCheckpointManager(tmp_path / "ck")
+    m.save(2, agent, metadata={"step": 2})
+    with np.load(tmp_path / "ck" / "ckpt_2.npz") as z:
+        assert "agent/critic/target_params/VmapQValueFunction_0/MultiHeadNetwork_0/layer_2/kernel" in z.files
+    a2 = MTSAC.initialize(exp.algorithm, exp.env, seed=11)
+    a2.update(ReplayBufferSamples(*batch()))
+    meta, _ = m.restore(m.latest_step(), a2)
+    assert meta == {"step": 2}
+    b, en, ec = batch(), eps(), eps()
+    agent.engine.update(b, en, ec)
+    a2.engine.update(b, en, ec)
+    assert agent.engine.logs() == a2.engine.logs()
+    for w in range(10):
+        np.testing.assert_array_equal(agent.engine.get_params(w), a2.engine.get_params(w))
+    assert [agent.engine.get_adam_count(i) for i in range(3)] == [a2.engine.get_adam_count(i) for i in range(3)]
+    assert agent.engine.param_count(L.CRITIC) == a2.engine.param_count(L.CRITIC)
