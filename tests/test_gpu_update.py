@@ -65,6 +65,9 @@ CONFIGS = {
     "deep2": dict(num_tasks=2, width=40, n=4, depth=2),
     "mt10_w400": dict(num_tasks=10, width=400, n=128),  # S1 / C1 at full batch
     "mt50_w400": dict(num_tasks=50, width=400, n=16),
+    # headline widths (S2 with its clip=True, S3's 50 tasks) at a batch the float64 oracle runs in seconds
+    "mt10_w2048_clip": dict(num_tasks=10, width=2048, n=16, clip=True),
+    "mt50_w2048": dict(num_tasks=50, width=2048, n=4),
 }
 
 
