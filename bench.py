@@ -9,8 +9,8 @@ with the updated params, actor backward + clip/Adam, temperature update.  Nothin
 is skipped inside the timed region; inputs are resident in HBM.
 
 Default workload (N=1): MT50 MTMHSAC-v2 at width 2048 (experiments/width_scaling/
-mt50_mtmhsac_v2_2048.py): T=50, B=6400, fp32.  With --gpus N (torchrun, one rank per
-GPU) the 50 tasks are sharded contiguously over the ranks and the trunk gradients
+mt50_mtmhsac_v2_2048.py): T=50, B=6400, fp32.  With --gpus N (torchrun, or N rank
+processes spawned here before anything touches a GPU; one rank per GPU) the 50 tasks are sharded contiguously over the ranks and the trunk gradients
 are all-reduced over RCCL; the problem size is fixed, so scaling is "strong".
 
 Prints ONE JSON line on rank 0 (keys per the driver contract, plus roofline and
@@ -89,27 +89,84 @@ def algorithmic_flops(T, W, n=128, A=4):
             + 2 * (2 * Cf - 2 * B * Ic * W + 2 * B * 4 * W))
 
 
-def cpu_baseline(T, W, clip, steps):
+def available_cores():
+    """Cores this process may run on: the affinity mask, capped by a cgroup CPU quota when
+    one is set (the GPU box grants a share of a larger host)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
+    except OSError:
+        return ""
+
+
+def cpu_time_steps(T, W, clip, steps, threads):
     import torch
     from oracle.cpu_baseline import CPUMTSAC
 
-    threads = min(16, len(os.sched_getaffinity(0)))
     torch.set_num_threads(threads)
     m = CPUMTSAC(T, 39 + T, W, 128, 100_000, clip=clip)
     m.step()  # warm-up
     t0 = time.perf_counter()
     for _ in range(steps):
         m.step()
-    dt = time.perf_counter() - t0
-    model = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
-    except OSError:
-        pass
-    return {"value": steps / dt, "unit": "SAC gradient-steps/sec", "cores": threads, "kind": "port",
-            "sample": f"{steps} full steps (B={128 * T}, W={W}, fp32 PyTorch-CPU autograd restatement, "
-                      f"oracle/cpu_baseline.py) after 1 warm-up step, {dt:.1f}s, {model}"}
+    return steps / (time.perf_counter() - t0), time.perf_counter() - t0
+
+
+def cpu_baseline(T, W, clip, steps, c0_steps):
+    """The oracle-side PyTorch-CPU restatement on this host's cores: the bench
+    workload on a bounded sample of steps, plus C0 (MT10/W400, the reference's own config)."""
+    threads, affinity, quota = available_cores()
+    sps, dt = cpu_time_steps(T, W, clip, steps, threads)
+    out = {"value": sps, "unit": "SAC gradient-steps/sec", "cores": threads, "kind": "port",
+           "sample": f"{steps} full steps (B={128 * T}, W={W}, fp32 PyTorch-CPU autograd restatement, "
+                     f"oracle/cpu_baseline.py) after 1 warm-up step, {dt:.1f}s on {threads} threads; "
+                     f"affinity {affinity} cpus, cgroup quota {quota or 'none'}; {cpu_model()}"}
+    if c0_steps > 0:
+        c0, dt0 = cpu_time_steps(10, 400, False, c0_steps, threads)
+        out["c0_mt10_w400"] = {"value": c0, "unit": "SAC gradient-steps/sec", "cores": threads,
+                               "sample": f"{c0_steps} steps of C0 (MT10 W=400 B=1280, experiments/mt10_mtmhsac.py), "
+                                         f"{dt0:.1f}s"}
+    return out
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` outside torchrun: start N fresh rank processes (nothing here has
+    touched the GPU), forward rank 0's output, exit with the worst return code."""
+    import subprocess
+
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
 
 
 def main():
@@ -120,29 +177,70 @@ def main():
     ap.add_argument("--workload", default="mt50_w2048", choices=sorted(WORKLOADS))
     ap.add_argument("--no-graph", action="store_true", help="same as --exec eager")
     ap.add_argument("--exec", default="auto", choices=["auto", "graph", "eager"],
-                    help="hipGraph replay (serial DAG) or eager 4-stream DAG; auto = faster of the two")
+                    help="hipGraph replay or eager multi-stream DAG; auto = faster of the two")
     ap.add_argument("--precision", default="split3", choices=sorted(PRECISIONS),
                     help="fp32: f32-input MFMA; split3: fp32-accurate 3-way bf16 split on bf16 MFMA")
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--settle-s", type=float, default=2.0,
+                    help="untimed steady-state seconds after the warm-up (DVFS settles under load)")
+    ap.add_argument("--cpu-steps", type=int, default=5)
+    ap.add_argument("--cpu-c0-steps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="control plane only (ranks, shards, timing reduction) on CPU/gloo; no engine")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         dist.init_process_group("gloo")  # host-side control plane only; gradients go over RCCL
 
+    from mtrl_amd.shard import allreduce_floats_per_step, shard_tasks
+
+    T, W, clip, desc = WORKLOADS[args.workload]
+    shards = [list(shard_tasks(T, world, r)) for r in range(world)]
+    tb, tc = shards[rank]
+    ar_bytes = 4 * allreduce_floats_per_step(39 + T, 4, W, 3, W, 3, 2) if world > 1 else 0
+    base = {
+        "metric": METRIC,
+        "unit": "SAC gradient-steps/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp32" if args.precision == "fp32" else "fp32 (3xbf16 split MFMA, fp32-accurate)",
+        "data": "synthetic (SURVEY.md §8d recipe, device-filled full buffer, cap=100000/task; random-init weights)",
+        "config": {"workload": desc, "num_tasks": T, "width": W, "batch_per_task": 128, "global_batch": 128 * T,
+                   "parallelism": f"task-shard{world}" if world > 1 else "single", "precision": args.precision,
+                   "task_shards": shards, "allreduce_bytes_per_step": ar_bytes},
+    }
+    if args.dry_run:
+        import torch
+
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        if dist:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if rank == 0:
+            print(json.dumps(dict(base, value=None, dry_run=True, nranks=world, max_over_ranks=float(t.item()))),
+                  flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
+
     from mtrl_amd import _lib as L
     from mtrl_amd.engine import MTSACEngine, make_config
     from mtrl_amd.init import init_mtsac
-    from mtrl_amd.shard import shard_tasks
 
-    T, W, clip, desc = WORKLOADS[args.workload]
-    tb, tc = shard_tasks(T, world, rank)
     cfg = make_config(num_tasks=T, task_begin=tb, task_count=tc, obs_dim=39 + T, actor_width=W, critic_width=W,
                       batch_per_task=128, capacity=100_000, clip=int(clip), precision=PRECISIONS[args.precision])
     eng = MTSACEngine(cfg, device=local_rank)
@@ -152,10 +250,12 @@ def main():
     eng.set_params(L.CRITIC_TARGET, critic)
     eng.buffer_fill_synthetic(1234)
     eng.seed_rng(1)  # every rank draws the same index vector (buffers.py:523-527)
+    nranks = 1
     if world > 1:
         uid = [MTSACEngine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init(uid[0], world, rank)
+        nranks = eng.comm_nranks()
 
     import torch
 
@@ -182,9 +282,22 @@ def main():
         eng.enable_graph(mode == "graph")
         eng.update_many(1)
         eng.synchronize()
+    # steady state: run untimed for --settle-s seconds (the same count on every rank)
+    settle = 0
+    if args.settle_s > 0:
+        a = time.perf_counter()
+        eng.update_many(5)
+        eng.synchronize()
+        per = max((time.perf_counter() - a) / 5, 1e-4)
+        settle = [int(args.settle_s / per)]
+        if dist:
+            dist.broadcast_object_list(settle, src=0)
+        settle = settle[0]
+        eng.update_many(settle)
+        eng.synchronize()
     # Eager issue: HIP events around every GEMM launch on the stream it runs on, live over the
     # timed steps (the step keeps its concurrent streams).  A graph replay cannot carry events:
-    # then the kernel timing comes from one extra eager step after the timed region.
+    # then the kernel timing comes from one extra serialised step after the timed region.
     live = mode == "eager"
     eng.set_timing(live)
     if dist:
@@ -210,8 +323,8 @@ def main():
     fam = {f: eng.timing(f) for f in names} if live else None
     # the same kernels solo: one extra step serialised on one stream.  Eager: context for the
     # fraction (under the step's concurrency a launch shares the CUs with its neighbours).
-    # Graph: the replays carry no events and run their segments almost serially, so this IS
-    # the measurement (rocprof's mean over the replays agrees within a few %).
+    # Graph: the replays carry no events, so this IS the measurement (rocprof's mean over the
+    # replays agrees within a few %).
     eng.set_timing(True, serial=True)
     eng.update_many(1)
     eng.synchronize()
@@ -233,22 +346,12 @@ def main():
 
     flops = algorithmic_flops(T, W)
     sps = args.steps / elapsed
-    out = {
-        "metric": METRIC,
+    out = dict(base)
+    out.update({
         "value": sps,
-        "unit": "SAC gradient-steps/sec",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
         "ms_per_step": 1e3 * elapsed / args.steps,
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "fp32" if args.precision == "fp32" else "fp32 (3xbf16 split MFMA, fp32-accurate)",
-        "data": "synthetic (SURVEY.md §8d recipe, device-filled full buffer, cap=100000/task; random-init weights)",
-        "config": {"workload": desc, "num_tasks": T, "width": W, "batch_per_task": 128, "global_batch": 128 * T,
-                   "parallelism": f"task-shard{world}" if world > 1 else "single", "exec": mode,
-                   "precision": args.precision},
+        "settle_steps": settle,
+        "nranks": nranks,
         "roofline": {"bound": "mfma", "kernel": names[dom], "achieved": achieved,
                      "peak": peak, "peak_basis": basis, "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": traffic, "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, gfx950-corrected)",
@@ -270,12 +373,13 @@ def main():
                                      "tflops": v[2] / (v[0] * 1e-3) / 1e12 if v[0] else 0.0}
                           for f, v in fam.items()},
         "logs": logs,
-    }
+    })
+    out["config"] = dict(out["config"], exec=mode)
+    eng.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(T, W, clip, args.cpu_steps)
+        out["cpu_baseline"] = cpu_baseline(T, W, clip, args.cpu_steps, args.cpu_c0_steps)
     elif rank == 0:
         out["cpu_baseline"] = None
-    eng.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

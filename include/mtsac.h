@@ -139,7 +139,13 @@ int mtsac_get_params(mtsac_engine* h, int which, float* dst, int64_t n);
 int mtsac_set_adam_count(mtsac_engine* h, int which /*0 actor,1 critic,2 alpha*/, int32_t count);
 int mtsac_get_adam_count(mtsac_engine* h, int which, int32_t* count);
 
-/* replay buffer (device resident; layout documented in DESIGN.md) */
+/* replay buffer (device resident; layout documented in DESIGN.md).
+ * buffer_add (buffers.py:426-474) does not block the host: the T_local rows are staged through
+ * a pinned ring and written + committed on the engine stream, ordered after every update issued
+ * before it and before every update issued after it.  Pass the five arrays all in host memory
+ * or all in device memory; device arrays are read after the work already queued on the legacy
+ * default stream (torch's default stream).  Reward min / max (normalize_rewards) are kept on
+ * the device. */
 int mtsac_buffer_add(mtsac_engine* h, const float* obs, const float* next_obs, const float* actions,
                      const float* rewards, const float* dones);
 int mtsac_buffer_write(mtsac_engine* h, int64_t slot_begin, int64_t n_slots, const float* obs,
@@ -151,6 +157,7 @@ int mtsac_buffer_fill_synthetic(mtsac_engine* h, uint64_t seed);
 int mtsac_buffer_set_state(mtsac_engine* h, int64_t pos, int32_t full);
 int mtsac_buffer_get_state(mtsac_engine* h, int64_t* pos, int32_t* full);
 int mtsac_buffer_set_reward_stats(mtsac_engine* h, const double* min_r, const double* max_r);
+int mtsac_buffer_get_reward_stats(mtsac_engine* h, double* min_r, double* max_r);
 int mtsac_rng_set(mtsac_engine* h, uint64_t state_hi, uint64_t state_lo, uint64_t inc_hi,
                   uint64_t inc_lo, int32_t has_uint32, uint32_t uinteger);
 int mtsac_rng_get(mtsac_engine* h, uint64_t* state_hi, uint64_t* state_lo, uint64_t* inc_hi,
@@ -177,6 +184,12 @@ int mtsac_sample_action(mtsac_engine* h, const float* obs, int32_t n, const floa
 int mtsac_comm_unique_id_size(void);
 int mtsac_comm_get_unique_id(void* id_out);
 int mtsac_comm_init(mtsac_engine* h, const void* unique_id, int32_t nranks, int32_t rank);
+/* device noise stream (used when no eps is injected): seed and step counter; setting them
+ * rebuilds the step graph (checkpoint / resume of the update noise) */
+int mtsac_get_noise_state(mtsac_engine* h, uint64_t* seed, uint64_t* counter);
+int mtsac_set_noise_state(mtsac_engine* h, uint64_t seed, uint64_t counter);
+/* ranks in the engine's communicator as RCCL reports them (ncclCommCount); 1 without one */
+int mtsac_comm_nranks(mtsac_engine* h, int32_t* nranks);
 /* Bring-your-own collective: when no RCCL communicator is set, the engine calls
  * fn(user, device_buffer, count) at each all-reduce point (after synchronising its
  * stream); fn must leave the element-wise SUM over all shards in the buffer before

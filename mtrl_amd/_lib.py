@@ -111,6 +111,7 @@ SIGNATURES = {
     "mtsac_buffer_set_state": (ctypes.c_int, [P, I64, I32]),
     "mtsac_buffer_get_state": (ctypes.c_int, [P, PI64, PI32]),
     "mtsac_buffer_set_reward_stats": (ctypes.c_int, [P, PD, PD]),
+    "mtsac_buffer_get_reward_stats": (ctypes.c_int, [P, PD, PD]),
     "mtsac_rng_set": (ctypes.c_int, [P, U64, U64, U64, U64, I32, U32]),
     "mtsac_rng_get": (ctypes.c_int, [P, PU64, PU64, PU64, PU64, PI32, PU32]),
     "mtsac_sample": (ctypes.c_int, [P, P, P, P, P, P, P]),
@@ -124,6 +125,9 @@ SIGNATURES = {
     "mtsac_comm_unique_id_size": (ctypes.c_int, []),
     "mtsac_comm_get_unique_id": (ctypes.c_int, [P]),
     "mtsac_comm_init": (ctypes.c_int, [P, P, I32, I32]),
+    "mtsac_comm_nranks": (ctypes.c_int, [P, P]),
+    "mtsac_get_noise_state": (ctypes.c_int, [P, P, P]),
+    "mtsac_set_noise_state": (ctypes.c_int, [P, ctypes.c_uint64, ctypes.c_uint64]),
     "mtsac_set_allreduce_hook": (ctypes.c_int, [P, ctypes.c_void_p, P]),
     "mtsac_memcpy": (ctypes.c_int, [P, P, I64]),
     "mtsac_set_timing": (ctypes.c_int, [P, I32]),

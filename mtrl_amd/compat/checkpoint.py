@@ -11,11 +11,15 @@ agent leaves in it by their flax tree path, ``MTSAC.state_dict()`` being
 Agent keys follow the flax auto-names of the reference networks (SURVEY.md §8 a16,
 mtrl/nn/multi_head.py:20-68, mtrl/rl/networks.py:21-67,208-222):
 
-    actor/params/MultiHeadNetwork_0/{VmapDense_0,layer_i}/{bias,kernel}
-    critic/params/VmapQValueFunction_0/MultiHeadNetwork_0/...      (leading axis = ensemble)
-    critic/target_params/VmapQValueFunction_0/MultiHeadNetwork_0/...
-    {actor,critic}/opt_state/{mu,nu}/<same path as params>, .../opt_state/count
-    alpha/params/log_alpha, alpha/opt_state/{mu,nu}/log_alpha, alpha/opt_state/count
+    actor/params/params/MultiHeadNetwork_0/{VmapDense_0,layer_i}/{bias,kernel}
+    critic/params/params/VmapQValueFunction_0/MultiHeadNetwork_0/...  (leading axis = ensemble)
+    critic/target_params/params/VmapQValueFunction_0/MultiHeadNetwork_0/...
+    {actor,critic}/opt_state/1/0/{mu,nu}/<params path>, .../opt_state/1/0/count   (clipped Adam)
+    alpha/params/params/log_alpha, alpha/opt_state/0/{mu,nu}/params/log_alpha, .../0/count
+    {actor,critic,alpha}/step, key
+
+(TrainState.params is the whole flax variables dict, hence ``params/params``; the optax
+state nesting follows ``OptimizerConfig.spawn``: see ``opt_prefix``.)
 
 so a converter from a reference orbax tree is a key rename at most.  The engine's flat
 vectors are in ravel_pytree order of exactly these trees (include/mtsac.h), which
@@ -29,8 +33,19 @@ import numpy as np
 from .. import _lib as L
 from ..init import leaf_shapes
 
-_ACTOR_ROOT = ("MultiHeadNetwork_0",)
-_CRITIC_ROOT = ("VmapQValueFunction_0", "MultiHeadNetwork_0")
+# params of every TrainState are the flax variables dict, so the collection name comes first
+# (``alpha.params["params"]["log_alpha"]``, mtsac.py:109,720,730; ``critic_state["intermediates"]
+# ["VmapQValueFunction_0"]``, sac.py:419)
+_ACTOR_ROOT = ("params", "MultiHeadNetwork_0")
+_CRITIC_ROOT = ("params", "VmapQValueFunction_0", "MultiHeadNetwork_0")
+
+
+def opt_prefix(max_grad_norm) -> tuple[str, ...]:
+    """Path of the Adam state inside a TrainState's opt_state (config/optim.py:26-43):
+    ``optax.chain(clip_by_global_norm, adam)`` when max_grad_norm is set -> (EmptyState,
+    (ScaleByAdamState, EmptyState)) -> ``1/0``; plain ``adam`` (the temperature optimizer,
+    max_grad_norm=None, mtsac.py:120) -> (ScaleByAdamState, EmptyState) -> ``0``."""
+    return ("1", "0") if max_grad_norm else ("0",)
 
 
 def _leaf_path(name: str) -> tuple[str, str]:
@@ -106,46 +121,94 @@ def _unflatten_paths(flat: dict, prefix: str) -> dict:
     return tree
 
 
-def agent_state(algo) -> dict[str, np.ndarray]:
-    """The agent pytree of an engine-backed MTSAC as {flax path: array}."""
-    eng, kw = algo.engine, algo._cfg_kwargs
+def agent_tree(kw: dict, get, count, key=None) -> dict[str, np.ndarray]:
+    """The MTSAC pytree (mtsac.py:130-151: actor / critic / alpha TrainStates + key) as
+    {flax path: array}.  ``get(which)`` returns an engine flat vector (include/mtsac.h ids),
+    ``count(i)`` the Adam count of actor (0) / critic (1) / alpha (2)."""
     ash, csh = network_shapes(kw, "actor"), network_shapes(kw, "critic")
+
+    def state(which_p, which_mu, which_nu, shapes, root, i, clip, extra=None):
+        n = np.int32(count(i))
+        adam = {"count": n, "mu": to_flax_tree(get(which_mu), shapes, root),
+                "nu": to_flax_tree(get(which_nu), shapes, root)}
+        opt: dict = {}
+        node = opt
+        pre = opt_prefix(clip)
+        for k in pre[:-1]:
+            node = node.setdefault(k, {})
+        node[pre[-1]] = adam
+        ts = {"params": to_flax_tree(get(which_p), shapes, root), "opt_state": opt, "step": n}
+        ts.update(extra or {})
+        return ts
+
     tree = {
-        "actor": {"params": to_flax_tree(eng.get_params(L.ACTOR), ash, _ACTOR_ROOT),
-                  "opt_state": {"mu": to_flax_tree(eng.get_params(L.ACTOR_ADAM_MU), ash, _ACTOR_ROOT),
-                                "nu": to_flax_tree(eng.get_params(L.ACTOR_ADAM_NU), ash, _ACTOR_ROOT),
-                                "count": np.int32(eng.get_adam_count(0))}},
-        "critic": {"params": to_flax_tree(eng.get_params(L.CRITIC), csh, _CRITIC_ROOT),
-                   "target_params": to_flax_tree(eng.get_params(L.CRITIC_TARGET), csh, _CRITIC_ROOT),
-                   "opt_state": {"mu": to_flax_tree(eng.get_params(L.CRITIC_ADAM_MU), csh, _CRITIC_ROOT),
-                                 "nu": to_flax_tree(eng.get_params(L.CRITIC_ADAM_NU), csh, _CRITIC_ROOT),
-                                 "count": np.int32(eng.get_adam_count(1))}},
-        "alpha": {"params": {"log_alpha": eng.get_params(L.LOG_ALPHA)},
-                  "opt_state": {"mu": {"log_alpha": eng.get_params(L.ALPHA_ADAM_MU)},
-                                "nu": {"log_alpha": eng.get_params(L.ALPHA_ADAM_NU)},
-                                "count": np.int32(eng.get_adam_count(2))}},
+        "actor": state(L.ACTOR, L.ACTOR_ADAM_MU, L.ACTOR_ADAM_NU, ash, _ACTOR_ROOT, 0,
+                       kw.get("actor_max_grad_norm")),
+        "critic": state(L.CRITIC, L.CRITIC_ADAM_MU, L.CRITIC_ADAM_NU, csh, _CRITIC_ROOT, 1,
+                        kw.get("critic_max_grad_norm"),
+                        {"target_params": to_flax_tree(get(L.CRITIC_TARGET), csh, _CRITIC_ROOT)}),
+        "alpha": {"params": {"params": {"log_alpha": np.asarray(get(L.LOG_ALPHA), np.float32)}},
+                  "step": np.int32(count(2))},
     }
+    a_opt: dict = {}
+    node = a_opt
+    pre = opt_prefix(kw.get("alpha_max_grad_norm"))
+    for k in pre[:-1]:
+        node = node.setdefault(k, {})
+    node[pre[-1]] = {"count": np.int32(count(2)),
+                     "mu": {"params": {"log_alpha": np.asarray(get(L.ALPHA_ADAM_MU), np.float32)}},
+                     "nu": {"params": {"log_alpha": np.asarray(get(L.ALPHA_ADAM_NU), np.float32)}}}
+    tree["alpha"]["opt_state"] = a_opt
+    if key is not None:
+        tree["key"] = np.asarray(key, np.uint32)
     out: dict = {}
     _flatten_paths(tree, "", out)
     return {k: np.asarray(v) for k, v in out.items()}
 
 
-def load_agent_state(algo, flat: dict) -> None:
-    """Inverse of ``agent_state``: push every leaf back into the engine."""
-    eng, kw = algo.engine, algo._cfg_kwargs
+def agent_state(algo) -> dict[str, np.ndarray]:
+    """The agent pytree of an engine-backed MTSAC as {flax path: array}.  ``key`` holds the
+    engine's action-noise stream position in place of the JAX PRNG key (threefry is not
+    reproduced): [noise seed, draws so far]."""
+    eng = algo.engine
+    return agent_tree(algo._cfg_kwargs, eng.get_params, eng.get_adam_count, key=algo.noise_key())
+
+
+def load_agent_tree(kw: dict, flat: dict, put, set_count) -> None:
+    """Inverse of ``agent_tree``: ``put(which, flat_vector)``, ``set_count(i, n)``."""
     ash, csh = network_shapes(kw, "actor"), network_shapes(kw, "critic")
     a = _unflatten_paths(flat, "actor")
     c = _unflatten_paths(flat, "critic")
     al = _unflatten_paths(flat, "alpha")
-    eng.set_params(L.ACTOR, from_flax_tree(a["params"], ash, _ACTOR_ROOT))
-    eng.set_params(L.ACTOR_ADAM_MU, from_flax_tree(a["opt_state"]["mu"], ash, _ACTOR_ROOT))
-    eng.set_params(L.ACTOR_ADAM_NU, from_flax_tree(a["opt_state"]["nu"], ash, _ACTOR_ROOT))
-    eng.set_params(L.CRITIC, from_flax_tree(c["params"], csh, _CRITIC_ROOT))
-    eng.set_params(L.CRITIC_TARGET, from_flax_tree(c["target_params"], csh, _CRITIC_ROOT))
-    eng.set_params(L.CRITIC_ADAM_MU, from_flax_tree(c["opt_state"]["mu"], csh, _CRITIC_ROOT))
-    eng.set_params(L.CRITIC_ADAM_NU, from_flax_tree(c["opt_state"]["nu"], csh, _CRITIC_ROOT))
-    eng.set_params(L.LOG_ALPHA, np.asarray(al["params"]["log_alpha"], np.float32))
-    eng.set_params(L.ALPHA_ADAM_MU, np.asarray(al["opt_state"]["mu"]["log_alpha"], np.float32))
-    eng.set_params(L.ALPHA_ADAM_NU, np.asarray(al["opt_state"]["nu"]["log_alpha"], np.float32))
-    for i, part in enumerate((a, c, al)):
-        eng.set_adam_count(i, int(part["opt_state"]["count"]))
+
+    def adam(ts, clip, what):
+        node = ts["opt_state"]
+        for k in opt_prefix(clip):
+            if k not in node:
+                raise KeyError(f"{what}/opt_state/{'/'.join(opt_prefix(clip))}: missing (max_grad_norm={clip})")
+            node = node[k]
+        return node
+
+    aa = adam(a, kw.get("actor_max_grad_norm"), "actor")
+    ca = adam(c, kw.get("critic_max_grad_norm"), "critic")
+    la = adam(al, kw.get("alpha_max_grad_norm"), "alpha")
+    put(L.ACTOR, from_flax_tree(a["params"], ash, _ACTOR_ROOT))
+    put(L.ACTOR_ADAM_MU, from_flax_tree(aa["mu"], ash, _ACTOR_ROOT))
+    put(L.ACTOR_ADAM_NU, from_flax_tree(aa["nu"], ash, _ACTOR_ROOT))
+    put(L.CRITIC, from_flax_tree(c["params"], csh, _CRITIC_ROOT))
+    put(L.CRITIC_TARGET, from_flax_tree(c["target_params"], csh, _CRITIC_ROOT))
+    put(L.CRITIC_ADAM_MU, from_flax_tree(ca["mu"], csh, _CRITIC_ROOT))
+    put(L.CRITIC_ADAM_NU, from_flax_tree(ca["nu"], csh, _CRITIC_ROOT))
+    put(L.LOG_ALPHA, np.asarray(al["params"]["params"]["log_alpha"], np.float32))
+    put(L.ALPHA_ADAM_MU, np.asarray(la["mu"]["params"]["log_alpha"], np.float32))
+    put(L.ALPHA_ADAM_NU, np.asarray(la["nu"]["params"]["log_alpha"], np.float32))
+    for i, st in enumerate((aa, ca, la)):
+        set_count(i, int(st["count"]))
+
+
+def load_agent_state(algo, flat: dict) -> None:
+    """Inverse of ``agent_state``: push every leaf back into the engine."""
+    eng = algo.engine
+    load_agent_tree(algo._cfg_kwargs, flat, eng.set_params, eng.set_adam_count)
+    if "key" in flat:
+        algo.set_noise_key(np.asarray(flat["key"]))

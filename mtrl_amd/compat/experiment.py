@@ -4,7 +4,8 @@ Same dataclass fields and ``enable_wandb`` / ``run`` flow: device check, env spa
 ``get_algorithm_for_config(...).initialize``, RNG seeding, optional resume, ``train``.
 orbax is not in this image, so checkpoints are ``.npz`` files holding the same items
 (agent tensors + Adam state, buffer arrays + PCG64 state, metadata, python/numpy RNG
-states) -- written by :class:`NpzCheckpointManager`.
+states, the agent's noise streams) -- written by :class:`NpzCheckpointManager`; ``restore``
+reinstates the RNG states like experiment.py:157-161.
 """
 
 from __future__ import annotations
@@ -20,6 +21,34 @@ import numpy as np
 from .config.rl import AlgorithmConfig, TrainingConfig
 from .envs import EnvConfig
 from .rl.algorithms import OffPolicyAlgorithm, get_algorithm_for_config
+
+
+def _rng_arrays(agent) -> dict:
+    """The reference's ``rngs`` item (checkpoint.py:76-79: python ``random`` state, numpy global
+    MT19937 state) plus the agent's action-noise Generator, as plain arrays (reloadable with
+    ``allow_pickle=False``)."""
+    ver, st, gauss = random.getstate()
+    name, keys, pos, has_gauss, cached = np.random.get_state()
+    out = {"rngs/python/version": np.int64(ver), "rngs/python/state": np.asarray(st, np.int64),
+           "rngs/python/gauss": np.float64(np.nan if gauss is None else gauss),
+           "rngs/numpy/keys": np.asarray(keys, np.uint32),
+           "rngs/numpy/pos_gauss": np.array([pos, has_gauss], np.int64), "rngs/numpy/cached": np.float64(cached)}
+    if hasattr(agent, "rng_state"):
+        st = agent.rng_state()
+        out["rngs/agent"] = np.array(json.dumps({**st, "state": {k: str(v) for k, v in st["state"].items()}}))
+    return out
+
+
+def _restore_rngs(z, agent) -> None:
+    g = float(z["rngs/python/gauss"])
+    random.setstate((int(z["rngs/python/version"]), tuple(int(v) for v in z["rngs/python/state"]),
+                     None if np.isnan(g) else g))
+    pos, has_gauss = (int(v) for v in z["rngs/numpy/pos_gauss"])
+    np.random.set_state(("MT19937", z["rngs/numpy/keys"], pos, has_gauss, float(z["rngs/numpy/cached"])))
+    if "rngs/agent" in z.files and hasattr(agent, "set_rng_state"):
+        st = json.loads(str(z["rngs/agent"]))
+        st["state"] = {k: int(v) for k, v in st["state"].items()}
+        agent.set_rng_state(st)
 
 
 class NpzCheckpointManager:
@@ -44,7 +73,7 @@ class NpzCheckpointManager:
             arrays["buffer/rng"] = np.array(json.dumps({**st, "state": {k: str(v) for k, v in st["state"].items()}}))
         arrays["metadata"] = np.array(json.dumps(metadata or {}))
         arrays["metrics"] = np.array(json.dumps(metrics or {}))
-        arrays["rngs/numpy"] = np.array(json.dumps(np.random.get_state(legacy=False), default=str))
+        arrays.update(_rng_arrays(agent))
         np.savez(self.dir / f"ckpt_{step}.npz", **arrays)
         for old in self._steps()[: -self.max_to_keep]:
             (self.dir / f"ckpt_{old}.npz").unlink(missing_ok=True)
@@ -60,6 +89,8 @@ class NpzCheckpointManager:
                         "rng_state": st}
             buf_ckpt["data"]["pos"] = int(buf_ckpt["data"]["pos"])
             buf_ckpt["data"]["full"] = bool(buf_ckpt["data"]["full"])
+        if "rngs/python/state" in z.files:
+            _restore_rngs(z, agent)
         return json.loads(str(z["metadata"])), buf_ckpt
 
 

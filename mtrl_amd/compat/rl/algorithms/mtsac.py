@@ -80,6 +80,7 @@ class MTSAC(OffPolicyAlgorithm):
         self.engine = engine
         self._cfg_kwargs = cfg_kwargs
         self._rng = np.random.default_rng(seed)  # action noise (replaces jax.random keys, mtsac.py:70-77)
+        self._buffer = None  # the replay buffer living in this engine, once spawned
         self.gamma, self.tau = config.gamma, config.tau
         self.target_entropy = -float(np.prod(env_config.action_space.shape))
 
@@ -118,9 +119,15 @@ class MTSAC(OffPolicyAlgorithm):
         return MTSAC(config, env_config, seed, eng, kw)
 
     def _rebuild(self, **changes) -> None:
-        """Re-create the engine with new buffer geometry, keeping parameters and optimizer state."""
+        """Re-create the engine with new batch / buffer geometry, keeping parameters, optimizer
+        state and the update-noise stream.  Refused once a replay buffer lives in the engine:
+        its transitions, pos/full and PCG64 stream would be lost."""
+        if self._buffer is not None:
+            raise ValueError(f"engine geometry change {changes} after the replay buffer was spawned "
+                             "(the device buffer would be lost); keep batch_size fixed for a run")
         keep = {w: self.engine.get_params(w) for w in range(10)}
         counts = [self.engine.get_adam_count(i) for i in range(3)]
+        noise = self.engine.noise_state()
         self._cfg_kwargs.update(changes)
         old = self.engine
         self.engine = MTSACEngine(make_config(**self._cfg_kwargs), device=old.device)
@@ -129,6 +136,23 @@ class MTSAC(OffPolicyAlgorithm):
             self.engine.set_params(w, v)
         for i, c in enumerate(counts):
             self.engine.set_adam_count(i, c)
+        self.engine.set_noise_state(*noise)
+
+    # the reference's MTSAC.key (mtsac.py:134) drives both the update and the action noise; here
+    # the update noise is the engine's counter stream and the action noise a numpy Generator
+    def noise_key(self) -> np.ndarray:
+        seed, counter = self.engine.noise_state()
+        return np.array([seed & 0xFFFFFFFF, counter & 0xFFFFFFFF], np.uint32)
+
+    def set_noise_key(self, key) -> None:
+        k = np.asarray(key, np.uint64).reshape(-1)
+        self.engine.set_noise_state(int(k[0]), int(k[1]))
+
+    def rng_state(self) -> dict:
+        return self._rng.bit_generator.state
+
+    def set_rng_state(self, st: dict) -> None:
+        self._rng.bit_generator.state = st
 
     def spawn_replay_buffer(self, env_config, config, seed: int = 1) -> MultiTaskReplayBuffer:
         T = self.num_tasks
@@ -138,8 +162,10 @@ class MTSAC(OffPolicyAlgorithm):
                                                         self._cfg_kwargs["batch_per_task"],
                                                         bool(self._cfg_kwargs.get("normalize_rewards", 0))):
             self._rebuild(capacity=cap, batch_per_task=n, normalize_rewards=int(config.normalize_rewards))
-        return MultiTaskReplayBuffer(config.buffer_size, T, env_config.observation_space, env_config.action_space,
-                                     seed=seed, normalize_rewards=config.normalize_rewards, engine=self.engine)
+        self._buffer = MultiTaskReplayBuffer(config.buffer_size, T, env_config.observation_space,
+                                             env_config.action_space, seed=seed,
+                                             normalize_rewards=config.normalize_rewards, engine=self.engine)
+        return self._buffer
 
     # ------------------------------------------------------------------ algorithm API
     def get_num_params(self) -> dict[str, int]:
@@ -157,7 +183,7 @@ class MTSAC(OffPolicyAlgorithm):
     def update(self, data):
         """mtsac.py:1249-1251: one gradient step on a ReplayBufferSamples batch."""
         n = np.asarray(data.rewards).shape[0] // self.num_tasks
-        if n != self._cfg_kwargs["batch_per_task"]:
+        if n != self._cfg_kwargs["batch_per_task"]:  # raises once a buffer lives in the engine
             self._rebuild(batch_per_task=n, capacity=max(self._cfg_kwargs["capacity"], n))
         self.engine.update(tuple(data))
         return self, _DeviceLogs(self.engine)

@@ -59,7 +59,10 @@ class MultiTaskReplayBuffer:
         pos, full = self.engine.buffer_state()
         return {
             "data": {"obs": obs, "actions": act, "rewards": rew[..., None], "next_obs": nobs,
-                     "dones": done[..., None], "pos": pos, "full": full},
+                     "dones": done[..., None], "pos": pos, "full": full,
+                     # return-normalisation statistics (buffers.py:319-321); return normalisation
+                     # is not on the MTSAC path, so they keep their initial values (:281-282)
+                     "returns_min": np.full(self.num_tasks, np.inf), "returns_max": np.full(self.num_tasks, -np.inf)},
             "rng_state": self.engine.get_rng_state(),
         }
 
@@ -70,6 +73,10 @@ class MultiTaskReplayBuffer:
         for key in ["obs", "actions", "rewards", "next_obs", "dones", "pos", "full"]:
             assert key in d
         T = self.num_tasks
+        for key, init in (("returns_min", np.inf), ("returns_max", -np.inf)):  # buffers.py:333-334
+            if key in d and not np.all(np.asarray(d[key]) == init):
+                raise NotImplementedError(f"checkpoint carries {key} statistics: return normalisation is not "
+                                          "on the MTSAC path")
         self.engine.buffer_write(0, np.asarray(d["obs"]).reshape(-1, d["obs"].shape[-1]),
                                  np.asarray(d["next_obs"]).reshape(-1, d["next_obs"].shape[-1]),
                                  np.asarray(d["actions"]).reshape(-1, d["actions"].shape[-1]),

@@ -119,8 +119,13 @@ struct mtsac_engine {
   PcgDev* rng = nullptr;
   unsigned long long* jump = nullptr;
   int* idx = nullptr;
-  double *rmin = nullptr, *rmax = nullptr;
-  std::vector<double> h_rmin, h_rmax;
+  double *rmin = nullptr, *rmax = nullptr;  // per-task reward min / max (device-authoritative)
+  // async add: pinned staging ring, each slot reusable once its event (after the H2D copy) fired
+  static constexpr int NSTAGE = 32;
+  float* stage_h = nullptr;
+  hipEvent_t stage_ev[NSTAGE] = {};
+  int stage_next = 0;
+  hipEvent_t add_ev = nullptr;  // orders device-pointer adds after the legacy default stream
   // inputs
   float *xa = nullptr, *xan = nullptr, *xc = nullptr, *xcn = nullptr, *xcp = nullptr;
   float *rew = nullptr, *done = nullptr, *tw = nullptr;
@@ -208,6 +213,10 @@ struct mtsac_engine {
     }
     if (comm) ncclCommDestroy(comm);
     for (void* p : allocs) (void)hipFree(p);
+    if (stage_h) (void)hipHostFree(stage_h);
+    for (hipEvent_t x : stage_ev)
+      if (x) (void)hipEventDestroy(x);
+    if (add_ev) (void)hipEventDestroy(add_ev);
     for (hipEvent_t e : evpool) (void)hipEventDestroy(e);
     for (hipStream_t x : {st, s1, s2, s3, s4})
       if (x) (void)hipStreamDestroy(x);
@@ -1153,8 +1162,17 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   std::vector<float> la(e->T_g, std::log(c.initial_temperature));
   if (hipMemcpy(e->log_alpha, la.data(), sizeof(float) * e->T_g, hipMemcpyHostToDevice) != hipSuccess)
     return bad(fail(-5, "log_alpha"));
-  e->h_rmin.assign(e->T_l, INFINITY);
-  e->h_rmax.assign(e->T_l, -INFINITY);
+  {
+    std::vector<double> mn(e->T_l, INFINITY), mx(e->T_l, -INFINITY);  // buffers.py:266-267
+    if (hipMemcpy(e->rmin, mn.data(), sizeof(double) * e->T_l, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(e->rmax, mx.data(), sizeof(double) * e->T_l, hipMemcpyHostToDevice) != hipSuccess)
+      return bad(fail(-5, "reward stats"));
+  }
+  if (hipHostMalloc((void**)&e->stage_h, sizeof(float) * mtsac_engine::NSTAGE * e->T_l * e->R) != hipSuccess)
+    return bad(fail(-12, "pinned staging"));
+  for (hipEvent_t& x : e->stage_ev)
+    if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) return bad(fail(-5, "event"));
+  if (hipEventCreateWithFlags(&e->add_ev, hipEventDisableTiming) != hipSuccess) return bad(fail(-5, "event"));
   *out = e;
   return 0;
 }
@@ -1256,43 +1274,88 @@ static int upload_size(mtsac_engine* h) {
   return 0;
 }
 
+// true for device (hipMalloc) memory; host pageable / pinned / unknown pointers are host
+static bool on_device(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice;
+}
+
+// n floats from a caller pointer (host or device) into host memory
+static int fetch(float* dst, const float* src, size_t n) {
+  if (n == 0) return 0;
+  HIP_TRY(hipMemcpy(dst, src, sizeof(float) * n, hipMemcpyDefault));
+  return 0;
+}
+
 static int write_slots(mtsac_engine* h, int64_t s0, int64_t ns, const float* obs, const float* nobs, const float* act,
                        const float* rew, const float* done) {
   const int T = h->T_l, D = h->D, A = h->A, R = h->R;
-  std::vector<float> rec((size_t)ns * T * R, 0.0f);
-  for (int64_t s = 0; s < ns; ++s)
-    for (int t = 0; t < T; ++t) {
-      float* r = &rec[((size_t)s * T + t) * R];
-      const size_t row = (size_t)s * T + t;
-      std::memcpy(r, obs + row * D, sizeof(float) * D);
-      std::memcpy(r + D, act + row * A, sizeof(float) * A);
-      r[D + A] = rew[row];
-      r[D + A + 1] = done[row];
-      std::memcpy(r + D + A + 2, nobs + row * D, sizeof(float) * D);
-    }
+  const size_t rows = (size_t)ns * T;
+  std::vector<float> o(rows * D), no(rows * D), a(rows * A), r(rows), d(rows);
+  int rc = 0;
+  if ((rc = fetch(o.data(), obs, o.size())) || (rc = fetch(no.data(), nobs, no.size())) ||
+      (rc = fetch(a.data(), act, a.size())) || (rc = fetch(r.data(), rew, rows)) || (rc = fetch(d.data(), done, rows)))
+    return rc;
+  std::vector<float> rec(rows * R, 0.0f);
+  for (size_t row = 0; row < rows; ++row) {
+    float* x = &rec[row * R];
+    std::memcpy(x, &o[row * D], sizeof(float) * D);
+    std::memcpy(x + D, &a[row * A], sizeof(float) * A);
+    x[D + A] = r[row];
+    x[D + A + 1] = d[row];
+    std::memcpy(x + D + A + 2, &no[row * D], sizeof(float) * D);
+  }
   HIP_TRY(hipStreamSynchronize(h->st));
   HIP_TRY(hipMemcpy(h->store + (size_t)s0 * T * R, rec.data(), sizeof(float) * rec.size(), hipMemcpyHostToDevice));
   return 0;
 }
 
+// add (buffers.py:426-474 + _advance_position :337-343) without blocking the host: the slot is
+// packed into a pinned staging slot (host pointers) or by a kernel (device pointers) and copied
+// / committed on the engine stream, so it lands after every update issued before it and before
+// every update issued after it; pos / full advance on the host, the sampled range and the
+// reward min / max on the device.
 int mtsac_buffer_add(mtsac_engine* h, const float* obs, const float* next_obs, const float* actions,
                      const float* rewards, const float* dones) {
   if (!h || !obs || !next_obs || !actions || !rewards || !dones) return fail(-22, "null argument");
-  int rc = write_slots(h, h->h_pos, 1, obs, next_obs, actions, rewards, dones);
-  if (rc) return rc;
-  if (h->cfg.normalize_rewards) {  // buffers.py:460-462
-    for (int t = 0; t < h->T_l; ++t) {
-      h->h_rmin[t] = std::min(h->h_rmin[t], (double)rewards[t]);
-      h->h_rmax[t] = std::max(h->h_rmax[t], (double)rewards[t]);
+  const int T = h->T_l, D = h->D, A = h->A, R = h->R;
+  const int ndev = (int)on_device(obs) + (int)on_device(next_obs) + (int)on_device(actions) +
+                   (int)on_device(rewards) + (int)on_device(dones);
+  if (ndev != 0 && ndev != 5) return fail(-22, "buffer_add: pass all five arrays in host memory or all in device memory");
+  float* slot = h->store + (size_t)h->h_pos * T * R;
+  if (ndev == 5) {
+    // the producer is assumed on the legacy default stream (torch's default): order after it
+    HIP_TRY(hipEventRecord(h->add_ev, nullptr));
+    HIP_TRY(hipStreamWaitEvent(h->st, h->add_ev, 0));
+    buffer_pack_slot(slot, T, R, D, A, obs, next_obs, actions, rewards, dones, h->st);
+  } else {
+    const int k = h->stage_next;
+    h->stage_next = (k + 1) % mtsac_engine::NSTAGE;
+    HIP_TRY(hipEventSynchronize(h->stage_ev[k]));  // that staging slot's previous copy is done
+    float* rec = h->stage_h + (size_t)k * T * R;
+    for (int t = 0; t < T; ++t) {
+      float* x = rec + (size_t)t * R;
+      std::memcpy(x, obs + (size_t)t * D, sizeof(float) * D);
+      std::memcpy(x + D, actions + (size_t)t * A, sizeof(float) * A);
+      x[D + A] = rewards[t];
+      x[D + A + 1] = dones[t];
+      std::memcpy(x + D + A + 2, next_obs + (size_t)t * D, sizeof(float) * D);
+      for (int c = 2 * D + A + 2; c < R; ++c) x[c] = 0.f;
     }
-    HIP_TRY(hipMemcpy(h->rmin, h->h_rmin.data(), sizeof(double) * h->T_l, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(h->rmax, h->h_rmax.data(), sizeof(double) * h->T_l, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyAsync(slot, rec, sizeof(float) * T * R, hipMemcpyHostToDevice, h->st));
+    HIP_TRY(hipEventRecord(h->stage_ev[k], h->st));
   }
-  // _advance_position(1)  (buffers.py:337-343)
-  long long np = h->h_pos + 1;
+  const long long np = h->h_pos + 1;
   if (np >= h->cfg.capacity) h->h_full = 1;
   h->h_pos = np % h->cfg.capacity;
-  return upload_size(h);
+  buffer_commit_slot(slot, T, R, D + A, h->cfg.normalize_rewards ? h->rmin : nullptr, h->rmax, h->buf_size,
+                     h->h_full ? h->cfg.capacity : h->h_pos, h->st);
+  HIP_TRY(hipGetLastError());
+  return 0;
 }
 
 int mtsac_buffer_write(mtsac_engine* h, int64_t s0, int64_t ns, const float* obs, const float* next_obs,
@@ -1315,19 +1378,25 @@ int mtsac_buffer_read(mtsac_engine* h, int64_t s0, int64_t ns, float* obs, float
   if (!h) return fail(-22, "null engine");
   if (s0 < 0 || ns < 0 || s0 + ns > h->cfg.capacity) return fail(-22, "slot range out of bounds");
   const int T = h->T_l, D = h->D, A = h->A, R = h->R;
-  std::vector<float> rec((size_t)ns * T * R);
+  const size_t rows = (size_t)ns * T;
+  std::vector<float> rec(rows * R);
   HIP_TRY(hipStreamSynchronize(h->st));
   HIP_TRY(hipMemcpy(rec.data(), h->store + (size_t)s0 * T * R, sizeof(float) * rec.size(), hipMemcpyDeviceToHost));
-  for (int64_t s = 0; s < ns; ++s)
-    for (int t = 0; t < T; ++t) {
-      const float* r = &rec[((size_t)s * T + t) * R];
-      const size_t row = (size_t)s * T + t;
-      if (obs) std::memcpy(obs + row * D, r, sizeof(float) * D);
-      if (actions) std::memcpy(actions + row * A, r + D, sizeof(float) * A);
-      if (rewards) rewards[row] = r[D + A];
-      if (dones) dones[row] = r[D + A + 1];
-      if (next_obs) std::memcpy(next_obs + row * D, r + D + A + 2, sizeof(float) * D);
-    }
+  std::vector<float> o(rows * D), no(rows * D), a(rows * A), r(rows), d(rows);
+  for (size_t row = 0; row < rows; ++row) {
+    const float* x = &rec[row * R];
+    std::memcpy(&o[row * D], x, sizeof(float) * D);
+    std::memcpy(&a[row * A], x + D, sizeof(float) * A);
+    r[row] = x[D + A];
+    d[row] = x[D + A + 1];
+    std::memcpy(&no[row * D], x + D + A + 2, sizeof(float) * D);
+  }
+  // the caller's pointers may be host or device memory
+  if (obs) HIP_TRY(hipMemcpy(obs, o.data(), sizeof(float) * o.size(), hipMemcpyDefault));
+  if (next_obs) HIP_TRY(hipMemcpy(next_obs, no.data(), sizeof(float) * no.size(), hipMemcpyDefault));
+  if (actions) HIP_TRY(hipMemcpy(actions, a.data(), sizeof(float) * a.size(), hipMemcpyDefault));
+  if (rewards) HIP_TRY(hipMemcpy(rewards, r.data(), sizeof(float) * rows, hipMemcpyDefault));
+  if (dones) HIP_TRY(hipMemcpy(dones, d.data(), sizeof(float) * rows, hipMemcpyDefault));
   return 0;
 }
 
@@ -1357,10 +1426,17 @@ int mtsac_buffer_get_state(mtsac_engine* h, int64_t* pos, int32_t* full) {
 
 int mtsac_buffer_set_reward_stats(mtsac_engine* h, const double* mn, const double* mx) {
   if (!h || !mn || !mx) return fail(-22, "null argument");
-  h->h_rmin.assign(mn, mn + h->T_l);
-  h->h_rmax.assign(mx, mx + h->T_l);
-  HIP_TRY(hipMemcpy(h->rmin, mn, sizeof(double) * h->T_l, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(h->rmax, mx, sizeof(double) * h->T_l, hipMemcpyHostToDevice));
+  HIP_TRY(hipStreamSynchronize(h->st));
+  HIP_TRY(hipMemcpy(h->rmin, mn, sizeof(double) * h->T_l, hipMemcpyDefault));
+  HIP_TRY(hipMemcpy(h->rmax, mx, sizeof(double) * h->T_l, hipMemcpyDefault));
+  return 0;
+}
+
+int mtsac_buffer_get_reward_stats(mtsac_engine* h, double* mn, double* mx) {
+  if (!h || !mn || !mx) return fail(-22, "null argument");
+  HIP_TRY(hipStreamSynchronize(h->st));
+  HIP_TRY(hipMemcpy(mn, h->rmin, sizeof(double) * h->T_l, hipMemcpyDefault));
+  HIP_TRY(hipMemcpy(mx, h->rmax, sizeof(double) * h->T_l, hipMemcpyDefault));
   return 0;
 }
 
@@ -1399,16 +1475,17 @@ int mtsac_sample(mtsac_engine* h, int64_t* indices, float* obs, float* actions, 
   if (indices) {
     std::vector<int> tmp(h->n);
     HIP_TRY(hipMemcpy(tmp.data(), h->idx, sizeof(int) * h->n, hipMemcpyDeviceToHost));
-    for (int i = 0; i < h->n; ++i) indices[i] = tmp[i];
+    std::vector<int64_t> wide(tmp.begin(), tmp.end());
+    HIP_TRY(hipMemcpy(indices, wide.data(), sizeof(int64_t) * h->n, hipMemcpyDefault));
   }
   if (obs) HIP_TRY(hipMemcpy2D(obs, sizeof(float) * D, h->xa, sizeof(float) * h->ld_a, sizeof(float) * D, B,
-                               hipMemcpyDeviceToHost));
+                               hipMemcpyDefault));
   if (next_obs) HIP_TRY(hipMemcpy2D(next_obs, sizeof(float) * D, h->xan, sizeof(float) * h->ld_a, sizeof(float) * D,
-                                    B, hipMemcpyDeviceToHost));
+                                    B, hipMemcpyDefault));
   if (actions) HIP_TRY(hipMemcpy2D(actions, sizeof(float) * A, h->xc, sizeof(float) * h->ld_c, sizeof(float) * A, B,
-                                   hipMemcpyDeviceToHost));
-  if (dones) HIP_TRY(hipMemcpy(dones, h->done, sizeof(float) * B, hipMemcpyDeviceToHost));
-  if (rewards) HIP_TRY(hipMemcpy(rewards, h->rew, sizeof(float) * B, hipMemcpyDeviceToHost));
+                                   hipMemcpyDefault));
+  if (dones) HIP_TRY(hipMemcpy(dones, h->done, sizeof(float) * B, hipMemcpyDefault));
+  if (rewards) HIP_TRY(hipMemcpy(rewards, h->rew, sizeof(float) * B, hipMemcpyDefault));
   return h->check_err();
 }
 
@@ -1472,7 +1549,7 @@ int mtsac_update_many(mtsac_engine* h, int32_t steps) {
 
 int mtsac_get_logs(mtsac_engine* h, float* logs) {
   if (!h || !logs) return fail(-22, "null argument");
-  HIP_TRY(hipMemcpyAsync(logs, h->logs, sizeof(float) * MTSAC_NUM_LOGS, hipMemcpyDeviceToHost, h->st));
+  HIP_TRY(hipMemcpyAsync(logs, h->logs, sizeof(float) * MTSAC_NUM_LOGS, hipMemcpyDefault, h->st));
   HIP_TRY(hipStreamSynchronize(h->st));
   return h->check_err();
 }
@@ -1570,6 +1647,44 @@ int mtsac_comm_init(mtsac_engine* h, const void* unique_id, int32_t nranks, int3
     h->gexec = nullptr;
     h->graph = nullptr;
   }
+  return 0;
+}
+
+int mtsac_get_noise_state(mtsac_engine* h, uint64_t* seed, uint64_t* counter) {
+  if (!h || !seed || !counter) return fail(-22, "null argument");
+  unsigned long long c = 0;
+  HIP_TRY(hipStreamSynchronize(h->st));
+  HIP_TRY(hipMemcpy(&c, h->counter, sizeof(c), hipMemcpyDeviceToHost));
+  *seed = h->cfg.noise_seed;
+  *counter = c;
+  return 0;
+}
+
+int mtsac_set_noise_state(mtsac_engine* h, uint64_t seed, uint64_t counter) {
+  if (!h) return fail(-22, "null engine");
+  unsigned long long c = counter;
+  HIP_TRY(hipStreamSynchronize(h->st));
+  HIP_TRY(hipMemcpy(h->counter, &c, sizeof(c), hipMemcpyHostToDevice));
+  if (seed != h->cfg.noise_seed) {  // the seed is a kernel argument inside the step graph
+    h->cfg.noise_seed = seed;
+    if (h->gexec) {
+      (void)hipGraphExecDestroy(h->gexec);
+      (void)hipGraphDestroy(h->graph);
+      h->gexec = nullptr;
+      h->graph = nullptr;
+    }
+  }
+  return 0;
+}
+
+int mtsac_comm_nranks(mtsac_engine* h, int32_t* nranks) {
+  if (!h || !nranks) return fail(-22, "null argument");
+  int n = 1;
+  if (h->comm) {
+    ncclResult_t r = ncclCommCount(h->comm, &n);
+    if (r != ncclSuccess) return fail(-5, std::string("ncclCommCount: ") + ncclGetErrorString(r));
+  }
+  *nranks = n;
   return 0;
 }
 

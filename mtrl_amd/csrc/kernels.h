@@ -130,6 +130,12 @@ void replay_gather(const GatherParams& p, hipStream_t st);
 // a user batch (ReplayBufferSamples layout) into the same input buffers
 void batch_scatter(const GatherParams& p, const float* obs, const float* act, const float* nobs,
                    const float* done, const float* rew, int B, hipStream_t st);
+// async add (engine.cpp mtsac_buffer_add): pack a slot from device arrays; commit it (reward
+// min/max, sampled range) on the device
+void buffer_pack_slot(float* rec, int T_l, int R, int D, int A, const float* obs, const float* nobs,
+                      const float* act, const float* rew, const float* done, hipStream_t st);
+void buffer_commit_slot(const float* rec, int T_l, int R, int rcol, double* rmin, double* rmax, long long* buf_size,
+                        long long size, hipStream_t st);
 void fill_synthetic(float* store, long long cap, int T_l, int R, int obs_dim, int act_dim, int T_glob,
                     int task_begin, unsigned long long seed, hipStream_t st);
 // stable per-task row lists: rows_of[t*max_rows + j], counts[t]

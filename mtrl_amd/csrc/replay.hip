@@ -264,3 +264,56 @@ void task_rows(const int* task, int B, int T_l, int* counts, int* rows, int max_
 }
 
 }  // namespace mtsac
+
+namespace mtsac {
+namespace {
+
+// One transition slot (T_l records) from five device arrays (T_l rows each) into store[slot]
+// (buffers.py:426-474 add: obs[pos] = obs, ...); one thread per record float.
+__global__ __launch_bounds__(256) void pack_slot_kernel(float* __restrict__ rec, int T_l, int R, int D, int A,
+                                                        const float* __restrict__ obs,
+                                                        const float* __restrict__ nobs,
+                                                        const float* __restrict__ act,
+                                                        const float* __restrict__ rew,
+                                                        const float* __restrict__ done) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= T_l * R) return;
+  const int t = i / R, c = i - t * R;
+  float v = 0.f;
+  if (c < D) v = obs[t * D + c];
+  else if (c < D + A) v = act[t * A + (c - D)];
+  else if (c == D + A) v = rew[t];
+  else if (c == D + A + 1) v = done[t];
+  else if (c < 2 * D + A + 2) v = nobs[t * D + (c - D - A - 2)];
+  rec[i] = v;
+}
+
+// after the slot is written: running per-task reward min / max in float64 (buffers.py:460-462)
+// and the sampled range pos-or-capacity (buffers.py:523) -- device-side, so adds never block
+__global__ __launch_bounds__(64) void commit_slot_kernel(const float* __restrict__ rec, int T_l, int R, int rcol,
+                                                         double* rmin, double* rmax, long long* buf_size,
+                                                         long long size) {
+  const int t = threadIdx.x;
+  if (rmin != nullptr && t < T_l) {
+    const double r = (double)rec[t * R + rcol];
+    rmin[t] = fmin(rmin[t], r);
+    rmax[t] = fmax(rmax[t], r);
+  }
+  if (t == 0) *buf_size = size;
+}
+
+}  // namespace
+
+void buffer_pack_slot(float* rec, int T_l, int R, int D, int A, const float* obs, const float* nobs,
+                      const float* act, const float* rew, const float* done, hipStream_t st) {
+  const int n = T_l * R;
+  hipLaunchKernelGGL(pack_slot_kernel, dim3((n + 255) / 256), dim3(256), 0, st, rec, T_l, R, D, A, obs, nobs, act, rew,
+                     done);
+}
+
+void buffer_commit_slot(const float* rec, int T_l, int R, int rcol, double* rmin, double* rmax, long long* buf_size,
+                        long long size, hipStream_t st) {
+  hipLaunchKernelGGL(commit_slot_kernel, dim3(1), dim3(64), 0, st, rec, T_l, R, rcol, rmin, rmax, buf_size, size);
+}
+
+}  // namespace mtsac

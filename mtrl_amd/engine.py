@@ -135,6 +135,11 @@ class MTSACEngine:
         mx = np.ascontiguousarray(max_r, dtype=np.float64)
         check(self.lib.mtsac_buffer_set_reward_stats(self._h, mn.ctypes.data_as(_lib.PD), mx.ctypes.data_as(_lib.PD)))
 
+    def reward_stats(self) -> tuple[np.ndarray, np.ndarray]:
+        mn, mx = np.empty(self.T_l, np.float64), np.empty(self.T_l, np.float64)
+        check(self.lib.mtsac_buffer_get_reward_stats(self._h, mn.ctypes.data_as(_lib.PD), mx.ctypes.data_as(_lib.PD)))
+        return mn, mx
+
     def set_rng_state(self, st: dict) -> None:
         """Load a numpy ``PCG64`` ``bit_generator.state`` dict (buffers.py:335)."""
         assert st["bit_generator"] == "PCG64"
@@ -222,6 +227,19 @@ class MTSACEngine:
     def comm_init(self, unique_id: bytes, nranks: int, rank: int) -> None:
         buf = ctypes.create_string_buffer(bytes(unique_id), len(unique_id))
         check(self.lib.mtsac_comm_init(self._h, buf, nranks, rank))
+
+    def noise_state(self) -> tuple[int, int]:
+        s, c = ctypes.c_uint64(), ctypes.c_uint64()
+        check(self.lib.mtsac_get_noise_state(self._h, ctypes.byref(s), ctypes.byref(c)))
+        return s.value, c.value
+
+    def set_noise_state(self, seed: int, counter: int) -> None:
+        check(self.lib.mtsac_set_noise_state(self._h, seed, counter))
+
+    def comm_nranks(self) -> int:
+        n = ctypes.c_int32()
+        check(self.lib.mtsac_comm_nranks(self._h, ctypes.byref(n)))
+        return n.value
 
     def set_allreduce_hook(self, fn) -> None:
         """``fn(device_ptr: int, count: int)`` must leave the SUM over shards in the buffer."""

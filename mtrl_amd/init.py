@@ -70,3 +70,21 @@ def init_mtsac(num_tasks: int, obs_dim: int, action_dim: int, actor_width: int, 
     pa = slice_tasks(pa, task_begin, task_count, False)
     pc = slice_tasks(pc, task_begin, task_count, True)
     return flatten(pa, ash_l), flatten(pc, csh_l)
+
+
+def slice_heads(flat, in_dim: int, width: int, depth: int, num_tasks: int, head_dim: int, ens: int | None,
+                begin: int, count: int) -> np.ndarray:
+    """A full-task flat parameter vector (flax leaf order) cut down to the heads of tasks
+    [begin, begin+count): the vector a task shard's engine holds."""
+    flat = np.asarray(flat).reshape(-1)
+    shapes = leaf_shapes(in_dim, width, depth, num_tasks, head_dim, ens)
+    if begin == 0 and count == num_tasks:
+        return flat
+    p, o = {}, 0
+    for k, s in shapes:
+        m = int(np.prod(s))
+        p[k] = flat[o:o + m].reshape(s)
+        o += m
+    q = slice_tasks(p, begin, count, ens is not None)
+    return np.concatenate([np.ascontiguousarray(q[k]).reshape(-1)
+                           for k, _ in leaf_shapes(in_dim, width, depth, count, head_dim, ens)])

@@ -67,3 +67,19 @@ class InProcessAllReduce:
             self.barrier.wait()
 
         return fn
+
+
+def allreduce_floats_per_step(obs_dim: int, action_dim: int, actor_width: int, actor_depth: int, critic_width: int,
+                              critic_depth: int, num_critics: int) -> int:
+    """Floats one rank all-reduces per gradient step: each network's contiguous trunk range
+    (leaves 64-float aligned, engine.cpp Net::layout) plus its 128-float scalar tail, and the
+    2 floats of head |p|^2 (engine.cpp step())."""
+    def trunk(in_dim, width, depth, ens):
+        n, fan = 0, in_dim
+        for _ in range(depth):
+            n += -(-width * ens // 64) * 64 + -(-fan * width * ens // 64) * 64
+            fan = width
+        return n
+
+    return (trunk(obs_dim, actor_width, actor_depth, 1) + 128
+            + trunk(obs_dim + action_dim, critic_width, critic_depth, num_critics) + 128 + 2)

@@ -1,0 +1,197 @@
+"""Full-batch GPU parity at the bench's own sizes ("do this" 1).
+
+The bench runs S3 (MT50/W2048, n=128 -> B=6400) on the 224x256-tile GEMM
+geometry with a ragged last row tile (6400 = 28*224 + 128), the full-K split
+choice and full-size plane buffers; S2 (MT10/W2048 clip, B=1280) and the 8-way
+MT50 task split (7,7,6,6,6,6,6,6 tasks x 128 rows) run other geometries and
+split-K choices.  Each case here is ONE complete gradient step on exactly those
+shapes, compared with the float64 oracle (oracle/mtsac.py, restating
+mtrl/rl/algorithms/mtsac.py:1173-1251) from the same fp32 parameters, batch and
+injected noise.  log_alpha starts away from 0 so the temperature loss is live.
+
+Bars (BASELINE.json north_star): losses within 1e-5 relative (qf_values
+included); grad and parameter norms within 1e-5 relative; parameters after the
+step elementwise within fp32 Adam tolerance (median |d| < 1e-6, max <= 2 lr).
+"""
+
+from __future__ import annotations
+
+import functools
+
+import numpy as np
+import pytest
+
+from helpers import synthetic_batch, synthetic_eps
+from oracle import mtsac as om
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+LOSS_KEYS = ("losses/qf_loss", "losses/actor_loss", "losses/alpha_loss", "losses/qf_values")
+NORM_KEYS = ("metrics/critic_grad_magnitude", "metrics/actor_grad_magnitude", "metrics/critic_params_norm",
+             "metrics/actor_params_norm", "alpha")
+
+CASES = {
+    "s3_mt50_w2048": dict(T=50, W=2048, n=128, clip=False),
+    "s2_mt10_w2048_clip": dict(T=10, W=2048, n=128, clip=True),
+}
+
+
+def _cfg(spec):
+    T, W = spec["T"], spec["W"]
+    return om.OracleConfig(num_tasks=T, obs_dim=39 + T, actor_width=W, critic_width=W, clip=spec["clip"])
+
+
+@functools.lru_cache(maxsize=None)
+def _problem(name):
+    """fp32-representable start state, one batch + noise, and the float64 oracle step (cached:
+    the same oracle result serves both precisions and the sharded run)."""
+    spec = CASES[name]
+    cfg = _cfg(spec)
+    T, n = spec["T"], spec["n"]
+    B = n * T
+    st = om.initialize(cfg, seed=11)
+    st.log_alpha = np.random.default_rng(12).uniform(-0.3, 0.3, T)
+    for k in ("actor", "critic", "critic_target", "log_alpha"):
+        setattr(st, k, getattr(st, k).astype(np.float32).astype(np.float64))
+    batch = synthetic_batch(T, B, seed=100, dtype=np.float32)
+    en, ec = synthetic_eps(B, seed=200, dtype=np.float32)
+    st1, want = om.update(cfg, st, [b.astype(np.float64) for b in batch], en.astype(np.float64),
+                          ec.astype(np.float64))
+    return cfg, st, batch, en, ec, st1, want
+
+
+def _engine(spec, precision, begin=0, count=None):
+    from mtrl_amd.engine import MTSACEngine, make_config
+
+    T, W, n = spec["T"], spec["W"], spec["n"]
+    c = make_config(num_tasks=T, task_begin=begin, task_count=T if count is None else count, obs_dim=39 + T,
+                    actor_width=W, critic_width=W, batch_per_task=n, capacity=n, clip=int(spec["clip"]),
+                    precision=precision)
+    e = MTSACEngine(c)
+    e.enable_graph(False)
+    return e
+
+
+def _load(e, st, begin=0, count=None):
+    from mtrl_amd import _lib as L
+    from mtrl_amd.init import slice_heads
+
+    T = st.log_alpha.size
+    count = T if count is None else count
+    cfg = e.config
+    e.set_params(L.ACTOR, slice_heads(st.actor, cfg.obs_dim, cfg.actor_width, cfg.actor_depth, T, 8, None, begin,
+                                      count))
+    for which, v in ((L.CRITIC, st.critic), (L.CRITIC_TARGET, st.critic_target)):
+        e.set_params(which, slice_heads(v, cfg.obs_dim + 4, cfg.critic_width, cfg.critic_depth, T, 1, 2, begin,
+                                        count))
+    e.set_params(L.LOG_ALPHA, st.log_alpha)
+
+
+def _check_logs(got, want, tag):
+    errs = {k: abs(got[k] - want[k]) / max(abs(want[k]), 1e-30) for k in LOSS_KEYS + NORM_KEYS}
+    print(tag, {k: f"{v:.2e}" for k, v in errs.items()})
+    for k in LOSS_KEYS + NORM_KEYS:
+        assert errs[k] <= RTOL, (tag, k, got[k], want[k], errs[k])
+    assert got["metrics/explore_loss"] == 0.0
+
+
+def _check_params(e, st1, tag, begin=0, count=None):
+    from mtrl_amd import _lib as L
+    from mtrl_amd.init import slice_heads
+
+    cfg = e.config
+    T = st1.log_alpha.size
+    count = T if count is None else count
+    refs = ((L.ACTOR, slice_heads(st1.actor, cfg.obs_dim, cfg.actor_width, cfg.actor_depth, T, 8, None, begin,
+                                  count)),
+            (L.CRITIC, slice_heads(st1.critic, cfg.obs_dim + 4, cfg.critic_width, cfg.critic_depth, T, 1, 2, begin,
+                                   count)),
+            (L.CRITIC_TARGET, slice_heads(st1.critic_target, cfg.obs_dim + 4, cfg.critic_width, cfg.critic_depth, T,
+                                          1, 2, begin, count)),
+            (L.LOG_ALPHA, st1.log_alpha))
+    for which, ref in refs:
+        d = np.abs(e.get_params(which).astype(np.float64) - ref)
+        assert np.median(d) < 1e-6, (tag, which, np.median(d))
+        assert d.max() < 2 * 3e-4 + 1e-6, (tag, which, d.max())
+
+
+@pytest.mark.parametrize("precision", [0, 1], ids=["fp32", "split3"])
+@pytest.mark.parametrize("name", list(CASES))
+def test_full_batch_step_matches_oracle(name, precision):
+    cfg, st, batch, en, ec, st1, want = _problem(name)
+    e = _engine(CASES[name], precision)
+    _load(e, st)
+    e.update(batch, en, ec)
+    _check_logs(e.logs(), want, f"{name}/p{precision}")
+    _check_params(e, st1, f"{name}/p{precision}")
+    assert e.get_adam_count(0) == 1 and e.get_adam_count(1) == 1 and e.get_adam_count(2) == 1
+    e.close()
+
+
+@pytest.mark.parametrize("precision", [0, 1], ids=["fp32", "split3"])
+def test_full_batch_8way_shard_matches_oracle(precision):
+    """The MT50 8-GPU task split (7,7,6,6,6,6,6,6 tasks, 128 rows each) as 8 engines on one
+    device reducing through the in-process hook (same reduction points as RCCL), against
+    the float64 oracle of the unsharded step."""
+    import threading
+
+    from mtrl_amd.shard import InProcessAllReduce, local_rows, shard_tasks
+
+    name, world = "s3_mt50_w2048", 8
+    spec = CASES[name]
+    cfg, st, batch, en, ec, st1, want = _problem(name)
+    T, n = spec["T"], spec["n"]
+    shards = []
+    for r in range(world):
+        b0, c0 = shard_tasks(T, world, r)
+        e = _engine(spec, precision, b0, c0)
+        _load(e, st, b0, c0)
+        shards.append(e)
+    group = InProcessAllReduce(world)
+    for r, e in enumerate(shards):
+        e.set_allreduce_hook(group.hook(r))
+    errs = []
+
+    def run(r):
+        try:
+            b0, c0 = shard_tasks(T, world, r)
+            rows = local_rows(T, n, b0, c0)
+            shards[r].update(tuple(x[rows] for x in batch), en[rows], ec[rows])
+        except Exception as ex:  # pragma: no cover
+            errs.append(ex)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert not errs, errs
+    logs = [e.logs() for e in shards]
+    assert all(lg == logs[0] for lg in logs)  # every logged scalar is reduced: ranks agree bitwise
+    _check_logs(logs[0], want, f"shard8/p{precision}")
+    for r, e in enumerate(shards):
+        b0, c0 = shard_tasks(T, world, r)
+        _check_params(e, st1, f"shard8/p{precision}/r{r}", b0, c0)
+        e.close()
+
+
+def test_full_batch_graph_replay_equals_eager():
+    """S3 at full size on the device-sampled path the bench times: 3 steps replayed from the
+    step graph give bitwise the logs, parameters and index-stream state of 3 eager steps."""
+    from mtrl_amd import _lib as L
+
+    spec = CASES["s3_mt50_w2048"]
+    _, st, *_ = _problem("s3_mt50_w2048")
+    outs = []
+    for graph in (False, True):
+        e = _engine(spec, 1)
+        _load(e, st)
+        e.enable_graph(graph)
+        e.buffer_fill_synthetic(1234)
+        e.seed_rng(1)
+        e.update_many(3)
+        outs.append((e.logs(), e.get_params(L.ACTOR), e.get_params(L.CRITIC), e.get_rng_state()))
+        e.close()
+    assert outs[0][0] == outs[1][0]
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    np.testing.assert_array_equal(outs[0][2], outs[1][2])
+    assert outs[0][3] == outs[1][3]

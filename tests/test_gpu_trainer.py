@@ -126,11 +126,13 @@ def test_flax_named_checkpoint_resumes_bitwise(tmp_path):
     m = NpzCheckpointManager(tmp_path / "ck")
     m.save(2, agent, metadata={"step": 2})
     with np.load(tmp_path / "ck" / "ckpt_2.npz") as z:
-        assert "agent/critic/target_params/VmapQValueFunction_0/MultiHeadNetwork_0/layer_2/kernel" in z.files
+        assert "agent/critic/target_params/params/VmapQValueFunction_0/MultiHeadNetwork_0/layer_2/kernel" in z.files
     a2 = MTSAC.initialize(exp.algorithm, exp.env, seed=11)
     a2.update(ReplayBufferSamples(*batch()))
     meta, _ = m.restore(m.latest_step(), a2)
     assert meta == {"step": 2}
+    np.testing.assert_array_equal(a2.noise_key(), agent.noise_key())  # update-noise stream position
+    assert a2.rng_state() == agent.rng_state()  # action-noise Generator
     b, en, ec = batch(), eps(), eps()
     agent.engine.update(b, en, ec)
     a2.engine.update(b, en, ec)

@@ -97,7 +97,7 @@ def test_update_matches_oracle(name, precision):
             if k == "losses/alpha_loss" and step == 0:
                 assert abs(got[k]) < 1e-6  # log_alpha = 0 at init -> loss is exactly 0
                 continue
-            tol = LOSS_RTOL if k != "losses/qf_values" else 1e-4
+            tol = LOSS_RTOL
             scale = max(abs(want[k]), 1e-3) if k == "losses/qf_values" else abs(want[k])
             assert abs(got[k] - want[k]) <= tol * scale, (name, step, k, got[k], want[k])
         for k in ("metrics/critic_grad_magnitude", "metrics/actor_grad_magnitude", "metrics/critic_params_norm",
