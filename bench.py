@@ -45,8 +45,8 @@ HBM_PEAK_GBS = 8000.0
 # enum mtsac_gemm_family (include/mtsac.h) -> the rocprof kernel(s) of that family, per precision
 GEMM_FAMILIES = {
     "split3": {
-        0: "gemm_x3p_kernel<Geo<224, 256, 1, 8, 3, 16, 0>, false, true, 1, *> (hidden-layer forward, planes: activations row-major x kernel k-major, bias+ReLU)",
-        1: "gemm_x3p_kernel<Geo<224, 256, 1, 8, 3, 16, 0>, false, false, 2, *> (hidden-layer data grad, NT on planes, ReLU mask)",
+        0: "gemm_x3p_kernel<Geo<224, 256, 1, 8, 3, 16, 0>, false, true, 1, *> (hidden-layer forward, planes)",
+        1: "gemm_x3p_kernel<Geo<224, 256, 1, 8, 3, 16, 0>, false, false, 2, *> (hidden-layer data grad, planes, ReLU mask)",
         2: "gemm_x3p_kernel<Geo<256, 256, 2, 4, 3, 16, 0>, true, true, 0, false> (hidden-layer weight grad, k-major planes, split-K)",
         3: "gemm_x3p_kernel<Geo<224, 256, 1, 8, 3, 16, 1>, false, true, 1, true> (input-layer forward, planes, K = in_dim padded to 32)",
         4: "gemm_x3_kernel<true, false, 0> (input-layer weight grad, on-the-fly split, split-K)",
@@ -319,7 +319,7 @@ def main():
     assert all(math.isfinite(v) for v in logs.values()), logs
 
     # dominant-kernel roofline from the per-launch HIP events
-    names = GEMM_FAMILIES[args.precision]
+    names = dict(GEMM_FAMILIES[args.precision])
     fam = {f: eng.timing(f) for f in names} if live else None
     # the same kernels solo: one extra step serialised on one stream.  Eager: context for the
     # fraction (under the step's concurrency a launch shares the CUs with its neighbours).
@@ -330,6 +330,10 @@ def main():
     eng.synchronize()
     solo = {f: eng.timing(f) for f in names}
     eng.set_timing(False)
+    for f in names:  # the kernel the engine actually launched for each family
+        k = eng.timing_kernel(f)
+        if k and k != "gemm_x3p_kernel":
+            names[f] = k + " (" + names[f].split(" (", 1)[1]
     if fam is None:
         fam = solo
     timed_steps = args.steps if live else 1

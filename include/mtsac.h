@@ -215,6 +215,8 @@ enum mtsac_gemm_family {
 int mtsac_set_timing(mtsac_engine* h, int32_t enable);
 int mtsac_get_timing(mtsac_engine* h, int32_t family, double* total_ms, int32_t* launches,
                      double* flops);
+/* the kernel behind a GEMM family at its last launch (labels for the bench and profiles) */
+int mtsac_get_timing_kernel(mtsac_engine* h, int32_t family, char* buf, int32_t n);
 
 #ifdef __cplusplus
 }

@@ -132,10 +132,13 @@ SIGNATURES = {
     "mtsac_memcpy": (ctypes.c_int, [P, P, I64]),
     "mtsac_set_timing": (ctypes.c_int, [P, I32]),
     "mtsac_get_timing": (ctypes.c_int, [P, I32, PD, PI32, PD]),
+    "mtsac_get_timing_kernel": (ctypes.c_int, [P, I32, P, I32]),
     "mtsac_debug_gemm_bench": (ctypes.c_int, [ctypes.c_int] * 8 + [PD]),
     "mtsac_debug_gemm_x3p": (ctypes.c_int, [ctypes.c_int] * 4 + [P, ctypes.c_int, P, ctypes.c_int, P, P, P, P]),
     "mtsac_debug_gemm_x3p_bench": (ctypes.c_int, [ctypes.c_int] * 6 + [PD]),
     "mtsac_debug_x3p_geo": (ctypes.c_int, [ctypes.c_int]),
+    "mtsac_debug_gemm_x3f": (ctypes.c_int, [ctypes.c_int] * 5 + [P] * 6),
+    "mtsac_debug_gemm_fwd_bench": (ctypes.c_int, [ctypes.c_int] * 7 + [PD]),
     "mtsac_debug_timed_launch": (ctypes.c_int, [P, I32, PI32, PD]),
     "mtsac_debug_gemm": (
         ctypes.c_int,

@@ -169,6 +169,139 @@ int mtsac_debug_gemm_x3p_bench(int epi, int batch, int M, int N, int K, int iter
   return 0;
 }
 
+// gemm_x3f (row-major x row-major planes, K % 64 == 0): C[M][N] = A[M][K] . B[N][K]^T from host
+// fp32 arrays, epi 1 bias+ReLU / 2 ReLU mask (fp32 mask, or with bit 8 of epi its bf16 high
+// plane); Csum (nullable) receives the sum of the written planes.  -95 when gemm_x3f does not take
+// the shape (too few tiles, layout).
+int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A, const float* B, float* C,
+                         const float* bias, const float* mask, float* Csum) {
+  const bool m16 = (epi >> 8) & 1;
+  epi &= 255;
+  if (M < 1 || N < 1 || K < 1 || batch < 1 || !A || !B || !C) return -22;
+  DevBuf d;
+  const size_t nA = (size_t)M * K * batch, nB = (size_t)N * K * batch, nC = (size_t)M * N * batch;
+  float* dA = d.get<float>(nA);
+  float* dB = d.get<float>(nB);
+  float* dC = d.get<float>(nC);
+  float* dbias = d.get<float>((size_t)N * batch);
+  float* dmask = d.get<float>(nC);
+  __bf16* dCp = d.get<__bf16>(3 * nC);
+  __bf16* dM16 = d.get<__bf16>(3 * nC);
+  if (!dA || !dB || !dC || !dbias || !dmask || !dCp || !dM16) return -12;
+  (void)hipMemcpy(dA, A, sizeof(float) * nA, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dB, B, sizeof(float) * nB, hipMemcpyHostToDevice);
+  if (bias) (void)hipMemcpy(dbias, bias, sizeof(float) * N * batch, hipMemcpyHostToDevice);
+  if (mask) (void)hipMemcpy(dmask, mask, sizeof(float) * nC, hipMemcpyHostToDevice);
+  const long long Kp = (K + 63) / 64 * 64;
+  __bf16* Ap = d.get<__bf16>((size_t)3 * M * Kp * batch);
+  __bf16* Bp = d.get<__bf16>((size_t)3 * N * Kp * batch);
+  if (!Ap || !Bp) return -12;
+  for (int z = 0; z < batch; ++z) {
+    SplitParams s{};
+    s.x = dA + (size_t)z * M * K; s.ldx = K; s.rows = M; s.cols = K;
+    s.out = Ap + (size_t)z * 3 * M * Kp; s.ldo = Kp; s.po = (long long)M * Kp; s.out_rows = M; s.out_cols = (int)Kp;
+    split_planes(s, false, 1, nullptr);
+    s.x = dB + (size_t)z * N * K; s.rows = N;
+    s.out = Bp + (size_t)z * 3 * N * Kp; s.po = (long long)N * Kp; s.out_rows = N;
+    split_planes(s, false, 1, nullptr);
+    if (m16) {  // planes of the mask, row stride N
+      s.x = dmask + (size_t)z * M * N; s.ldx = N; s.rows = M; s.cols = N;
+      s.out = dM16 + (size_t)z * 3 * M * N; s.ldo = N; s.po = (long long)M * N; s.out_rows = M; s.out_cols = N;
+      split_planes(s, false, 1, nullptr);
+    }
+  }
+  SplitGemmParams g{};
+  g.A = Ap; g.lda = Kp; g.pA = (long long)M * Kp; g.sA = 3 * g.pA;
+  g.B = Bp; g.ldb = Kp; g.pB = (long long)N * Kp; g.sB = 3 * g.pB;
+  g.C = dC; g.ldc = N; g.sC = (long long)M * N;
+  g.bias = dbias; g.sBias = N;
+  g.mask = dmask; g.ldm = N; g.sMask = (long long)M * N;
+  if (m16) {
+    g.mask16 = dM16;
+    g.sMask = 3ll * M * N;
+  }
+  if (Csum) {
+    g.Cp = dCp; g.ldcp = N; g.pC = (long long)M * N; g.sCp = 3 * g.pC;
+  }
+  g.M = M; g.N = N; g.K = (int)Kp;
+  if (!gemm_x3f_ok(g, epi, batch)) return -95;
+  gemm_x3f(g, epi, batch, nullptr);
+  if (hipDeviceSynchronize() != hipSuccess) return -5;
+  if (hipMemcpy(C, dC, sizeof(float) * nC, hipMemcpyDeviceToHost) != hipSuccess) return -5;
+  if (Csum) {
+    std::vector<__bf16> h(3 * nC);
+    if (hipMemcpy(h.data(), dCp, sizeof(__bf16) * h.size(), hipMemcpyDeviceToHost) != hipSuccess) return -5;
+    const size_t n = (size_t)M * N;
+    for (int z = 0; z < batch; ++z)
+      for (size_t i = 0; i < n; ++i) {
+        const __bf16* q = &h[(size_t)z * 3 * n];
+        Csum[(size_t)z * n + i] = ((float)q[i] + (float)q[n + i]) + (float)q[2 * n + i];
+      }
+  }
+  return 0;
+}
+
+// time iters launches of the forward-shaped plane GEMM (C = relu(A . B^T + bias) with planes out)
+// on device-resident random planes; which: 0 = gemm_x3p (row-major A, k-major B: the engine's
+// current forward), 1 = gemm_x3f (row-major both)
+int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int K, int iters, double* ms_per_launch) {
+  const int outs = (epi >> 8) & 3;  // 0: fp32 + planes, 1: planes only, 2: fp32 only
+  epi &= 255;
+  if (M < 1 || N < 1 || K < 1 || batch < 1 || iters < 1 || !ms_per_launch) return -22;
+  DevBuf d;
+  const long long Kp = (K + 63) / 64 * 64;
+  float* fa = d.get<float>((size_t)M * Kp);
+  float* fb = d.get<float>((size_t)N * Kp);
+  float* C = d.get<float>((size_t)M * N * batch);
+  float* bias = d.get<float>((size_t)N * batch);
+  __bf16* Cp = d.get<__bf16>((size_t)3 * M * N * batch);
+  if (!fa || !fb || !C || !bias || !Cp) return -12;
+  hipLaunchKernelGGL(fill_rand_f32, dim3((unsigned)(((long long)M * Kp + 255) / 256)), dim3(256), 0, nullptr, fa,
+                     (long long)M * Kp, 3u);
+  hipLaunchKernelGGL(fill_rand_f32, dim3((unsigned)(((long long)N * Kp + 255) / 256)), dim3(256), 0, nullptr, fb,
+                     (long long)N * Kp, 5u);
+  const bool bk = which == 0;  // gemm_x3p forward: B k-major [K][N]
+  long long lda, pa, ldb, pb;
+  plane_geom(M, (int)Kp, false, lda, pa);
+  plane_geom(N, (int)Kp, bk, ldb, pb);
+  __bf16* Ap = d.get<__bf16>((size_t)3 * pa * batch);
+  __bf16* Bp = d.get<__bf16>((size_t)3 * pb * batch);
+  if (!Ap || !Bp) return -12;
+  for (int z = 0; z < batch; ++z) {
+    split_into(fa, M, (int)Kp, false, Ap + 3 * pa * z);
+    split_into(fb, N, (int)Kp, bk, Bp + 3 * pb * z);
+  }
+  SplitGemmParams g{};
+  g.A = Ap; g.lda = lda; g.pA = pa; g.sA = 3 * pa;
+  g.B = Bp; g.ldb = ldb; g.pB = pb; g.sB = 3 * pb; g.b_kmajor = bk;
+  g.C = C; g.ldc = N; g.sC = (long long)M * N;
+  g.bias = bias; g.sBias = N;
+  g.mask = C; g.ldm = N; g.sMask = (long long)M * N;
+  g.Cp = Cp; g.ldcp = N; g.pC = (long long)M * N; g.sCp = 3 * g.pC;
+  if (outs == 1) g.C = nullptr;
+  if (outs == 2) g.Cp = nullptr;
+  g.M = M; g.N = N; g.K = (int)Kp;
+  g.splits = 1;
+  if (which == 1 && !gemm_x3f_ok(g, epi, batch)) return -95;
+  auto run = [&]() {
+    if (which == 1) gemm_x3f(g, epi, batch, nullptr);
+    else gemm_x3p(g, epi, batch, nullptr);
+  };
+  run();
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return -5;
+  (void)hipEventRecord(e0, nullptr);
+  for (int i = 0; i < iters; ++i) run();
+  (void)hipEventRecord(e1, nullptr);
+  if (hipEventSynchronize(e1) != hipSuccess) return -5;
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  *ms_per_launch = ms / iters;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return 0;
+}
+
 int mtsac_debug_x3p_geo(int geo) {
   const int old = g_x3p_geo;
   if (geo < 0) {  // restore the default (e.g. the value this function returned)

@@ -69,6 +69,12 @@ struct Net {
   // ald = width rounded up to 32).
   __bf16* wp[2][MAXD] = {};
   long long wld = 0, wrows = 0, arows = 0, ald = 0;
+  // gemm_x3f path (row-major x row-major, gemm_x3f.hip) for the hidden layers' forward and data
+  // grad: W_i^T planes ([E][3][width (out)][ald (in)], i >= 1) of p ([0]) and tgt ([1]); hidden
+  // activations then keep planes only (their ReLU mask is read from the high plane)
+  bool x3f = false;
+  __bf16* wtp[2][MAXD] = {};
+  long long wtps() const { return (long long)width * ald; }
   long long xld = 0;  // input planes' row stride = layer-0 kernel plane rows (in_dim rounded up to 32)
   long long aps() const { return arows * ald; }  // plane stride of activation planes
   long long wps() const { return wrows * wld; }  // plane stride of hidden kernel planes
@@ -290,6 +296,9 @@ struct mtsac_engine {
     t_end();
   }
 
+  // kernel behind each GEMM family at its last launch (bench / profile labels)
+  std::string fam_kernel[8];
+
   void gemmp(const SplitGemmParams& p, int epi, int batch, int family) {
     t_begin(family, 2.0 * (double)p.M * p.N * p.K * batch);
     if (timing) {
@@ -298,7 +307,14 @@ struct mtsac_engine {
       tl[tl_next].K = p.K;
       tl[tl_next].batch = batch;
     }
-    gemm_x3p(p, epi, batch, cur);
+    if (gemm_x3f_ok(p, epi, batch)) {
+      gemm_x3f(p, epi, batch, cur);
+      fam_kernel[family] = std::string("gemm_x3f_kernel<208, ") + (epi == EPI_BIAS_RELU ? "bias+ReLU" : "ReLU mask") +
+                           (p.mask16 ? " from bf16 high plane" : "") + ", *>";
+    } else {
+      gemm_x3p(p, epi, batch, cur);
+      fam_kernel[family] = "gemm_x3p_kernel";
+    }
     t_end();
   }
 
@@ -338,6 +354,35 @@ struct mtsac_engine {
     }
     for (int i = 0; i < net.depth; ++i) {
       const bool last = i == net.depth - 1;
+      if (pl && i > 0 && net.x3f) {  // on planes, both row-major: h_{i-1} . (W_i^T)^T (gemm_x3f)
+        SplitGemmParams g{};
+        g.A = actp[i - 1];
+        g.lda = net.ald;
+        g.pA = net.aps();
+        g.sA = 3 * net.aps();
+        g.B = net.wtp[which][i];
+        g.ldb = net.ald;
+        g.pB = net.wtps();
+        g.sB = 3 * net.wtps();
+        if (last) {  // the heads read fp32
+          g.C = acts[i];
+          g.ldc = net.width;
+          g.sC = (long long)M * net.width;
+        } else {  // the next layer and the data grad's ReLU mask read the planes only
+          g.Cp = actp[i];
+          g.ldcp = net.ald;
+          g.pC = net.aps();
+          g.sCp = 3 * net.aps();
+        }
+        g.bias = params + net.off_b[i];
+        g.sBias = net.ms_b;
+        g.M = M;
+        g.N = net.width;
+        g.K = (int)net.ald;
+        g.splits = 1;
+        gemmp(g, EPI_BIAS_RELU, net.E, MTSAC_FAM_FORWARD);
+        continue;
+      }
       if (pl && (i > 0 || xp)) {  // on planes: input (row-major) . W_i (k-major)
         SplitGemmParams g{};
         g.A = i == 0 ? xp : actp[i - 1];
@@ -417,6 +462,21 @@ struct mtsac_engine {
       sp.out_cols = (int)net.wld;
       sp.out = net.wp[which][i];
       if (!(fused && planes_fusable(net))) split_planes(sp, false, net.E, s);
+      if (net.x3f && i > 0) {  // W_i^T planes for the gemm_x3f forward
+        SplitParams st{};
+        st.x = params + net.off_W[i];
+        st.ldx = net.width;
+        st.sx = net.ms_W[i];
+        st.rows = net.width;  // in
+        st.cols = net.width;  // out
+        st.out = net.wtp[which][i];
+        st.ldo = net.ald;
+        st.po = net.wtps();
+        st.so = 3 * net.wtps();
+        st.out_rows = net.width;
+        st.out_cols = (int)net.ald;
+        split_planes(st, true, net.E, s);
+      }
     }
   }
 
@@ -472,7 +532,8 @@ struct mtsac_engine {
     gemm(g, GEMM_TN, EPI_STORE, net.E, i == 0 ? MTSAC_FAM_INPUT_WEIGHT_GRAD : MTSAC_FAM_WEIGHT_GRAD);
   }
 
-  void dgrad_layer(Net& net, const float* params, float** acts, float** dz, __bf16** dzp, int i, int M) {
+  void dgrad_layer(Net& net, const float* params, float** acts, __bf16** actp, float** dz, __bf16** dzp, int i,
+                   int M) {
     if (planes && dzp) {  // NT on planes: dz[i] . W_i^T, W_i planes read as [N = in][K = out]
       SplitGemmParams g{};
       g.A = dzp[i];
@@ -486,9 +547,15 @@ struct mtsac_engine {
       g.C = dz[i - 1];
       g.ldc = net.width;
       g.sC = (long long)M * net.width;
-      g.mask = acts[i - 1];
-      g.ldm = net.width;
-      g.sMask = (long long)M * net.width;
+      if (net.x3f) {  // hidden activations keep planes only: h > 0 <=> its bf16 high plane > 0
+        g.mask16 = actp[i - 1];
+        g.ldm = (int)net.ald;
+        g.sMask = 3 * net.aps();
+      } else {
+        g.mask = acts[i - 1];
+        g.ldm = net.width;
+        g.sMask = (long long)M * net.width;
+      }
       if (dzp[i - 1]) {
         g.Cp = dzp[i - 1];
         g.ldcp = net.ald;
@@ -669,7 +736,7 @@ struct mtsac_engine {
         rprev = rprev < 0 ? seg({wprev}, 4, [&, b, e] { allreduce(net.g + b, (size_t)(e - b)); })
                           : seg({wprev, rprev}, 4, [&, b, e] { allreduce(net.g + b, (size_t)(e - b)); });
       }
-      if (i > 0) dprev = seg({dprev}, 1, [&, i] { dgrad_layer(net, params, acts, dz, dzp, i, M); });
+      if (i > 0) dprev = seg({dprev}, 1, [&, i] { dgrad_layer(net, params, acts, actp, dz, dzp, i, M); });
     }
     if (rprev >= 0) return seg({dprev, wprev, rprev}, 1, [] {});  // join point
     return seg({dprev, wprev}, 1, [] {});
@@ -806,7 +873,7 @@ struct mtsac_engine {
       c.inv_norm = 1.0f / (float)B_glob;
       critic_head(c, cur);
       head_backward_data(c.head, dq, Bl, dzc[critic.depth - 1], cur, top_planes(critic, dzcp));
-      for (int i = critic.depth - 1; i > 0; --i) dgrad_layer(critic, critic.p, hc, dzc, dzcp, i, Bl);
+      for (int i = critic.depth - 1; i > 0; --i) dgrad_layer(critic, critic.p, hc, hcp, dzc, dzcp, i, Bl);
       ActionGradParams ag{};
       ag.dz1 = dzc[0];
       ag.W0 = critic.p + critic.off_W[0];
@@ -1054,6 +1121,8 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     net->ald = align_up(net->width, 32);
     net->xld = align_up(net->in_dim, 32);
     net->arows = align_up(e->B, 32);
+    // gemm_x3f takes the hidden layers when its 208 x 256 tiles fill the chip (gemm_x3f_ok)
+    net->x3f = e->planes && net->depth > 1 && net->ald % 64 == 0 && gemm_x3f_tiles(e->B, net->width, net->E) >= 192;
     for (int w = 0; w < (net == &e->critic ? 2 : 1); ++w)
       for (int i = 0; i < net->depth; ++i) {
         if (!e->planes) {
@@ -1061,6 +1130,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
           continue;
         }
         if ((rc = e->alloc(&net->wp[w][i], (size_t)net->E * 3 * net->kps(i)))) return bad(rc);
+        if (net->x3f && i > 0 && (rc = e->alloc(&net->wtp[w][i], (size_t)net->E * 3 * net->wtps()))) return bad(rc);
       }
   }
   {  // split-K workspaces: the largest GEMM that splits, per lane
@@ -1724,6 +1794,13 @@ int mtsac_get_timing(mtsac_engine* h, int32_t family, double* total_ms, int32_t*
   *total_ms = ms;
   *launches = nl;
   *flops = fl;
+  return 0;
+}
+
+int mtsac_get_timing_kernel(mtsac_engine* h, int32_t family, char* buf, int32_t n) {
+  if (!h || !buf || n < 1) return fail(-22, "null argument");
+  if (family < 0 || family >= 8) return fail(-22, "unknown family");
+  std::snprintf(buf, (size_t)n, "%s", h->fam_kernel[family].c_str());
   return 0;
 }
 

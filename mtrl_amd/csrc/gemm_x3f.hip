@@ -1,0 +1,300 @@
+// gemm_x3f.hip -- fp32-accurate plane GEMM for the trunk forward and data-grad products (gfx950).
+//
+//   C[z][m][n] = sum_k A(m, k) B(n, k), both operands ROW-MAJOR bf16 planes ([3][rows][ld], k
+//   contiguous, x = x_h + x_m + x_l exactly), K a multiple of 64 (zero padded).
+//
+// Design (MI355X_MICROARCH.md / cdna_hip_programming.md §5):
+//   * v_mfma_f32_16x16x32_bf16: the same issue cost per flop as the 32x32x16 form but it holds a
+//     higher clock under load (MI355X_MICROARCH.md, DVFS item 7); 6 products per 16x16 tile and
+//     32-deep k slice (m*m, h*l, l*h, h*m, m*h, h*h: small terms first), fp32 accumulation.
+//   * 512 threads = 8 waves, 2 per SIMD; the workgroup tile is BM x 256, wave w owns the BM x 32
+//     column slab [32w, 32w + 32) -- 13 x 2 accumulator tiles at BM = 208 (104 AGPRs).
+//   * A (the activations, shared by all 8 waves) is staged through LDS by LDS-DMA in FULL 128-B
+//     lines: one stage = 64 k, one DMA wave-instruction = 8 rows x 128 B of one plane, written
+//     lane-linearly into a [row][8 x 16 B] image whose 16-B chunks are XOR-swizzled by row & 7 on
+//     the SOURCE address, so the fragment reads (ds_read_b128, lane = row l & 15, chunk l >> 4)
+//     are bank-conflict free.  Two stages (2 x 78 KB at BM = 208), one barrier per 64-deep step,
+//     the refill of the next stage spread over the current step's MFMAs.
+//   * B (the weights, each wave its own 32 columns: nothing to share inside the workgroup) goes
+//     straight from L2 to registers as MFMA fragments (global_load_dwordx4, 16 rows x 64 B per
+//     instruction), double-buffered per 32-deep half step.  Both load queues are counted by hand
+//     (inline asm), so the compiler never drains the LDS-DMA early.
+//   * M is cut into BM = 208-row tiles: B = 6400 rows -> 31 row tiles x 8 column tiles = 248
+//     workgroups on 256 CUs (E = 1), 496 in two full rounds (E = 2).
+//   * Epilogue per 16-row block through a wave-private LDS scratch: 32 B of fp32 per lane (whole
+//     128-B row segments) and 16 B per bf16 plane; bias+ReLU or ReLU mask (fp32 or the bf16 high
+//     plane of the activation: h > 0 <=> h_hi > 0 for every normal h).
+#include <algorithm>
+#include <type_traits>
+
+#include "gemm_x3p_impl.h"
+
+namespace mtsac {
+namespace x3fk {
+
+using x3pk::glds16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BN = 256;  // 8 waves x 32 columns
+constexpr int KS = 64;   // k per stage / main-loop step
+
+// One B fragment: 16 B of row n at byte offset voff from the wave-uniform base (no compiler wait)
+__device__ inline bf16x8 gload_frag(const __bf16* base, unsigned voff) {
+  bf16x8 r;
+  asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(r) : "v"(voff), "s"(base) : "memory");
+  return r;
+}
+
+template <int N>
+__device__ inline void wait_vm6(bf16x8 (&b)[2][3]) {
+  asm volatile("s_waitcnt vmcnt(%6)"
+               : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[0][2]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[1][2])
+               : "n"(N)
+               : "memory");
+}
+
+template <int BM, int EPI, bool C_OUT, bool P_OUT, bool MASK16>
+__global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
+  constexpr int TI = BM / 16;            // 16-row accumulator tiles per wave
+  constexpr int PLANE = BM * 128;        // bytes of one plane of one stage
+  constexpr int STAGE = 3 * PLANE;
+  constexpr int NJ = 3 * BM / 8;         // DMA wave-instructions per stage
+  constexpr int PMAX = (NJ + 7) / 8;     // per wave (the first NJ % 8 waves), others PMAX - 1
+  constexpr int P0 = (PMAX + 1) / 2;     // issued in the first half step
+  static_assert(BM % 16 == 0 && 2 * STAGE <= 160 * 1024, "tile");
+  static_assert(PMAX - 1 >= P0 || NJ % 8 == 0, "every wave issues >= P0 pieces in the first half step");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const unsigned lds_base = (unsigned)(unsigned long long)(x3pk::lds_void*)smem;
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  __builtin_assume(wave >= 0 && wave < 8);
+  const int mine = (wave < NJ % 8 || NJ % 8 == 0) ? PMAX : PMAX - 1;  // DMA pieces of this wave
+
+  // XCD-contiguous tile order (as gemm_x3p): N tile fastest inside an XCD's run
+  const int ny = (p.N + BN - 1) / BN, nx = (p.M + BM - 1) / BM;
+  int lin = blockIdx.x;
+  {
+    const int n = gridDim.x, q8 = n / 8, r8 = n % 8, x = lin % 8;
+    lin = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + lin / 8;
+  }
+  const int by = lin % ny, bx = (lin / ny) % nx, z = lin / (ny * nx);
+  const int m0 = bx * BM, n0 = by * BN;
+  const __bf16* __restrict__ A = p.A + z * p.sA;
+  const __bf16* B = p.B + z * p.sB;
+  const int nk = p.K / KS;
+
+  // ---- A: LDS-DMA piece j of the stage at k0 into stage buffer `st` (byte address)
+  auto piece = [&](int j, int k0, unsigned st) {
+    const int q = j / (BM / 8), rg = j % (BM / 8);
+    int row = m0 + 8 * rg + (lane >> 3);
+    const int pc = lane & 7;                       // physical 16-B chunk
+    const int c = pc ^ (row & 7);                  // logical chunk it holds (8 k each)
+    row = row < p.M ? row : p.M - 1;               // rows past M feed discarded outputs
+    glds16(A + q * p.pA + (long long)row * p.lda + k0 + 8 * c, st + q * PLANE + rg * 1024);
+  };
+  auto wave_piece = [&](int qi, int k0, unsigned st) {  // this wave's qi-th piece of a stage
+    const int j = wave + 8 * qi;
+    if (j < NJ) piece(j, k0, st);
+  };
+  // A fragment (row tile i, 32-k half s, plane q) from stage buffer `cur`
+  auto afrag = [&](const char* cur, int i, int s, int q) {
+    const int r = 16 * i + (lane & 15);
+    const int c = 4 * s + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(cur + q * PLANE + r * 128 + 16 * (c ^ (r & 7)));
+  };
+
+  // ---- B: per lane, rows n0 + 32 wave + 16 j + (lane & 15), k chunk (lane >> 4)
+  unsigned boff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    int n = n0 + 32 * wave + 16 * j + (lane & 15);
+    n = n < p.N ? n : p.N - 1;
+    boff[j] = (unsigned)(((long long)n * p.ldb + 8 * (lane >> 4)) * 2);
+  }
+  auto bload = [&](bf16x8 (&b)[2][3], int k) {  // the 32-deep half step at k
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const __bf16* base = B + q * p.pB + k;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j][q] = gload_frag(base, boff[j]);
+    }
+  };
+
+  f32x4 acc[TI][2];
+#pragma unroll
+  for (int i = 0; i < TI; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 b0[2][3], b1[2][3];
+  // prologue: stage 0 + B of the first half step
+#pragma unroll
+  for (int qi = 0; qi < PMAX; ++qi) wave_piece(qi, 0, lds_base);
+  bload(b0, 0);
+
+  // one 64-deep step; MORE: the next stage and B half step are loaded during it (all but the last)
+  auto step = [&](int kt, auto more_c) {
+    constexpr bool MORE = decltype(more_c)::value;
+    // stage kt and B(kt, 0) have landed for this wave; after the barrier for every wave, and
+    // every wave is done with step kt-1 (its stage buffer is refilled below)
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const int kn = (kt + 1) * KS;
+    const unsigned nst = lds_base + ((kt + 1) & 1) * STAGE;
+    const char* cur = smem + (kt & 1) * STAGE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8(&b)[2][3] = s == 0 ? b0 : b1;
+      if (s == 0) {
+        bload(b1, kt * KS + 32);  // second half of this step
+      } else {
+        wait_vm6<MORE ? P0 : 0>(b1);  // B(kt, 1) landed; this half step's DMA pieces may not have
+        if (MORE) bload(b0, kn);      // first half of the next step
+      }
+      bf16x8 a[2][3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[0][q] = afrag(cur, 0, s, q);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        if (i + 1 < TI) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) a[(i + 1) & 1][q] = afrag(cur, i + 1, s, q);
+        }
+        if (MORE) {  // this half step's DMA pieces of the next stage, spread over the row tiles
+          constexpr int lo = 0;
+          const int a0 = s == 0 ? lo : P0, a1 = s == 0 ? P0 : PMAX;
+#pragma unroll
+          for (int qi = a0 + (i * (a1 - a0)) / TI; qi < a0 + ((i + 1) * (a1 - a0)) / TI; ++qi)
+            if (qi < mine) wave_piece(qi, kn, nst);
+        }
+        const bf16x8(&x)[3] = a[i & 1];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 c = acc[i][j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], b[j][1], c, 0, 0, 0);  // m*m
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][2], c, 0, 0, 0);  // h*l
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[2], b[j][0], c, 0, 0, 0);  // l*h
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][1], c, 0, 0, 0);  // h*m
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], b[j][0], c, 0, 0, 0);  // m*h
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][0], c, 0, 0, 0);  // h*h
+          acc[i][j] = c;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  for (int kt = 0; kt + 1 < nk; ++kt) step(kt, std::integral_constant<bool, true>{});
+  step(nk - 1, std::integral_constant<bool, false>{});
+
+  // ---------------------------------------------------------------- epilogue
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // the ring is free: scratch
+  __builtin_amdgcn_sched_barrier(0);
+  float* scr = reinterpret_cast<float*>(smem) + wave * (16 * 36);
+  const int rr = lane >> 2, c8 = 8 * (lane & 3);
+  const int col = n0 + 32 * wave + c8;
+  const bool colok = col < p.N;  // N % 8 == 0: a lane's 8 columns are all in or all out
+  float bias[8];
+  if (EPI == EPI_BIAS_RELU && colok) {
+    const float4 u = *reinterpret_cast<const float4*>(p.bias + z * p.sBias + col);
+    const float4 v = *reinterpret_cast<const float4*>(p.bias + z * p.sBias + col + 4);
+    bias[0] = u.x; bias[1] = u.y; bias[2] = u.z; bias[3] = u.w;
+    bias[4] = v.x; bias[5] = v.y; bias[6] = v.z; bias[7] = v.w;
+  }
+  float* C = C_OUT ? p.C + z * p.sC : nullptr;
+  __bf16* Cp = P_OUT ? p.Cp + z * p.sCp : nullptr;
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) scr[(4 * (lane >> 4) + r) * 36 + 16 * j + (lane & 15)] = acc[i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const float4 u = *reinterpret_cast<const float4*>(scr + rr * 36 + c8);
+    const float4 v = *reinterpret_cast<const float4*>(scr + rr * 36 + c8 + 4);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int row = m0 + 16 * i + rr;
+    if (row >= p.M || !colok) continue;
+    float e[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+    if (EPI == EPI_BIAS_RELU) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) e[c] = fmaxf(e[c] + bias[c], 0.f);
+    }
+    if (EPI == EPI_RELU_MASK) {
+      if (MASK16) {
+        const bf16x8 mk = *reinterpret_cast<const bf16x8*>(p.mask16 + z * p.sMask + (long long)row * p.ldm + col);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) e[c] = (float)mk[c] > 0.f ? e[c] : 0.f;
+      } else {
+        const float* mp = p.mask + z * p.sMask + (long long)row * p.ldm + col;
+        const float4 a0 = *reinterpret_cast<const float4*>(mp), a1 = *reinterpret_cast<const float4*>(mp + 4);
+        const float mk[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) e[c] = mk[c] > 0.f ? e[c] : 0.f;
+      }
+    }
+    if (C_OUT) {
+      float* cp = C + (long long)row * p.ldc + col;
+      *reinterpret_cast<float4*>(cp) = make_float4(e[0], e[1], e[2], e[3]);
+      *reinterpret_cast<float4*>(cp + 4) = make_float4(e[4], e[5], e[6], e[7]);
+    }
+    if (P_OUT) {
+      bf16x8 h, m, l;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        __bf16 a_, b_, c_;
+        split3_dev(e[c], a_, b_, c_);
+        h[c] = a_; m[c] = b_; l[c] = c_;
+      }
+      __bf16* pp = Cp + (long long)row * p.ldcp + col;
+      *reinterpret_cast<bf16x8*>(pp) = h;
+      *reinterpret_cast<bf16x8*>(pp + p.pC) = m;
+      *reinterpret_cast<bf16x8*>(pp + 2 * p.pC) = l;
+    }
+  }
+}
+
+constexpr int BM0 = 208;
+
+template <int EPI, bool C_OUT, bool P_OUT, bool MASK16>
+void launch(const SplitGemmParams& p, dim3 grid, hipStream_t st) {
+  hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16>), grid, dim3(512), 0, st, p);
+}
+
+}  // namespace x3fk
+
+int gemm_x3f_tiles(int M, int N, int batch) {
+  return ((M + x3fk::BM0 - 1) / x3fk::BM0) * ((N + x3fk::BN - 1) / x3fk::BN) * batch;
+}
+
+bool gemm_x3f_ok(const SplitGemmParams& p, int epi, int batch) {
+  return !p.a_kmajor && !p.b_kmajor && p.K % x3fk::KS == 0 && p.N % 8 == 0 && p.lda % 8 == 0 && p.ldb % 8 == 0 &&
+         (!p.C || p.ldc % 4 == 0) && (!p.Cp || p.ldcp % 8 == 0) && (epi != EPI_RELU_MASK || p.ldm % 8 == 0) &&
+         (epi != EPI_STORE) && gemm_x3f_tiles(p.M, p.N, batch) >= 192 && (p.C || p.Cp) &&
+         (long long)p.N * p.ldb * 2 < (1ll << 31);
+}
+
+void gemm_x3f(const SplitGemmParams& p, int epi, int batch, hipStream_t st) {
+  using namespace x3fk;
+  const dim3 grid((unsigned)gemm_x3f_tiles(p.M, p.N, batch));
+  const bool c = p.C != nullptr, pl = p.Cp != nullptr, m16 = p.mask16 != nullptr;
+  if (epi == EPI_BIAS_RELU) {
+    if (c && pl) launch<EPI_BIAS_RELU, true, true, false>(p, grid, st);
+    else if (c) launch<EPI_BIAS_RELU, true, false, false>(p, grid, st);
+    else launch<EPI_BIAS_RELU, false, true, false>(p, grid, st);
+  } else {
+    if (m16) {
+      if (c && pl) launch<EPI_RELU_MASK, true, true, true>(p, grid, st);
+      else if (c) launch<EPI_RELU_MASK, true, false, true>(p, grid, st);
+      else launch<EPI_RELU_MASK, false, true, true>(p, grid, st);
+    } else {
+      if (c && pl) launch<EPI_RELU_MASK, true, true, false>(p, grid, st);
+      else if (c) launch<EPI_RELU_MASK, true, false, false>(p, grid, st);
+      else launch<EPI_RELU_MASK, false, true, false>(p, grid, st);
+    }
+  }
+}
+
+}  // namespace mtsac

@@ -66,6 +66,7 @@ struct SplitGemmParams {
   const float* mask;
   int ldm;
   long long sMask;
+  const __bf16* mask16;   // gemm_x3f: ReLU mask from the bf16 high plane [rows][ldm] instead of mask
   __bf16* Cp;             // optional split planes of C: [3][M][ldcp]
   long long ldcp, pC, sCp;
   int M, N, K;
@@ -78,6 +79,11 @@ void gemm_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
 // auto split-K slices (1 = none) for a plane GEMM; kmajor = the k-major x k-major form
 int gemm_x3p_splits(int M, int N, int K, int batch, bool kmajor);
 long long gemm_x3p_ws_floats(int M, int N, int K, int batch, bool kmajor);
+// row-major x row-major plane GEMM on 16x16x32 MFMA, 208 x 256 tiles (gemm_x3f.hip): forward
+// (EPI_BIAS_RELU) and data grad (EPI_RELU_MASK) when gemm_x3f_ok
+bool gemm_x3f_ok(const SplitGemmParams& p, int epi, int batch);
+void gemm_x3f(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
+int gemm_x3f_tiles(int M, int N, int batch);
 extern int g_x3p_geo;  // tile geometry of gemm_x3p (-1: by operand form, 0..3: forced; see gemm_x3p.hip)
 extern int g_x3p_dbg;  // experiment bits OR-ed into SplitGemmParams::dbg
 extern int g_x3_dbg;   // experiments on gemm_x3: bit0 skip loads after the first tile, bit1 skip MFMA, bit2 skip split

@@ -267,6 +267,11 @@ class MTSACEngine:
         the step on one stream (solo kernel durations), else the step keeps its streams."""
         check(self.lib.mtsac_set_timing(self._h, (2 if serial else 1) if on else 0))
 
+    def timing_kernel(self, family: int) -> str:
+        buf = ctypes.create_string_buffer(256)
+        check(self.lib.mtsac_get_timing_kernel(self._h, family, buf, 256))
+        return buf.value.decode()
+
     def timing(self, family: int) -> tuple[float, int, float]:
         ms, n, fl = ctypes.c_double(), ctypes.c_int32(), ctypes.c_double()
         check(self.lib.mtsac_get_timing(self._h, family, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl)))

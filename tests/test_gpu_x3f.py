@@ -1,0 +1,86 @@
+"""gemm_x3f (mtrl_amd/csrc/gemm_x3f.hip): the row-major x row-major plane GEMM of the trunk
+forward and data grad, 16x16x32 MFMA, 208 x 256 tiles, A through LDS in full lines, B straight
+to registers.  Checked against float64 numpy with the fp32-GEMM bound |err| <= 4e-6 sum|a b|
+(what an fp32 GEMM with fp32 accumulation meets at these K), on the bench's own shape and on
+ragged ones (rows past M, a partial last column tile, batch > 1), every epilogue."""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(epi, A, B, bias=None, mask=None, planes=True, m16=False):
+    from mtrl_amd import _lib as L
+
+    lib = L.load()
+    E, M, K = A.shape
+    N = B.shape[1]
+    C = np.zeros((E, M, N), np.float32)
+    Cs = np.zeros((E, M, N), np.float32) if planes else None
+    p = lambda a: None if a is None else np.ascontiguousarray(a, np.float32).ctypes.data
+    rc = lib.mtsac_debug_gemm_x3f(epi | (256 if m16 else 0), E, M, N, K, p(A), p(B), C.ctypes.data, p(bias), p(mask),
+                                  None if Cs is None else Cs.ctypes.data)
+    L.check(rc)
+    return C, Cs
+
+
+def _ref(A, B):
+    A64, B64 = A.astype(np.float64), B.astype(np.float64)
+    acc = np.einsum("emk,enk->emn", A64, B64)
+    scale = np.einsum("emk,enk->emn", np.abs(A64), np.abs(B64))
+    return acc, scale
+
+
+@pytest.mark.parametrize("E,M,N,K", [(1, 6400, 2048, 2048), (2, 6300, 2040, 192), (1, 6240, 2048, 128)],
+                         ids=["s3_fwd", "ragged_e2", "exact_rows"])
+def test_bias_relu_with_planes(E, M, N, K):
+    rng = np.random.default_rng(M + K)
+    A = rng.standard_normal((E, M, K)).astype(np.float32)
+    B = (rng.standard_normal((E, N, K)) / np.sqrt(K)).astype(np.float32)
+    bias = rng.standard_normal((E, N)).astype(np.float32) * 0.1
+    C, Cs = _run(1, A, B, bias=bias)
+    acc, scale = _ref(A, B)
+    want = np.maximum(acc + bias[:, None, :], 0)
+    err = np.abs(C - want)
+    assert np.all(err <= 4e-6 * (scale + np.abs(bias[:, None, :])) + 1e-30), float((err / (scale + 1e-30)).max())
+    np.testing.assert_array_equal(Cs, C)  # the planes sum back to the fp32 output exactly
+
+
+@pytest.mark.parametrize("m16", [False, True], ids=["mask_f32", "mask_bf16_hi"])
+def test_relu_mask(m16):
+    rng = np.random.default_rng(7)
+    E, M, N, K = 2, 6400, 2048, 256
+    A = rng.standard_normal((E, M, K)).astype(np.float32)
+    B = rng.standard_normal((E, N, K)).astype(np.float32)
+    mask = np.maximum(rng.standard_normal((E, M, N)), 0).astype(np.float32)  # a ReLU output: >= 0
+    mask[:, :, :7] = 1e-30  # tiny positive activations still pass through the bf16 high plane
+    C, Cs = _run(2, A, B, mask=mask, m16=m16)
+    acc, scale = _ref(A, B)
+    want = np.where(mask > 0, acc, 0.0)
+    assert np.all(np.abs(C - want) <= 4e-6 * scale + 1e-30)
+    np.testing.assert_array_equal(Cs, C)
+
+
+def test_fp32_only_output():
+    rng = np.random.default_rng(3)
+    A = rng.standard_normal((1, 6400, 64)).astype(np.float32)
+    B = rng.standard_normal((1, 2048, 64)).astype(np.float32)
+    C, _ = _run(1, A, B, bias=np.zeros((1, 2048), np.float32), planes=False)
+    acc, scale = _ref(A, B)
+    assert np.all(np.abs(C - np.maximum(acc, 0)) <= 4e-6 * scale + 1e-30)
+
+
+def test_rejects_small_grids():
+    from mtrl_amd import _lib as L
+
+    lib = L.load()
+    A = np.zeros((1, 416, 64), np.float32)
+    B = np.zeros((1, 256, 64), np.float32)
+    C = np.zeros((1, 416, 256), np.float32)
+    assert lib.mtsac_debug_gemm_x3f(1, 1, 416, 256, 64, A.ctypes.data, B.ctypes.data, C.ctypes.data, None, None,
+                                    None) == -95
