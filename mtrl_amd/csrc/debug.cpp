@@ -282,9 +282,10 @@ int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int 
   if (outs == 2) g.Cp = nullptr;
   g.M = M; g.N = N; g.K = (int)Kp;
   g.splits = 1;
-  if (which == 1 && !gemm_x3f_ok(g, epi, batch)) return -95;
+  if (which >= 1 && !gemm_x3f_ok(g, epi, batch)) return -95;
   auto run = [&]() {
-    if (which == 1) gemm_x3f(g, epi, batch, nullptr);
+    if (which >= 2) gemm_x3f_ablate(g, which - 2, batch, nullptr);  // 2 + ablation bits (planes out)
+    else if (which == 1) gemm_x3f(g, epi, batch, nullptr);
     else gemm_x3p(g, epi, batch, nullptr);
   };
   run();

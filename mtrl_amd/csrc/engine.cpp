@@ -74,7 +74,8 @@ struct Net {
   // activations then keep planes only (their ReLU mask is read from the high plane)
   bool x3f = false;
   __bf16* wtp[2][MAXD] = {};
-  long long wtps() const { return (long long)width * ald; }
+  long long wtk(int i) const { return i == 0 ? xld : ald; }  // K (padded in-dim) of layer i
+  long long wtps(int i = 1) const { return (long long)width * wtk(i); }
   long long xld = 0;  // input planes' row stride = layer-0 kernel plane rows (in_dim rounded up to 32)
   long long aps() const { return arows * ald; }  // plane stride of activation planes
   long long wps() const { return wrows * wld; }  // plane stride of hidden kernel planes
@@ -354,16 +355,16 @@ struct mtsac_engine {
     }
     for (int i = 0; i < net.depth; ++i) {
       const bool last = i == net.depth - 1;
-      if (pl && i > 0 && net.x3f) {  // on planes, both row-major: h_{i-1} . (W_i^T)^T (gemm_x3f)
+      if (pl && net.x3f && (i > 0 || xp)) {  // on planes, both row-major: in_i . (W_i^T)^T (gemm_x3f)
         SplitGemmParams g{};
-        g.A = actp[i - 1];
-        g.lda = net.ald;
-        g.pA = net.aps();
-        g.sA = 3 * net.aps();
+        g.A = i == 0 ? xp : actp[i - 1];
+        g.lda = i == 0 ? net.xld : net.ald;
+        g.pA = i == 0 ? net.arows * net.xld : net.aps();
+        g.sA = i == 0 ? 0 : 3 * net.aps();  // the input is shared by the ensemble members
         g.B = net.wtp[which][i];
-        g.ldb = net.ald;
-        g.pB = net.wtps();
-        g.sB = 3 * net.wtps();
+        g.ldb = net.wtk(i);
+        g.pB = net.wtps(i);
+        g.sB = 3 * net.wtps(i);
         if (last) {  // the heads read fp32
           g.C = acts[i];
           g.ldc = net.width;
@@ -378,9 +379,9 @@ struct mtsac_engine {
         g.sBias = net.ms_b;
         g.M = M;
         g.N = net.width;
-        g.K = (int)net.ald;
+        g.K = (int)net.wtk(i);
         g.splits = 1;
-        gemmp(g, EPI_BIAS_RELU, net.E, MTSAC_FAM_FORWARD);
+        gemmp(g, EPI_BIAS_RELU, net.E, i == 0 ? MTSAC_FAM_INPUT_FORWARD : MTSAC_FAM_FORWARD);
         continue;
       }
       if (pl && (i > 0 || xp)) {  // on planes: input (row-major) . W_i (k-major)
@@ -462,19 +463,19 @@ struct mtsac_engine {
       sp.out_cols = (int)net.wld;
       sp.out = net.wp[which][i];
       if (!(fused && planes_fusable(net))) split_planes(sp, false, net.E, s);
-      if (net.x3f && i > 0) {  // W_i^T planes for the gemm_x3f forward
+      if (net.x3f) {  // W_i^T planes for the gemm_x3f forward (zeros past the in-dim)
         SplitParams st{};
         st.x = params + net.off_W[i];
         st.ldx = net.width;
         st.sx = net.ms_W[i];
-        st.rows = net.width;  // in
-        st.cols = net.width;  // out
+        st.rows = i == 0 ? net.in_dim : net.width;  // in
+        st.cols = net.width;                        // out
         st.out = net.wtp[which][i];
-        st.ldo = net.ald;
-        st.po = net.wtps();
-        st.so = 3 * net.wtps();
+        st.ldo = net.wtk(i);
+        st.po = net.wtps(i);
+        st.so = 3 * net.wtps(i);
         st.out_rows = net.width;
-        st.out_cols = (int)net.ald;
+        st.out_cols = (int)net.wtk(i);
         split_planes(st, true, net.E, s);
       }
     }
@@ -1123,6 +1124,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     net->arows = align_up(e->B, 32);
     // gemm_x3f takes the hidden layers when its 208 x 256 tiles fill the chip (gemm_x3f_ok)
     net->x3f = e->planes && net->depth > 1 && net->ald % 64 == 0 && gemm_x3f_tiles(e->B, net->width, net->E) >= 192;
+    if (net->x3f) net->xld = align_up(net->in_dim, 64);  // gemm_x3f steps K by 64
     for (int w = 0; w < (net == &e->critic ? 2 : 1); ++w)
       for (int i = 0; i < net->depth; ++i) {
         if (!e->planes) {
@@ -1130,7 +1132,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
           continue;
         }
         if ((rc = e->alloc(&net->wp[w][i], (size_t)net->E * 3 * net->kps(i)))) return bad(rc);
-        if (net->x3f && i > 0 && (rc = e->alloc(&net->wtp[w][i], (size_t)net->E * 3 * net->wtps()))) return bad(rc);
+        if (net->x3f && (rc = e->alloc(&net->wtp[w][i], (size_t)net->E * 3 * net->wtps(i)))) return bad(rc);
       }
   }
   {  // split-K workspaces: the largest GEMM that splits, per lane

@@ -53,7 +53,9 @@ __device__ inline void wait_vm6(bf16x8 (&b)[2][3]) {
                : "memory");
 }
 
-template <int BM, int EPI, bool C_OUT, bool P_OUT, bool MASK16>
+// ABL: ablation bits for experiments only (tools/x3f_ablate.py; results are wrong): 1 = no A
+// refills after the prologue, 2 = no B reloads after the prologue, 4 = s_setprio 1 for waves 4-7
+template <int BM, int EPI, bool C_OUT, bool P_OUT, bool MASK16, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
   constexpr int TI = BM / 16;            // 16-row accumulator tiles per wave
   constexpr int PLANE = BM * 128;        // bytes of one plane of one stage
@@ -126,6 +128,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
   for (int i = 0; i < TI; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   bf16x8 b0[2][3], b1[2][3];
+  if ((ABL & 4) && wave >= 4) __builtin_amdgcn_s_setprio(1);
   // prologue: stage 0 + B of the first half step
 #pragma unroll
   for (int qi = 0; qi < PMAX; ++qi) wave_piece(qi, 0, lds_base);
@@ -145,10 +148,11 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
     for (int s = 0; s < 2; ++s) {
       bf16x8(&b)[2][3] = s == 0 ? b0 : b1;
       if (s == 0) {
-        bload(b1, kt * KS + 32);  // second half of this step
+        if (!(ABL & 2) || kt == 0) bload(b1, kt * KS + 32);  // second half of this step
       } else {
-        wait_vm6<MORE ? P0 : 0>(b1);  // B(kt, 1) landed; this half step's DMA pieces may not have
-        if (MORE) bload(b0, kn);      // first half of the next step
+        if (ABL & 1) wait_vm6<0>(b1);
+        else wait_vm6<MORE ? P0 : 0>(b1);  // B(kt, 1) landed; this half step's DMA pieces may not have
+        if (MORE && !(ABL & 2)) bload(b0, kn);  // first half of the next step
       }
       bf16x8 a[2][3];
 #pragma unroll
@@ -159,7 +163,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
 #pragma unroll
           for (int q = 0; q < 3; ++q) a[(i + 1) & 1][q] = afrag(cur, i + 1, s, q);
         }
-        if (MORE) {  // this half step's DMA pieces of the next stage, spread over the row tiles
+        if (MORE && !(ABL & 1)) {  // this half step's DMA pieces of the next stage, spread over the row tiles
           constexpr int lo = 0;
           const int a0 = s == 0 ? lo : P0, a1 = s == 0 ? P0 : PMAX;
 #pragma unroll
@@ -264,6 +268,19 @@ void launch(const SplitGemmParams& p, dim3 grid, hipStream_t st) {
 }
 
 }  // namespace x3fk
+
+// experiments: the bench-shape forward (bias+ReLU, planes out) with ablation bits abl
+void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t st) {
+  using namespace x3fk;
+  const dim3 grid((unsigned)gemm_x3f_tiles(p.M, p.N, batch)), blk(512);
+  switch (abl) {
+    case 1: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 1>), grid, blk, 0, st, p); break;
+    case 2: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 2>), grid, blk, 0, st, p); break;
+    case 3: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 3>), grid, blk, 0, st, p); break;
+    case 4: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 4>), grid, blk, 0, st, p); break;
+    default: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 0>), grid, blk, 0, st, p); break;
+  }
+}
 
 int gemm_x3f_tiles(int M, int N, int batch) {
   return ((M + x3fk::BM0 - 1) / x3fk::BM0) * ((N + x3fk::BN - 1) / x3fk::BN) * batch;

@@ -20,6 +20,8 @@ O = sys.argv[1]
 tot = collections.defaultdict(float); n = collections.defaultdict(int)
 for f in glob.glob(O + "/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
+        if "gemm_x3" not in r["Kernel_Name"]:
+            continue  # fills / splits of the harness
         k = r["Counter_Name"]; tot[k] += float(r["Counter_Value"]); n[k] += 1
 disp = max(n.values()) if n else 1
 with open(O + "/summary.txt", "w") as out:
