@@ -310,8 +310,11 @@ struct mtsac_engine {
     }
     if (gemm_x3f_ok(p, epi, batch)) {
       gemm_x3f(p, epi, batch, cur);
-      fam_kernel[family] = std::string("gemm_x3f_kernel<208, ") + (epi == EPI_BIAS_RELU ? "bias+ReLU" : "ReLU mask") +
-                           (p.mask16 ? " from bf16 high plane" : "") + ", *>";
+      // the rocprof symbol: gemm_x3f_kernel<BM, EPI, C_OUT, P_OUT, MASK16, TAG>
+      const bool tagged = epi == EPI_BIAS_RELU && p.tag == 1 && p.Cp && !p.C;
+      fam_kernel[family] = std::string("gemm_x3f_kernel<208, ") + std::to_string(epi) + ", " +
+                           (p.C ? "true" : "false") + ", " + (p.Cp ? "true" : "false") + ", " +
+                           (p.mask16 ? "true" : "false") + ", " + (tagged ? "8" : "0") + ">";
     } else {
       gemm_x3p(p, epi, batch, cur);
       fam_kernel[family] = "gemm_x3p_kernel";
@@ -380,6 +383,7 @@ struct mtsac_engine {
         g.M = M;
         g.N = net.width;
         g.K = (int)net.wtk(i);
+        g.tag = i == 0 ? 1 : 0;
         g.splits = 1;
         gemmp(g, EPI_BIAS_RELU, net.E, i == 0 ? MTSAC_FAM_INPUT_FORWARD : MTSAC_FAM_FORWARD);
         continue;

@@ -12,18 +12,20 @@ import sys
 
 FAMILY_KEYS = {
     "split3": {
-        0: "gemm_x3p_kernel<mtsac::x3pk::Geo<224, 256, 1, 8, 3, 16, 0>, false, true, 1,",
-        1: "gemm_x3p_kernel<mtsac::x3pk::Geo<224, 256, 1, 8, 3, 16, 0>, false, false, 2,",
-        2: "gemm_x3p_kernel<mtsac::x3pk::Geo<256, 256, 2, 4, 3, 16, 0>, true, true, 0,",
-        3: "gemm_x3p_kernel<mtsac::x3pk::Geo<224, 256, 1, 8, 3, 16, 1>, false, true, 1,",
-        4: "gemm_x3_kernel<true, false, 0>",
+        # gemm_x3f_kernel<BM, EPI, C_OUT, P_OUT, MASK16, TAG>: TAG 8 = input-layer launches
+        0: ("gemm_x3f_kernel<208, 1, false, true, false, 0>", "gemm_x3f_kernel<208, 1, true, false, false, 0>",
+            "gemm_x3f_kernel<208, 1, true, true, false, 0>"),
+        1: ("gemm_x3f_kernel<208, 2,",),
+        2: ("gemm_x3p_kernel<mtsac::x3pk::Geo<256, 256, 2, 4, 3, 16, 0>, true, true, 0,",),
+        3: ("gemm_x3f_kernel<208, 1, false, true, false, 8>",),
+        4: ("gemm_x3_kernel<true, false, 0>",),
     },
     "fp32": {
-        0: "gemm_f32_kernel<false, true, 1>",
-        1: "gemm_f32_kernel<false, true, 2>",
-        2: "gemm_f32_kernel<true, false, 0>",
-        3: "gemm_f32_kernel<false, false, 1>",
-        4: "gemm_f32_kernel<true, false, 0>",
+        0: ("gemm_f32_kernel<false, true, 1>",),
+        1: ("gemm_f32_kernel<false, true, 2>",),
+        2: ("gemm_f32_kernel<true, false, 0>",),
+        3: ("gemm_f32_kernel<false, false, 1>",),
+        4: ("gemm_f32_kernel<true, false, 0>",),
     },
 }
 
@@ -48,7 +50,7 @@ def per_dispatch(path, counter):
 def family_means(rows, keys, scale):
     res = {}
     for fam, key in keys.items():
-        vals = [v for (name, v) in rows.values() if key in name]
+        vals = [v for (name, v) in rows.values() if any(k in name for k in key)]
         if vals:
             res[fam] = (sum(vals) / len(vals) * scale, len(vals))
     return res
@@ -66,7 +68,7 @@ def main():
     fam_out = {}
     for fam in keys:
         if fam in fetch and fam in write:
-            fam_out[str(fam)] = {"kernel": keys[fam], "hbm_bytes_per_launch": fetch[fam][0] + write[fam][0],
+            fam_out[str(fam)] = {"kernel": " | ".join(keys[fam]), "hbm_bytes_per_launch": fetch[fam][0] + write[fam][0],
                                  "fetch_bytes_per_launch": fetch[fam][0], "write_bytes_per_launch": write[fam][0],
                                  "dispatches": fetch[fam][1],
                                  "correction": "FETCH_SIZE (KiB) x 2 (gfx950 half-count) + WRITE_SIZE (KiB)"}
