@@ -176,6 +176,7 @@ int mtsac_debug_gemm_x3p_bench(int epi, int batch, int M, int N, int K, int iter
 int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A, const float* B, float* C,
                          const float* bias, const float* mask, float* Csum) {
   const bool m16 = (epi >> 8) & 1;
+  const bool small = (epi >> 9) & 1;  // gemm_x3s instead
   epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || !A || !B || !C) return -22;
   DevBuf d;
@@ -224,8 +225,13 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
     g.Cp = dCp; g.ldcp = N; g.pC = (long long)M * N; g.sCp = 3 * g.pC;
   }
   g.M = M; g.N = N; g.K = (int)Kp;
-  if (!gemm_x3f_ok(g, epi, batch)) return -95;
-  gemm_x3f(g, epi, batch, nullptr);
+  if (small) {
+    if (!gemm_x3s_ok(g, epi, batch)) return -95;
+    gemm_x3s(g, epi, batch, nullptr);
+  } else {
+    if (!gemm_x3f_ok(g, epi, batch)) return -95;
+    gemm_x3f(g, epi, batch, nullptr);
+  }
   if (hipDeviceSynchronize() != hipSuccess) return -5;
   if (hipMemcpy(C, dC, sizeof(float) * nC, hipMemcpyDeviceToHost) != hipSuccess) return -5;
   if (Csum) {
@@ -283,8 +289,11 @@ int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int 
   g.M = M; g.N = N; g.K = (int)Kp;
   g.splits = 1;
   if (which >= 1 && !gemm_x3f_ok(g, epi, batch)) return -95;
+  if (which < 0 && !gemm_x3s_ok(g, epi, batch)) return -95;
   auto run = [&]() {
-    if (which >= 2) gemm_x3f_ablate(g, which - 2, batch, nullptr);  // 2 + ablation bits (planes out)
+    if (which == -1) gemm_x3s(g, epi, batch, nullptr);
+    else if (which < -1) gemm_x3s_ablate(g, -1 - which, batch, nullptr);  // -2 no loads, -3 no MFMAs
+    else if (which >= 2) gemm_x3f_ablate(g, which - 2, batch, nullptr);  // 2 + ablation bits (planes out)
     else if (which == 1) gemm_x3f(g, epi, batch, nullptr);
     else gemm_x3p(g, epi, batch, nullptr);
   };
@@ -316,5 +325,7 @@ int mtsac_debug_x3p_geo(int geo) {
   g_x3_dbg = (geo >> 16) & 255;
   return old;
 }
+
+int mtsac_debug_x3s_ti(int M, int N, int batch) { return gemm_x3s_ti(M, N, batch); }
 
 }  // extern "C"

@@ -315,6 +315,12 @@ struct mtsac_engine {
       fam_kernel[family] = std::string("gemm_x3f_kernel<208, ") + std::to_string(epi) + ", " +
                            (p.C ? "true" : "false") + ", " + (p.Cp ? "true" : "false") + ", " +
                            (p.mask16 ? "true" : "false") + ", " + (tagged ? "8" : "0") + ">";
+    } else if (gemm_x3s_ok(p, epi, batch)) {
+      gemm_x3s(p, epi, batch, cur);
+      const bool tagged = epi == EPI_BIAS_RELU && p.tag == 1 && p.Cp && !p.C;
+      fam_kernel[family] = std::string("gemm_x3s_kernel<") + std::to_string(gemm_x3s_ti(p.M, p.N, batch)) + ", " +
+                           std::to_string(epi) + ", " + (p.C ? "true" : "false") + ", " + (p.Cp ? "true" : "false") +
+                           ", " + (p.mask16 ? "true" : "false") + ", " + (tagged ? "8" : "0") + ">";
     } else {
       gemm_x3p(p, epi, batch, cur);
       fam_kernel[family] = "gemm_x3p_kernel";
@@ -1126,8 +1132,15 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     net->ald = align_up(net->width, 32);
     net->xld = align_up(net->in_dim, 32);
     net->arows = align_up(e->B, 32);
-    // gemm_x3f takes the hidden layers when its 208 x 256 tiles fill the chip (gemm_x3f_ok)
-    net->x3f = e->planes && net->depth > 1 && net->ald % 64 == 0 && gemm_x3f_tiles(e->B, net->width, net->E) >= 192;
+    // row-major x row-major plane GEMMs for the trunk forward and data grad (hidden activations
+    // then keep planes only): gemm_x3f when its 208 x 256 tiles fill the chip, gemm_x3s for narrow
+    // trunks (K <= 512: W = 400).  Wide trunks on few rows (task shards, MT10 at W = 2048) stay on
+    // gemm_x3p + split-K: there the 16 TI x 64 tiles of gemm_x3s are bound by the per-CU operand
+    // ingest (texture-address unit busy 94 %, tools/x3s_ablate.py), and so are
+    // narrow trunks on many rows (MT50 at W = 400: gemm_x3p's 256 x 128 tiles win there).
+    net->x3f = e->planes && net->depth > 1 &&
+               ((net->ald % 64 == 0 && gemm_x3f_tiles(e->B, net->width, net->E) >= 192) ||
+                (net->ald <= 512 && e->B <= 2048));
     if (net->x3f) net->xld = align_up(net->in_dim, 64);  // gemm_x3f steps K by 64
     for (int w = 0; w < (net == &e->critic ? 2 : 1); ++w)
       for (int i = 0; i < net->depth; ++i) {

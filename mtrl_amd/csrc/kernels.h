@@ -85,6 +85,12 @@ bool gemm_x3f_ok(const SplitGemmParams& p, int epi, int batch);
 void gemm_x3f(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
 int gemm_x3f_tiles(int M, int N, int batch);
 void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t st);  // experiments
+// the same contract for small row counts (task shards, MT10): 16 TI x 64 tiles, 4 waves splitting
+// K inside the workgroup (gemm_x3s.hip); the ReLU mask comes from mask16
+bool gemm_x3s_ok(const SplitGemmParams& p, int epi, int batch);
+void gemm_x3s(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
+int gemm_x3s_ti(int M, int N, int batch);
+void gemm_x3s_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t st);  // experiments
 extern int g_x3p_geo;  // tile geometry of gemm_x3p (-1: by operand form, 0..3: forced; see gemm_x3p.hip)
 extern int g_x3p_dbg;  // experiment bits OR-ed into SplitGemmParams::dbg
 extern int g_x3_dbg;   // experiments on gemm_x3: bit0 skip loads after the first tile, bit1 skip MFMA, bit2 skip split
