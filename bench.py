@@ -40,7 +40,7 @@ WORKLOADS = {
 }
 FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
-PRECISIONS = {"fp32": 0, "split3": 1}
+PRECISIONS = {"fp32": 0, "split3": 1, "bf16": 2}
 HBM_PEAK_GBS = 8000.0
 # enum mtsac_gemm_family (include/mtsac.h) -> the rocprof kernel(s) of that family, per precision
 GEMM_FAMILIES = {
@@ -179,7 +179,8 @@ def main():
     ap.add_argument("--exec", default="auto", choices=["auto", "graph", "eager"],
                     help="hipGraph replay or eager multi-stream DAG; auto = faster of the two")
     ap.add_argument("--precision", default="split3", choices=sorted(PRECISIONS),
-                    help="fp32: f32-input MFMA; split3: fp32-accurate 3-way bf16 split on bf16 MFMA")
+                    help="fp32: f32-input MFMA; split3: fp32-accurate 3-way bf16 split on bf16 MFMA; "
+                         "bf16: perf-only, trunk GEMM operands rounded to bf16 (one MFMA per product)")
     ap.add_argument("--settle-s", type=float, default=2.0,
                     help="untimed steady-state seconds after the warm-up (DVFS settles under load)")
     ap.add_argument("--cpu-steps", type=int, default=5)
@@ -218,7 +219,8 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "fp32" if args.precision == "fp32" else "fp32 (3xbf16 split MFMA, fp32-accurate)",
+        "dtype": {"fp32": "fp32", "split3": "fp32 (3xbf16 split MFMA, fp32-accurate)",
+                  "bf16": "bf16 trunk GEMMs (fp32 accumulate, fp32 master weights / Adam / heads)"}[args.precision],
         "data": "synthetic (SURVEY.md §8d recipe, device-filled full buffer, cap=100000/task; random-init weights)",
         "config": {"workload": desc, "num_tasks": T, "width": W, "batch_per_task": 128, "global_batch": 128 * T,
                    "parallelism": f"task-shard{world}" if world > 1 else "single", "precision": args.precision,
@@ -319,7 +321,7 @@ def main():
     assert all(math.isfinite(v) for v in logs.values()), logs
 
     # dominant-kernel roofline from the per-launch HIP events
-    names = dict(GEMM_FAMILIES[args.precision])
+    names = dict(GEMM_FAMILIES["split3" if args.precision == "bf16" else args.precision])
     fam = {f: eng.timing(f) for f in names} if live else None
     # the same kernels solo: one extra step serialised on one stream.  Eager: context for the
     # fraction (under the step's concurrency a launch shares the CUs with its neighbours).
@@ -345,6 +347,8 @@ def main():
     traffic, traffic_src = pmc_traffic(args.precision, dom)
     if args.precision == "split3":  # 6 bf16 MFMA products per fp32 multiply-add
         peak, basis = BF16_MFMA_PEAK_TF / 6.0, "bf16 dense MFMA peak / 6 products (fp32-accurate split)"
+    elif args.precision == "bf16":
+        peak, basis = BF16_MFMA_PEAK_TF, "bf16 dense MFMA peak"
     else:
         peak, basis = FP32_MFMA_PEAK_TF, "f32-input MFMA dense peak"
 

@@ -79,9 +79,13 @@ enum mtsac_tensor {
 
 enum mtsac_precision {
   MTSAC_FP32 = 0,       /* f32-input MFMA (v_mfma_f32_32x32x2_f32), fp32 everywhere          */
-  MTSAC_FP32_SPLIT3 = 1 /* fp32-accurate trunk GEMMs on bf16 MFMA: each fp32 operand split
+  MTSAC_FP32_SPLIT3 = 1, /* fp32-accurate trunk GEMMs on bf16 MFMA: each fp32 operand split
                            exactly into 3 bf16 terms, 6 cross products accumulated in fp32
                            (dropped terms <= 2^-23 relative); everything else fp32           */
+  MTSAC_BF16 = 2         /* perf-only: the trunk GEMMs' operands rounded to bf16 (the high
+                           term of the same split), one bf16 MFMA per product, fp32
+                           accumulation; master weights, Adam, heads, losses stay fp32.
+                           NOT the reference's arithmetic (fp32): losses drift ~1e-3 rel  */
 };
 
 /* Hyper-parameters: MTSACConfig (mtsac.py:116-127) + AlgorithmConfig

@@ -15,6 +15,9 @@ _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = pathlib.Path(os.environ.get("MTSAC_LIB", _HERE / "libmtsac.so"))
 
 NUM_LOGS = 10
+# enum mtsac_precision (include/mtsac.h)
+FP32, FP32_SPLIT3, BF16 = 0, 1, 2
+PRECISIONS = {"fp32": FP32, "split3": FP32_SPLIT3, "bf16": BF16}
 LOG_KEYS = (
     "losses/qf_values",
     "losses/qf_loss",

@@ -106,7 +106,7 @@ class MTSAC(OffPolicyAlgorithm):
             alpha_max_grad_norm=config.temperature_optimizer_config.max_grad_norm,
             adam_eps=net_a.optimizer.adam_eps, initial_temperature=config.initial_temperature,
             log_std_min=config.actor_config.log_std_min, log_std_max=config.actor_config.log_std_max,
-            batch_per_task=128, capacity=128, precision=1 if precision == "split3" else 0, noise_seed=seed + 1,
+            batch_per_task=128, capacity=128, precision=L.PRECISIONS[precision], noise_seed=seed + 1,
         )
         eng = MTSACEngine(make_config(**kw), device=device)
         a, q = init_mtsac(T, obs_dim, act_dim, net_a.width, net_a.depth, net_c.width, net_c.depth,

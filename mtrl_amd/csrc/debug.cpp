@@ -177,6 +177,7 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
                          const float* bias, const float* mask, float* Csum) {
   const bool m16 = (epi >> 8) & 1;
   const bool small = (epi >> 9) & 1;  // gemm_x3s instead
+  const int np = ((epi >> 10) & 1) ? 1 : 3;  // bf16: the high plane only
   epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || !A || !B || !C) return -22;
   DevBuf d;
@@ -225,6 +226,7 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
     g.Cp = dCp; g.ldcp = N; g.pC = (long long)M * N; g.sCp = 3 * g.pC;
   }
   g.M = M; g.N = N; g.K = (int)Kp;
+  g.np = np;
   if (small) {
     if (!gemm_x3s_ok(g, epi, batch)) return -95;
     gemm_x3s(g, epi, batch, nullptr);
@@ -252,6 +254,7 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
 // current forward), 1 = gemm_x3f (row-major both)
 int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int K, int iters, double* ms_per_launch) {
   const int outs = (epi >> 8) & 3;  // 0: fp32 + planes, 1: planes only, 2: fp32 only
+  const int np = ((epi >> 10) & 1) ? 1 : 3;  // bf16: the high plane only
   epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || iters < 1 || !ms_per_launch) return -22;
   DevBuf d;
@@ -288,6 +291,7 @@ int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int 
   if (outs == 2) g.Cp = nullptr;
   g.M = M; g.N = N; g.K = (int)Kp;
   g.splits = 1;
+  g.np = np;
   if (which >= 1 && !gemm_x3f_ok(g, epi, batch)) return -95;
   if (which < 0 && !gemm_x3s_ok(g, epi, batch)) return -95;
   auto run = [&]() {

@@ -150,6 +150,7 @@ struct mtsac_engine {
   float* dzc[MAXD] = {};
   // split3 planes of the GEMM operands among them (layers 0..D-2 of activations, 1..D-1 of grads)
   bool planes = false;
+  int np = 3;  // operand planes the plane GEMMs read: 3 (split3) or 1 (bf16)
   __bf16* hap[MAXD] = {};
   __bf16* hanp[MAXD] = {};
   __bf16* hcp[MAXD] = {};
@@ -290,7 +291,7 @@ struct mtsac_engine {
       tl[tl_next].K = p.K;
       tl[tl_next].batch = batch;
     }
-    if (cfg.precision == MTSAC_FP32_SPLIT3)
+    if (planes)  // split3 / bf16: the plain fp32-operand GEMMs (input-layer weight grad) stay fp32-accurate
       gemm_x3(p, kind, epi, batch, cur);
     else
       gemm_f32(p, kind, epi, batch, cur);
@@ -366,6 +367,7 @@ struct mtsac_engine {
       const bool last = i == net.depth - 1;
       if (pl && net.x3f && (i > 0 || xp)) {  // on planes, both row-major: in_i . (W_i^T)^T (gemm_x3f)
         SplitGemmParams g{};
+        g.np = np;
         g.A = i == 0 ? xp : actp[i - 1];
         g.lda = i == 0 ? net.xld : net.ald;
         g.pA = i == 0 ? net.arows * net.xld : net.aps();
@@ -396,6 +398,7 @@ struct mtsac_engine {
       }
       if (pl && (i > 0 || xp)) {  // on planes: input (row-major) . W_i (k-major)
         SplitGemmParams g{};
+        g.np = np;
         g.A = i == 0 ? xp : actp[i - 1];
         g.lda = i == 0 ? net.xld : net.ald;
         g.pA = i == 0 ? net.arows * net.xld : net.aps();
@@ -499,6 +502,7 @@ struct mtsac_engine {
     const __bf16* xp = (planes && i == 0) ? in_planes(X) : nullptr;
     if (planes && (i > 0 || xp) && actp && dzp && dzp[i]) {  // TN on k-major planes; bias grad by column sums
       SplitGemmParams g{};
+      g.np = np;
       g.A = i == 0 ? xp : actp[i - 1];
       g.lda = i == 0 ? net.xld : net.ald;
       g.pA = i == 0 ? net.arows * net.xld : net.aps();
@@ -547,6 +551,7 @@ struct mtsac_engine {
                    int M) {
     if (planes && dzp) {  // NT on planes: dz[i] . W_i^T, W_i planes read as [N = in][K = out]
       SplitGemmParams g{};
+      g.np = np;
       g.A = dzp[i];
       g.lda = net.ald;
       g.pA = net.aps();
@@ -1083,7 +1088,8 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   if (c.batch_per_task < 1) return fail(-22, "batch_per_task must be positive");
   if (c.capacity < c.batch_per_task || c.capacity >= (1ll << 31))
     return fail(-22, "capacity must be in [batch_per_task, 2^31)");
-  if (c.precision != MTSAC_FP32 && c.precision != MTSAC_FP32_SPLIT3) return fail(-22, "unsupported precision");
+  if (c.precision != MTSAC_FP32 && c.precision != MTSAC_FP32_SPLIT3 && c.precision != MTSAC_BF16)
+    return fail(-22, "unsupported precision");
   hipError_t he = hipSetDevice(hip_device);
   if (he != hipSuccess) return fail(-19, std::string("hipSetDevice: ") + hipGetErrorString(he));
 
@@ -1125,7 +1131,8 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     if ((rc = e->alloc(&net->sc, 1))) return bad(rc);
   }
   if ((rc = e->alloc(&e->critic.tgt, e->critic.n_flat))) return bad(rc);
-  e->planes = c.precision == MTSAC_FP32_SPLIT3;
+  e->planes = c.precision == MTSAC_FP32_SPLIT3 || c.precision == MTSAC_BF16;
+  e->np = c.precision == MTSAC_BF16 ? 1 : 3;
   for (Net* net : {&e->actor, &e->critic}) {
     net->wld = align_up(net->width, 32);
     net->wrows = align_up(net->width, 32);

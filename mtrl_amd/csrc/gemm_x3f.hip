@@ -46,24 +46,29 @@ __device__ inline bf16x8 gload_frag(const __bf16* base, unsigned voff) {
   return r;
 }
 
-template <int N>
-__device__ inline void wait_vm6(bf16x8 (&b)[2][3]) {
-  asm volatile("s_waitcnt vmcnt(%6)"
-               : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[0][2]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[1][2])
-               : "n"(N)
-               : "memory");
+// s_waitcnt vmcnt(N) that also pins the B fragments it covers (the compiler cannot see the asm loads)
+template <int N, int NP>
+__device__ inline void wait_vm(bf16x8 (&b)[2][NP]) {
+  if constexpr (NP == 3)
+    asm volatile("s_waitcnt vmcnt(%6)"
+                 : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[0][2]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[1][2])
+                 : "n"(N)
+                 : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(b[0][0]), "+v"(b[1][0]) : "n"(N) : "memory");
 }
 
 // ABL: ablation bits for experiments only (tools/x3f_ablate.py; results are wrong): 1 = no A
 // refills after the prologue, 2 = no B reloads after the prologue, 4 = s_setprio 1 for waves 4-7.
 // ABL == TAG_INPUT changes nothing: it only gives input-layer launches their own kernel symbol, so
 // rocprof stats and PMC passes separate them from the hidden layers.
-template <int BM, int EPI, bool C_OUT, bool P_OUT, bool MASK16, int ABL = 0>
+// NP: operand planes read (3: 6 products, fp32-accurate; 1: the high plane only, precision bf16)
+template <int BM, int EPI, bool C_OUT, bool P_OUT, bool MASK16, int ABL = 0, int NP = 3>
 __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
   constexpr int TI = BM / 16;            // 16-row accumulator tiles per wave
   constexpr int PLANE = BM * 128;        // bytes of one plane of one stage
-  constexpr int STAGE = 3 * PLANE;
-  constexpr int NJ = 3 * BM / 8;         // DMA wave-instructions per stage
+  constexpr int STAGE = NP * PLANE;
+  constexpr int NJ = NP * BM / 8;        // DMA wave-instructions per stage
   constexpr int PMAX = (NJ + 7) / 8;     // per wave (the first NJ % 8 waves), others PMAX - 1
   constexpr int P0 = (PMAX + 1) / 2;     // issued in the first half step
   static_assert(BM % 16 == 0 && 2 * STAGE <= 160 * 1024, "tile");
@@ -117,9 +122,9 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
     n = n < p.N ? n : p.N - 1;
     boff[j] = (unsigned)(((long long)n * p.ldb + 8 * (lane >> 4)) * 2);
   }
-  auto bload = [&](bf16x8 (&b)[2][3], int k) {  // the 32-deep half step at k
+  auto bload = [&](bf16x8 (&b)[2][NP], int k) {  // the 32-deep half step at k
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
+    for (int q = 0; q < NP; ++q) {
       const __bf16* base = B + q * p.pB + k;
 #pragma unroll
       for (int j = 0; j < 2; ++j) b[j][q] = gload_frag(base, boff[j]);
@@ -130,7 +135,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
 #pragma unroll
   for (int i = 0; i < TI; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 b0[2][3], b1[2][3];
+  bf16x8 b0[2][NP], b1[2][NP];
   if ((ABL & 4) && wave >= 4) __builtin_amdgcn_s_setprio(1);
   // prologue: stage 0 + B of the first half step
 #pragma unroll
@@ -149,22 +154,22 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
     const char* cur = smem + (kt & 1) * STAGE;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8(&b)[2][3] = s == 0 ? b0 : b1;
+      bf16x8(&b)[2][NP] = s == 0 ? b0 : b1;
       if (s == 0) {
         if (!(ABL & 2) || kt == 0) bload(b1, kt * KS + 32);  // second half of this step
       } else {
-        if (ABL & 1) wait_vm6<0>(b1);
-        else wait_vm6<MORE ? P0 : 0>(b1);  // B(kt, 1) landed; this half step's DMA pieces may not have
+        if (ABL & 1) wait_vm<0, NP>(b1);
+        else wait_vm<MORE ? P0 : 0, NP>(b1);  // B(kt, 1) landed; this half step's DMA pieces may not have
         if (MORE && !(ABL & 2)) bload(b0, kn);  // first half of the next step
       }
-      bf16x8 a[2][3];
+      bf16x8 a[2][NP];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) a[0][q] = afrag(cur, 0, s, q);
+      for (int q = 0; q < NP; ++q) a[0][q] = afrag(cur, 0, s, q);
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         if (i + 1 < TI) {
 #pragma unroll
-          for (int q = 0; q < 3; ++q) a[(i + 1) & 1][q] = afrag(cur, i + 1, s, q);
+          for (int q = 0; q < NP; ++q) a[(i + 1) & 1][q] = afrag(cur, i + 1, s, q);
         }
         if (MORE && !(ABL & 1)) {  // this half step's DMA pieces of the next stage, spread over the row tiles
           constexpr int lo = 0;
@@ -173,15 +178,17 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
           for (int qi = a0 + (i * (a1 - a0)) / TI; qi < a0 + ((i + 1) * (a1 - a0)) / TI; ++qi)
             if (qi < mine) wave_piece(qi, kn, nst);
         }
-        const bf16x8(&x)[3] = a[i & 1];
+        const bf16x8(&x)[NP] = a[i & 1];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           f32x4 c = acc[i][j];
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], b[j][1], c, 0, 0, 0);  // m*m
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][2], c, 0, 0, 0);  // h*l
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[2], b[j][0], c, 0, 0, 0);  // l*h
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][1], c, 0, 0, 0);  // h*m
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], b[j][0], c, 0, 0, 0);  // m*h
+          if constexpr (NP == 3) {
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], b[j][1], c, 0, 0, 0);  // m*m
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][2], c, 0, 0, 0);  // h*l
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[2], b[j][0], c, 0, 0, 0);  // l*h
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][1], c, 0, 0, 0);  // h*m
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], b[j][0], c, 0, 0, 0);  // m*h
+          }
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][0], c, 0, 0, 0);  // h*h
           acc[i][j] = c;
         }
@@ -267,7 +274,8 @@ constexpr int BM0 = 208;
 
 template <int EPI, bool C_OUT, bool P_OUT, bool MASK16, int TAG = 0>
 void launch(const SplitGemmParams& p, dim3 grid, hipStream_t st) {
-  hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG>), grid, dim3(512), 0, st, p);
+  if (p.np == 1) hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, dim3(512), 0, st, p);
+  else hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 3>), grid, dim3(512), 0, st, p);
 }
 
 }  // namespace x3fk

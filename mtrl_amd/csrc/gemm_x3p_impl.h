@@ -47,16 +47,17 @@ __device__ inline void glds16(const void* src, unsigned lds_addr) {
                "s"(__builtin_amdgcn_readfirstlane(lds_addr))
                : "memory");
 }
-// One operand's image of a K-step: R rows (M or N) x KS k, three planes.
-template <int R, bool KM, int KS>
+// One operand's image of a K-step: R rows (M or N) x KS k, NP planes (3: the fp32-accurate split;
+// 1: the high plane only, precision bf16).
+template <int R, bool KM, int KS, int NP = 3>
 struct Oper {
   static constexpr int PLANE = R * KS * 2;  // bytes per plane
-  static constexpr int BYTES = 3 * PLANE;
-  static constexpr int NJ = 3 * PLANE / 1024;  // 1-KiB wave-instructions per stage
+  static constexpr int BYTES = NP * PLANE;
+  static constexpr int NJ = NP * PLANE / 1024;  // 1-KiB wave-instructions per stage
   static constexpr int ROWB = KM ? 2 * R : 2 * KS;
   static constexpr int RPI = 1024 / ROWB;   // image rows per wave-instruction
   static constexpr int LPR = ROWB / 16;     // lanes per image row
-  static constexpr int PER_PLANE = NJ / 3;
+  static constexpr int PER_PLANE = NJ / NP;
   static_assert(!KM || LPR >= 16, "k-major swizzle needs >= 16 chunks per row");
 
   // physical 16-B chunk of logical chunk c in image row irow (conflict-free reads, see header)
@@ -130,10 +131,11 @@ struct Geo {
   static constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
 };
 
-template <class G, bool AKM, bool BKM, int EPI, bool PLANES_OUT>
+// NP: operand planes read (3: 6 products per tile and slice, fp32-accurate; 1: h*h only, bf16)
+template <class G, bool AKM, bool BKM, int EPI, bool PLANES_OUT, int NP = 3>
 __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) {
-  using OA = Oper<G::BM, AKM, G::KS>;
-  using OB = Oper<G::BN, BKM, G::KS>;
+  using OA = Oper<G::BM, AKM, G::KS, NP>;
+  using OB = Oper<G::BN, BKM, G::KS, NP>;
   constexpr int STAGE = OA::BYTES + OB::BYTES;
   // the stage's wave-instructions are dealt round robin: waves < DMA_X issue one more
   constexpr int DMA_LO = (OA::NJ + OB::NJ) / G::NW, DMA_X = (OA::NJ + OB::NJ) % G::NW;
@@ -211,15 +213,15 @@ __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) 
       const char* cur = lds + (kt % G::STAGES) * STAGE;
 #pragma unroll
       for (int ks = 0; ks < G::KS / 16; ++ks) {
-        bf16x8 a[G::TI][3], b[G::TJ][3];
+        bf16x8 a[G::TI][NP], b[G::TJ][NP];
 #pragma unroll
         for (int i = 0; i < G::TI; ++i)
 #pragma unroll
-          for (int q = 0; q < 3; ++q) a[i][q] = OA::frag(cur, q, wm + 32 * i, ks, lane);
+          for (int q = 0; q < NP; ++q) a[i][q] = OA::frag(cur, q, wm + 32 * i, ks, lane);
 #pragma unroll
         for (int j = 0; j < G::TJ; ++j)
 #pragma unroll
-          for (int q = 0; q < 3; ++q) b[j][q] = OB::frag(cur + OA::BYTES, q, wn + 32 * j, ks, lane);
+          for (int q = 0; q < NP; ++q) b[j][q] = OB::frag(cur + OA::BYTES, q, wn + 32 * j, ks, lane);
         if (p.dbg & 2) {
 #pragma unroll
           for (int i = 0; i < G::TI; ++i)
@@ -240,11 +242,13 @@ __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) 
               for (int q = slot * PIECES / SLOTS; q < (slot + 1) * PIECES / SLOTS; ++q) piece(rs, rk, q);
             }
             f32x16 c = acc[i][j];
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], c, 0, 0, 0);  // m*m
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], c, 0, 0, 0);  // h*l
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], c, 0, 0, 0);  // l*h
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], c, 0, 0, 0);  // h*m
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], c, 0, 0, 0);  // m*h
+            if constexpr (NP == 3) {
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], c, 0, 0, 0);  // m*m
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], c, 0, 0, 0);  // h*l
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], c, 0, 0, 0);  // l*h
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], c, 0, 0, 0);  // h*m
+              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], c, 0, 0, 0);  // m*h
+            }
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], c, 0, 0, 0);  // h*h
             acc[i][j] = c;
           }
@@ -309,20 +313,26 @@ using GeoBig16In = Geo<256, 256, 2, 4, 3, 16, 1>;  // GeoBig16 for input-layer l
 using GeoTall224 = Geo<224, 256, 1, 8, 3, 16>;
 using GeoTall224In = Geo<224, 256, 1, 8, 3, 16, 1>;  // input-layer launches (own symbol)
 
-template <class G, bool AKM, bool BKM>
-void launch_x3p_v(const SplitGemmParams& p, int epi, dim3 grid, hipStream_t st) {
+template <class G, bool AKM, bool BKM, int NP>
+void launch_x3p_np(const SplitGemmParams& p, int epi, dim3 grid, hipStream_t st) {
   const bool planes = p.Cp != nullptr;
   const dim3 block(G::NTH);
   if (epi == EPI_BIAS_RELU) {
-    if (planes) hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_BIAS_RELU, true>), grid, block, 0, st, p);
-    else hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_BIAS_RELU, false>), grid, block, 0, st, p);
+    if (planes) hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_BIAS_RELU, true, NP>), grid, block, 0, st, p);
+    else hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_BIAS_RELU, false, NP>), grid, block, 0, st, p);
   } else if (epi == EPI_RELU_MASK) {
-    if (planes) hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_RELU_MASK, true>), grid, block, 0, st, p);
-    else hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_RELU_MASK, false>), grid, block, 0, st, p);
+    if (planes) hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_RELU_MASK, true, NP>), grid, block, 0, st, p);
+    else hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_RELU_MASK, false, NP>), grid, block, 0, st, p);
   } else {
-    if (planes) hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_STORE, true>), grid, block, 0, st, p);
-    else hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_STORE, false>), grid, block, 0, st, p);
+    if (planes) hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_STORE, true, NP>), grid, block, 0, st, p);
+    else hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_STORE, false, NP>), grid, block, 0, st, p);
   }
+}
+
+template <class G, bool AKM, bool BKM>
+void launch_x3p_v(const SplitGemmParams& p, int epi, dim3 grid, hipStream_t st) {
+  if (p.np == 1) launch_x3p_np<G, AKM, BKM, 1>(p, epi, grid, st);
+  else launch_x3p_np<G, AKM, BKM, 3>(p, epi, grid, st);
 }
 
 // operand forms in MASK (bit f: f = a_kmajor | 2 b_kmajor)

@@ -43,7 +43,8 @@ constexpr int TAG_INPUT = 8;
 // prologue, bit 32 = no MFMAs
 constexpr int ABL_NOLOAD = 16, ABL_NOMFMA = 32;
 
-template <int TI, int EPI, bool C_OUT, bool P_OUT, bool MASK16, int TAG = 0>
+// NP: operand planes read (3: 6 products, fp32-accurate; 1: the high plane only, precision bf16)
+template <int TI, int EPI, bool C_OUT, bool P_OUT, bool MASK16, int TAG = 0, int NP = 3>
 __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
   constexpr int BM = 16 * TI;
   constexpr int RLD = BN + 4;  // floats per row of a wave's partial tile in LDS
@@ -92,14 +93,14 @@ __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
   // still tracks every load's vmcnt
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, -1, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, -1, 0x00020000);
-  auto load_a = [&](bf16x8 (&a)[3], int i, int k) {
+  auto load_a = [&](bf16x8 (&a)[NP], int i, int k) {
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
+    for (int q = 0; q < NP; ++q)
       a[q] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, aoff[i], (int)(2 * (q * p.pA + k)), 0));
   };
-  auto load_bh = [&](bf16x8 (&b)[JB][3], int j0, int k) {  // column blocks j0 .. j0 + JB / 2 - 1
+  auto load_bh = [&](bf16x8 (&b)[JB][NP], int j0, int k) {  // column blocks j0 .. j0 + JB / 2 - 1
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
+    for (int q = 0; q < NP; ++q)
 #pragma unroll
       for (int j = j0; j < j0 + JB / 2; ++j)
         b[j][q] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rb, boff[j], (int)(2 * (q * p.pB + k)), 0));
@@ -117,7 +118,7 @@ __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
   // the second half's B blocks and A row block i (after its second-half MFMAs) half a step or more
   // ahead of their next use.  Every step body is straight-line code (MORE is a template
   // constant), with scheduling barriers between its groups.
-  bf16x8 a[TI][3], b[JB][3];
+  bf16x8 a[TI][NP], b[JB][NP];
   // One 16 x 16 output block, 32-deep slice: the 6 split products accumulated IN PLACE.  Inline asm
   // with the accumulator tied ("+a"): with the builtin the compiler rotates the accumulators of
   // this loop through a scratch AGPR quad (4 moves + an MFMA drain per chain).  Hazards the
@@ -125,6 +126,10 @@ __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
   // wait states; the epilogue drains the pipe (s_nop) before it reads the accumulators.
   auto mfma6 = [&](int i, int j) {
     if (TAG & ABL_NOMFMA) return;
+    if constexpr (NP == 1) {
+      asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[i][0]), "v"(b[j][0]));  // h*h
+      return;
+    }
     asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"   // m*m
         "v_mfma_f32_16x16x32_bf16 %0, %3, %4, %0\n\t"   // h*l
         "v_mfma_f32_16x16x32_bf16 %0, %5, %6, %0\n\t"   // l*h
@@ -165,7 +170,9 @@ __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
     int u = 0;
     if (cnt & 1) {
 #pragma unroll
-      for (int i = 0; i < TI; ++i) a[i][0] = a[i][1] = a[i][2] = bf16x8{};
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int q = 0; q < NP; ++q) a[i][q] = bf16x8{};
       u = -1;  // the phantom step loads step 0 as its next
     } else {
 #pragma unroll
@@ -250,7 +257,10 @@ __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
 template <int TI, int EPI, bool C_OUT, bool P_OUT, bool MASK16, int TAG = 0>
 void launch(const SplitGemmParams& p, int batch, hipStream_t st) {
   const unsigned grid = (unsigned)(((p.M + 16 * TI - 1) / (16 * TI)) * ((p.N + BN - 1) / BN) * batch);
-  hipLaunchKernelGGL((gemm_x3s_kernel<TI, EPI, C_OUT, P_OUT, MASK16, TAG>), dim3(grid), dim3(64 * NW), 0, st, p);
+  if (p.np == 1)
+    hipLaunchKernelGGL((gemm_x3s_kernel<TI, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), dim3(grid), dim3(64 * NW), 0, st, p);
+  else
+    hipLaunchKernelGGL((gemm_x3s_kernel<TI, EPI, C_OUT, P_OUT, MASK16, TAG, 3>), dim3(grid), dim3(64 * NW), 0, st, p);
 }
 
 template <int TI>

@@ -74,6 +74,8 @@ struct SplitGemmParams {
   float* ws;
   int dbg;                // experiments only: bit0 skip steady-state loads, bit1 skip MFMA
   int tag;                // 1: input-layer launch (separate kernel symbol for profiles)
+  int np;                 // operand planes the products read: 3 (0 = default; fp32-accurate split) or 1
+                          // (precision bf16: the high plane only, one MFMA per product)
 };
 void gemm_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
 // auto split-K slices (1 = none) for a plane GEMM; kmajor = the k-major x k-major form

@@ -195,3 +195,33 @@ def test_full_batch_graph_replay_equals_eager():
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
     np.testing.assert_array_equal(outs[0][2], outs[1][2])
     assert outs[0][3] == outs[1][3]
+
+
+# Precision bf16 (perf-only, BASELINE configs[2] "bf16 MFMA"): the trunk GEMM operands are rounded
+# to bf16 (one MFMA per product, fp32 accumulation), everything else fp32.  Not the reference's
+# arithmetic, so it is held to a stated drift bound instead of the 1e-5 parity bar: one full step
+# from the same start state, batch and noise against the float64 oracle.  Measured (MI355X): losses
+# <= 1.5e-4, grad norms <= 9.3e-5 relative (qf_values of S2 the largest); the bound is 1e-3.
+BF16_LOSS_RTOL = 1e-3
+BF16_NORM_RTOL = 1e-3
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_full_batch_bf16_drift_bound(name):
+    cfg, st, batch, en, ec, st1, want = _problem(name)
+    e = _engine(CASES[name], 2)
+    _load(e, st)
+    e.update(batch, en, ec)
+    got = e.logs()
+    errs = {k: abs(got[k] - want[k]) / max(abs(want[k]), 1e-30) for k in LOSS_KEYS + NORM_KEYS}
+    print(f"{name}/bf16", {k: f"{v:.2e}" for k, v in errs.items()})
+    for k in LOSS_KEYS:
+        assert errs[k] <= BF16_LOSS_RTOL, (name, k, got[k], want[k], errs[k])
+    for k in NORM_KEYS:
+        assert errs[k] <= BF16_NORM_RTOL, (name, k, got[k], want[k], errs[k])
+    # the update still moves every parameter the way the fp32 step does
+    from mtrl_amd import _lib as L
+
+    d = np.abs(e.get_params(L.CRITIC).astype(np.float64) - st1.critic)
+    assert np.median(d) < 1e-5, np.median(d)
+    e.close()

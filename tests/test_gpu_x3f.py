@@ -84,3 +84,20 @@ def test_rejects_small_grids():
     C = np.zeros((1, 416, 256), np.float32)
     assert lib.mtsac_debug_gemm_x3f(1, 1, 416, 256, 64, A.ctypes.data, B.ctypes.data, C.ctypes.data, None, None,
                                     None) == -95
+
+
+
+def test_bf16_products():
+    """Precision bf16 on gemm_x3f: exactly the products of the bf16-rounded operands, fp32 sums."""
+    import torch
+
+    rng = np.random.default_rng(31)
+    A = rng.standard_normal((2, 6400, 256)).astype(np.float32)
+    B = (rng.standard_normal((2, 2048, 256)) / 16).astype(np.float32)
+    bias = rng.standard_normal((2, 2048)).astype(np.float32) * 0.1
+    C, _ = _run(1 | 1024, A, B, bias=bias)
+    Ar = torch.from_numpy(A).to(torch.bfloat16).to(torch.float64).numpy()
+    Br = torch.from_numpy(B).to(torch.bfloat16).to(torch.float64).numpy()
+    acc, scale = _ref(Ar, Br)
+    want = np.maximum(acc + bias[:, None, :], 0)
+    assert np.all(np.abs(C - want) <= 4e-6 * (scale + np.abs(bias[:, None, :])) + 1e-30)

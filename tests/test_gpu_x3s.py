@@ -96,3 +96,24 @@ def test_fp32_mask_rejected():
     C = np.zeros((1, 896, 256), np.float32)
     assert lib.mtsac_debug_gemm_x3f(2 | SMALL, 1, 896, 256, 64, A.ctypes.data, B.ctypes.data, C.ctypes.data, None,
                                     A.ctypes.data, None) == -95
+
+
+BF16 = 1024  # epi bit 10: precision bf16 (the operands' high planes only, one MFMA per product)
+
+
+@pytest.mark.parametrize("E,M,N,K", SHAPES[:3], ids=IDS[:3])
+def test_bf16_products(E, M, N, K):
+    """Precision bf16: C = sum_k bf16(a) bf16(b) in fp32, i.e. exactly the product of the
+    rounded operands up to fp32 accumulation."""
+    rng = np.random.default_rng(21 + M)
+    A = rng.standard_normal((E, M, K)).astype(np.float32)
+    B = (rng.standard_normal((E, N, K)) / np.sqrt(K)).astype(np.float32)
+    bias = rng.standard_normal((E, N)).astype(np.float32) * 0.1
+    C, _ = _run(1 | BF16, A, B, bias=bias)
+    import torch
+
+    Ar = torch.from_numpy(A).to(torch.bfloat16).to(torch.float64).numpy()
+    Br = torch.from_numpy(B).to(torch.bfloat16).to(torch.float64).numpy()
+    acc, scale = _ref(Ar, Br)
+    want = np.maximum(acc + bias[:, None, :], 0)
+    assert np.all(np.abs(C - want) <= 4e-6 * (scale + np.abs(bias[:, None, :])) + 1e-30)
