@@ -222,6 +222,31 @@ int mtsac_get_timing(mtsac_engine* h, int32_t family, double* total_ms, int32_t*
 /* the kernel behind a GEMM family at its last launch (labels for the bench and profiles) */
 int mtsac_get_timing_kernel(mtsac_engine* h, int32_t family, char* buf, int32_t n);
 
+/* ---- eval-time gradient-conflict statistics (MTSAC.compute_weights, mtsac.py:870-1170;
+ * compute_gram_metrics :733-771, compute_support_metrics :774-867; vmap_cos_sim /
+ * compute_conflict_metrics, algorithms/utils.py:49-174).  Unsharded engines only (-95).
+ * mtsac_task_gradients: per-task gradients of each task's own loss (critic MSE over its n rows,
+ * actor loss over its rows) on the CURRENT parameters, into device matrices [T][P] in flax ravel
+ * order (which 0 = critic, P = mtsac_task_gradient_size(h, 0); 1 = actor).  batch NULL = sample
+ * on device; rows must be interleaved i*T + t (as MultiTaskReplayBuffer.sample returns them).
+ * eps_next (the reference samples these from pi(.|s), mtsac.py:1000-1004) / eps_cur: [B][A]
+ * injected noise, or both NULL (device noise).  Nothing is updated.
+ * mtsac_task_gradient_select: values[t*2+k] = the ranks[t*2+k]-th smallest |g_t| (0-based),
+ * the two order statistics of jnp.quantile's linear interpolation.
+ * mtsac_task_gradient_stats: one pass over G with support S_t = |g_t| >= thresholds[t]:
+ * gram[T*T] = G G^T, l1[T] = sum |g_t|, counts[4][T*T] = #(g_i g_j < 0), #(S_i & S_j),
+ * #(S_i & S_j & g_i g_j < 0), #(|g_i| < eps & |g_j| > tau); near_zero[T] = #(|g_t| < eps).
+ * The T x T algebra on top is host code (mtrl_amd/conflict.py). */
+int mtsac_task_gradients(mtsac_engine* h, const mtsac_batch* batch, const float* eps_next,
+                         const float* eps_cur);
+int64_t mtsac_task_gradient_size(const mtsac_engine* h, int which);
+int mtsac_get_task_gradients(mtsac_engine* h, int which, float* dst, int64_t n);
+int mtsac_set_task_gradients(mtsac_engine* h, int which, const float* src, int64_t n);
+int mtsac_task_gradient_select(mtsac_engine* h, int which, const int64_t* ranks, float* values);
+int mtsac_task_gradient_stats(mtsac_engine* h, int which, const float* thresholds, float eps,
+                              float tau, double* gram, double* l1, int64_t* counts,
+                              int64_t* near_zero);
+
 #ifdef __cplusplus
 }
 #endif

@@ -136,6 +136,12 @@ SIGNATURES = {
     "mtsac_set_timing": (ctypes.c_int, [P, I32]),
     "mtsac_get_timing": (ctypes.c_int, [P, I32, PD, PI32, PD]),
     "mtsac_get_timing_kernel": (ctypes.c_int, [P, I32, P, I32]),
+    "mtsac_task_gradients": (ctypes.c_int, [P, ctypes.POINTER(Batch), P, P]),
+    "mtsac_task_gradient_size": (I64, [P, ctypes.c_int]),
+    "mtsac_get_task_gradients": (ctypes.c_int, [P, ctypes.c_int, P, I64]),
+    "mtsac_set_task_gradients": (ctypes.c_int, [P, ctypes.c_int, P, I64]),
+    "mtsac_task_gradient_select": (ctypes.c_int, [P, ctypes.c_int, P, P]),
+    "mtsac_task_gradient_stats": (ctypes.c_int, [P, ctypes.c_int, P, ctypes.c_float, ctypes.c_float, P, P, P, P]),
     "mtsac_debug_gemm_bench": (ctypes.c_int, [ctypes.c_int] * 8 + [PD]),
     "mtsac_debug_gemm_x3p": (ctypes.c_int, [ctypes.c_int] * 4 + [P, ctypes.c_int, P, ctypes.c_int, P, P, P, P]),
     "mtsac_debug_gemm_x3p_bench": (ctypes.c_int, [ctypes.c_int] * 6 + [PD]),

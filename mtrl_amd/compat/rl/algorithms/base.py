@@ -6,7 +6,8 @@ update per global step once ``global_step > warmstart_steps``, SPS print every 1
 steps, evaluation every ``evaluation_frequency`` finished episodes.  When the replay
 buffer lives in the same engine as the networks, the sample + update pair runs as ONE
 device call (``MTSACEngine.update_many(1)``): no host round trip per gradient step.
-Gradient-conflict metrics (``compute_weights``, base.py:280-288) are out of scope.
+At every evaluation the gradient-conflict metrics run on a balanced sample (``compute_weights``,
+base.py:279-288): ``config.batch_size`` rows, the reference's 128 per task in every target config.
 """
 
 from __future__ import annotations
@@ -124,6 +125,13 @@ class OffPolicyAlgorithm(Algorithm):
                           f" return: {mean_returns:.4f}")
                     if track:
                         wandb.log(eval_metrics, step=total_steps)
+                    if hasattr(self, "compute_weights"):  # base.py:279-288
+                        # the reference samples envs.num_envs * 128 rows; the engine's batch is
+                        # config.batch_size, which is 128 per task in every target config
+                        metrics_data = replay_buffer.sample(config.batch_size)
+                        self, update_logs = self.compute_weights(metrics_data)
+                        if track:
+                            wandb.log(update_logs, step=total_steps)
                     if checkpoint_manager is not None:
                         checkpoint_manager.save(total_steps, agent=self, buffer=replay_buffer,
                                                 metadata={"timestamp": run_timestamp, "step": global_step,

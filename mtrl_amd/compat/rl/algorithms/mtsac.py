@@ -195,6 +195,22 @@ class MTSAC(OffPolicyAlgorithm):
             return self, _DeviceLogs(self.engine)
         return super().update_from_buffer(replay_buffer, batch_size, want_logs)
 
+    def compute_weights(self, data):
+        """mtsac.py:870-1170: per-task gradient-conflict metrics at evaluation time (no update).
+        Per-task gradients, Gram matrix, conflict / support / interference counts on the device
+        (mtrl_amd/conflict.py); the 66 log entries of the reference's dict.  The reference
+        samples one (n, A) noise draw per vmapped task from a single key (mtsac.py:892, 1052);
+        that structure is kept: one draw repeated for every task's rows."""
+        from ....conflict import compute_weights
+
+        T, A = self.num_tasks, self.engine.action_dim
+        n = np.asarray(data.rewards).shape[0] // T
+        if n != self._cfg_kwargs["batch_per_task"]:
+            self._rebuild(batch_per_task=n, capacity=max(self._cfg_kwargs["capacity"], n))
+        e_next = np.repeat(self._rng.standard_normal((n, A)), T, axis=0).astype(np.float32)  # row i*T + t
+        e_cur = np.repeat(self._rng.standard_normal((n, A)), T, axis=0).astype(np.float32)
+        return self, compute_weights(self.engine, tuple(data), e_next, e_cur)
+
     # ------------------------------------------------------------------ state (checkpoint)
     def state_dict(self) -> dict[str, np.ndarray]:
         """Agent pytree keyed by flax path (compat/checkpoint.py), e.g.

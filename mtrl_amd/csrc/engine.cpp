@@ -951,6 +951,224 @@ struct mtsac_engine {
     cur = st;
   }
 
+  // ------------------------------------------------------------ per-task gradients (eval metrics)
+  // MTSAC.compute_weights (mtsac.py:870-1090, MSE critic): for every task t the gradient of its
+  // own loss -- the critic MSE over the task's n rows (mean over E x n), the actor loss over its
+  // rows (mean over n) -- w.r.t. the whole network, as dense [T][P] matrices in flax ravel order
+  // (leaves back to back, no alignment padding), on the CURRENT parameters (nothing is updated).
+  // Kept from the reference: the critic's "next" actions are sampled from pi(.|s) of the
+  // OBSERVATIONS (mtsac.py:1000-1004) and scored by the target critic at s' (:1005-1007).
+  // Every GEMM here runs on fp32 operands (gemm_x3 / gemm_f32): the per-task weight gradient of
+  // layer i is ONE batched TN GEMM over the tasks, X_t^T dZ_t with task t's rows t, t + T, ...
+  // addressed by a row stride of T rows (rows interleaved i*T + t, as the buffer samples), its
+  // column sums (bias gradient) fused.
+  float* tg[2] = {};       // [T][P] critic (0), actor (1)
+  long long tgP[2] = {};
+  unsigned* sel_prefix = nullptr;
+  long long* sel_rank = nullptr;
+  unsigned* sel_hist = nullptr;
+  double *ps_gram_part = nullptr, *ps_l1_part = nullptr, *ps_gram = nullptr, *ps_l1 = nullptr;
+  unsigned long long *ps_counts = nullptr, *ps_nz = nullptr;
+  float* ps_thr = nullptr;
+  static constexpr int PS_GRID = 512;
+
+  static std::vector<long long> dense_offsets(const Net& net) {  // flax leaf offsets, no padding
+    std::vector<long long> off;
+    long long o = 0;
+    for (const auto& lf : net.leaves) {
+      off.push_back(o);
+      o += lf.second;
+    }
+    off.push_back(o);
+    return off;
+  }
+
+  int ensure_task_grad_buffers() {
+    int rc = 0;
+    for (int w = 0; w < 2; ++w) {
+      const Net& net = w == 0 ? critic : actor;
+      tgP[w] = net.n_params;
+      if (!tg[w] && (rc = alloc(&tg[w], (size_t)T_l * tgP[w]))) return rc;
+    }
+    if (!sel_prefix) {
+      if ((rc = alloc(&sel_prefix, 2 * 64)) || (rc = alloc(&sel_rank, 2 * 64)) || (rc = alloc(&sel_hist, 512 * 64)) ||
+          (rc = alloc(&ps_gram_part, (size_t)PS_GRID * 64 * 64)) || (rc = alloc(&ps_l1_part, (size_t)PS_GRID * 64)) ||
+          (rc = alloc(&ps_gram, 64 * 64)) || (rc = alloc(&ps_l1, 64)) || (rc = alloc(&ps_counts, 4 * 64 * 64)) ||
+          (rc = alloc(&ps_nz, 64)) || (rc = alloc(&ps_thr, 64)))
+        return rc;
+    }
+    return 0;
+  }
+
+  // dW_t, db_t of trunk layer i for every task t (one batched TN GEMM per ensemble member)
+  void task_wgrad(Net& net, int w, const float* X, int ldx, float** acts, float** dz, int i) {
+    const std::vector<long long> off = dense_offsets(net);
+    const int fan = i == 0 ? net.in_dim : net.width;
+    const int n_rows = B / T_l;
+    for (int e = 0; e < net.E; ++e) {
+      GemmParams g{};
+      g.A = i == 0 ? X : acts[i - 1] + (long long)e * B * net.width;
+      g.lda = (i == 0 ? ldx : net.width) * T_l;
+      g.sA = i == 0 ? ldx : net.width;
+      g.B = dz[i] + (long long)e * B * net.width;
+      g.ldb = net.width * T_l;
+      g.sB = net.width;
+      g.C = tg[w] + off[3 + 2 * i] + (long long)e * fan * net.width;
+      g.ldc = net.width;
+      g.sC = tgP[w];
+      g.db = tg[w] + off[2 + 2 * i] + (long long)e * net.width;
+      g.sDb = tgP[w];
+      g.M = fan;
+      g.N = net.width;
+      g.K = n_rows;
+      g.splits = 1;
+      gemm(g, GEMM_TN, EPI_STORE, T_l, MTSAC_FAM_WEIGHT_GRAD);
+    }
+  }
+
+  // the task's own head block (bias, kernel) of the padded gradient buffer into its dense row
+  void task_heads(Net& net, int w) {
+    const std::vector<long long> off = dense_offsets(net);
+    scatter_task_blocks(net.g, net.off_hb, net.ms_hb, tg[w], tgP[w], off[0], (long long)T_l * net.hd, net.E, T_l,
+                        net.hd, cur);
+    scatter_task_blocks(net.g, net.off_hW, net.ms_hW, tg[w], tgP[w], off[1], (long long)T_l * net.width * net.hd,
+                        net.E, T_l, (long long)net.width * net.hd, cur);
+  }
+
+  void task_grads(bool device_batch, bool device_noise) {
+    const int Bl = B, n_rows = B / T_l;
+    cur = st;
+    cur_lane = 0;
+    GatherParams gp = gather_params();
+    if (device_batch) {
+      replay_indices(rng, jump, buf_size, n, idx, cur);
+      replay_gather(gp, cur);
+    } else {
+      batch_scatter(gp, u_obs, u_act, u_nobs, u_done, u_rew, Bl, cur);
+    }
+    check_interleaved(task, Bl, T_l, err, cur);
+    task_rows(task, Bl, T_l, counts, rows, Bl, cur);
+    if (cfg.use_task_weights) row_alpha(task, cfg.task_begin, log_alpha, T_g, Bl, 1, row_c, tw, cur);
+    const float* twp = cfg.use_task_weights ? tw : nullptr;
+    for (int w = 0; w < 2; ++w) (void)hipMemsetAsync(tg[w], 0, sizeof(float) * T_l * tgP[w], cur);
+    PolicyParams pp{};
+    pp.seed = cfg.noise_seed;
+    pp.counter = counter;
+    pp.A = A;
+    pp.ls_min = cfg.log_std_min;
+    pp.ls_max = cfg.log_std_max;
+    pp.ld_a_out = ld_c;
+    pp.counts = counts;
+    pp.rows = rows;
+    pp.max_rows = Bl;
+    pp.T_l = T_l;
+    pp.max_count = n_rows;
+    CriticHeadParams ch{};
+    ch.rew = rew;
+    ch.done = done;
+    ch.log_alpha = log_alpha;
+    ch.task = task;
+    ch.task_begin = cfg.task_begin;
+    ch.tw = twp;
+    ch.gamma = cfg.gamma;
+    ch.clip = cfg.clip;
+    ch.T_glob = T_g;
+    const int Dc = critic.depth, Da = actor.depth;
+
+    // ---- critic (mtsac.py:1000-1048): a_n ~ pi(.|s), y from the target critic at (s', a_n)
+    trunk_forward(actor, actor.p, 0, xa, ld_a, han, nullptr, Bl);
+    {
+      PolicyParams q = pp;
+      q.head = head(actor, actor.p, han[Da - 1], Bl, task);
+      q.eps = device_noise ? nullptr : eps_n;
+      q.stream_id = 3;
+      q.a_out = xcn;
+      q.logpi = logpi_n;
+      policy_head(q, cur);
+    }
+    trunk_forward(critic, critic.tgt, 1, xcn, ld_c, hct, nullptr, Bl);
+    {
+      CriticHeadParams c = ch;
+      c.head = head(critic, critic.tgt, hct[Dc - 1], Bl, task);
+      c.mode = CH_TARGET;
+      c.logpi = logpi_n;
+      c.y_out = y;
+      critic_head(c, cur);
+    }
+    trunk_forward(critic, critic.p, 0, xc, ld_c, hc, nullptr, Bl);
+    const HeadParams chp = head(critic, critic.p, hc[Dc - 1], Bl, task);
+    {
+      CriticHeadParams c = ch;
+      c.head = chp;
+      c.mode = CH_CRITIC;
+      c.y = y;
+      c.dq = dq;
+      c.row_a = row_a;
+      c.row_b = row_b;
+      c.inv_norm = 1.0f / ((float)critic.E * (float)n_rows);  // per-task mean over E x n
+      critic_head(c, cur);
+    }
+    head_backward_data(chp, dq, Bl, dzc[Dc - 1], cur);
+    head_backward_weight(chp, dq, Bl, counts, rows, Bl, critic.g + critic.off_hW, critic.g + critic.off_hb, cur);
+    task_heads(critic, 0);
+    for (int i = Dc - 1; i >= 0; --i) {
+      task_wgrad(critic, 0, xc, ld_c, hc, dzc, i);
+      if (i > 0) dgrad_layer(critic, critic.p, hc, nullptr, dzc, nullptr, i, Bl);
+    }
+
+    // ---- actor (mtsac.py:1051-1090): the current critic, per-task mean over n rows
+    trunk_forward(actor, actor.p, 0, xa, ld_a, ha, nullptr, Bl);
+    {
+      PolicyParams q = pp;
+      q.head = head(actor, actor.p, ha[Da - 1], Bl, task);
+      q.eps = device_noise ? nullptr : eps_c;
+      q.stream_id = 4;
+      q.a_out = xcp;
+      q.logpi = logpi;
+      q.cache = cache;
+      policy_head(q, cur);
+    }
+    trunk_forward(critic, critic.p, 0, xcp, ld_c, hc, nullptr, Bl);
+    {
+      CriticHeadParams c = ch;
+      c.head = head(critic, critic.p, hc[Dc - 1], Bl, task);
+      c.mode = CH_ACTOR;
+      c.logpi = logpi;
+      c.dq = dq;
+      c.row_a = row_c;
+      c.alpha_w = alpha_w;
+      c.inv_norm = 1.0f / (float)n_rows;
+      critic_head(c, cur);
+      head_backward_data(c.head, dq, Bl, dzc[Dc - 1], cur);
+    }
+    for (int i = Dc - 1; i > 0; --i) dgrad_layer(critic, critic.p, hc, nullptr, dzc, nullptr, i, Bl);
+    {
+      ActionGradParams ag{};
+      ag.dz1 = dzc[0];
+      ag.W0 = critic.p + critic.off_W[0];
+      ag.s_dz = (long long)Bl * critic.width;
+      ag.s_W0 = critic.ms_W[0];
+      ag.E = critic.E;
+      ag.B = Bl;
+      ag.Wc = critic.width;
+      ag.A = A;
+      ag.cache = cache;
+      ag.alpha_w = alpha_w;
+      ag.ls_min = cfg.log_std_min;
+      ag.ls_max = cfg.log_std_max;
+      ag.dout = dout_a;
+      action_grad(ag, cur);
+    }
+    const HeadParams ahp = head(actor, actor.p, ha[Da - 1], Bl, task);
+    head_backward_data(ahp, dout_a, 0, dza[Da - 1], cur);
+    head_backward_weight(ahp, dout_a, 0, counts, rows, Bl, actor.g + actor.off_hW, actor.g + actor.off_hb, cur);
+    task_heads(actor, 1);
+    for (int i = Da - 1; i >= 0; --i) {
+      task_wgrad(actor, 1, xa, ld_a, ha, dza, i);
+      if (i > 0) dgrad_layer(actor, actor.p, ha, nullptr, dza, nullptr, i, Bl);
+    }
+  }
+
   AlphaParams alpha_params() {
     AlphaParams al{};
     al.logpi = logpi;
@@ -1607,6 +1825,120 @@ int mtsac_update(mtsac_engine* h, const mtsac_batch* b, const float* eps_next, c
   h->step(b == nullptr, eps_next == nullptr);
   HIP_TRY(hipGetLastError());
   if (b || eps_next) HIP_TRY(hipStreamSynchronize(h->st));  // borrowed host pointers
+  return 0;
+}
+
+// ---------------------------------------------------------------- gradient-conflict metrics
+static int task_grad_ready(mtsac_engine* h, int which) {
+  if (!h) return fail(-22, "null engine");
+  if (which != 0 && which != 1) return fail(-22, "which: 0 critic, 1 actor");
+  if (!h->tg[which]) return fail(-22, "no per-task gradients yet (mtsac_task_gradients)");
+  return 0;
+}
+
+int mtsac_task_gradients(mtsac_engine* h, const mtsac_batch* b, const float* eps_next, const float* eps_cur) {
+  if (!h) return fail(-22, "null engine");
+  if (h->T_l != h->T_g) return fail(-95, "per-task gradients need every task on one engine (unsharded)");
+  if ((eps_next == nullptr) != (eps_cur == nullptr)) return fail(-22, "inject both eps_next and eps_cur or neither");
+  int rc = h->ensure_task_grad_buffers();
+  if (rc) return rc;
+  const int B = h->B, D = h->D, A = h->A;
+  if (b) {
+    if (!b->observations || !b->actions || !b->next_observations || !b->dones || !b->rewards)
+      return fail(-22, "incomplete batch");
+    HIP_TRY(hipMemcpyAsync(h->u_obs, b->observations, sizeof(float) * B * D, hipMemcpyDefault, h->st));
+    HIP_TRY(hipMemcpyAsync(h->u_nobs, b->next_observations, sizeof(float) * B * D, hipMemcpyDefault, h->st));
+    HIP_TRY(hipMemcpyAsync(h->u_act, b->actions, sizeof(float) * B * A, hipMemcpyDefault, h->st));
+    HIP_TRY(hipMemcpyAsync(h->u_done, b->dones, sizeof(float) * B, hipMemcpyDefault, h->st));
+    HIP_TRY(hipMemcpyAsync(h->u_rew, b->rewards, sizeof(float) * B, hipMemcpyDefault, h->st));
+  }
+  if (eps_next) {
+    HIP_TRY(hipMemcpyAsync(h->eps_n, eps_next, sizeof(float) * B * A, hipMemcpyDefault, h->st));
+    HIP_TRY(hipMemcpyAsync(h->eps_c, eps_cur, sizeof(float) * B * A, hipMemcpyDefault, h->st));
+  }
+  const bool timing = h->timing;
+  h->timing = false;
+  h->task_grads(b == nullptr, eps_next == nullptr);
+  h->timing = timing;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(h->st));
+  int e = 0;
+  HIP_TRY(hipMemcpy(&e, h->err, sizeof(int), hipMemcpyDeviceToHost));
+  if (e) {
+    int z = 0;
+    HIP_TRY(hipMemcpy(h->err, &z, sizeof(int), hipMemcpyHostToDevice));
+    return fail(-22, "batch rows must be interleaved i*T + t with exact one-hot task ids (as the buffer samples)");
+  }
+  return 0;
+}
+
+int64_t mtsac_task_gradient_size(const mtsac_engine* h, int which) {
+  if (!h || (which != 0 && which != 1)) return -22;
+  return which == 0 ? h->critic.n_params : h->actor.n_params;
+}
+
+static int copy_task_grads(mtsac_engine* h, int which, float* host, int64_t n, bool to_device) {
+  if (!h) return fail(-22, "null engine");
+  if (to_device && !h->tg[which]) {
+    int rc = h->ensure_task_grad_buffers();
+    if (rc) return rc;
+  }
+  int rc = task_grad_ready(h, which);
+  if (rc) return rc;
+  if (!host || n != (int64_t)h->T_l * h->tgP[which]) return fail(-22, "size must be T * P");
+  HIP_TRY(hipStreamSynchronize(h->st));
+  if (to_device) HIP_TRY(hipMemcpy(h->tg[which], host, sizeof(float) * n, hipMemcpyDefault));
+  else HIP_TRY(hipMemcpy(host, h->tg[which], sizeof(float) * n, hipMemcpyDefault));
+  return 0;
+}
+
+int mtsac_get_task_gradients(mtsac_engine* h, int which, float* dst, int64_t n) {
+  return copy_task_grads(h, which, dst, n, false);
+}
+
+int mtsac_set_task_gradients(mtsac_engine* h, int which, const float* src, int64_t n) {
+  if (h && h->T_l != h->T_g) return fail(-95, "per-task gradients need every task on one engine (unsharded)");
+  return copy_task_grads(h, which, const_cast<float*>(src), n, true);
+}
+
+int mtsac_task_gradient_select(mtsac_engine* h, int which, const int64_t* ranks, float* values) {
+  int rc = task_grad_ready(h, which);
+  if (rc) return rc;
+  if (!ranks || !values) return fail(-22, "null argument");
+  const long long P = h->tgP[which];
+  for (int k = 0; k < 2 * h->T_l; ++k)
+    if (ranks[k] < 0 || ranks[k] >= P) return fail(-22, "rank out of range");
+  std::vector<long long> r(ranks, ranks + 2 * h->T_l);
+  task_select(h->tg[which], h->T_l, P, r.data(), values, h->sel_prefix, h->sel_rank, h->sel_hist, h->st);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int mtsac_task_gradient_stats(mtsac_engine* h, int which, const float* thresholds, float eps, float tau, double* gram,
+                              double* l1, int64_t* counts, int64_t* near_zero) {
+  int rc = task_grad_ready(h, which);
+  if (rc) return rc;
+  if (!thresholds || !gram || !l1 || !counts || !near_zero) return fail(-22, "null argument");
+  const int T = h->T_l;
+  HIP_TRY(hipMemcpyAsync(h->ps_thr, thresholds, sizeof(float) * T, hipMemcpyHostToDevice, h->st));
+  task_pair_stats(h->tg[which], T, h->tgP[which], h->ps_thr, eps, tau, mtsac_engine::PS_GRID, h->ps_gram_part,
+                  h->ps_l1_part, h->ps_counts, h->ps_nz, h->ps_gram, h->ps_l1, h->st);
+  HIP_TRY(hipGetLastError());
+  std::vector<double> g(64 * 64), l(64);
+  std::vector<unsigned long long> c(4 * 64 * 64), z(64);
+  HIP_TRY(hipMemcpyAsync(g.data(), h->ps_gram, sizeof(double) * g.size(), hipMemcpyDeviceToHost, h->st));
+  HIP_TRY(hipMemcpyAsync(l.data(), h->ps_l1, sizeof(double) * l.size(), hipMemcpyDeviceToHost, h->st));
+  HIP_TRY(hipMemcpyAsync(c.data(), h->ps_counts, sizeof(unsigned long long) * c.size(), hipMemcpyDeviceToHost, h->st));
+  HIP_TRY(hipMemcpyAsync(z.data(), h->ps_nz, sizeof(unsigned long long) * z.size(), hipMemcpyDeviceToHost, h->st));
+  HIP_TRY(hipStreamSynchronize(h->st));
+  for (int i = 0; i < T; ++i) {
+    l1[i] = l[i];
+    near_zero[i] = (int64_t)z[i];
+    for (int j = 0; j < T; ++j) {
+      gram[i * T + j] = g[i * 64 + j];
+      for (int q = 0; q < 4; ++q) counts[(long long)q * T * T + i * T + j] = (int64_t)c[(long long)q * 64 * 64 + i * 64 + j];
+    }
+  }
   return 0;
 }
 

@@ -314,4 +314,21 @@ struct LogParams {
 void write_logs(const LogParams& p, hipStream_t st);
 void bump_counter(unsigned long long* c, hipStream_t st);
 
+// ------------------------------------------------------------------ gradient-conflict statistics
+// (conflict.hip; MTSAC.compute_weights, mtsac.py:733-1170 and algorithms/utils.py:49-174)
+// G: per-task gradients [T][P] (flax ravel order, T <= 64).  values[t*2 + k] = the ranks[t*2 + k]-th
+// smallest |G[t][:]| (0-based); blocking (returns to the host).
+void task_select(const float* G, int T, long long P, const long long* ranks, float* values, unsigned* ws_prefix,
+                 long long* ws_rank, unsigned* ws_hist, hipStream_t st);
+// one pass over G: gram[64*64] (fp64), l1[64], counts[4][64*64] = #(g_i g_j < 0), #(S_i & S_j),
+// #(S_i & S_j & g_i g_j < 0), #(|g_i| < eps & |g_j| > tau) with S_t = |g_t| >= thr[t]; nz[t] = #(|g_t| < eps)
+void task_pair_stats(const float* G, int T, long long P, const float* thr, float eps, float tau, int grid,
+                     double* ws_gram_part, double* ws_l1_part, unsigned long long* counts, unsigned long long* nz,
+                     double* gram, double* l1, hipStream_t st);
+// dst[t*P + dst_off + e*dst_ms + t*blk + i] = src[src_off + e*src_ms + t*blk + i], i < blk (per-task head blocks)
+void scatter_task_blocks(const float* src, long long src_off, long long src_ms, float* dst, long long P,
+                         long long dst_off, long long dst_ms, int E, int T, long long blk, hipStream_t st);
+// *err |= 1 unless task[r] == r % T_l for every row (rows interleaved i*T + t, as the buffer samples)
+void check_interleaved(const int* task, int B, int T_l, int* err, hipStream_t st);
+
 }  // namespace mtsac

@@ -187,6 +187,49 @@ class MTSACEngine:
         keep.extend([en, ec])
         check(self.lib.mtsac_update(self._h, bp, en[0] or None, ec[0] or None))
 
+    # ------------------------------------------------------------------ gradient-conflict metrics
+    def task_gradients(self, batch=None, eps_next=None, eps_cur=None) -> None:
+        """Per-task gradients on the current parameters (include/mtsac.h, mtsac_task_gradients)."""
+        keep = []
+        bp = None
+        if batch is not None:
+            ptrs = [_ptr(x) for x in batch]
+            keep.extend(ptrs)
+            b = Batch(*[p[0] for p in ptrs])
+            bp = ctypes.byref(b)
+        en, ec = _ptr(eps_next), _ptr(eps_cur)
+        keep.extend([en, ec])
+        check(self.lib.mtsac_task_gradients(self._h, bp, en[0] or None, ec[0] or None))
+
+    def task_gradient_size(self, which: int) -> int:
+        return check(self.lib.mtsac_task_gradient_size(self._h, which))
+
+    def get_task_gradients(self, which: int) -> np.ndarray:
+        P = self.task_gradient_size(which)
+        out = np.empty((self.T_l, P), np.float32)
+        check(self.lib.mtsac_get_task_gradients(self._h, which, out.ctypes.data, out.size))
+        return out
+
+    def set_task_gradients(self, which: int, G) -> None:
+        G = np.ascontiguousarray(G, np.float32)
+        check(self.lib.mtsac_set_task_gradients(self._h, which, G.ctypes.data, G.size))
+
+    def task_gradient_select(self, which: int, ranks) -> np.ndarray:
+        r = np.ascontiguousarray(ranks, np.int64).reshape(self.T_l, 2)
+        out = np.empty((self.T_l, 2), np.float32)
+        check(self.lib.mtsac_task_gradient_select(self._h, which, r.ctypes.data, out.ctypes.data))
+        return out
+
+    def task_gradient_stats(self, which: int, thresholds, eps: float, tau: float) -> dict:
+        T = self.T_l
+        thr = np.ascontiguousarray(thresholds, np.float32).reshape(T)
+        gram, l1 = np.empty((T, T), np.float64), np.empty(T, np.float64)
+        counts, nz = np.empty((4, T, T), np.int64), np.empty(T, np.int64)
+        check(self.lib.mtsac_task_gradient_stats(self._h, which, thr.ctypes.data, eps, tau, gram.ctypes.data,
+                                                 l1.ctypes.data, counts.ctypes.data, nz.ctypes.data))
+        return {"gram": gram, "l1": l1, "conflict": counts[0], "intersection": counts[1], "genuine": counts[2],
+                "mismatch": counts[3], "near_zero": nz}
+
     def update_many(self, steps: int) -> None:
         check(self.lib.mtsac_update_many(self._h, steps))
 
