@@ -457,6 +457,7 @@ struct mtsac_engine {
   // after every write of params: Net::wt[which] (fp32) or the planes wp[which] (split3);
   // fused: the optimizer already wrote them (see optimize())
   void refresh_wt(Net& net, const float* params, int which, hipStream_t s, bool fused = false) {
+    if (fused && tiles_fusable(net)) return;  // the optimizer wrote every plane the GEMMs read
     for (int i = planes ? 0 : 1; i < net.depth; ++i) {
       if (!planes) {
         transpose_f32(params + net.off_W[i], net.ms_W[i], net.wt[which][i], net.ms_W[i], net.width, net.width, net.E,
@@ -666,6 +667,35 @@ struct mtsac_engine {
     a.g += net.trunk_off;
     if (a.target) a.target += net.trunk_off;
     a.n = net.n_flat - net.trunk_off;
+    if (tiles_fusable(net)) {  // kernel leaves in tiles: natural + transposed planes from the update
+      TileParams tp{};
+      for (int i = 0; i < net.depth; ++i) {
+        TileLeaf& lf = tp.leaf[tp.n++];
+        lf.off = net.off_W[i] - net.trunk_off;
+        lf.ms = net.ms_W[i];
+        lf.rows = i == 0 ? net.in_dim : net.width;
+        lf.cols = net.width;
+        lf.members = net.E;
+        lf.tiles_r = (lf.rows + 63) / 64;
+        lf.tiles_c = (lf.cols + 63) / 64;
+        lf.tile_begin = tp.total;
+        tp.total += lf.tiles_r * lf.tiles_c * lf.members;
+        lf.nat[0] = i > 0 ? net.wp[0][i] : nullptr;  // the data grad's B (layer 0 has none)
+        lf.nat_ld = net.wld;
+        lf.nat_ps = net.kps(i);
+        lf.tr[0] = net.wtp[0][i];
+        lf.tr[1] = polyak ? net.wtp[1][i] : nullptr;
+        lf.tr_ld = net.wtk(i);
+        lf.tr_ps = net.wtps(i);
+        a.skip_b[a.nskip] = lf.off / 4;
+        a.skip_e[a.nskip++] = (lf.off + lf.ms * net.E) / 4;
+      }
+      int na = adam_update(a, max_norm, 0, PART, cur);
+      a.p_partials = partials + na;
+      int nt = adam_update_tiles(a, tp, max_norm, PART, cur);
+      sum_partials(partials, na + nt, pn + slot, cur);
+      return;
+    }
     if (planes_fusable(net))  // hidden kernels' planes (params and Polyak target) from the update
       for (int i = 0; i < net.depth && a.nseg + 2 <= MAX_PLANE_SEGS; ++i) {
         a.seg[a.nseg++] = PlaneSeg{net.off_W[i] - net.trunk_off, net.ms_W[i], net.E, net.wp[0][i], net.kps(i), 0};
@@ -674,6 +704,12 @@ struct mtsac_engine {
       }
     int na = adam_update(a, max_norm, 0, PART, cur);
     sum_partials(partials, na, pn + slot, cur);
+  }
+
+  // gemm_x3f / gemm_x3s nets: every plane the GEMMs read comes out of the tiled update
+  // (adam_update_tiles): W_i^T planes of params and target, W_i planes of params (i >= 1)
+  bool tiles_fusable(const Net& net) const {
+    return planes && net.x3f && net.depth <= MAX_TILE_LEAVES && net.width % 4 == 0;
   }
 
   // the kernel planes can come straight out of the flat update when their layout is the leaf's
@@ -1449,7 +1485,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   if ((rc = e->alloc(&e->dq, (size_t)c.num_critics * B))) return bad(rc);
   if ((rc = e->alloc(&e->cache, (size_t)B * 5 * e->A))) return bad(rc);
   if ((rc = e->alloc(&e->dout_a, (size_t)B * 2 * e->A))) return bad(rc);
-  if ((rc = e->alloc(&e->partials, PART))) return bad(rc);
+  if ((rc = e->alloc(&e->partials, 2 * PART))) return bad(rc);  // elementwise + tiled update
   if ((rc = e->alloc(&e->pn, 4))) return bad(rc);
   if ((rc = e->alloc(&e->log_alpha, e->T_g))) return bad(rc);
   if ((rc = e->alloc(&e->la_m, e->T_g))) return bad(rc);

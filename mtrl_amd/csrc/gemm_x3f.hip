@@ -59,7 +59,8 @@ __device__ inline void wait_vm(bf16x8 (&b)[2][NP]) {
 }
 
 // ABL: ablation bits for experiments only (tools/x3f_ablate.py; results are wrong): 1 = no A
-// refills after the prologue, 2 = no B reloads after the prologue, 4 = s_setprio 1 for waves 4-7.
+// refills after the prologue, 2 = no B reloads after the prologue, 4 = s_setprio 1 for waves 4-7,
+// 64 = each B wave-instruction reads 1 KB contiguous (8 full lines) instead of 16 rows x 64 B.
 // ABL == TAG_INPUT changes nothing: it only gives input-layer launches their own kernel symbol, so
 // rocprof stats and PMC passes separate them from the hidden layers.
 // NP: operand planes read (3: 6 products, fp32-accurate; 1: the high plane only, precision bf16)
@@ -121,6 +122,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
     int n = n0 + 32 * wave + 16 * j + (lane & 15);
     n = n < p.N ? n : p.N - 1;
     boff[j] = (unsigned)(((long long)n * p.ldb + 8 * (lane >> 4)) * 2);
+    if (ABL & 64) boff[j] = (unsigned)((long long)(n0 + 32 * wave + 16 * j) * p.ldb * 2 + 16 * lane);
   }
   auto bload = [&](bf16x8 (&b)[2][NP], int k) {  // the 32-deep half step at k
 #pragma unroll
@@ -289,6 +291,7 @@ void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t s
     case 2: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 2>), grid, blk, 0, st, p); break;
     case 3: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 3>), grid, blk, 0, st, p); break;
     case 4: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 4>), grid, blk, 0, st, p); break;
+    case 64: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 64>), grid, blk, 0, st, p); break;
     default: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 0>), grid, blk, 0, st, p); break;
   }
 }

@@ -276,9 +276,32 @@ struct AdamParams {
   float* p_partials;    // sum of squares of new params per block
   int nseg;             // planes of the new params to write (offsets relative to p)
   PlaneSeg seg[MAX_PLANE_SEGS];
+  int nskip;            // float4 ranges [skip_b, skip_e) of p left to adam_update_tiles
+  long long skip_b[MAX_PLANE_SEGS], skip_e[MAX_PLANE_SEGS];
 };
 // p_partials accumulate |p_new|^2 over [norm_from, n) only (the replicated trunk range)
 int adam_update(const AdamParams& a, float max_norm, long long norm_from, int max_blocks, hipStream_t st);
+// The same update over dense kernel leaves [members][rows][cols] (cols % 4 == 0) in 64 x 64 tiles
+// through LDS, writing the bf16 planes of the new params / target in the natural layout
+// ([e][3][rows][nat_ld], the data grad's B) and transposed ([e][3][cols][tr_ld], k = row
+// contiguous: the row-major forward's B) -- replaces the separate transposing split of
+// refresh_wt.  Per-element arithmetic is adam_kernel's; |p_new|^2 partials, one per block, go to
+// a.p_partials (blocks <= max_blocks).  Offsets relative to a.p.
+struct TileLeaf {
+  long long off, ms;    // first member's offset, member stride (floats)
+  int rows, cols, members;
+  int tiles_r, tiles_c, tile_begin;
+  __bf16* nat[2];       // [0] params, [1] target (null: not wanted)
+  long long nat_ld, nat_ps;
+  __bf16* tr[2];
+  long long tr_ld, tr_ps;
+};
+constexpr int MAX_TILE_LEAVES = 8;
+struct TileParams {
+  int n, total;
+  TileLeaf leaf[MAX_TILE_LEAVES];
+};
+int adam_update_tiles(const AdamParams& a, const TileParams& tp, float max_norm, int max_blocks, hipStream_t st);
 // s0->pnorm = sqrt(trunk_sq[0] + head_sq[0]); s1 likewise with index 1
 void pnorm_finalize(const float* trunk_sq, const float* head_sq, OptScalars* s0, OptScalars* s1, hipStream_t st);
 // *out = sum(partials)  (one block, double accumulation)

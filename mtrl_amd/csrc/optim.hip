@@ -11,7 +11,9 @@
 // fused clip / Adam / Polyak / param-norm pass (7 x 4 B per parameter, +8 B for the
 // target).  All reductions have a fixed shape, so results are run-to-run bitwise
 // reproducible.
-#include "kernels.h"
+#include <algorithm>
+
+#include "gemm_common.h"
 
 namespace mtsac {
 
@@ -100,6 +102,9 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm,
   const float4* g4 = reinterpret_cast<const float4*>(a.g);
   float4* t4 = reinterpret_cast<float4*>(a.target);
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    bool skip = false;
+    for (int k = 0; k < a.nskip; ++k) skip |= i >= a.skip_b[k] && i < a.skip_e[k];
+    if (skip) continue;  // a tiled leaf (adam_tiles_kernel)
     float4 g = g4[i], p = p4[i], m = m4[i], v = v4[i];
     float* gp = &g.x;
     float* pp = &p.x;
@@ -153,6 +158,128 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm,
       *reinterpret_cast<bf16x4*>(dst + ps.ps) = mm;
       *reinterpret_cast<bf16x4*>(dst + 2 * ps.ps) = l;
     }
+  }
+  acc = block_sum256(acc);
+  if (threadIdx.x == 0) a.p_partials[blockIdx.x] = acc;
+}
+
+// 64 x 64 tiles of dense kernel leaves: thread t updates rows r0 + (t >> 4) + 16 j (j < 4), columns
+// c0 + 4 (t & 15) .. + 3 (16-B loads, a row's 64 columns by 16 lanes); the new values go through
+// LDS so the transposed planes leave as 2 x 16 B per lane (16 k of one output row).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <bool POLYAK>
+__global__ __launch_bounds__(256) void adam_tiles_kernel(AdamParams a, TileParams tp, float max_norm) {
+  __shared__ float sp[64][65];
+  __shared__ float stg[POLYAK ? 64 : 1][65];
+  const OptScalars sc = *a.sc;
+  const bool clip = (max_norm > 0.f) && !(sc.gnorm < max_norm);
+  const float gn = sc.gnorm;
+  const float bc1 = 1.0f - powf(a.b1, (float)sc.count);
+  const float bc2 = 1.0f - powf(a.b2, (float)sc.count);
+  const float omb1 = 1.0f - a.b1, omb2 = 1.0f - a.b2, neg_lr = -a.lr;
+  const float omtau = 1.0f - a.tau;
+  const int t = threadIdx.x, rr = t >> 4, c4 = 4 * (t & 15);
+  float acc = 0.f;
+  for (int tile = blockIdx.x; tile < tp.total; tile += gridDim.x) {
+    int L = 0;
+    while (L + 1 < tp.n && tile >= tp.leaf[L + 1].tile_begin) ++L;
+    const TileLeaf& lf = tp.leaf[L];
+    int loc = tile - lf.tile_begin;
+    const int per = lf.tiles_r * lf.tiles_c;
+    const int e = loc / per;
+    loc -= e * per;
+    const int r0 = 64 * (loc / lf.tiles_c), c0 = 64 * (loc % lf.tiles_c);
+    const long long base = lf.off + e * lf.ms;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = r0 + rr + 16 * j, c = c0 + c4;
+      float4 p = make_float4(0.f, 0.f, 0.f, 0.f), tv = p;
+      if (r < lf.rows && c < lf.cols) {
+        const long long i4 = (base + (long long)r * lf.cols + c) >> 2;
+        float4 g = reinterpret_cast<const float4*>(a.g)[i4];
+        float4 m = reinterpret_cast<float4*>(a.m)[i4], v = reinterpret_cast<float4*>(a.v)[i4];
+        p = reinterpret_cast<float4*>(a.p)[i4];
+        float* gp = &g.x;
+        float* pp = &p.x;
+        float* mp = &m.x;
+        float* vp = &v.x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float gk = gp[k];
+          if (clip) gk = (gk / gn) * max_norm;
+          mp[k] = omb1 * gk + a.b1 * mp[k];
+          vp[k] = omb2 * (gk * gk) + a.b2 * vp[k];
+          const float mh = mp[k] / bc1;
+          const float vh = vp[k] / bc2;
+          const float u = mh / (sqrtf(vh) + a.eps);
+          pp[k] = pp[k] + u * neg_lr;
+          acc += pp[k] * pp[k];
+        }
+        reinterpret_cast<float4*>(a.p)[i4] = p;
+        reinterpret_cast<float4*>(a.m)[i4] = m;
+        reinterpret_cast<float4*>(a.v)[i4] = v;
+        if (POLYAK) {
+          tv = reinterpret_cast<float4*>(a.target)[i4];
+          tv.x = a.tau * p.x + omtau * tv.x;
+          tv.y = a.tau * p.y + omtau * tv.y;
+          tv.z = a.tau * p.z + omtau * tv.z;
+          tv.w = a.tau * p.w + omtau * tv.w;
+          reinterpret_cast<float4*>(a.target)[i4] = tv;
+        }
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+          __bf16* np_ = lf.nat[w];
+          if (np_ == nullptr || (w == 1 && !POLYAK)) continue;
+          const float* src = w ? &tv.x : &p.x;
+          bf16x4_t h, mm, l;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            __bf16 x0, x1, x2;
+            split3_dev(src[k], x0, x1, x2);
+            h[k] = x0; mm[k] = x1; l[k] = x2;
+          }
+          __bf16* dst = np_ + e * 3 * lf.nat_ps + (long long)r * lf.nat_ld + c;
+          *reinterpret_cast<bf16x4_t*>(dst) = h;
+          *reinterpret_cast<bf16x4_t*>(dst + lf.nat_ps) = mm;
+          *reinterpret_cast<bf16x4_t*>(dst + 2 * lf.nat_ps) = l;
+        }
+      }
+      const int lr_ = rr + 16 * j;
+      sp[lr_][c4] = p.x; sp[lr_][c4 + 1] = p.y; sp[lr_][c4 + 2] = p.z; sp[lr_][c4 + 3] = p.w;
+      if (POLYAK) {
+        stg[lr_][c4] = tv.x; stg[lr_][c4 + 1] = tv.y; stg[lr_][c4 + 2] = tv.z; stg[lr_][c4 + 3] = tv.w;
+      }
+    }
+    __syncthreads();
+    {  // transposed planes: output row o (a column of the leaf), k = r0 + 16 (t & 3) .. + 15
+      const int oc = t >> 2, kq = 16 * (t & 3);
+      const int o = c0 + oc, k = r0 + kq;
+      if (o < lf.cols && k < lf.tr_ld) {
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+          __bf16* tp_ = lf.tr[w];
+          if (tp_ == nullptr || (w == 1 && !POLYAK)) continue;
+          bf16x8 h[2], mm[2], l[2];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const float x = w ? stg[POLYAK ? kq + q : 0][oc] : sp[kq + q][oc];
+            __bf16 x0, x1, x2;
+            split3_dev(x, x0, x1, x2);
+            h[q >> 3][q & 7] = x0; mm[q >> 3][q & 7] = x1; l[q >> 3][q & 7] = x2;
+          }
+          __bf16* dst = tp_ + e * 3 * lf.tr_ps + (long long)o * lf.tr_ld + k;
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            if (k + 8 * hh >= lf.tr_ld) break;
+            *reinterpret_cast<bf16x8*>(dst + 8 * hh) = h[hh];
+            *reinterpret_cast<bf16x8*>(dst + lf.tr_ps + 8 * hh) = mm[hh];
+            *reinterpret_cast<bf16x8*>(dst + 2 * lf.tr_ps + 8 * hh) = l[hh];
+          }
+        }
+      }
+    }
+    __syncthreads();
   }
   acc = block_sum256(acc);
   if (threadIdx.x == 0) a.p_partials[blockIdx.x] = acc;
@@ -284,6 +411,16 @@ int adam_update(const AdamParams& a, float max_norm, long long norm_from, int ma
   else
     hipLaunchKernelGGL(adam_kernel<false>, dim3((unsigned)g), dim3(256), 0, st, a, max_norm, norm_from >> 2);
   return (int)g;
+}
+
+int adam_update_tiles(const AdamParams& a, const TileParams& tp, float max_norm, int max_blocks, hipStream_t st) {
+  int g = std::min(tp.total, max_blocks);
+  if (g < 1) g = 1;
+  if (a.target)
+    hipLaunchKernelGGL(adam_tiles_kernel<true>, dim3((unsigned)g), dim3(256), 0, st, a, tp, max_norm);
+  else
+    hipLaunchKernelGGL(adam_tiles_kernel<false>, dim3((unsigned)g), dim3(256), 0, st, a, tp, max_norm);
+  return g;
 }
 
 __global__ void pnorm_finalize_kernel(const float* __restrict__ trunk_sq, const float* __restrict__ head_sq,

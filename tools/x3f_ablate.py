@@ -1,5 +1,6 @@
 """gemm_x3f ablations at the bench shape (E=2, 6400 x 2048 x 2048, bias+ReLU, planes out):
-0 full kernel, 1 no A refills, 2 no B reloads, 3 neither, 4 s_setprio 1 for waves 4-7.
+0 full kernel, 1 no A refills, 2 no B reloads, 3 neither, 4 s_setprio 1 for waves 4-7,
+64 B read as contiguous 1-KB blocks (TA pattern probe).
 Ablated results are wrong; only the time matters.  usage: python tools/x3f_ablate.py [iters]"""
 import ctypes
 import os
@@ -12,7 +13,7 @@ lib = L.load()
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 E, M, N, K = 2, 6400, 2048, 2048
 for rep in range(2):
-    for abl in (0, 1, 2, 3, 4):
+    for abl in [int(a) for a in os.environ.get("X3F_ABL", "0 1 2 3 4 64").split()]:
         ms = ctypes.c_double()
         L.check(lib.mtsac_debug_gemm_fwd_bench(2 + abl, 1 | 256, E, M, N, K, iters, ctypes.byref(ms)))
         tf = 2.0 * M * N * K * E / (ms.value * 1e-3) / 1e12
