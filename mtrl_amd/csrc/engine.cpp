@@ -74,6 +74,10 @@ struct Net {
   // activations then keep planes only (their ReLU mask is read from the high plane)
   bool x3f = false;
   __bf16* wtp[2][MAXD] = {};
+  // column-sum partials of dz[i] written by the pass that produces it (head backward, gemm_x3f data
+  // grad): [E][chunks][width]; dbp_chunks[i] > 0 when the current step's dz[i] came with them
+  float* dbp[MAXD] = {};
+  int dbp_chunks[MAXD] = {};
   long long wtk(int i) const { return i == 0 ? xld : ald; }  // K (padded in-dim) of layer i
   long long wtps(int i = 1) const { return (long long)width * wtk(i); }
   long long xld = 0;  // input planes' row stride = layer-0 kernel plane rows (in_dim rounded up to 32)
@@ -342,6 +346,21 @@ struct mtsac_engine {
     return po;
   }
 
+  // head backward into the top layer's data grad.  With planes the GEMMs read only the planes: the
+  // fp32 dz is skipped and (want_db) the bias grad's column sums come out of the same pass.
+  void head_bwd(Net& net, const HeadParams& hp, const float* dout, long long s_dout, float** dz, __bf16** dzp,
+                bool want_db) {
+    const int top = net.depth - 1;
+    const PlaneOut po = top_planes(net, dzp);
+    if (po.p == nullptr) {
+      head_backward_data(hp, dout, s_dout, dz[top], counts, rows, B, T_l, cur, po);
+      net.dbp_chunks[top] = 0;
+      return;
+    }
+    head_backward_data(hp, dout, s_dout, nullptr, counts, rows, B, T_l, cur, po, want_db ? net.dbp[top] : nullptr);
+    if (want_db) net.dbp_chunks[top] = head_backward_chunks(T_l);
+  }
+
   // ------------------------------------------------------------ trunk passes
   // acts[i] = relu(in_i @ W_i + b_i) for every member (batched over the ensemble)
   // which: 0 / 1 = params is Net::p / Net::tgt (their transposed copies or planes are current),
@@ -524,8 +543,11 @@ struct mtsac_engine {
       g.splits = -1;  // by tile count (gemm_x3p_splits); the lane workspace is sized for it
       g.ws = ws_lane[cur_lane];
       gemmp(g, EPI_STORE, net.E, i == 0 ? MTSAC_FAM_INPUT_WEIGHT_GRAD : MTSAC_FAM_WEIGHT_GRAD);
-      colsum(dz[i], M, net.width, net.width, (long long)M * net.width, net.E, cs_part, net.g + net.off_b[i], net.ms_b,
-             cur);
+      if (net.dbp_chunks[i] > 0)  // dz[i]'s producer left its column sums
+        colsum_finish(net.dbp[i], net.width, net.dbp_chunks[i], net.E, net.g + net.off_b[i], net.ms_b, cur);
+      else
+        colsum(dz[i], M, net.width, net.width, (long long)M * net.width, net.E, cs_part, net.g + net.off_b[i],
+               net.ms_b, cur);
       return;
     }
     GemmParams g{};
@@ -548,8 +570,12 @@ struct mtsac_engine {
     gemm(g, GEMM_TN, EPI_STORE, net.E, i == 0 ? MTSAC_FAM_INPUT_WEIGHT_GRAD : MTSAC_FAM_WEIGHT_GRAD);
   }
 
+  // want_db: the weight grad of layer i - 1 follows (the trunk backward), so dz[i-1]'s bias-grad
+  // column sums are wanted; without it (the actor step's pass through the critic) only the data
+  // flows on.  Hidden layers on gemm_x3f keep planes only: their bias grad comes from the
+  // epilogue's column sums.
   void dgrad_layer(Net& net, const float* params, float** acts, __bf16** actp, float** dz, __bf16** dzp, int i,
-                   int M) {
+                   int M, bool want_db = true) {
     if (planes && dzp) {  // NT on planes: dz[i] . W_i^T, W_i planes read as [N = in][K = out]
       SplitGemmParams g{};
       g.np = np;
@@ -584,6 +610,16 @@ struct mtsac_engine {
       g.K = (int)net.ald;
       g.splits = -1;
       g.ws = ws_lane[cur_lane];
+      if (i - 1 >= 1 && g.Cp) {  // dz[i-1]'s fp32 copy only fed the bias grad's column sums
+        SplitGemmParams q = g;
+        q.C = nullptr;
+        const bool on_x3f = gemm_x3f_ok(q, EPI_RELU_MASK, net.E);
+        if (on_x3f) g.C = nullptr;
+        if (want_db) {
+          if (on_x3f) g.dbp = net.dbp[i - 1];
+          net.dbp_chunks[i - 1] = on_x3f ? gemm_x3f_row_tiles(M) : 0;
+        }
+      }
       gemmp(g, EPI_RELU_MASK, net.E, MTSAC_FAM_DATA_GRAD);
       return;
     }
@@ -896,7 +932,7 @@ struct mtsac_engine {
       c.row_b = row_b;
       c.inv_norm = 1.0f / ((float)critic.E * (float)B_glob);
       critic_head(c, cur);
-      head_backward_data(chp, dq, Bl, dzc[critic.depth - 1], cur, top_planes(critic, dzcp));
+      head_bwd(critic, chp, dq, Bl, dzc, dzcp, true);
       const float* ins[2] = {row_a, row_b};
       reduce_rows(ins, 2, Bl, critic.g + critic.n_flat + 1, cur);
     });
@@ -924,8 +960,8 @@ struct mtsac_engine {
       c.alpha_w = alpha_w;
       c.inv_norm = 1.0f / (float)B_glob;
       critic_head(c, cur);
-      head_backward_data(c.head, dq, Bl, dzc[critic.depth - 1], cur, top_planes(critic, dzcp));
-      for (int i = critic.depth - 1; i > 0; --i) dgrad_layer(critic, critic.p, hc, hcp, dzc, dzcp, i, Bl);
+      head_bwd(critic, c.head, dq, Bl, dzc, dzcp, false);
+      for (int i = critic.depth - 1; i > 0; --i) dgrad_layer(critic, critic.p, hc, hcp, dzc, dzcp, i, Bl, false);
       ActionGradParams ag{};
       ag.dz1 = dzc[0];
       ag.W0 = critic.p + critic.off_W[0];
@@ -949,7 +985,7 @@ struct mtsac_engine {
       head_backward_weight(ahp, dout_a, 0, counts, rows, Bl, actor.g + actor.off_hW, actor.g + actor.off_hb, cur);
     });
     const int s_ad = seg({s_ap}, 1, [&] {
-      head_backward_data(ahp, dout_a, 0, dza[actor.depth - 1], cur, top_planes(actor, dzap));
+      head_bwd(actor, ahp, dout_a, 0, dza, dzap, true);
     });
     const int s_ab = backward_segs(actor, actor.p, xa, ld_a, ha, hap, dza, dzap, s_ad, s_ahw, Bl);
     seg({s_ab}, 1, [&] {
@@ -1144,7 +1180,7 @@ struct mtsac_engine {
       c.inv_norm = 1.0f / ((float)critic.E * (float)n_rows);  // per-task mean over E x n
       critic_head(c, cur);
     }
-    head_backward_data(chp, dq, Bl, dzc[Dc - 1], cur);
+    head_backward_data(chp, dq, Bl, dzc[Dc - 1], counts, rows, Bl, T_l, cur);
     head_backward_weight(chp, dq, Bl, counts, rows, Bl, critic.g + critic.off_hW, critic.g + critic.off_hb, cur);
     task_heads(critic, 0);
     for (int i = Dc - 1; i >= 0; --i) {
@@ -1175,7 +1211,7 @@ struct mtsac_engine {
       c.alpha_w = alpha_w;
       c.inv_norm = 1.0f / (float)n_rows;
       critic_head(c, cur);
-      head_backward_data(c.head, dq, Bl, dzc[Dc - 1], cur);
+      head_backward_data(c.head, dq, Bl, dzc[Dc - 1], counts, rows, Bl, T_l, cur);
     }
     for (int i = Dc - 1; i > 0; --i) dgrad_layer(critic, critic.p, hc, nullptr, dzc, nullptr, i, Bl);
     {
@@ -1196,7 +1232,7 @@ struct mtsac_engine {
       action_grad(ag, cur);
     }
     const HeadParams ahp = head(actor, actor.p, ha[Da - 1], Bl, task);
-    head_backward_data(ahp, dout_a, 0, dza[Da - 1], cur);
+    head_backward_data(ahp, dout_a, 0, dza[Da - 1], counts, rows, Bl, T_l, cur);
     head_backward_weight(ahp, dout_a, 0, counts, rows, Bl, actor.g + actor.off_hW, actor.g + actor.off_hb, cur);
     task_heads(actor, 1);
     for (int i = Da - 1; i >= 0; --i) {
@@ -1470,6 +1506,9 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
       // kernel, cheaper than writing the planes in the data-grad epilogue (tools/step_gemms.py)
       for (int i = 1; i < net->depth; ++i)
         if ((rc = e->alloc(cr ? &e->dzcp[i] : &e->dzap[i], np))) return bad(rc);
+      const long long chunks = std::max<long long>({(long long)COLSUM_CHUNKS, gemm_x3f_row_tiles(e->B), head_backward_chunks(e->T_l)});
+      for (int i = 1; i < net->depth; ++i)
+        if ((rc = e->alloc(&net->dbp[i], (size_t)(net->E * chunks * net->width)))) return bad(rc);
     }
     {
       const float* xs[5] = {e->xa, e->xan, e->xc, e->xcn, e->xcp};

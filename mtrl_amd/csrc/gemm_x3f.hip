@@ -217,6 +217,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
   }
   float* C = C_OUT ? p.C + z * p.sC : nullptr;
   __bf16* Cp = P_OUT ? p.Cp + z * p.sCp : nullptr;
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums over this lane's rows (dbp)
 #pragma unroll
   for (int i = 0; i < TI; ++i) {
 #pragma unroll
@@ -251,6 +252,8 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
         for (int c = 0; c < 8; ++c) e[c] = mk[c] > 0.f ? e[c] : 0.f;
       }
     }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) csum[c] += e[c];
     if (C_OUT) {
       float* cp = C + (long long)row * p.ldc + col;
       *reinterpret_cast<float4*>(cp) = make_float4(e[0], e[1], e[2], e[3]);
@@ -268,6 +271,22 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
       *reinterpret_cast<bf16x8*>(pp) = h;
       *reinterpret_cast<bf16x8*>(pp + p.pC) = m;
       *reinterpret_cast<bf16x8*>(pp + 2 * p.pC) = l;
+    }
+  }
+  if (p.dbp) {  // the tile's column sums: lanes with equal lane & 3 hold the same 8 columns
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float v = csum[c];
+      v += __shfl_xor(v, 4);
+      v += __shfl_xor(v, 8);
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      csum[c] = v;
+    }
+    if (lane < 4 && colok) {
+      float* d = p.dbp + ((long long)z * nx + bx) * p.N + col;
+      *reinterpret_cast<float4*>(d) = make_float4(csum[0], csum[1], csum[2], csum[3]);
+      *reinterpret_cast<float4*>(d + 4) = make_float4(csum[4], csum[5], csum[6], csum[7]);
     }
   }
 }
@@ -295,6 +314,8 @@ void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t s
     default: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 0>), grid, blk, 0, st, p); break;
   }
 }
+
+int gemm_x3f_row_tiles(int M) { return (M + x3fk::BM0 - 1) / x3fk::BM0; }
 
 int gemm_x3f_tiles(int M, int N, int batch) {
   return ((M + x3fk::BM0 - 1) / x3fk::BM0) * ((N + x3fk::BN - 1) / x3fk::BN) * batch;

@@ -135,13 +135,29 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
   }
 }
 
+// block: 64 columns x 4 chunk lanes; lane group g sums chunks g, g + 4, ... (8 loads in flight),
+// the 4 groups are added in order
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int cols, int chunks,
                                                            float* __restrict__ db, long long sdb) {
-  const int z = blockIdx.z, c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
+  __shared__ float red[4][64];
+  const int z = blockIdx.z, cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (int ch = 0; ch < chunks; ++ch) s += part[((long long)z * chunks + ch) * cols + c];
-  db[z * sdb + c] = s;
+  if (c < cols) {
+    const float* pz = part + (long long)z * chunks * cols + c;
+    int ch = g;
+    for (; ch + 28 < chunks; ch += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = pz[(long long)(ch + 4 * u) * cols];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; ch < chunks; ch += 4) s += pz[(long long)ch * cols];
+  }
+  red[g][cl] = s;
+  __syncthreads();
+  if (g == 0 && c < cols) db[z * sdb + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
 }
 
 // scalar fallback (cols or ld not multiples of 4)
@@ -357,6 +373,11 @@ void split_planes(const SplitParams& s, bool transpose, int batch, hipStream_t s
     hipLaunchKernelGGL(split_kernel<false>, grid, dim3(256), 0, st, s);
 }
 
+void colsum_finish(const float* part, int cols, int chunks, int batch, float* db, long long sdb, hipStream_t st) {
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 63) / 64, 1, batch), dim3(256), 0, st, part, cols, chunks, db,
+                     sdb);
+}
+
 void colsum(const float* x, int rows, int cols, int ld, long long sx, int batch, float* part, float* db,
             long long sdb, hipStream_t st) {
   // ~256 rows per chunk keeps every lane streaming; COLSUM_CHUNKS bounds the partials
@@ -367,8 +388,7 @@ void colsum(const float* x, int rows, int cols, int ld, long long sx, int batch,
   else
     hipLaunchKernelGGL(colsum_partial_scalar_kernel, dim3((cols + 255) / 256, chunks, batch), dim3(256), 0, st, x,
                        rows, cols, ld, sx, chunks, part);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256, 1, batch), dim3(256), 0, st, part, cols, chunks, db,
-                     sdb);
+  colsum_finish(part, cols, chunks, batch, db, sdb, st);
 }
 
 }  // namespace mtsac

@@ -8,6 +8,8 @@
 // One wavefront per batch row; the head kernels stream the last trunk activation
 // (W floats per row) exactly once.
 #include "devrng.h"
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace mtsac {
@@ -238,26 +240,24 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
 }
 
 // ------------------------------------------------------------------ head backward (data)
+// Grouped by task: block (256 columns, task t, row slice rs, member e); the lane's 4 x HD head
+// weights stay in registers while wave rl walks the task's rows j = 4 rs + rl + 4 HB_RS k (rows
+// from task_rows; two per iteration for loads in flight).  dbp: the (task, slice) column sums
+// (the bias gradient's partials, [e][T_l * HB_RS][W]; waves added in order), so the trunk's bias
+// grad needs no pass over an fp32 dz.  dz (fp32) may be null.
+constexpr int HB_RS = 4;
+
 template <int HD>
-__global__ __launch_bounds__(256) void head_bwd_data_kernel(HeadParams hp, const float* __restrict__ dout,
-                                                            long long s_dout, float* __restrict__ dz, PlaneOut po) {
-  const int W4 = hp.W >> 2;
-  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long per = (long long)hp.B * W4;
-  if (gid >= per * hp.E) return;
-  const int e = (int)(gid / per);
-  const long long r = gid - e * per;
-  const int b = (int)(r / W4);
-  const int w = (int)(r - (long long)b * W4) * 4;
-  const int t = hp.task[b];
-  const float* Wt = hp.Wh + e * hp.sWh + ((long long)t * hp.W + w) * HD;
+__device__ inline float4 head_bwd_row(const HeadParams& hp, const float* __restrict__ dout, long long s_dout, int e,
+                                      int b, int w, const float (&wt)[4][HD], float* __restrict__ dz,
+                                      const PlaneOut& po) {
   const float* d = dout + e * s_dout + (long long)b * HD;
   float g[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     float s = 0.f;
 #pragma unroll
-    for (int o = 0; o < HD; ++o) s += d[o] * Wt[k * HD + o];
+    for (int o = 0; o < HD; ++o) s += d[o] * wt[k][o];
     g[k] = s;
   }
   const long long off = e * hp.sh + (long long)b * hp.W + w;
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256) void head_bwd_data_kernel(HeadParams hp, const
   out.y = h.y > 0.f ? g[1] : 0.f;
   out.z = h.z > 0.f ? g[2] : 0.f;
   out.w = h.w > 0.f ? g[3] : 0.f;
-  *reinterpret_cast<float4*>(dz + off) = out;
+  if (dz) *reinterpret_cast<float4*>(dz + off) = out;
   if (po.p) {  // the bf16 split planes the next GEMMs read
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
     const float v[4] = {out.x, out.y, out.z, out.w};
@@ -285,6 +285,54 @@ __global__ __launch_bounds__(256) void head_bwd_data_kernel(HeadParams hp, const
     *reinterpret_cast<bf16x4*>(q) = ph;
     *reinterpret_cast<bf16x4*>(q + po.ps) = pm;
     *reinterpret_cast<bf16x4*>(q + 2 * po.ps) = pl;
+  }
+  return out;
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void head_bwd_data_kernel(HeadParams hp, const float* __restrict__ dout,
+                                                            long long s_dout, float* __restrict__ dz, PlaneOut po,
+                                                            float* __restrict__ dbp, const int* __restrict__ counts,
+                                                            const int* __restrict__ rows, int max_rows) {
+  __shared__ float4 red[4][64];
+  const int e = blockIdx.z, t = blockIdx.y / HB_RS, rs = blockIdx.y - t * HB_RS;
+  const int lane = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int w = blockIdx.x * 256 + 4 * lane;
+  const bool ok = w < hp.W;
+  const int n = counts[t];
+  const int* rw = rows + (long long)t * max_rows;
+  float wt[4][HD];
+  if (ok) {
+    const float* Wt = hp.Wh + e * hp.sWh + ((long long)t * hp.W + w) * HD;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int o = 0; o < HD; ++o) wt[k][o] = Wt[k * HD + o];
+  }
+  float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok) {
+    constexpr int STRIDE = 4 * HB_RS;
+    int j = 4 * rs + rl;
+    for (; j + STRIDE < n; j += 2 * STRIDE) {
+      const int b0 = rw[j], b1 = rw[j + STRIDE];
+      const float4 o0 = head_bwd_row<HD>(hp, dout, s_dout, e, b0, w, wt, dz, po);
+      const float4 o1 = head_bwd_row<HD>(hp, dout, s_dout, e, b1, w, wt, dz, po);
+      cs.x += o0.x; cs.y += o0.y; cs.z += o0.z; cs.w += o0.w;
+      cs.x += o1.x; cs.y += o1.y; cs.z += o1.z; cs.w += o1.w;
+    }
+    if (j < n) {
+      const float4 o0 = head_bwd_row<HD>(hp, dout, s_dout, e, rw[j], w, wt, dz, po);
+      cs.x += o0.x; cs.y += o0.y; cs.z += o0.z; cs.w += o0.w;
+    }
+  }
+  if (dbp == nullptr) return;
+  red[rl][lane] = cs;
+  __syncthreads();
+  if (rl == 0 && ok) {
+    const float4 a = red[0][lane], b = red[1][lane], c = red[2][lane], d = red[3][lane];
+    *reinterpret_cast<float4*>(dbp + ((long long)e * gridDim.y + blockIdx.y) * hp.W + w) =
+        make_float4(((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y, ((a.z + b.z) + c.z) + d.z,
+                    ((a.w + b.w) + c.w) + d.w);
   }
 }
 
@@ -545,18 +593,23 @@ void critic_head(const CriticHeadParams& p, hipStream_t st) {
   hipLaunchKernelGGL(critic_head_kernel, dim3((p.head.B + 3) / 4), dim3(256), 0, st, p);
 }
 
-void head_backward_data(const HeadParams& hp, const float* dout, long long s_dout, float* dz, hipStream_t st,
-                        PlaneOut po) {
-  const long long n = (long long)hp.E * hp.B * (hp.W / 4);
-  dim3 grid((unsigned)((n + 255) / 256));
+void head_backward_data(const HeadParams& hp, const float* dout, long long s_dout, float* dz, const int* counts,
+                        const int* rows, int max_rows, int T_l, hipStream_t st, PlaneOut po, float* dbp) {
+  const dim3 grid((unsigned)((hp.W + 255) / 256), (unsigned)(T_l * HB_RS), (unsigned)hp.E);
+#define HBD_LAUNCH(HDV)                                                                                  \
+  hipLaunchKernelGGL(head_bwd_data_kernel<HDV>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po, dbp, counts, \
+                     rows, max_rows)
   switch (hp.hd) {
-    case 1: hipLaunchKernelGGL(head_bwd_data_kernel<1>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po); break;
-    case 2: hipLaunchKernelGGL(head_bwd_data_kernel<2>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po); break;
-    case 4: hipLaunchKernelGGL(head_bwd_data_kernel<4>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po); break;
-    case 6: hipLaunchKernelGGL(head_bwd_data_kernel<6>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po); break;
-    default: hipLaunchKernelGGL(head_bwd_data_kernel<8>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po); break;
+    case 1: HBD_LAUNCH(1); break;
+    case 2: HBD_LAUNCH(2); break;
+    case 4: HBD_LAUNCH(4); break;
+    case 6: HBD_LAUNCH(6); break;
+    default: HBD_LAUNCH(8); break;
   }
+#undef HBD_LAUNCH
 }
+
+int head_backward_chunks(int T_l) { return T_l * HB_RS; }
 
 void head_backward_weight(const HeadParams& hp, const float* dout, long long s_dout, const int* counts,
                           const int* rows, int max_rows, float* dWh, float* dbh, hipStream_t st) {

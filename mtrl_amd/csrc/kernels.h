@@ -76,6 +76,8 @@ struct SplitGemmParams {
   int tag;                // 1: input-layer launch (separate kernel symbol for profiles)
   int np;                 // operand planes the products read: 3 (0 = default; fp32-accurate split) or 1
                           // (precision bf16: the high plane only, one MFMA per product)
+  float* dbp;             // gemm_x3f: column sums of the epilogue's output per row tile, [z][row tiles][N]
+                          // (the next weight grad's bias grad, finished by colsum_finish), or null
 };
 void gemm_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
 // auto split-K slices (1 = none) for a plane GEMM; kmajor = the k-major x k-major form
@@ -86,6 +88,7 @@ long long gemm_x3p_ws_floats(int M, int N, int K, int batch, bool kmajor);
 bool gemm_x3f_ok(const SplitGemmParams& p, int epi, int batch);
 void gemm_x3f(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
 int gemm_x3f_tiles(int M, int N, int batch);
+int gemm_x3f_row_tiles(int M);  // row tiles of M (the dbp partials' chunk count)
 void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t st);  // experiments
 // the same contract for small row counts (task shards, MT10): 16 TI x 64 tiles, 4 waves splitting
 // K inside the workgroup (gemm_x3s.hip); the ReLU mask comes from mask16
@@ -110,6 +113,9 @@ struct SplitParams {
 void split_planes(const SplitParams& s, bool transpose, int batch, hipStream_t st);
 // db[z][c] = sum_r x[z][r][c] (deterministic two-pass; part holds batch*COLSUM_CHUNKS*cols floats)
 constexpr int COLSUM_CHUNKS = 64;
+// db[z][c] = sum over chunks (in order) of part[z][chunks][cols]: the second pass of colsum for
+// partials written by a producing kernel's epilogue (head backward, gemm_x3f data grad)
+void colsum_finish(const float* part, int cols, int chunks, int batch, float* db, long long sdb, hipStream_t st);
 void colsum(const float* x, int rows, int cols, int ld, long long sx, int batch, float* part, float* db,
             long long sdb, hipStream_t st);
 
@@ -219,9 +225,14 @@ struct PlaneOut {
   __bf16* p;
   long long ld, ps, sm;
 };
-// dz[e][b][w] = (sum_o dout[e][b][o] * Wh[e][t_b][w][o]) * (h[e][b][w] > 0)  (+ its planes)
-void head_backward_data(const HeadParams& hp, const float* dout, long long s_dout, float* dz, hipStream_t st,
-                        PlaneOut po = PlaneOut{});
+// dz[e][b][w] = (sum_o dout[e][b][o] * Wh[e][t_b][w][o]) * (h[e][b][w] > 0)  (+ its planes), rows
+// walked per task (counts / rows of task_rows); dz may be null (planes only).  dbp (nullable):
+// column sums of dz per (task, row slice), [e][head_backward_chunks(T_l)][W], finished by
+// colsum_finish.  W % 4 == 0.
+void head_backward_data(const HeadParams& hp, const float* dout, long long s_dout, float* dz, const int* counts,
+                        const int* rows, int max_rows, int T_l, hipStream_t st, PlaneOut po = PlaneOut{},
+                        float* dbp = nullptr);
+int head_backward_chunks(int T_l);
 // dWh[e][t][w][o] = sum_{b in t} h[e][b][w] dout[e][b][o];  dbh[e][t][o] = sum dout
 void head_backward_weight(const HeadParams& hp, const float* dout, long long s_dout, const int* counts,
                           const int* rows, int max_rows, float* dWh, float* dbh, hipStream_t st);

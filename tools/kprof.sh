@@ -1,0 +1,14 @@
+#!/bin/bash
+# kprof.sh TAG TL... -- serialised-step kernel sums (tools/kernel_sums.py) for each task count TL
+set -o pipefail
+TAG=$1; shift
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+for TL in "$@"; do
+  timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/kt$TL -o run -- python $R/tools/shard_prof.py $TL > $O/kt$TL.log 2>&1 || exit 1
+  python $R/tools/kernel_sums.py $O/kt$TL/run_kernel_trace.csv 45 > $O/sums_$TL.txt || exit 1
+  rm -rf $O/kt$TL
+done
+echo done
