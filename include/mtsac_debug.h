@@ -50,13 +50,15 @@ int mtsac_debug_x3p_geo(int geo);
 /* Row-major x row-major plane GEMM (gemm_x3f.hip, 16x16x32 MFMA, K padded to 64): per batch entry
  * C[M][N] = epi(A[M][K] . B[N][K]^T); epi 1 bias+ReLU, 2 ReLU mask (bit 8: mask read from the
  * bf16 high plane of `mask`; bit 9: run gemm_x3s.hip, the small-row-count kernel, instead; bit 10:
- * precision bf16, the products on the operands' high planes only);
+ * precision bf16, the products on the operands' high planes only; bit 11: split-K by the
+ * launcher's choice, with a workspace, as the engine runs task shards);
  * Csum (nullable): sum of the written output planes.  -95 when the kernel does not take the shape. */
 int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A, const float* B, float* C,
                          const float* bias, const float* mask, float* Csum);
 /* Time iters launches of the forward-shaped plane GEMM: which 0 = gemm_x3p (B k-major), 1 = gemm_x3f,
  * -1 = gemm_x3s (-2 / -3: its TI = 7 instance without operand loads / without MFMAs, experiments);
- * epi bits 8-9: outputs 0 = fp32 + planes, 1 = planes only, 2 = fp32 only; bit 10: precision bf16. */
+ * epi bits 8-9: outputs 0 = fp32 + planes, 1 = planes only, 2 = fp32 only; bit 10: precision bf16;
+ * bit 11: split-K by the launcher's choice (gemm_x3p and gemm_x3f), with a workspace. */
 int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int K, int iters, double* ms_per_launch);
 /* Rows per gemm_x3s tile / 16 (TI, 4..8) the cost model picks for an M x N output, batch entries. */
 int mtsac_debug_x3s_ti(int M, int N, int batch);

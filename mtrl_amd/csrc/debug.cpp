@@ -178,6 +178,7 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
   const bool m16 = (epi >> 8) & 1;
   const bool small = (epi >> 9) & 1;  // gemm_x3s instead
   const int np = ((epi >> 10) & 1) ? 1 : 3;  // bf16: the high plane only
+  const bool autosplit = (epi >> 11) & 1;     // split-K by the launcher's own choice (workspace given)
   epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || !A || !B || !C) return -22;
   DevBuf d;
@@ -227,6 +228,11 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
   }
   g.M = M; g.N = N; g.K = (int)Kp;
   g.np = np;
+  if (autosplit) {
+    g.ws = d.get<float>((size_t)std::max(gemm_x3f_ws_floats(M, N, (int)Kp, batch), 1LL));
+    if (!g.ws) return -12;
+    g.splits = -1;
+  }
   if (small) {
     if (!gemm_x3s_ok(g, epi, batch)) return -95;
     gemm_x3s(g, epi, batch, nullptr);
@@ -255,6 +261,7 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
 int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int K, int iters, double* ms_per_launch) {
   const int outs = (epi >> 8) & 3;  // 0: fp32 + planes, 1: planes only, 2: fp32 only
   const int np = ((epi >> 10) & 1) ? 1 : 3;  // bf16: the high plane only
+  const bool autosplit = (epi >> 11) & 1;     // split-K by the launcher's own choice (workspace given)
   epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || iters < 1 || !ms_per_launch) return -22;
   DevBuf d;
@@ -292,6 +299,12 @@ int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int 
   g.M = M; g.N = N; g.K = (int)Kp;
   g.splits = 1;
   g.np = np;
+  if (autosplit) {
+    const long long wsf = std::max(gemm_x3f_ws_floats(M, N, (int)Kp, batch), gemm_x3p_ws_floats(M, N, (int)Kp, batch, false));
+    g.ws = d.get<float>((size_t)std::max(wsf, 1LL));
+    if (!g.ws) return -12;
+    g.splits = -1;
+  }
   if (which >= 1 && !gemm_x3f_ok(g, epi, batch)) return -95;
   if (which < 0 && !gemm_x3s_ok(g, epi, batch)) return -95;
   auto run = [&]() {

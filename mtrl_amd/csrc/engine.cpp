@@ -411,7 +411,8 @@ struct mtsac_engine {
         g.N = net.width;
         g.K = (int)net.wtk(i);
         g.tag = i == 0 ? 1 : 0;
-        g.splits = 1;
+        g.splits = -1;  // split-K when the row tiles do not fill the chip (task shards)
+        g.ws = ws_lane[cur_lane];
         gemmp(g, EPI_BIAS_RELU, net.E, i == 0 ? MTSAC_FAM_INPUT_FORWARD : MTSAC_FAM_FORWARD);
         continue;
       }
@@ -610,14 +611,16 @@ struct mtsac_engine {
       g.K = (int)net.ald;
       g.splits = -1;
       g.ws = ws_lane[cur_lane];
-      if (i - 1 >= 1 && g.Cp) {  // dz[i-1]'s fp32 copy only fed the bias grad's column sums
-        SplitGemmParams q = g;
-        q.C = nullptr;
-        const bool on_x3f = gemm_x3f_ok(q, EPI_RELU_MASK, net.E);
-        if (on_x3f) g.C = nullptr;
-        if (want_db) {
-          if (on_x3f) g.dbp = net.dbp[i - 1];
-          net.dbp_chunks[i - 1] = on_x3f ? gemm_x3f_row_tiles(M) : 0;
+      if (i - 1 >= 1 && g.Cp) {  // dz[i-1]'s fp32 copy only feeds the bias grad's column sums
+        if (!want_db) {
+          g.C = nullptr;
+        } else {  // one gemm_x3f pass (no split-K) writes the planes and the column sums
+          SplitGemmParams q = g;
+          q.C = nullptr;
+          q.dbp = net.dbp[i - 1];
+          const bool fused = gemm_x3f_ok(q, EPI_RELU_MASK, net.E);
+          if (fused) g = q;
+          net.dbp_chunks[i - 1] = fused ? gemm_x3f_row_tiles(M) : 0;
         }
       }
       gemmp(g, EPI_RELU_MASK, net.E, MTSAC_FAM_DATA_GRAD);
@@ -1430,13 +1433,16 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     net->xld = align_up(net->in_dim, 32);
     net->arows = align_up(e->B, 32);
     // row-major x row-major plane GEMMs for the trunk forward and data grad (hidden activations
-    // then keep planes only): gemm_x3f when its 208 x 256 tiles fill the chip, gemm_x3s for narrow
-    // trunks (K <= 512: W = 400).  Wide trunks on few rows (task shards, MT10 at W = 2048) stay on
-    // gemm_x3p + split-K: there the 16 TI x 64 tiles of gemm_x3s are bound by the per-CU operand
-    // ingest (texture-address unit busy 94 %, tools/x3s_ablate.py), and so are
-    // narrow trunks on many rows (MT50 at W = 400: gemm_x3p's 256 x 128 tiles win there).
+    // then keep planes only): gemm_x3f when its 208 x 256 tiles fill the chip (with split-K when
+    // they do not), gemm_x3s for narrow trunks (K <= 512: W = 400).  The 16 TI x 64 tiles of
+    // gemm_x3s are bound by the per-CU operand ingest on wide trunks (texture-address unit busy
+    // 94 %, tools/x3s_ablate.py), and narrow trunks on many rows (MT50 at
+    // W = 400) run faster on gemm_x3p's 256 x 128 tiles.
+    // Task shards of wide trunks (B = 768..1280 at W = 2048): gemm_x3f + split-K beats gemm_x3p +
+    // split-K for the twin critic (E = 2: 64-80 row x column tiles, 8-20 % per launch,
+    // tools/x3f_split_bench.py) but not for the actor (E = 1), which stays on gemm_x3p.
     net->x3f = e->planes && net->depth > 1 &&
-               ((net->ald % 64 == 0 && gemm_x3f_tiles(e->B, net->width, net->E) >= 192) ||
+               ((net->ald % 64 == 0 && gemm_x3f_tiles(e->B, net->width, net->E) >= 64) ||
                 (net->ald <= 512 && e->B <= 2048));
     if (net->x3f) net->xld = align_up(net->in_dim, 64);  // gemm_x3f steps K by 64
     for (int w = 0; w < (net == &e->critic ? 2 : 1); ++w)
@@ -1459,6 +1465,8 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
           ws = std::max(ws, gemm_x3p_ws_floats(M, net->width, (int)net->arows, net->E, true));  // weight grad
           ws = std::max(ws, gemm_x3p_ws_floats(e->B, net->width, (int)(i == 0 ? net->xld : net->ald), net->E,
                                                false));  // forward / data grad
+          ws = std::max(ws, gemm_x3f_ws_floats(e->B, net->width, (int)(i == 0 ? align_up(net->in_dim, 64) : net->ald),
+                                               net->E));
         }
       }
     for (float*& w : e->ws_lane)

@@ -89,11 +89,17 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
     const int n = gridDim.x, q8 = n / 8, r8 = n % 8, x = lin % 8;
     lin = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + lin / 8;
   }
+  // split-K (p.splits > 1): slice s of K, raw partial slab out (EPI_STORE into p.C = workspace)
+  const int nsplit = p.splits > 1 ? p.splits : 1;
+  const int tiles = ny * nx * (int)(gridDim.x / nsplit / (ny * nx));
+  const int sl = lin / tiles;
+  lin -= sl * tiles;
   const int by = lin % ny, bx = (lin / ny) % nx, z = lin / (ny * nx);
   const int m0 = bx * BM, n0 = by * BN;
-  const __bf16* __restrict__ A = p.A + z * p.sA;
-  const __bf16* B = p.B + z * p.sB;
-  const int nk = p.K / KS;
+  const int k0 = nsplit > 1 ? sl * p.kchunk : 0;
+  const __bf16* __restrict__ A = p.A + z * p.sA + k0;
+  const __bf16* B = p.B + z * p.sB + k0;
+  const int nk = (nsplit > 1 ? min(p.kchunk, p.K - k0) : p.K) / KS;
 
   // ---- A: LDS-DMA piece j of the stage at k0 into stage buffer `st` (byte address)
   auto piece = [&](int j, int k0, unsigned st) {
@@ -215,7 +221,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
     bias[0] = u.x; bias[1] = u.y; bias[2] = u.z; bias[3] = u.w;
     bias[4] = v.x; bias[5] = v.y; bias[6] = v.z; bias[7] = v.w;
   }
-  float* C = C_OUT ? p.C + z * p.sC : nullptr;
+  float* C = C_OUT ? p.C + z * p.sC + (long long)sl * p.M * p.ldc : nullptr;
   __bf16* Cp = P_OUT ? p.Cp + z * p.sCp : nullptr;
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums over this lane's rows (dbp)
 #pragma unroll
@@ -317,19 +323,75 @@ void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t s
 
 int gemm_x3f_row_tiles(int M) { return (M + x3fk::BM0 - 1) / x3fk::BM0; }
 
+// split-K slices for row counts whose tiles do not fill the chip (task shards): least
+// (rounds of tiles x S workgroups) / S, plus ~4 % of a round per extra slice (its partial slab
+// traffic and the finishing pass); >= 4 64-deep steps per slice
+int gemm_x3f_splits(int M, int N, int K, int batch) {
+  const long long tiles = (long long)gemm_x3f_tiles(M, N, batch);
+  if (tiles >= 192) return 1;
+  const int smax = std::min(8, std::max(1, K / x3fk::KS / 4));
+  int best = 1;
+  double best_cost = 1e30;
+  for (int sp = 1; sp <= smax; ++sp) {
+    const double cost = (double)((tiles * sp + 255) / 256) / sp + 0.04 * (sp - 1);
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = sp;
+    }
+  }
+  return best;
+}
+
+long long gemm_x3f_ws_floats(int M, int N, int K, int batch) {
+  const int s = gemm_x3f_splits(M, N, K, batch);
+  return s > 1 ? (long long)batch * s * M * N : 0;
+}
+
 int gemm_x3f_tiles(int M, int N, int batch) {
   return ((M + x3fk::BM0 - 1) / x3fk::BM0) * ((N + x3fk::BN - 1) / x3fk::BN) * batch;
+}
+
+// slices this launch would use: 1, or gemm_x3f_splits when the caller allows split-K
+// (splits < 0, a workspace given) and the finishing pass can apply the epilogue
+static int x3f_slices(const SplitGemmParams& p, int epi, int batch) {
+  if (p.splits >= 0 || p.ws == nullptr || p.dbp != nullptr) return 1;
+  if (epi == EPI_RELU_MASK && !p.mask16 && !p.mask) return 1;
+  if (p.N % 4 != 0 || (p.C && p.ldc % 4 != 0) || (p.Cp && p.ldcp % 4 != 0)) return 1;
+  return gemm_x3f_splits(p.M, p.N, p.K, batch);
 }
 
 bool gemm_x3f_ok(const SplitGemmParams& p, int epi, int batch) {
   return !p.a_kmajor && !p.b_kmajor && p.K % x3fk::KS == 0 && p.N % 8 == 0 && p.lda % 8 == 0 && p.ldb % 8 == 0 &&
          (!p.C || p.ldc % 4 == 0) && (!p.Cp || p.ldcp % 8 == 0) && (epi != EPI_RELU_MASK || p.ldm % 8 == 0) &&
-         (epi != EPI_STORE) && gemm_x3f_tiles(p.M, p.N, batch) >= 192 && (p.C || p.Cp) &&
-         (long long)p.N * p.ldb * 2 < (1ll << 31);
+         (epi != EPI_STORE) && (long long)gemm_x3f_tiles(p.M, p.N, batch) * x3f_slices(p, epi, batch) >= 192 &&
+         (p.C || p.Cp) && (long long)p.N * p.ldb * 2 < (1ll << 31);
 }
 
-void gemm_x3f(const SplitGemmParams& p, int epi, int batch, hipStream_t st) {
+void gemm_x3f(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
   using namespace x3fk;
+  const int S = x3f_slices(p0, epi, batch);
+  if (S > 1) {  // raw partial slabs [z][S][M][N] into the workspace, then the epilogue pass
+    SplitGemmParams q = p0;
+    q.splits = S;
+    q.kchunk = (p0.K / KS + S - 1) / S * KS;
+    q.C = p0.ws;
+    q.ldc = p0.N;
+    q.sC = (long long)S * p0.M * p0.N;
+    q.Cp = nullptr;
+    q.dbp = nullptr;
+    const int S_eff = (p0.K + q.kchunk - 1) / q.kchunk;
+    q.splits = S_eff;
+    const dim3 grid((unsigned)(gemm_x3f_tiles(p0.M, p0.N, batch) * S_eff));
+    if (p0.np == 1)
+      hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_STORE, true, false, false, 0, 1>), grid, dim3(512), 0, st, q);
+    else
+      hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_STORE, true, false, false, 0, 3>), grid, dim3(512), 0, st, q);
+    SplitGemmParams f = p0;
+    f.sC = p0.sC;
+    splitk_finish(f, epi, S_eff, batch, st);
+    return;
+  }
+  const SplitGemmParams& p = p0;
   const dim3 grid((unsigned)gemm_x3f_tiles(p.M, p.N, batch));
   const bool c = p.C != nullptr, pl = p.Cp != nullptr, m16 = p.mask16 != nullptr;
   if (epi == EPI_BIAS_RELU && p.tag == 1 && pl && !c) {

@@ -288,7 +288,11 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(SplitGemmParams p,
     e[0] = fmaxf(e[0] + b.x, 0.f); e[1] = fmaxf(e[1] + b.y, 0.f);
     e[2] = fmaxf(e[2] + b.z, 0.f); e[3] = fmaxf(e[3] + b.w, 0.f);
   }
-  if (EPI == EPI_RELU_MASK) {
+  if (EPI == EPI_RELU_MASK && p.mask16) {  // the activation's bf16 high plane (gemm_x3f nets)
+    const bf16x4_t mk = *reinterpret_cast<const bf16x4_t*>(p.mask16 + z * p.sMask + (long long)row * p.ldm + col);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e[j] = (float)mk[j] > 0.f ? e[j] : 0.f;
+  } else if (EPI == EPI_RELU_MASK) {
     const float4 mk = *reinterpret_cast<const float4*>(p.mask + z * p.sMask + (long long)row * p.ldm + col);
     e[0] = mk.x > 0.f ? e[0] : 0.f; e[1] = mk.y > 0.f ? e[1] : 0.f;
     e[2] = mk.z > 0.f ? e[2] : 0.f; e[3] = mk.w > 0.f ? e[3] : 0.f;
@@ -350,6 +354,10 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
     splitk_reduce(r, batch, S, st);
     return;
   }
+  splitk_finish(p, epi, S, batch, st);
+}
+
+void splitk_finish(const SplitGemmParams& p, int epi, int S, int batch, hipStream_t st) {
   const long long n = (long long)batch * p.M * (p.N / 4);
   const dim3 grid((unsigned)((n + 255) / 256));
   if (epi == EPI_BIAS_RELU)

@@ -80,6 +80,9 @@ struct SplitGemmParams {
                           // (the next weight grad's bias grad, finished by colsum_finish), or null
 };
 void gemm_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
+// split-K finishing pass: C / Cp = epi(sum over the S slabs of p.ws, in slice order); the ReLU mask
+// from p.mask16 when set, else p.mask
+void splitk_finish(const SplitGemmParams& p, int epi, int S, int batch, hipStream_t st);
 // auto split-K slices (1 = none) for a plane GEMM; kmajor = the k-major x k-major form
 int gemm_x3p_splits(int M, int N, int K, int batch, bool kmajor);
 long long gemm_x3p_ws_floats(int M, int N, int K, int batch, bool kmajor);
@@ -89,6 +92,10 @@ bool gemm_x3f_ok(const SplitGemmParams& p, int epi, int batch);
 void gemm_x3f(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
 int gemm_x3f_tiles(int M, int N, int batch);
 int gemm_x3f_row_tiles(int M);  // row tiles of M (the dbp partials' chunk count)
+// split-K for few rows: slices (1 = none) and workspace floats; gemm_x3f splits when the params
+// allow it (splits < 0, ws given, no dbp)
+int gemm_x3f_splits(int M, int N, int K, int batch);
+long long gemm_x3f_ws_floats(int M, int N, int K, int batch);
 void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t st);  // experiments
 // the same contract for small row counts (task shards, MT10): 16 TI x 64 tiles, 4 waves splitting
 // K inside the workgroup (gemm_x3s.hip); the ReLU mask comes from mask16

@@ -101,3 +101,34 @@ def test_bf16_products():
     acc, scale = _ref(Ar, Br)
     want = np.maximum(acc + bias[:, None, :], 0)
     assert np.all(np.abs(C - want) <= 4e-6 * (scale + np.abs(bias[:, None, :])) + 1e-30)
+
+
+@pytest.mark.parametrize("E,M,N,K,epi,m16", [(2, 896, 2048, 2048, 1, False), (2, 768, 2048, 2048, 2, True),
+                                             (2, 1280, 2040, 512, 2, False), (1, 1800, 2048, 1024, 1, False)],
+                         ids=["shard7_fwd", "shard6_dgrad_m16", "mt10_ragged_dgrad", "e1_ragged_fwd"])
+def test_split_k_task_shards(E, M, N, K, epi, m16):
+    """Few rows (task shards): K split over workgroups, raw partial slabs, then the finishing
+    pass applies bias+ReLU or the ReLU mask (fp32 or the bf16 high plane) and writes the planes."""
+    from mtrl_amd import _lib as L
+
+    lib = L.load()
+    rng = np.random.default_rng(M + K + epi)
+    A = rng.standard_normal((E, M, K)).astype(np.float32)
+    B = (rng.standard_normal((E, N, K)) / np.sqrt(K)).astype(np.float32)
+    bias = rng.standard_normal((E, N)).astype(np.float32) * 0.1
+    mask = np.maximum(rng.standard_normal((E, M, N)), 0).astype(np.float32)
+    C = np.zeros((E, M, N), np.float32)
+    Cs = np.zeros((E, M, N), np.float32)
+    p = lambda a: np.ascontiguousarray(a, np.float32).ctypes.data
+    L.check(lib.mtsac_debug_gemm_x3f(epi | (256 if m16 else 0) | 2048, E, M, N, K, p(A), p(B), C.ctypes.data,
+                                     p(bias), p(mask), Cs.ctypes.data))
+    acc, scale = _ref(A, B)
+    if epi == 1:
+        want = np.maximum(acc + bias[:, None, :], 0)
+        tol = 4e-6 * (scale + np.abs(bias[:, None, :])) + 1e-30
+    else:
+        want = np.where(mask > 0, acc, 0.0)  # h > 0 <=> its bf16 high plane > 0
+        tol = 4e-6 * scale + 1e-30
+    err = np.abs(C - want)
+    assert np.all(err <= tol), float((err / (scale + 1e-30)).max())
+    np.testing.assert_array_equal(Cs, C)
