@@ -183,6 +183,7 @@ struct mtsac_engine {
   float* pn = nullptr;  // [critic trunk |p|^2, actor trunk, critic heads, actor heads]
   float* log_alpha = nullptr;
   float *la_m = nullptr, *la_v = nullptr;
+  float* alpha_tmp = nullptr;  // per-task temperature-loss terms (alpha_grad)
   OptScalars* sc_alpha = nullptr;
   float* logs = nullptr;
   unsigned long long* counter = nullptr;
@@ -1260,6 +1261,7 @@ struct mtsac_engine {
     al.v = la_v;
     al.grad = actor.g + actor.n_flat + 3;
     al.loss_part = actor.g + actor.n_flat + 2;
+    al.task_loss = alpha_tmp;
     al.sc = sc_alpha;
     return al;
   }
@@ -1537,6 +1539,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   if ((rc = e->alloc(&e->log_alpha, e->T_g))) return bad(rc);
   if ((rc = e->alloc(&e->la_m, e->T_g))) return bad(rc);
   if ((rc = e->alloc(&e->la_v, e->T_g))) return bad(rc);
+  if ((rc = e->alloc(&e->alpha_tmp, e->T_g))) return bad(rc);
   if ((rc = e->alloc(&e->sc_alpha, 1))) return bad(rc);
   if ((rc = e->alloc(&e->logs, MTSAC_NUM_LOGS))) return bad(rc);
   if ((rc = e->alloc(&e->counter, 1))) return bad(rc);

@@ -337,6 +337,7 @@ struct AlphaParams {
   float* m; float* v;
   float* grad;          // [T_glob] scratch (allreduced in multi-GPU)
   float* loss_part;     // scalar scratch: sum over rows of -(log_alpha_t)(logpi + H)
+  float* task_loss;     // [T_glob] scratch: that sum per task
   OptScalars* sc;
 };
 void alpha_grad(const AlphaParams& a, hipStream_t st);

@@ -308,27 +308,29 @@ __global__ __launch_bounds__(1024) void reduce_rows_kernel(RowPtrs in, int n_in,
 
 // temperature gradient: d/dlogalpha_t mean_b(-(x_b . logalpha)(logpi_b + H))
 //   = -(1/B) sum_{b in t}(logpi_b + H)    (x one-hot, validated by the gather)
-__global__ __launch_bounds__(256) void alpha_grad_kernel(AlphaParams a) {
-  __shared__ float red[4];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int i = threadIdx.x; i < a.T_glob; i += 256) a.grad[i] = 0.f;
-  __syncthreads();
-  float loss_acc = 0.f;  // lane-0 accumulators per wave
-  for (int t = wave; t < a.T_l; t += 4) {
+// one wave per global task (zero outside this shard's tasks); the loss term of each task goes to
+// task_loss[t], summed in task order by alpha_loss_kernel
+__global__ __launch_bounds__(64) void alpha_grad_kernel(AlphaParams a) {
+  const int tg = blockIdx.x, lane = threadIdx.x;
+  const int t = tg - a.task_begin;
+  float s = 0.f;
+  if (t >= 0 && t < a.T_l) {
     const int n = a.counts[t];
     const int* rl = a.rows + (long long)t * a.max_rows;
-    float s = 0.f;
     for (int j = lane; j < n; j += 64) s += a.logpi[rl[j]] + a.target_entropy;
     s = wsumf(s);
-    const int tg = a.task_begin + t;
-    if (lane == 0) {
-      a.grad[tg] = -s / (float)a.B_glob;
-      loss_acc += -a.log_alpha[tg] * s;
-    }
   }
-  if (lane == 0) red[wave] = loss_acc;
-  __syncthreads();
-  if (threadIdx.x == 0) *a.loss_part = (red[0] + red[1]) + (red[2] + red[3]);
+  if (lane == 0) {
+    a.grad[tg] = (t >= 0 && t < a.T_l) ? -s / (float)a.B_glob : 0.f;
+    a.task_loss[tg] = (t >= 0 && t < a.T_l) ? -a.log_alpha[tg] * s : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(64) void alpha_loss_kernel(AlphaParams a) {
+  float s = 0.f;
+  for (int t = threadIdx.x; t < a.T_glob; t += 64) s += a.task_loss[t];
+  s = wsumf(s);
+  if (threadIdx.x == 0) *a.loss_part = s;
 }
 
 __global__ __launch_bounds__(64) void alpha_adam_kernel(AlphaParams a, float lr, float b1, float b2, float eps,
@@ -438,7 +440,8 @@ void sum_partials(const float* partials, int nparts, float* out, hipStream_t st)
 }
 
 void alpha_grad(const AlphaParams& a, hipStream_t st) {
-  hipLaunchKernelGGL(alpha_grad_kernel, dim3(1), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(alpha_grad_kernel, dim3((unsigned)a.T_glob), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(alpha_loss_kernel, dim3(1), dim3(64), 0, st, a);
 }
 
 void alpha_adam(const AlphaParams& a, float lr, float b1, float b2, float eps, float max_norm, hipStream_t st) {
