@@ -21,9 +21,9 @@
 //     (inline asm), so the compiler never drains the LDS-DMA early.
 //   * M is cut into BM = 208-row tiles: B = 6400 rows -> 31 row tiles x 8 column tiles = 248
 //     workgroups on 256 CUs (E = 1), 496 in two full rounds (E = 2).
-//   * Epilogue per 16-row block through a wave-private LDS scratch: 32 B of fp32 per lane (whole
-//     128-B row segments) and 16 B per bf16 plane; bias+ReLU or ReLU mask (fp32 or the bf16 high
-//     plane of the activation: h > 0 <=> h_hi > 0 for every normal h).
+//   * Epilogue per 16-row block through an LDS image of the workgroup's 16 x 256 outputs, so every
+//     output row leaves in whole lines (1 KB fp32, 512 B per bf16 plane); bias+ReLU or ReLU mask
+//     (fp32 or the bf16 high plane of the activation: h > 0 <=> h_hi > 0 for every normal h).
 #include <algorithm>
 #include <type_traits>
 
@@ -60,7 +60,8 @@ __device__ inline void wait_vm(bf16x8 (&b)[2][NP]) {
 
 // ABL: ablation bits for experiments only (tools/x3f_ablate.py; results are wrong): 1 = no A
 // refills after the prologue, 2 = no B reloads after the prologue, 4 = s_setprio 1 for waves 4-7,
-// 64 = each B wave-instruction reads 1 KB contiguous (8 full lines) instead of 16 rows x 64 B.
+// 64 = each B wave-instruction reads 1 KB contiguous (8 full lines) instead of 16 rows x 64 B,
+// 128 = no epilogue stores.
 // ABL == TAG_INPUT changes nothing: it only gives input-layer launches their own kernel symbol, so
 // rocprof stats and PMC passes separate them from the hidden layers.
 // NP: operand planes read (3: 6 products, fp32-accurate; 1: the high plane only, precision bf16)
@@ -208,11 +209,16 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
   step(nk - 1, std::integral_constant<bool, false>{});
 
   // ---------------------------------------------------------------- epilogue
+  // Per 16-row block, the 8 waves' 16 x 32 pieces meet in an LDS image of the block's 16 x 256
+  // outputs (two buffers: one barrier per block); wave w then finishes rows 2w, 2w + 1, lane l
+  // taking 8 columns 8 (l & 31): every fp32 row leaves as 1 KB and every plane row as 512 B of
+  // contiguous 16-B lane stores (whole lines), instead of 16 rows x 64 B per instruction.
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // the ring is free: scratch
   __builtin_amdgcn_sched_barrier(0);
-  float* scr = reinterpret_cast<float*>(smem) + wave * (16 * 36);
-  const int rr = lane >> 2, c8 = 8 * (lane & 3);
-  const int col = n0 + 32 * wave + c8;
+  constexpr int TS = BN + 4;  // image row stride (floats): the 4 row groups of a write land 16 banks apart
+  float* img = reinterpret_cast<float*>(smem);
+  const int orow = 2 * wave + (lane >> 5), oc = 8 * (lane & 31);
+  const int col = n0 + oc;
   const bool colok = col < p.N;  // N % 8 == 0: a lane's 8 columns are all in or all out
   float bias[8];
   if (EPI == EPI_BIAS_RELU && colok) {
@@ -226,20 +232,17 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums over this lane's rows (dbp)
 #pragma unroll
   for (int i = 0; i < TI; ++i) {
+    float* tb = img + (i & 1) * 16 * TS;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) scr[(4 * (lane >> 4) + r) * 36 + 16 * j + (lane & 15)] = acc[i][j][r];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const float4 u = *reinterpret_cast<const float4*>(scr + rr * 36 + c8);
-    const float4 v = *reinterpret_cast<const float4*>(scr + rr * 36 + c8 + 4);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int row = m0 + 16 * i + rr;
+      for (int r = 0; r < 4; ++r) tb[(4 * (lane >> 4) + r) * TS + 32 * wave + 16 * j + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+    const float4 u = *reinterpret_cast<const float4*>(tb + orow * TS + oc);
+    const float4 v = *reinterpret_cast<const float4*>(tb + orow * TS + oc + 4);
+    const int row = m0 + 16 * i + orow;
     if (row >= p.M || !colok) continue;
+    if ((ABL & 128) && p.M > 0) continue;  // ablation: no epilogue stores (p.M > 0 keeps the MFMAs live)
     float e[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
     if (EPI == EPI_BIAS_RELU) {
 #pragma unroll
@@ -279,20 +282,27 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
       *reinterpret_cast<bf16x8*>(pp + 2 * p.pC) = l;
     }
   }
-  if (p.dbp) {  // the tile's column sums: lanes with equal lane & 3 hold the same 8 columns
+  if (p.dbp) {  // the tile's column sums: lanes l, l + 32 of every wave hold the same 8 columns
+    float* red = img + 2 * 16 * TS;  // [8 waves][256]
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      float v = csum[c];
-      v += __shfl_xor(v, 4);
-      v += __shfl_xor(v, 8);
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      csum[c] = v;
+    for (int c = 0; c < 8; ++c) csum[c] += __shfl_xor(csum[c], 32);
+    if (lane < 32) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) red[wave * BN + oc + c] = csum[c];
     }
-    if (lane < 4 && colok) {
+    __syncthreads();
+    if (wave == 0 && lane < 32 && colok) {
+      float t[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float a = red[oc + c];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) a += red[w * BN + oc + c];
+        t[c] = a;
+      }
       float* d = p.dbp + ((long long)z * nx + bx) * p.N + col;
-      *reinterpret_cast<float4*>(d) = make_float4(csum[0], csum[1], csum[2], csum[3]);
-      *reinterpret_cast<float4*>(d + 4) = make_float4(csum[4], csum[5], csum[6], csum[7]);
+      *reinterpret_cast<float4*>(d) = make_float4(t[0], t[1], t[2], t[3]);
+      *reinterpret_cast<float4*>(d + 4) = make_float4(t[4], t[5], t[6], t[7]);
     }
   }
 }
@@ -317,6 +327,8 @@ void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t s
     case 3: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 3>), grid, blk, 0, st, p); break;
     case 4: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 4>), grid, blk, 0, st, p); break;
     case 64: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 64>), grid, blk, 0, st, p); break;
+    case 128: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 128>), grid, blk, 0, st, p); break;
+    case 131: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 131>), grid, blk, 0, st, p); break;
     default: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 0>), grid, blk, 0, st, p); break;
   }
 }
