@@ -61,7 +61,8 @@ __device__ inline void wait_vm(bf16x8 (&b)[2][NP]) {
 // ABL: ablation bits for experiments only (tools/x3f_ablate.py; results are wrong): 1 = no A
 // refills after the prologue, 2 = no B reloads after the prologue, 4 = s_setprio 1 for waves 4-7,
 // 64 = each B wave-instruction reads 1 KB contiguous (8 full lines) instead of 16 rows x 64 B,
-// 128 = no epilogue stores.
+// 128 = no epilogue stores (131: no loads or stores -- MFMA, LDS reads and barriers only; interleaving
+// two row tiles' MFMA chains changed nothing there).
 // ABL == TAG_INPUT changes nothing: it only gives input-layer launches their own kernel symbol, so
 // rocprof stats and PMC passes separate them from the hidden layers.
 // NP: operand planes read (3: 6 products, fp32-accurate; 1: the high plane only, precision bf16)
