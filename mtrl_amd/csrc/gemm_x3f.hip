@@ -73,9 +73,12 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
   constexpr int STAGE = NP * PLANE;
   constexpr int NJ = NP * BM / 8;        // DMA wave-instructions per stage
   constexpr int PMAX = (NJ + 7) / 8;     // per wave (the first NJ % 8 waves), others PMAX - 1
-  constexpr int P0 = (PMAX + 1) / 2;     // issued in the first half step
+  // every piece of the next stage is issued in the FIRST half step (spread over its row tiles), so
+  // each has at least a half step to land before the drain at the next step's barrier
+  constexpr int P0 = (ABL & 512) ? (PMAX + 1) / 2 : PMAX;  // 512: the old even split (experiments)
+  constexpr int PW = (ABL & 512) ? P0 : PMAX - 1;  // pieces every wave has issued after B(kt, 1)
   static_assert(BM % 16 == 0 && 2 * STAGE <= 160 * 1024, "tile");
-  static_assert(PMAX - 1 >= P0 || NJ % 8 == 0, "every wave issues >= P0 pieces in the first half step");
+  static_assert(PMAX - 1 >= PW || NJ % 8 == 0, "every wave issues >= PW pieces in the first half step");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const unsigned lds_base = (unsigned)(unsigned long long)(x3pk::lds_void*)smem;
 
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
         if (!(ABL & 2) || kt == 0) bload(b1, kt * KS + 32);  // second half of this step
       } else {
         if (ABL & 1) wait_vm<0, NP>(b1);
-        else wait_vm<MORE ? P0 : 0, NP>(b1);  // B(kt, 1) landed; this half step's DMA pieces may not have
+        else wait_vm<MORE ? PW : 0, NP>(b1);  // B(kt, 1) landed; the DMA pieces issued after it may not have
         if (MORE && !(ABL & 2)) bload(b0, kn);  // first half of the next step
       }
       bf16x8 a[2][NP];
@@ -330,6 +333,7 @@ void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t s
     case 64: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 64>), grid, blk, 0, st, p); break;
     case 128: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 128>), grid, blk, 0, st, p); break;
     case 131: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 131>), grid, blk, 0, st, p); break;
+    case 512: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 512>), grid, blk, 0, st, p); break;
     default: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 0>), grid, blk, 0, st, p); break;
   }
 }
