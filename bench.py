@@ -45,10 +45,10 @@ HBM_PEAK_GBS = 8000.0
 # enum mtsac_gemm_family (include/mtsac.h) -> the rocprof kernel(s) of that family, per precision
 GEMM_FAMILIES = {
     "split3": {
-        0: "gemm_x3f_kernel<208, 1, *, *, false, 0> (hidden-layer forward, planes, bias+ReLU)",
-        1: "gemm_x3f_kernel<208, 2, *, *, true, 0> (hidden-layer data grad, planes, ReLU mask from the bf16 high plane)",
-        2: "gemm_x3p_kernel<Geo<256, 256, 2, 4, 3, 16, 0>, true, true, 0, false> (hidden-layer weight grad, k-major planes, split-K)",
-        3: "gemm_x3f_kernel<208, 1, false, true, false, 8> (input-layer forward, planes, K = in_dim padded to 64)",
+        0: "gemm_x3f_kernel<208, 1, *, *, false, 0, 3> (hidden-layer forward, planes, bias+ReLU)",
+        1: "gemm_x3f_kernel<208, 2, *, *, true, 0, 3> (hidden-layer data grad, planes, ReLU mask from the bf16 high plane)",
+        2: "gemm_x3p_kernel<Geo<256, 256, 2, 4, 3, 16, 0>, true, true, 0, false, 3> (hidden-layer weight grad, k-major planes, split-K)",
+        3: "gemm_x3f_kernel<208, 1, false, true, false, 8, 3> (input-layer forward, planes, K = in_dim padded to 64)",
         4: "gemm_x3_kernel<true, false, 0> (input-layer weight grad, on-the-fly split, split-K)",
     },
     "fp32": {

@@ -315,18 +315,23 @@ struct mtsac_engine {
       tl[tl_next].batch = batch;
     }
     if (gemm_x3f_ok(p, epi, batch)) {
-      gemm_x3f(p, epi, batch, cur);
-      // the rocprof symbol: gemm_x3f_kernel<BM, EPI, C_OUT, P_OUT, MASK16, TAG>
+      const bool split = gemm_x3f(p, epi, batch, cur) > 1;
+      // the rocprof symbol: gemm_x3f_kernel<BM, EPI, C_OUT, P_OUT, MASK16, TAG, NP> (split-K launches
+      // run the raw-slab instance <208, 0, true, false, false, 0, NP> plus a finishing pass)
       const bool tagged = epi == EPI_BIAS_RELU && p.tag == 1 && p.Cp && !p.C;
-      fam_kernel[family] = std::string("gemm_x3f_kernel<208, ") + std::to_string(epi) + ", " +
-                           (p.C ? "true" : "false") + ", " + (p.Cp ? "true" : "false") + ", " +
-                           (p.mask16 ? "true" : "false") + ", " + (tagged ? "8" : "0") + ">";
+      fam_kernel[family] = split ? std::string("gemm_x3f_kernel<208, 0, true, false, false, 0, ") +
+                                       (p.np == 1 ? "1" : "3") + "> + splitk_epilogue_kernel"
+                                 : std::string("gemm_x3f_kernel<208, ") + std::to_string(epi) + ", " +
+                                       (p.C ? "true" : "false") + ", " + (p.Cp ? "true" : "false") + ", " +
+                                       (p.mask16 ? "true" : "false") + ", " + (tagged ? "8" : "0") + ", " +
+                                       (p.np == 1 ? "1" : "3") + ">";
     } else if (gemm_x3s_ok(p, epi, batch)) {
       gemm_x3s(p, epi, batch, cur);
       const bool tagged = epi == EPI_BIAS_RELU && p.tag == 1 && p.Cp && !p.C;
       fam_kernel[family] = std::string("gemm_x3s_kernel<") + std::to_string(gemm_x3s_ti(p.M, p.N, batch)) + ", " +
                            std::to_string(epi) + ", " + (p.C ? "true" : "false") + ", " + (p.Cp ? "true" : "false") +
-                           ", " + (p.mask16 ? "true" : "false") + ", " + (tagged ? "8" : "0") + ">";
+                           ", " + (p.mask16 ? "true" : "false") + ", " + (tagged ? "8" : "0") + ", " +
+                           (p.np == 1 ? "1" : "3") + ">";
     } else {
       gemm_x3p(p, epi, batch, cur);
       fam_kernel[family] = "gemm_x3p_kernel";

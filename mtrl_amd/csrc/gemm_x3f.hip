@@ -384,7 +384,7 @@ bool gemm_x3f_ok(const SplitGemmParams& p, int epi, int batch) {
          (p.C || p.Cp) && (long long)p.N * p.ldb * 2 < (1ll << 31);
 }
 
-void gemm_x3f(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
+int gemm_x3f(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
   using namespace x3fk;
   const int S = x3f_slices(p0, epi, batch);
   if (S > 1) {  // raw partial slabs [z][S][M][N] into the workspace, then the epilogue pass
@@ -406,7 +406,7 @@ void gemm_x3f(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
     SplitGemmParams f = p0;
     f.sC = p0.sC;
     splitk_finish(f, epi, S_eff, batch, st);
-    return;
+    return S_eff;
   }
   const SplitGemmParams& p = p0;
   const dim3 grid((unsigned)gemm_x3f_tiles(p.M, p.N, batch));
@@ -428,6 +428,7 @@ void gemm_x3f(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
       else launch<EPI_RELU_MASK, false, true, false>(p, grid, st);
     }
   }
+  return 1;
 }
 
 }  // namespace mtsac

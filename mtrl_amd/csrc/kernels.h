@@ -89,7 +89,7 @@ long long gemm_x3p_ws_floats(int M, int N, int K, int batch, bool kmajor);
 // row-major x row-major plane GEMM on 16x16x32 MFMA, 208 x 256 tiles (gemm_x3f.hip): forward
 // (EPI_BIAS_RELU) and data grad (EPI_RELU_MASK) when gemm_x3f_ok
 bool gemm_x3f_ok(const SplitGemmParams& p, int epi, int batch);
-void gemm_x3f(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
+int gemm_x3f(const SplitGemmParams& p, int epi, int batch, hipStream_t st);  // returns the K slices used
 int gemm_x3f_tiles(int M, int N, int batch);
 int gemm_x3f_row_tiles(int M);  // row tiles of M (the dbp partials' chunk count)
 // split-K for few rows: slices (1 = none) and workspace floats; gemm_x3f splits when the params

@@ -12,12 +12,12 @@ import sys
 
 FAMILY_KEYS = {
     "split3": {
-        # gemm_x3f_kernel<BM, EPI, C_OUT, P_OUT, MASK16, TAG>: TAG 8 = input-layer launches
-        0: ("gemm_x3f_kernel<208, 1, false, true, false, 0>", "gemm_x3f_kernel<208, 1, true, false, false, 0>",
-            "gemm_x3f_kernel<208, 1, true, true, false, 0>"),
+        # gemm_x3f_kernel<BM, EPI, C_OUT, P_OUT, MASK16, TAG, NP>: TAG 8 = input-layer launches
+        0: ("gemm_x3f_kernel<208, 1, false, true, false, 0,", "gemm_x3f_kernel<208, 1, true, false, false, 0,",
+            "gemm_x3f_kernel<208, 1, true, true, false, 0,"),
         1: ("gemm_x3f_kernel<208, 2,",),
         2: ("gemm_x3p_kernel<mtsac::x3pk::Geo<256, 256, 2, 4, 3, 16, 0>, true, true, 0,",),
-        3: ("gemm_x3f_kernel<208, 1, false, true, false, 8>",),
+        3: ("gemm_x3f_kernel<208, 1, false, true, false, 8,",),
         4: ("gemm_x3_kernel<true, false, 0>",),
     },
     "fp32": {
