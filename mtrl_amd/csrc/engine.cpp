@@ -700,6 +700,7 @@ struct mtsac_engine {
     a.eps = cfg.adam_eps;
     a.tau = cfg.tau;
     a.sc = net.sc;
+    a.np = np;
     a.p_partials = partials;
     // heads and trunk as two launches so the trunk's reduction tree does not depend on the
     // shard's head count (bitwise-identical replicated trunks and norms on every rank)

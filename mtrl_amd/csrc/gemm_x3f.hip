@@ -282,8 +282,10 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
       }
       __bf16* pp = Cp + (long long)row * p.ldcp + col;
       *reinterpret_cast<bf16x8*>(pp) = h;
-      *reinterpret_cast<bf16x8*>(pp + p.pC) = m;
-      *reinterpret_cast<bf16x8*>(pp + 2 * p.pC) = l;
+      if (NP == 3) {  // precision bf16 reads the high plane only
+        *reinterpret_cast<bf16x8*>(pp + p.pC) = m;
+        *reinterpret_cast<bf16x8*>(pp + 2 * p.pC) = l;
+      }
     }
   }
   if (p.dbp) {  // the tile's column sums: lanes l, l + 32 of every wave hold the same 8 columns

@@ -308,8 +308,10 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(SplitGemmParams p,
     }
     __bf16* cp = p.Cp + z * p.sCp + (long long)row * p.ldcp + col;
     *reinterpret_cast<bf16x4_t*>(cp) = h;
-    *reinterpret_cast<bf16x4_t*>(cp + p.pC) = m;
-    *reinterpret_cast<bf16x4_t*>(cp + 2 * p.pC) = l;
+    if (p.np != 1) {  // precision bf16 reads the high plane only
+      *reinterpret_cast<bf16x4_t*>(cp + p.pC) = m;
+      *reinterpret_cast<bf16x4_t*>(cp + 2 * p.pC) = l;
+    }
   }
 }
 

@@ -294,6 +294,7 @@ struct AdamParams {
   float* p_partials;    // sum of squares of new params per block
   int nseg;             // planes of the new params to write (offsets relative to p)
   PlaneSeg seg[MAX_PLANE_SEGS];
+  int np;               // planes the GEMMs read: 1 (precision bf16) writes only the high plane
   int nskip;            // float4 ranges [skip_b, skip_e) of p left to adam_update_tiles
   long long skip_b[MAX_PLANE_SEGS], skip_e[MAX_PLANE_SEGS];
 };

@@ -155,8 +155,10 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm,
       }
       __bf16* dst = ps.planes + e * 3 * ps.ps + k;
       *reinterpret_cast<bf16x4*>(dst) = h;
-      *reinterpret_cast<bf16x4*>(dst + ps.ps) = mm;
-      *reinterpret_cast<bf16x4*>(dst + 2 * ps.ps) = l;
+      if (a.np != 1) {
+        *reinterpret_cast<bf16x4*>(dst + ps.ps) = mm;
+        *reinterpret_cast<bf16x4*>(dst + 2 * ps.ps) = l;
+      }
     }
   }
   acc = block_sum256(acc);
@@ -241,8 +243,10 @@ __global__ __launch_bounds__(256) void adam_tiles_kernel(AdamParams a, TileParam
           }
           __bf16* dst = np_ + e * 3 * lf.nat_ps + (long long)r * lf.nat_ld + c;
           *reinterpret_cast<bf16x4_t*>(dst) = h;
-          *reinterpret_cast<bf16x4_t*>(dst + lf.nat_ps) = mm;
-          *reinterpret_cast<bf16x4_t*>(dst + 2 * lf.nat_ps) = l;
+          if (a.np != 1) {
+            *reinterpret_cast<bf16x4_t*>(dst + lf.nat_ps) = mm;
+            *reinterpret_cast<bf16x4_t*>(dst + 2 * lf.nat_ps) = l;
+          }
         }
       }
       const int lr_ = rr + 16 * j;
@@ -273,8 +277,10 @@ __global__ __launch_bounds__(256) void adam_tiles_kernel(AdamParams a, TileParam
           for (int hh = 0; hh < 2; ++hh) {
             if (k + 8 * hh >= lf.tr_ld) break;
             *reinterpret_cast<bf16x8*>(dst + 8 * hh) = h[hh];
-            *reinterpret_cast<bf16x8*>(dst + lf.tr_ps + 8 * hh) = mm[hh];
-            *reinterpret_cast<bf16x8*>(dst + 2 * lf.tr_ps + 8 * hh) = l[hh];
+            if (a.np != 1) {
+              *reinterpret_cast<bf16x8*>(dst + lf.tr_ps + 8 * hh) = mm[hh];
+              *reinterpret_cast<bf16x8*>(dst + 2 * lf.tr_ps + 8 * hh) = l[hh];
+            }
           }
         }
       }
