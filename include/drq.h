@@ -1,0 +1,87 @@
+/* drq.h -- C ABI of the MI355X DrQ-eps update engine (libmtsac.so), SURVEY.md section 8(f) row 4.
+ *
+ * Replaces, for experiments/atari.py's multi-task Atari agent, the device part of
+ *   DrQ.update / DrQ._update_inner   (mtrl/rl/algorithms/drqeps.py:268-335, 337-343):
+ *   augment (mtrl/nn/augmentation.py:101-117) of obs and next_obs, the online and target
+ *   ImpalaDQN forwards at s' (greedy a*, C51 projection of the target distribution), the online
+ *   forward + backward at s (cross entropy at the taken action), optax.adamw (lr, eps, weight
+ *   decay; no clip) and the Polyak target, with the same LogDict.
+ * The network is ImpalaDQN (mtrl/rl/networks.py:127-149): IMPALA encoder (stacks 8/16/16 x scale,
+ * 2 residual blocks each, mtrl/nn/impala.py:13-48) ++ unit-norm task embedding, LayerNorm,
+ * DistributionalDense (Dense 512 x scale, LayerNorm, ReLU, dueling adv/value over n_atoms).
+ *
+ * Conventions (as include/mtsac.h): plain pointers and sizes, negative errno on failure with
+ * drq_last_error(), the engine owns device memory, one engine per GPU, all work on its stream.
+ * Parameter vectors cross the boundary as ONE flat float array in flax ravel_pytree order (dict
+ * keys sorted at every level), the same order oracle/drq.py's param_spec() lists.
+ * The reference draws the augmentation's crop offsets and intensity factors from jax.random
+ * (threefry, not reproduced): they are inputs here.
+ */
+#ifndef MTSAC_DRQ_H
+#define MTSAC_DRQ_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct drq_config {
+  int num_tasks;    /* 26 (experiments/atari.py:31) */
+  int n_actions;    /* 18 (ALE full action set) */
+  int n_atoms;      /* 51 (ImpalaDQN.num_atoms default; the config's 101 is not passed through) */
+  int in_ch;        /* 4 stacked frames */
+  int hw;           /* 84 */
+  int scale;        /* ImpalaEncoderConfig.scale (atari.py Args.scale = 1) */
+  int embed_dim;    /* 32 */
+  int n_hidden;     /* 512 (times scale) */
+  int batch;        /* samples per update (DrQTrainingConfig.batch_size = 256) */
+  int nstep;        /* 3 */
+  float gamma, v_min, v_max, tau;                 /* 0.99, -10, 10, 0.005 */
+  float lr, b1, b2, eps, weight_decay, ln_eps;    /* 1e-4, 0.9, 0.999, 1.5e-4, 0.05, 1e-6 */
+} drq_config;
+
+typedef struct drq_engine drq_engine;
+
+/* One update's inputs (host or device pointers): observations uint8 [batch][in_ch][hw][hw]
+ * (NCHW, as the Atari buffer stores them), actions int [batch], rewards / dones float [batch]
+ * (n-step returns and terminal flags), task ids int [batch], and the augmentation draws:
+ * crop offsets int [batch][2] in [0, 8] and intensity factors float [batch] for obs and next_obs. */
+typedef struct drq_batch {
+  const unsigned char* obs;
+  const int* actions;
+  const unsigned char* next_obs;
+  const float* dones;
+  const float* rewards;
+  const int* task_ids;
+  const int* crop_obs;
+  const float* noise_obs;
+  const int* crop_next;
+  const float* noise_next;
+} drq_batch;
+
+#define DRQ_PARAMS 0
+#define DRQ_TARGET 1
+#define DRQ_ADAM_MU 2
+#define DRQ_ADAM_NU 3
+#define DRQ_GRAD 4 /* the last update's gradient (get only) */
+#define DRQ_NUM_LOGS 4 /* losses/online_logits, metrics/critic_grad_magnitude,
+                          metrics/critic_params_norm, losses/critic_loss (drqeps.py:309-335) */
+
+int drq_create(const drq_config* cfg, int device, drq_engine** out);
+void drq_destroy(drq_engine* e);
+long long drq_num_params(const drq_engine* e);
+/* which: DRQ_PARAMS / DRQ_TARGET / DRQ_ADAM_MU / DRQ_ADAM_NU (/ DRQ_GRAD for get); n = drq_num_params */
+int drq_set_params(drq_engine* e, int which, const float* flat, long long n);
+int drq_get_params(drq_engine* e, int which, float* flat, long long n);
+int drq_set_step(drq_engine* e, int adam_count);
+/* stage one batch and run one update on it (asynchronous on the engine's stream) */
+int drq_update(drq_engine* e, const drq_batch* batch);
+/* run `steps` more updates on the batch already resident on the device (benchmarks) */
+int drq_update_resident(drq_engine* e, int steps);
+int drq_get_logs(drq_engine* e, float* out /* DRQ_NUM_LOGS */);
+int drq_synchronize(drq_engine* e);
+const char* drq_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

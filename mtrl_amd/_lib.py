@@ -157,6 +157,37 @@ SIGNATURES = {
     ),
 }
 
+
+class DrqConfig(ctypes.Structure):  # include/drq.h
+    _fields_ = [(n, ctypes.c_int32) for n in ("num_tasks", "n_actions", "n_atoms", "in_ch", "hw", "scale",
+                                              "embed_dim", "n_hidden", "batch", "nstep")] + \
+               [(n, ctypes.c_float) for n in ("gamma", "v_min", "v_max", "tau", "lr", "b1", "b2", "eps",
+                                              "weight_decay", "ln_eps")]
+
+
+class DrqBatch(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("obs", "actions", "next_obs", "dones", "rewards", "task_ids",
+                                               "crop_obs", "noise_obs", "crop_next", "noise_next")]
+
+
+DRQ_PARAMS, DRQ_TARGET, DRQ_ADAM_MU, DRQ_ADAM_NU, DRQ_GRAD = 0, 1, 2, 3, 4
+DRQ_NUM_LOGS = 4
+DRQ_LOG_KEYS = ("losses/online_logits", "metrics/critic_grad_magnitude", "metrics/critic_params_norm",
+                "losses/critic_loss")
+SIGNATURES.update({
+    "drq_last_error": (ctypes.c_char_p, []),
+    "drq_create": (ctypes.c_int, [ctypes.POINTER(DrqConfig), ctypes.c_int, ctypes.POINTER(P)]),
+    "drq_destroy": (None, [P]),
+    "drq_num_params": (I64, [P]),
+    "drq_set_params": (ctypes.c_int, [P, ctypes.c_int, P, I64]),
+    "drq_get_params": (ctypes.c_int, [P, ctypes.c_int, P, I64]),
+    "drq_set_step": (ctypes.c_int, [P, ctypes.c_int]),
+    "drq_update": (ctypes.c_int, [P, ctypes.POINTER(DrqBatch)]),
+    "drq_update_resident": (ctypes.c_int, [P, ctypes.c_int]),
+    "drq_get_logs": (ctypes.c_int, [P, P]),
+    "drq_synchronize": (ctypes.c_int, [P]),
+})
+
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
 
 _lib = None

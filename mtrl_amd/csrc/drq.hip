@@ -1,0 +1,772 @@
+// drq.hip -- the DrQ-eps update path (distributional dueling DQN on an IMPALA CNN) for gfx950.
+//
+// Reference: mtrl/rl/algorithms/drqeps.py:268-335 (_update_inner), mtrl/nn/impala.py:13-48,
+// mtrl/rl/networks.py:99-149, mtrl/nn/augmentation.py:36-117, mtrl/nn/task_embedding.py:5-12.
+//
+// Shapes are tiny (3x3 convs with 4-16 channels on 84x84 -> 11x11 NHWC images, 26 games, batch
+// 256): every conv here is a direct convolution, one lane per output (or input) pixel with all of
+// that pixel's channels in registers and the 3x3 x Cin x Cout weights in LDS (read as broadcasts).
+// These passes are bound by the per-CU LDS/VALU issue of the weight broadcasts and the L2-served
+// neighbour reads, not by HBM or MFMA (Cout <= 16 leaves MFMA tiles mostly empty); the dense head
+// runs on gemm_f32 (exact fp32).  Weight gradients reduce over batch x pixels into per-block
+// partials summed in a fixed order (bitwise reproducible).
+#include <algorithm>
+
+#include "drq_kernels.h"
+
+namespace mtsac {
+namespace drq {
+
+namespace {
+
+__device__ inline float wsum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ inline float wmax(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// ------------------------------------------------------------------ augmentation
+// augment (augmentation.py:101-117) with its draws given: uint8 [B][C][H][W] -> NHWC float in
+// [-1, 1], edge pad 4 (= clamped reads), crop at (ox, oy), times the intensity factor.
+__global__ void augment_kernel(const unsigned char* __restrict__ obs, const int* __restrict__ crop,
+                               const float* __restrict__ noise, float* __restrict__ out, int B, int C, int H, int W,
+                               int pad) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long n = (long long)B * H * W * C;
+  if (i >= n) return;
+  const int c = (int)(i % C);
+  long long r = i / C;
+  const int x = (int)(r % W);
+  r /= W;
+  const int y = (int)(r % H);
+  const int b = (int)(r / H);
+  const int sy = min(max(y + crop[2 * b] - pad, 0), H - 1);
+  const int sx = min(max(x + crop[2 * b + 1] - pad, 0), W - 1);
+  const float v = (float)obs[(((long long)b * C + c) * H + sy) * W + sx];
+  out[i] = ((v / 255.0f - 0.5f) * 2.0f) * noise[b];
+}
+
+// ------------------------------------------------------------------ convolutions
+// out[b][y][x][:] = bias + sum_{dy,dx,ci} act(in[b][y+dy-1][x+dx-1][ci]) w[dy][dx][ci][:]
+// (+ res[b][y][x][:]); act = relu when RELU_IN.  One lane per output pixel.
+template <int CI, int CO, bool RELU_IN, bool ADD_RES>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ in, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, const float* __restrict__ res,
+                                                       float* __restrict__ out, int B, int H, int W) {
+  __shared__ float ws[9 * CI * CO];
+  for (int i = threadIdx.x; i < 9 * CI * CO; i += 256) ws[i] = w[i];
+  __syncthreads();
+  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (pix >= (long long)B * H * W) return;
+  const int x = (int)(pix % W), y = (int)((pix / W) % H);
+  const long long b = pix / ((long long)H * W);
+  float acc[CO];
+#pragma unroll
+  for (int co = 0; co < CO; ++co) acc[co] = bias[co];
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy) {
+    const int yy = y + dy - 1;
+    if (yy < 0 || yy >= H) continue;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const int xx = x + dx - 1;
+      if (xx < 0 || xx >= W) continue;
+      const float* ip = in + ((b * H + yy) * W + xx) * CI;
+      float v[CI];
+#pragma unroll
+      for (int c4 = 0; c4 < CI; c4 += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(ip + c4);
+        v[c4] = q.x; v[c4 + 1] = q.y; v[c4 + 2] = q.z; v[c4 + 3] = q.w;
+      }
+      const float* wt = ws + (dy * 3 + dx) * CI * CO;
+#pragma unroll
+      for (int ci = 0; ci < CI; ++ci) {
+        const float a = RELU_IN ? fmaxf(v[ci], 0.f) : v[ci];
+#pragma unroll
+        for (int co = 0; co < CO; ++co) acc[co] = fmaf(a, wt[ci * CO + co], acc[co]);
+      }
+    }
+  }
+  float* op = out + pix * CO;
+  const float* rp = ADD_RES ? res + pix * CO : nullptr;
+#pragma unroll
+  for (int c4 = 0; c4 < CO; c4 += 4) {
+    float4 o = make_float4(acc[c4], acc[c4 + 1], acc[c4 + 2], acc[c4 + 3]);
+    if (ADD_RES) {
+      const float4 r = *reinterpret_cast<const float4*>(rp + c4);
+      o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+    }
+    *reinterpret_cast<float4*>(op + c4) = o;
+  }
+}
+
+// din[b][y][x][ci] = (sum_{dy,dx,co} dout[b][y-dy+1][x-dx+1][co] w[dy][dx][ci][co]) * [mask > 0]
+// (MASK: the ReLU in front of the conv) (+ dres[b][y][x][ci]).  One lane per input pixel.
+template <int CI, int CO, bool MASK, bool ADD_RES>
+__global__ __launch_bounds__(256) void conv_bwd_data_kernel(const float* __restrict__ dout, const float* __restrict__ w,
+                                                            const float* __restrict__ mask,
+                                                            const float* __restrict__ dres, float* __restrict__ din,
+                                                            int B, int H, int W) {
+  __shared__ float ws[9 * CI * CO];
+  for (int i = threadIdx.x; i < 9 * CI * CO; i += 256) ws[i] = w[i];
+  __syncthreads();
+  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (pix >= (long long)B * H * W) return;
+  const int x = (int)(pix % W), y = (int)((pix / W) % H);
+  const long long b = pix / ((long long)H * W);
+  float acc[CI];
+#pragma unroll
+  for (int ci = 0; ci < CI; ++ci) acc[ci] = 0.f;
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy) {
+    const int yy = y - dy + 1;
+    if (yy < 0 || yy >= H) continue;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const int xx = x - dx + 1;
+      if (xx < 0 || xx >= W) continue;
+      const float* gp = dout + ((b * H + yy) * W + xx) * CO;
+      float g[CO];
+#pragma unroll
+      for (int c4 = 0; c4 < CO; c4 += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(gp + c4);
+        g[c4] = q.x; g[c4 + 1] = q.y; g[c4 + 2] = q.z; g[c4 + 3] = q.w;
+      }
+      const float* wt = ws + (dy * 3 + dx) * CI * CO;
+#pragma unroll
+      for (int ci = 0; ci < CI; ++ci) {
+        float s = acc[ci];
+#pragma unroll
+        for (int co = 0; co < CO; ++co) s = fmaf(g[co], wt[ci * CO + co], s);
+        acc[ci] = s;
+      }
+    }
+  }
+  float* op = din + pix * CI;
+#pragma unroll
+  for (int c4 = 0; c4 < CI; c4 += 4) {
+    float4 o = make_float4(acc[c4], acc[c4 + 1], acc[c4 + 2], acc[c4 + 3]);
+    if (MASK) {
+      const float4 m = *reinterpret_cast<const float4*>(mask + pix * CI + c4);
+      o.x = m.x > 0.f ? o.x : 0.f; o.y = m.y > 0.f ? o.y : 0.f;
+      o.z = m.z > 0.f ? o.z : 0.f; o.w = m.w > 0.f ? o.w : 0.f;
+    }
+    if (ADD_RES) {
+      const float4 r = *reinterpret_cast<const float4*>(dres + pix * CI + c4);
+      o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+    }
+    *reinterpret_cast<float4*>(op + c4) = o;
+  }
+}
+
+// Weight gradient partials: block g takes 64-pixel tiles g, g + G, ... (G = gridDim.x); the
+// tile's im2col rows (act applied, zero outside the image) and dout go through LDS; lane t owns
+// taps (tap * CI + ci, co) t, t + 256, ... and the bias entries co = t (< CO), summed over the
+// tile's pixels in order.  part[g][9 CI CO + CO], summed over g in order by sum_parts_kernel.
+template <int CI, int CO, bool RELU_IN>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict__ in, const float* __restrict__ dout,
+                                                         float* __restrict__ part, int B, int H, int W) {
+  constexpr int NW = 9 * CI * CO;
+  constexpr int PER = (NW + 255) / 256;
+  constexpr int TP = 64;
+  __shared__ float sin_[TP][9 * CI];
+  __shared__ float sg[TP][CO];
+  const int t = threadIdx.x;
+  float acc[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) acc[k] = 0.f;
+  float bacc = 0.f;
+  const long long npix = (long long)B * H * W;
+  for (long long p0 = (long long)blockIdx.x * TP; p0 < npix; p0 += (long long)gridDim.x * TP) {
+    __syncthreads();
+    for (int pr = t; pr < TP * 9; pr += 256) {
+      const int q = pr / 9, tap = pr - 9 * q;
+      const long long pix = p0 + q;
+      float v[CI];
+#pragma unroll
+      for (int ci = 0; ci < CI; ++ci) v[ci] = 0.f;
+      if (pix < npix) {
+        const int x = (int)(pix % W), y = (int)((pix / W) % H);
+        const long long b = pix / ((long long)H * W);
+        const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+          const float* ip = in + ((b * H + yy) * W + xx) * CI;
+#pragma unroll
+          for (int c4 = 0; c4 < CI; c4 += 4) {
+            const float4 u = *reinterpret_cast<const float4*>(ip + c4);
+            v[c4] = u.x; v[c4 + 1] = u.y; v[c4 + 2] = u.z; v[c4 + 3] = u.w;
+          }
+        }
+      }
+#pragma unroll
+      for (int ci = 0; ci < CI; ++ci) sin_[q][tap * CI + ci] = RELU_IN ? fmaxf(v[ci], 0.f) : v[ci];
+    }
+    for (int pr = t; pr < TP * CO; pr += 256) {
+      const int q = pr / CO, co = pr - CO * q;
+      const long long pix = p0 + q;
+      sg[q][co] = pix < npix ? dout[pix * CO + co] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = t + 256 * k;
+      if (e < NW) {
+        const int tc = e / CO, co = e - tc * CO;  // tc = tap * CI + ci
+        float s = acc[k];
+        for (int q = 0; q < TP; ++q) s = fmaf(sin_[q][tc], sg[q][co], s);
+        acc[k] = s;
+      }
+    }
+    if (t < CO) {
+      float s = bacc;
+      for (int q = 0; q < TP; ++q) s += sg[q][t];
+      bacc = s;
+    }
+  }
+  float* pp = part + (long long)blockIdx.x * (NW + CO);
+#pragma unroll
+  for (int k = 0; k < PER; ++k)
+    if (t + 256 * k < NW) pp[t + 256 * k] = acc[k];
+  if (t < CO) pp[NW + t] = bacc;
+}
+
+// dw[e] / db[e - nw] = sum_g part[g][e] in g order (e < n)
+__global__ void sum_parts_kernel(const float* __restrict__ part, int G, int n, float* __restrict__ dst_w,
+                                 float* __restrict__ dst_b, int nw) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  double s = 0.0;  // the partials of up to ~10^5 pixels x 9 taps: no further fp32 rounding here
+  for (int g = 0; g < G; ++g) s += (double)part[(long long)g * n + e];
+  if (e < nw) dst_w[e] = (float)s;
+  else dst_b[e - nw] = (float)s;
+}
+
+// ------------------------------------------------------------------ max pool 3x3 / 2 / SAME
+// out[b][oy][ox][c] = max over the window (lo padding, -inf outside); arg = argmax tap (0..8,
+// first in row-major order on ties -- lax.reduce_window's max has no defined tie rule for the
+// gradient; jax's select-and-scatter takes the first maximum, as here)
+__global__ void maxpool_fwd_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                   unsigned char* __restrict__ arg, int B, int H, int W, int C, int Ho, int Wo, int lo) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * Ho * Wo * C) return;
+  const int c = (int)(i % C);
+  long long r = i / C;
+  const int ox = (int)(r % Wo);
+  r /= Wo;
+  const int oy = (int)(r % Ho);
+  const long long b = r / Ho;
+  float best = -INFINITY;
+  int bi = 0;
+  for (int tap = 0; tap < 9; ++tap) {
+    const int y = 2 * oy - lo + tap / 3, x = 2 * ox - lo + tap % 3;
+    if (y < 0 || y >= H || x < 0 || x >= W) continue;
+    const float v = in[((b * H + y) * W + x) * C + c];
+    if (v > best) {
+      best = v;
+      bi = tap;
+    }
+  }
+  out[i] = best;
+  arg[i] = (unsigned char)bi;
+}
+
+// din[b][y][x][c] = sum over the windows whose argmax is (y, x) of dout (a gather: deterministic)
+__global__ void maxpool_bwd_kernel(const float* __restrict__ dout, const unsigned char* __restrict__ arg,
+                                   float* __restrict__ din, int B, int H, int W, int C, int Ho, int Wo, int lo) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * H * W * C) return;
+  const int c = (int)(i % C);
+  long long r = i / C;
+  const int x = (int)(r % W);
+  r /= W;
+  const int y = (int)(r % H);
+  const long long b = r / H;
+  float s = 0.f;
+  // windows o with 2 o - lo <= y <= 2 o - lo + 2, in order
+  const int oy0 = y + lo - 2 <= 0 ? 0 : (y + lo - 1) / 2, oy1 = min((y + lo) / 2, Ho - 1);
+  const int ox0 = x + lo - 2 <= 0 ? 0 : (x + lo - 1) / 2, ox1 = min((x + lo) / 2, Wo - 1);
+  for (int oy = oy0; oy <= oy1; ++oy) {
+    const int ty = y - (2 * oy - lo);
+    if (ty < 0 || ty > 2) continue;
+    for (int ox = ox0; ox <= ox1; ++ox) {
+      const int tx = x - (2 * ox - lo);
+      if (tx < 0 || tx > 2) continue;
+      const long long o = ((b * Ho + oy) * Wo + ox) * C + c;
+      if (arg[o] == ty * 3 + tx) s += dout[o];
+    }
+  }
+  din[i] = s;
+}
+
+// ------------------------------------------------------------------ encoder output + embedding
+// feat[b] = [relu(enc[b]) (NHWC flatten) | emb[task_b] / (|emb| + 1e-8)], row stride ldf
+__global__ void concat_kernel(const float* __restrict__ enc, int nenc, const float* __restrict__ emb, int D,
+                              const int* __restrict__ task, float* __restrict__ feat, int ldf, int B) {
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  for (int i = threadIdx.x; i < nenc; i += blockDim.x) feat[(long long)b * ldf + i] = fmaxf(enc[(long long)b * nenc + i], 0.f);
+  if (threadIdx.x < 64) {
+    const int t = task[b];
+    float s = 0.f;
+    for (int d = threadIdx.x; d < D; d += 64) s += emb[t * D + d] * emb[t * D + d];
+    s = wsum(s);
+    const float nrm = sqrtf(s) + 1e-8f;
+    for (int d = threadIdx.x; d < D; d += 64) feat[(long long)b * ldf + nenc + d] = emb[t * D + d] / nrm;
+  }
+}
+
+// ------------------------------------------------------------------ LayerNorm (flax, fast variance)
+// y = (x + xb - mu) rstd scale + bias over F columns (xb: the preceding Dense bias, may be null);
+// saves xhat (normalised) and rstd for the backward; RELU: y = max(y, 0).  One wave per row.
+template <bool RELU>
+__global__ void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ xb, int ldx, int F,
+                              const float* __restrict__ scale, const float* __restrict__ bias, float eps,
+                              float* __restrict__ y, int ldy, float* __restrict__ xhat, float* __restrict__ rstd,
+                              int B) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B) return;
+  const float* xr = x + (long long)row * ldx;
+  float s = 0.f, s2 = 0.f;
+  for (int i = lane; i < F; i += 64) {
+    const float v = xr[i] + (xb ? xb[i] : 0.f);
+    s += v;
+    s2 += v * v;
+  }
+  s = wsum(s);
+  s2 = wsum(s2);
+  const float mu = s / (float)F;
+  const float var = fmaxf(s2 / (float)F - mu * mu, 0.f);
+  const float r = 1.0f / sqrtf(var + eps);
+  for (int i = lane; i < F; i += 64) {
+    const float v = xr[i] + (xb ? xb[i] : 0.f);
+    const float h = (v - mu) * r;
+    xhat[(long long)row * F + i] = h;
+    const float o = h * scale[i] + bias[i];
+    y[(long long)row * ldy + i] = RELU ? fmaxf(o, 0.f) : o;
+  }
+  if (lane == 0) rstd[row] = r;
+}
+
+// dx = rstd (g - mean(g) - xhat mean(g xhat)), g = dy scale (dy masked by y > 0 when RELU).
+// Column partials of dscale = sum dy xhat and dbias = sum dy per block of 4 rows: part[blk][2F].
+template <bool RELU>
+__global__ void ln_bwd_kernel(const float* __restrict__ dy, int lddy, const float* __restrict__ y, int ldy,
+                              const float* __restrict__ xhat, const float* __restrict__ rstd,
+                              const float* __restrict__ scale, int F, float* __restrict__ dx, int lddx, int B) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B) return;
+  float sg = 0.f, sgx = 0.f;
+  for (int i = lane; i < F; i += 64) {
+    float d = dy[(long long)row * lddy + i];
+    if (RELU && !(y[(long long)row * ldy + i] > 0.f)) d = 0.f;
+    const float g = d * scale[i];
+    sg += g;
+    sgx += g * xhat[(long long)row * F + i];
+  }
+  sg = wsum(sg) / (float)F;
+  sgx = wsum(sgx) / (float)F;
+  const float r = rstd[row];
+  for (int i = lane; i < F; i += 64) {
+    float d = dy[(long long)row * lddy + i];
+    if (RELU && !(y[(long long)row * ldy + i] > 0.f)) d = 0.f;
+    const float g = d * scale[i];
+    dx[(long long)row * lddx + i] = r * (g - sg - xhat[(long long)row * F + i] * sgx);
+  }
+}
+
+// dscale[i] = sum_b dy xhat, dbias[i] = sum_b dy (masked like ln_bwd), rows in order per column
+template <bool RELU>
+__global__ void ln_param_grad_kernel(const float* __restrict__ dy, int lddy, const float* __restrict__ y, int ldy,
+                                     const float* __restrict__ xhat, int F, int B, float* __restrict__ dscale,
+                                     float* __restrict__ dbias, float* __restrict__ dxb) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= F) return;
+  float a = 0.f, c = 0.f;
+  for (int b = 0; b < B; ++b) {
+    float d = dy[(long long)b * lddy + i];
+    if (RELU && !(y[(long long)b * ldy + i] > 0.f)) d = 0.f;
+    a += d * xhat[(long long)b * F + i];
+    c += d;
+  }
+  dscale[i] = a;
+  dbias[i] = c;
+  (void)dxb;
+}
+
+// column sums (the Dense_0 bias grad) of x[B][ld] over F columns
+__global__ void colsum_rows_kernel(const float* __restrict__ x, int ld, int F, int B, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= F) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += x[(long long)b * ld + i];
+  out[i] = s;
+}
+
+// ------------------------------------------------------------------ dueling head + C51
+// logits[b][a][z] = (val[b][z] + bv[z]) + (adv[b][a z] + ba[a z]) - mean_a(adv + ba)[z]
+// from the combined head output hc[b][ldh] = [adv (A Z) | val (Z)] (bias hb likewise)
+__device__ inline float head_logit(const float* hc, const float* hb, int A, int Z, int a, int z, float madv) {
+  return (hc[A * Z + z] + hb[A * Z + z]) + ((hc[a * Z + z] + hb[a * Z + z]) - madv);
+}
+
+// One wave per sample: online logits at s' -> greedy a*, target distribution at a*, projected onto
+// the support (drqeps.py:273-298); m[b][Z].  NZ: atoms per lane (Z <= 64 * NZ).
+__global__ void c51_target_kernel(const float* __restrict__ hc_on, const float* __restrict__ hc_tg, int ldh,
+                                  const float* __restrict__ hb_on, const float* __restrict__ hb_tg, int A, int Z,
+                                  const float* __restrict__ rew, const float* __restrict__ done, float gamma_n,
+                                  float vmin, float vmax, float* __restrict__ m, int* __restrict__ a_next, int B) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= B) return;
+  const float* on = hc_on + (long long)b * ldh;
+  const float* tg = hc_tg + (long long)b * ldh;
+  const bool zl = lane < Z;
+  const float dz = (vmax - vmin) / (float)(Z - 1);
+  const float sup = vmin + dz * (float)lane;  // jnp.linspace: start + step * i
+  // mean over actions of the advantage (per atom), online and target
+  float mon = 0.f, mtg = 0.f;
+  if (zl) {
+    for (int a = 0; a < A; ++a) {
+      mon += on[a * Z + lane] + hb_on[a * Z + lane];
+      mtg += tg[a * Z + lane] + hb_tg[a * Z + lane];
+    }
+    mon /= (float)A;
+    mtg /= (float)A;
+  }
+  float bestq = -INFINITY;
+  int besta = 0;
+  for (int a = 0; a < A; ++a) {
+    const float l = zl ? head_logit(on, hb_on, A, Z, a, lane, mon) : -INFINITY;
+    const float mx = wmax(l);
+    const float e = zl ? expf(l - mx) : 0.f;
+    const float se = wsum(e);
+    const float q = wsum(zl ? (e / se) * sup : 0.f);
+    if (q > bestq) {  // argmax: first maximum
+      bestq = q;
+      besta = a;
+    }
+  }
+  const float lt = zl ? head_logit(tg, hb_tg, A, Z, besta, lane, mtg) : -INFINITY;
+  const float mx = wmax(lt);
+  const float e = zl ? expf(lt - mx) : 0.f;
+  const float p = e / wsum(e);
+  float tz = rew[b] + gamma_n * (1.0f - done[b]) * sup;
+  tz = fminf(fmaxf(tz, vmin), vmax);
+  const float bb = (tz - vmin) / dz;
+  const float lf = floorf(bb), uf = ceilf(bb);
+  const int li = (int)lf, ui = (int)uf;
+  // m[l] += p (u - b); m[u] += p (b - l): gathered per destination atom, in source order
+  float acc = 0.f;
+  for (int j = 0; j < Z; ++j) {
+    const int lj = __shfl(li, j), uj = __shfl(ui, j);
+    const float pj = __shfl(p, j), bj = __shfl(bb, j), lfj = __shfl(lf, j), ufj = __shfl(uf, j);
+    if (lj == lane) acc += pj * (ufj - bj);
+    if (uj == lane) acc += pj * (bj - lfj);
+  }
+  if (zl) m[(long long)b * Z + lane] = acc;
+  if (lane == 0) a_next[b] = besta;
+}
+
+// Cross entropy at the taken action and its gradient (drqeps.py:300-309): per sample
+// loss_b = -sum_z m log_softmax(logit[act]); d logit[act] = (softmax sum(m) - m) / B, then through
+// the dueling combination: d val = d logit[act], d adv[a] = d logit[act] (delta(a, act) - 1 / A).
+// dh[b][ldh] = [d adv | d val]; per-sample loss and mean logit into small arrays.
+__global__ void c51_loss_kernel(const float* __restrict__ hc, int ldh, const float* __restrict__ hb, int A, int Z,
+                                const int* __restrict__ act, const float* __restrict__ m, float inv_b,
+                                float* __restrict__ dh, float* __restrict__ loss_b, float* __restrict__ logit_b,
+                                int B) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= B) return;
+  const float* h = hc + (long long)b * ldh;
+  const bool zl = lane < Z;
+  float madv = 0.f;
+  if (zl) {
+    for (int a = 0; a < A; ++a) madv += h[a * Z + lane] + hb[a * Z + lane];
+    madv /= (float)A;
+  }
+  const int ab = act[b];
+  const float l = zl ? head_logit(h, hb, A, Z, ab, lane, madv) : -INFINITY;
+  const float mx = wmax(l);
+  const float e = zl ? expf(l - mx) : 0.f;
+  const float se = wsum(e);
+  const float lse = mx + logf(se);
+  const float mz = zl ? m[(long long)b * Z + lane] : 0.f;
+  const float lossb = -wsum(zl ? mz * (l - lse) : 0.f);
+  const float msum = wsum(mz);
+  const float g = zl ? ((e / se) * msum - mz) * inv_b : 0.f;
+  float* d = dh + (long long)b * ldh;
+  if (zl) {
+    d[A * Z + lane] = g;
+    for (int a = 0; a < A; ++a) d[a * Z + lane] = g * ((a == ab ? 1.0f : 0.0f) - 1.0f / (float)A);
+  }
+  const float ls = wsum(zl ? l : 0.f);
+  if (lane == 0) {
+    loss_b[b] = lossb;
+    logit_b[b] = ls;
+  }
+}
+
+// embedding backward: dE[t] = sum over the task's rows of d(e / (|e| + 1e-8)) / de (rows in order)
+__global__ void embed_bwd_kernel(const float* __restrict__ dfeat, int ldf, int off, const float* __restrict__ emb,
+                                 int D, const int* __restrict__ task, int B, float* __restrict__ demb) {
+  const int t = blockIdx.x, lane = threadIdx.x;
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) s += emb[t * D + d] * emb[t * D + d];
+  s = wsum(s);
+  const float n = sqrtf(s), ne = n + 1e-8f;
+  for (int d0 = 0; d0 < D; d0 += 64) {
+    const int d = d0 + lane;
+    float acc = 0.f;
+    for (int b = 0; b < B; ++b) {
+      if (task[b] != t) continue;
+      const float* g = dfeat + (long long)b * ldf + off;
+      float wg = 0.f;
+      for (int k = lane; k < D; k += 64) wg += emb[t * D + k] * g[k];
+      wg = wsum(wg);
+      if (d < D) acc += g[d] / ne - emb[t * D + d] * wg / (n * ne * ne);
+    }
+    if (d < D) demb[t * D + d] = acc;
+  }
+}
+
+// d enc = d feat[:, :nenc] * [enc > 0]   (the encoder's final ReLU)
+__global__ void enc_grad_kernel(const float* __restrict__ dfeat, int ldf, const float* __restrict__ enc, int nenc,
+                                float* __restrict__ denc, int B) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * nenc) return;
+  const long long b = i / nenc;
+  const int k = (int)(i - b * nenc);
+  denc[i] = enc[i] > 0.f ? dfeat[b * ldf + k] : 0.f;
+}
+
+// ------------------------------------------------------------------ AdamW + Polyak + norms
+// optax.adamw (weight decay on every leaf, no clip); target = tau p + (1 - tau) target;
+// sumsq partials of g and of the PRE-update p (the logged norms)
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float* __restrict__ mu,
+                                                    float* __restrict__ nu, const float* __restrict__ g,
+                                                    float* __restrict__ tgt, long long n, float lr, float b1,
+                                                    float b2, float eps, float wd, float tau, int count,
+                                                    float* __restrict__ part) {
+  const float bc1 = 1.0f - powf(b1, (float)count), bc2 = 1.0f - powf(b2, (float)count);
+  float sg = 0.f, sp = 0.f;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const float gi = g[i], pi = p[i];
+    sg += gi * gi;
+    sp += pi * pi;
+    const float m = (1.0f - b1) * gi + b1 * mu[i];
+    const float v = (1.0f - b2) * (gi * gi) + b2 * nu[i];
+    mu[i] = m;
+    nu[i] = v;
+    const float u = (m / bc1) / (sqrtf(v / bc2) + eps) + wd * pi;
+    const float np = pi + (-lr) * u;
+    p[i] = np;
+    tgt[i] = tau * np + (1.0f - tau) * tgt[i];
+  }
+  __shared__ float red[2][4];
+  sg = wsum(sg);
+  sp = wsum(sp);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = sg;
+    red[1][threadIdx.x >> 6] = sp;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    part[2 * blockIdx.x + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  }
+}
+
+// logs: [mean online logit, |g|, |p_pre|, loss]
+__global__ void drq_logs_kernel(const float* __restrict__ part, int G, const float* __restrict__ loss_b,
+                                const float* __restrict__ logit_b, int B, int Z, float* __restrict__ logs) {
+  __shared__ double red[4][4];
+  double a = 0, b = 0, c = 0, d = 0;
+  for (int i = threadIdx.x; i < G; i += 256) {
+    a += part[2 * i];
+    b += part[2 * i + 1];
+  }
+  for (int i = threadIdx.x; i < B; i += 256) {
+    c += loss_b[i];
+    d += logit_b[i];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o);
+    b += __shfl_xor(b, o);
+    c += __shfl_xor(c, o);
+    d += __shfl_xor(d, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = a;
+    red[1][threadIdx.x >> 6] = b;
+    red[2][threadIdx.x >> 6] = c;
+    red[3][threadIdx.x >> 6] = d;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double r[4];
+    for (int k = 0; k < 4; ++k) r[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
+    logs[0] = (float)(r[3] / ((double)B * Z));
+    logs[1] = (float)sqrt(r[0]);
+    logs[2] = (float)sqrt(r[1]);
+    logs[3] = (float)(r[2] / B);
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ launchers
+static unsigned blocks(long long n, int t = 256) { return (unsigned)((n + t - 1) / t); }
+
+void augment(const unsigned char* obs, const int* crop, const float* noise, float* out, int B, int C, int H, int W,
+             int pad, hipStream_t st) {
+  const long long n = (long long)B * C * H * W;
+  hipLaunchKernelGGL(augment_kernel, dim3(blocks(n)), dim3(256), 0, st, obs, crop, noise, out, B, C, H, W, pad);
+}
+
+#define CONV_CASES(M)                   \
+  M(4, 8) M(8, 8) M(8, 16) M(16, 16)
+
+bool conv_supported(int ci, int co) {
+#define C_OK(a, b) if (ci == a && co == b) return true;
+  CONV_CASES(C_OK)
+#undef C_OK
+  return false;
+}
+
+void conv_fwd(const float* in, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
+              int ci, int co, bool relu_in, hipStream_t st) {
+  const dim3 g(blocks((long long)B * H * W)), t(256);
+#define C_FWD(a, b)                                                                                                  \
+  if (ci == a && co == b) {                                                                                          \
+    if (relu_in && res) hipLaunchKernelGGL((conv_fwd_kernel<a, b, true, true>), g, t, 0, st, in, w, bias, res, out, B, H, W); \
+    else if (relu_in) hipLaunchKernelGGL((conv_fwd_kernel<a, b, true, false>), g, t, 0, st, in, w, bias, res, out, B, H, W); \
+    else if (res) hipLaunchKernelGGL((conv_fwd_kernel<a, b, false, true>), g, t, 0, st, in, w, bias, res, out, B, H, W); \
+    else hipLaunchKernelGGL((conv_fwd_kernel<a, b, false, false>), g, t, 0, st, in, w, bias, res, out, B, H, W);        \
+    return;                                                                                                          \
+  }
+  CONV_CASES(C_FWD)
+#undef C_FWD
+}
+
+void conv_bwd_data(const float* dout, const float* w, const float* mask, const float* dres, float* din, int B, int H,
+                   int W, int ci, int co, hipStream_t st) {
+  const dim3 g(blocks((long long)B * H * W)), t(256);
+#define C_BD(a, b)                                                                                                   \
+  if (ci == a && co == b) {                                                                                          \
+    if (mask && dres) hipLaunchKernelGGL((conv_bwd_data_kernel<a, b, true, true>), g, t, 0, st, dout, w, mask, dres, din, B, H, W); \
+    else if (mask) hipLaunchKernelGGL((conv_bwd_data_kernel<a, b, true, false>), g, t, 0, st, dout, w, mask, dres, din, B, H, W); \
+    else if (dres) hipLaunchKernelGGL((conv_bwd_data_kernel<a, b, false, true>), g, t, 0, st, dout, w, mask, dres, din, B, H, W); \
+    else hipLaunchKernelGGL((conv_bwd_data_kernel<a, b, false, false>), g, t, 0, st, dout, w, mask, dres, din, B, H, W); \
+    return;                                                                                                          \
+  }
+  CONV_CASES(C_BD)
+#undef C_BD
+}
+
+int conv_wgrad_blocks(long long npix) { return (int)std::min<long long>(512, std::max<long long>(1, (npix + 63) / 64)); }
+
+void conv_wgrad(const float* in, const float* dout, float* part, float* dw, float* db, int B, int H, int W, int ci,
+                int co, bool relu_in, hipStream_t st) {
+  const int G = conv_wgrad_blocks((long long)B * H * W);
+#define C_WG(a, b)                                                                                             \
+  if (ci == a && co == b) {                                                                                    \
+    if (relu_in) hipLaunchKernelGGL((conv_wgrad_kernel<a, b, true>), dim3(G), dim3(256), 0, st, in, dout, part, B, H, W); \
+    else hipLaunchKernelGGL((conv_wgrad_kernel<a, b, false>), dim3(G), dim3(256), 0, st, in, dout, part, B, H, W);        \
+  }
+  CONV_CASES(C_WG)
+#undef C_WG
+  const int nw = 9 * ci * co, n = nw + co;
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(blocks(n)), dim3(256), 0, st, part, G, n, dw, db, nw);
+}
+
+void maxpool_fwd(const float* in, float* out, unsigned char* arg, int B, int H, int W, int C, hipStream_t st) {
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  const int lo = std::max((Ho - 1) * 2 + 3 - H, 0) / 2;
+  const long long n = (long long)B * Ho * Wo * C;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(blocks(n)), dim3(256), 0, st, in, out, arg, B, H, W, C, Ho, Wo, lo);
+}
+
+void maxpool_bwd(const float* dout, const unsigned char* arg, float* din, int B, int H, int W, int C, hipStream_t st) {
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  const int lo = std::max((Ho - 1) * 2 + 3 - H, 0) / 2;
+  const long long n = (long long)B * H * W * C;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(blocks(n)), dim3(256), 0, st, dout, arg, din, B, H, W, C, Ho, Wo, lo);
+}
+
+void concat_feat(const float* enc, int nenc, const float* emb, int D, const int* task, float* feat, int ldf, int B,
+                 hipStream_t st) {
+  hipLaunchKernelGGL(concat_kernel, dim3(B), dim3(256), 0, st, enc, nenc, emb, D, task, feat, ldf, B);
+}
+
+void ln_fwd(const float* x, const float* xb, int ldx, int F, const float* scale, const float* bias, float eps,
+            float* y, int ldy, float* xhat, float* rstd, int B, bool relu, hipStream_t st) {
+  if (relu)
+    hipLaunchKernelGGL(ln_fwd_kernel<true>, dim3((B + 3) / 4), dim3(256), 0, st, x, xb, ldx, F, scale, bias, eps, y, ldy,
+                       xhat, rstd, B);
+  else
+    hipLaunchKernelGGL(ln_fwd_kernel<false>, dim3((B + 3) / 4), dim3(256), 0, st, x, xb, ldx, F, scale, bias, eps, y,
+                       ldy, xhat, rstd, B);
+}
+
+void ln_bwd(const float* dy, int lddy, const float* y, int ldy, const float* xhat, const float* rstd,
+            const float* scale, int F, float* dx, int lddx, float* dscale, float* dbias, int B, bool relu,
+            hipStream_t st) {
+  if (relu) {
+    hipLaunchKernelGGL(ln_bwd_kernel<true>, dim3((B + 3) / 4), dim3(256), 0, st, dy, lddy, y, ldy, xhat, rstd, scale, F,
+                       dx, lddx, B);
+    hipLaunchKernelGGL(ln_param_grad_kernel<true>, dim3(blocks(F)), dim3(256), 0, st, dy, lddy, y, ldy, xhat, F, B,
+                       dscale, dbias, nullptr);
+  } else {
+    hipLaunchKernelGGL(ln_bwd_kernel<false>, dim3((B + 3) / 4), dim3(256), 0, st, dy, lddy, y, ldy, xhat, rstd, scale,
+                       F, dx, lddx, B);
+    hipLaunchKernelGGL(ln_param_grad_kernel<false>, dim3(blocks(F)), dim3(256), 0, st, dy, lddy, y, ldy, xhat, F, B,
+                       dscale, dbias, nullptr);
+  }
+}
+
+void colsum_rows(const float* x, int ld, int F, int B, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(colsum_rows_kernel, dim3(blocks(F)), dim3(256), 0, st, x, ld, F, B, out);
+}
+
+void c51_target(const float* hc_on, const float* hc_tg, int ldh, const float* hb_on, const float* hb_tg, int A, int Z,
+                const float* rew, const float* done, float gamma_n, float vmin, float vmax, float* m, int* a_next,
+                int B, hipStream_t st) {
+  hipLaunchKernelGGL(c51_target_kernel, dim3((B + 3) / 4), dim3(256), 0, st, hc_on, hc_tg, ldh, hb_on, hb_tg, A, Z, rew,
+                     done, gamma_n, vmin, vmax, m, a_next, B);
+}
+
+void c51_loss(const float* hc, int ldh, const float* hb, int A, int Z, const int* act, const float* m, float* dh,
+              float* loss_b, float* logit_b, int B, hipStream_t st) {
+  hipLaunchKernelGGL(c51_loss_kernel, dim3((B + 3) / 4), dim3(256), 0, st, hc, ldh, hb, A, Z, act, m, 1.0f / (float)B,
+                     dh, loss_b, logit_b, B);
+}
+
+void embed_bwd(const float* dfeat, int ldf, int off, const float* emb, int D, const int* task, int B, int T,
+               float* demb, hipStream_t st) {
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(T), dim3(64), 0, st, dfeat, ldf, off, emb, D, task, B, demb);
+}
+
+void enc_grad(const float* dfeat, int ldf, const float* enc, int nenc, float* denc, int B, hipStream_t st) {
+  hipLaunchKernelGGL(enc_grad_kernel, dim3(blocks((long long)B * nenc)), dim3(256), 0, st, dfeat, ldf, enc, nenc, denc,
+                     B);
+}
+
+int adamw(float* p, float* mu, float* nu, const float* g, float* tgt, long long n, float lr, float b1, float b2,
+          float eps, float wd, float tau, int count, float* part, int max_blocks, hipStream_t st) {
+  const int G = (int)std::min<long long>(max_blocks, std::max<long long>(1, (n + 255) / 256));
+  hipLaunchKernelGGL(adamw_kernel, dim3(G), dim3(256), 0, st, p, mu, nu, g, tgt, n, lr, b1, b2, eps, wd, tau, count,
+                     part);
+  return G;
+}
+
+void drq_logs(const float* part, int G, const float* loss_b, const float* logit_b, int B, int Z, float* logs,
+              hipStream_t st) {
+  hipLaunchKernelGGL(drq_logs_kernel, dim3(1), dim3(256), 0, st, part, G, loss_b, logit_b, B, Z, logs);
+}
+
+}  // namespace drq
+}  // namespace mtsac

@@ -1,0 +1,440 @@
+// drq_engine.cpp -- the DrQ-eps update engine behind include/drq.h.
+//
+// One update (DrQ.update + _update_inner, mtrl/rl/algorithms/drqeps.py:268-343) on the engine's
+// stream: augment obs / next_obs; online and target forwards at s' -> greedy action and the C51
+// target m; the online forward at s saving its activations; cross entropy at the taken action;
+// the backward (dueling head -> LayerNorms -> embedding and the IMPALA stacks in reverse); AdamW,
+// Polyak, logs.  Dense layers run on gemm_f32 (exact fp32), everything else on drq.hip.
+//
+// Parameters live in an internal layout (each leaf 256-B aligned; Dense_1 (advantage) and Dense_2
+// (value) side by side as one [H][A Z + Z (+pad)] matrix so the head is one GEMM); set/get
+// translate from / to the flax ravel order of oracle/drq.py:param_spec().
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/drq.h"
+#include "drq_kernels.h"
+#include "kernels.h"
+
+using namespace mtsac;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int rc, const std::string& msg) {
+  g_err = msg;
+  return rc;
+}
+
+long long al(long long x) { return (x + 63) / 64 * 64; }
+
+struct Stack {
+  int hin, ci, co, ho;
+  long long cb[5], cw[5];  // bias / kernel offsets of Conv_0..Conv_4 (internal layout)
+  // saved activations of the online pass at s (stack 0's input: the augmented obs, xin_own)
+  float* xin_own = nullptr;
+  float* conv0 = nullptr;  // [B][hin][hin][co] pre-pool
+  unsigned char* arg = nullptr;
+  float* c[3] = {};        // block inputs / output, [B][ho][ho][co]
+  float* r[2] = {};        // residual blocks' inner pre-activations
+};
+
+}  // namespace
+
+struct drq_engine {
+  drq_config cfg{};
+  hipStream_t st = nullptr;
+  int B = 0, A = 0, Z = 0, T = 0, D = 0, H = 0, F = 0, NENC = 0, NC = 0, count = 0;
+  float gamma_n = 0.f;
+  Stack stk[3];
+  long long off_emb = 0, off_ln1b = 0, off_ln1s = 0, off_w0 = 0, off_b0 = 0, off_ln2b = 0, off_ln2s = 0, off_wc = 0,
+            off_bc = 0, n_int = 0, n_flax = 0;
+  // flax order -> internal: (flax offset, internal offset, count, row stride in the internal
+  // matrix (0 = contiguous), rows)
+  struct Map {
+    long long f, i, n, ld, rows;
+  };
+  std::vector<Map> map;
+  float *p = nullptr, *g = nullptr, *mu = nullptr, *nu = nullptr, *tgt = nullptr;
+  // inputs
+  unsigned char *obs_u8 = nullptr, *nobs_u8 = nullptr;
+  int *act = nullptr, *task = nullptr, *crop_o = nullptr, *crop_n = nullptr, *a_next = nullptr;
+  float *rew = nullptr, *done = nullptr, *noise_o = nullptr, *noise_n = nullptr;
+  float* nobs = nullptr;  // augmented next_obs
+  // head activations
+  float *feat = nullptr, *xhat1 = nullptr, *rstd1 = nullptr, *ln1 = nullptr, *z1 = nullptr, *xhat2 = nullptr,
+        *rstd2 = nullptr, *h2 = nullptr, *hc = nullptr, *hc_on = nullptr, *hc_tg = nullptr, *m = nullptr;
+  // backward
+  float *dhc = nullptr, *dh2 = nullptr, *dz1 = nullptr, *dln1 = nullptr, *dfeat = nullptr;
+  float *ga = nullptr, *gb = nullptr, *gc = nullptr;  // conv activation grads (largest tensor)
+  float *wpart = nullptr, *ws = nullptr, *part = nullptr, *loss_b = nullptr, *logit_b = nullptr, *logs = nullptr;
+  long long ws_floats = 0;
+  std::vector<void*> allocs;
+
+  template <class T_>
+  int alloc(T_** ptr, long long n) {
+    void* q = nullptr;
+    if (hipMalloc(&q, sizeof(T_) * (size_t)std::max(n, 1LL)) != hipSuccess) return fail(-12, "hipMalloc failed");
+    if (hipMemsetAsync(q, 0, sizeof(T_) * (size_t)std::max(n, 1LL), st) != hipSuccess) return fail(-5, "memset");
+    allocs.push_back(q);
+    *ptr = static_cast<T_*>(q);
+    return 0;
+  }
+
+  // ------------------------------------------------------------------ forward
+  // ImpalaDQN at params P on augmented images X -> combined head output out[B][NC] (no bias);
+  // the saved activations of the backward are written in every pass (the s pass runs last)
+  void forward(const float* P, const float* X, float* out) {
+    const float* x = X;
+    for (int s = 0; s < 3; ++s) {
+      Stack& k = stk[s];
+      drq::conv_fwd(x, P + k.cw[0], P + k.cb[0], nullptr, k.conv0, B, k.hin, k.hin, k.ci, k.co, false, st);
+      drq::maxpool_fwd(k.conv0, k.c[0], k.arg, B, k.hin, k.hin, k.co, st);
+      for (int b = 0; b < cfg_blocks(); ++b) {
+        drq::conv_fwd(k.c[b], P + k.cw[1 + 2 * b], P + k.cb[1 + 2 * b], nullptr, k.r[b], B, k.ho, k.ho, k.co, k.co,
+                      true, st);
+        drq::conv_fwd(k.r[b], P + k.cw[2 + 2 * b], P + k.cb[2 + 2 * b], k.c[b], k.c[b + 1], B, k.ho, k.ho, k.co, k.co,
+                      true, st);
+      }
+      x = k.c[2];
+    }
+    drq::concat_feat(stk[2].c[2], NENC, P + off_emb, D, task, feat, F, B, st);
+    drq::ln_fwd(feat, nullptr, F, F, P + off_ln1s, P + off_ln1b, cfg.ln_eps, ln1, F, xhat1, rstd1, B, false, st);
+    GemmParams gp{};
+    gp.A = ln1; gp.lda = F;
+    gp.B = P + off_w0; gp.ldb = H;
+    gp.C = z1; gp.ldc = H;
+    gp.M = B; gp.N = H; gp.K = F;
+    gemm_f32(gp, GEMM_NN, EPI_STORE, 1, st);
+    drq::ln_fwd(z1, P + off_b0, H, H, P + off_ln2s, P + off_ln2b, cfg.ln_eps, h2, H, xhat2, rstd2, B, true, st);
+    GemmParams gh{};
+    gh.A = h2; gh.lda = H;
+    gh.B = P + off_wc; gh.ldb = NC;
+    gh.C = out; gh.ldc = NC;
+    gh.M = B; gh.N = NC; gh.K = H;
+    gemm_f32(gh, GEMM_NN, EPI_STORE, 1, st);
+  }
+  int cfg_blocks() const { return 2; }
+
+  void wgrad_gemm(const float* Aop, int lda, const float* Bop, int ldb, float* C, float* db, int M, int N) {
+    GemmParams gp{};
+    gp.A = Aop; gp.lda = lda;  // [K = B][M]
+    gp.B = Bop; gp.ldb = ldb;  // [K = B][N]
+    gp.C = C; gp.ldc = N;
+    gp.db = db;
+    gp.M = M; gp.N = N; gp.K = B;
+    gp.splits = gemm_splits(M, N, B, 1);
+    gp.ws = ws;
+    gemm_f32(gp, GEMM_TN, EPI_STORE, 1, st);
+  }
+
+  // ------------------------------------------------------------------ one update on the staged batch
+  void step() {
+    const int C0 = cfg.in_ch;
+    drq::augment(nobs_u8, crop_n, noise_n, nobs, B, C0, cfg.hw, cfg.hw, 4, st);
+    drq::augment(obs_u8, crop_o, noise_o, stk[0].xin_own, B, C0, cfg.hw, cfg.hw, 4, st);
+    forward(p, nobs, hc_on);
+    forward(tgt, nobs, hc_tg);
+    drq::c51_target(hc_on, hc_tg, NC, p + off_bc, tgt + off_bc, A, Z, rew, done, gamma_n, cfg.v_min, cfg.v_max, m,
+                    a_next, B, st);
+    forward(p, stk[0].xin_own, hc);
+    drq::c51_loss(hc, NC, p + off_bc, A, Z, act, m, dhc, loss_b, logit_b, B, st);
+    // ---- head backward
+    wgrad_gemm(h2, H, dhc, NC, g + off_wc, g + off_bc, H, NC);
+    {
+      GemmParams gp{};
+      gp.A = dhc; gp.lda = NC;
+      gp.B = p + off_wc; gp.ldb = NC;  // [N = H][K = NC]
+      gp.C = dh2; gp.ldc = H;
+      gp.M = B; gp.N = H; gp.K = NC;
+      gemm_f32(gp, GEMM_NT, EPI_STORE, 1, st);
+    }
+    drq::ln_bwd(dh2, H, h2, H, xhat2, rstd2, p + off_ln2s, H, dz1, H, g + off_ln2s, g + off_ln2b, B, true, st);
+    drq::colsum_rows(dz1, H, H, B, g + off_b0, st);
+    wgrad_gemm(ln1, F, dz1, H, g + off_w0, nullptr, F, H);
+    {
+      GemmParams gp{};
+      gp.A = dz1; gp.lda = H;
+      gp.B = p + off_w0; gp.ldb = H;  // [N = F][K = H]
+      gp.C = dln1; gp.ldc = F;
+      gp.M = B; gp.N = F; gp.K = H;
+      gemm_f32(gp, GEMM_NT, EPI_STORE, 1, st);
+    }
+    drq::ln_bwd(dln1, F, nullptr, 0, xhat1, rstd1, p + off_ln1s, F, dfeat, F, g + off_ln1s, g + off_ln1b, B, false, st);
+    drq::embed_bwd(dfeat, F, NENC, p + off_emb, D, task, B, T, g + off_emb, st);
+    // ---- encoder backward, stacks in reverse
+    // dc: grad wrt the current block / stack output; dr: scratch; dn: the grad being produced
+    float *dc = ga, *dr = gb, *dn = gc;
+    drq::enc_grad(dfeat, F, stk[2].c[2], NENC, dc, B, st);
+    for (int s = 2; s >= 0; --s) {
+      Stack& k = stk[s];
+      for (int b = 1; b >= 0; --b) {  // c[b + 1] = conv_k2(relu(r[b])) + c[b], r[b] = conv_k1(relu(c[b]))
+        const int k2 = 2 + 2 * b, k1 = 1 + 2 * b;
+        drq::conv_wgrad(k.r[b], dc, wpart, g + k.cw[k2], g + k.cb[k2], B, k.ho, k.ho, k.co, k.co, true, st);
+        drq::conv_bwd_data(dc, p + k.cw[k2], k.r[b], nullptr, dr, B, k.ho, k.ho, k.co, k.co, st);
+        drq::conv_wgrad(k.c[b], dr, wpart, g + k.cw[k1], g + k.cb[k1], B, k.ho, k.ho, k.co, k.co, true, st);
+        drq::conv_bwd_data(dr, p + k.cw[k1], k.c[b], dc, dn, B, k.ho, k.ho, k.co, k.co, st);
+        std::swap(dc, dn);
+      }
+      drq::maxpool_bwd(dc, k.arg, dn, B, k.hin, k.hin, k.co, st);  // dn: grad wrt conv0's output
+      const float* xin = s == 0 ? stk[0].xin_own : stk[s - 1].c[2];
+      drq::conv_wgrad(xin, dn, wpart, g + k.cw[0], g + k.cb[0], B, k.hin, k.hin, k.ci, k.co, false, st);
+      if (s > 0) drq::conv_bwd_data(dn, p + k.cw[0], nullptr, nullptr, dc, B, k.hin, k.hin, k.ci, k.co, st);
+    }
+    // ---- optimizer
+    ++count;
+    const int G = drq::adamw(p, mu, nu, g, tgt, n_int, cfg.lr, cfg.b1, cfg.b2, cfg.eps, cfg.weight_decay, cfg.tau,
+                             count, part, 1024, st);
+    drq::drq_logs(part, G, loss_b, logit_b, B, Z, logs, st);
+  }
+};
+
+namespace {
+
+int copy_in(void* dst, const void* src, size_t bytes, hipStream_t st) {
+  if (!src) return fail(-22, "null input pointer");
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st) == hipSuccess ? 0 : fail(-5, "hipMemcpyAsync");
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* drq_last_error(void) { return g_err.c_str(); }
+
+int drq_create(const drq_config* c, int device, drq_engine** out) {
+  if (!c || !out) return fail(-22, "null argument");
+  *out = nullptr;
+  if (c->num_tasks < 1 || c->n_actions < 1 || c->n_atoms < 2 || c->n_atoms > 64 || c->batch < 1 || c->hw < 4 ||
+      c->scale < 1 || c->embed_dim < 1 || c->embed_dim > 64 || c->n_hidden < 4)
+    return fail(-22, "bad drq_config");
+  if (hipSetDevice(device) != hipSuccess) return fail(-19, "hipSetDevice failed");
+  drq_engine* e = new drq_engine();
+  e->cfg = *c;
+  auto bad = [&](int rc) {
+    drq_destroy(e);
+    return rc;
+  };
+  if (hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) != hipSuccess) return bad(fail(-5, "stream"));
+  const int B = e->B = c->batch;
+  e->A = c->n_actions;
+  e->Z = c->n_atoms;
+  e->T = c->num_tasks;
+  e->D = c->embed_dim;
+  e->H = c->n_hidden * c->scale;
+  e->gamma_n = (float)std::pow((double)c->gamma, (double)c->nstep);
+  // layout: stacks
+  const int chans[3] = {8 * c->scale, 16 * c->scale, 16 * c->scale};
+  int h = c->hw, ci = c->in_ch;
+  long long o = 0;
+  for (int s = 0; s < 3; ++s) {
+    Stack& k = e->stk[s];
+    k.hin = h;
+    k.ci = ci;
+    k.co = chans[s];
+    k.ho = (h + 1) / 2;
+    if (!drq::conv_supported(k.ci, k.co) || !drq::conv_supported(k.co, k.co)) {
+      delete e;
+      return fail(-95, "conv channel counts not instantiated (scale 1, in_ch 4)");
+    }
+    for (int q = 0; q < 5; ++q) {
+      const int cin = q == 0 ? k.ci : k.co;
+      k.cb[q] = o;
+      o = al(o + k.co);
+      k.cw[q] = o;
+      o = al(o + 9LL * cin * k.co);
+    }
+    h = k.ho;
+    ci = k.co;
+  }
+  e->NENC = e->stk[2].ho * e->stk[2].ho * e->stk[2].co;
+  e->F = e->NENC + e->D;
+  if (e->F % 4 != 0 || e->H % 4 != 0) {
+    delete e;
+    return fail(-95, "feature / hidden widths must be multiples of 4");
+  }
+  e->NC = (int)((e->A * e->Z + e->Z + 3) / 4 * 4);
+  const int F = e->F, H = e->H, NC = e->NC, A = e->A, Z = e->Z;
+  e->off_emb = o; o = al(o + (long long)e->T * e->D);
+  e->off_ln1b = o; o = al(o + F);
+  e->off_ln1s = o; o = al(o + F);
+  e->off_w0 = o; o = al(o + (long long)F * H);
+  e->off_b0 = o; o = al(o + H);
+  e->off_ln2b = o; o = al(o + H);
+  e->off_ln2s = o; o = al(o + H);
+  e->off_wc = o; o = al(o + (long long)H * NC);
+  e->off_bc = o; o = al(o + NC);
+  e->n_int = o;
+  // flax ravel order (oracle/drq.py:param_spec)
+  long long f = 0;
+  auto add = [&](long long i, long long n, long long ld = 0, long long rows = 1) {
+    e->map.push_back({f, i, n, ld, rows});
+    f += n * rows;
+  };
+  add(e->off_b0, H);                       // Dense_0/bias
+  add(e->off_w0, (long long)F * H);        // Dense_0/kernel
+  add(e->off_bc, (long long)A * Z);        // Dense_1/bias (advantage)
+  add(e->off_wc, (long long)A * Z, NC, H); // Dense_1/kernel rows
+  add(e->off_bc + (long long)A * Z, Z);    // Dense_2/bias (value)
+  add(e->off_wc + (long long)A * Z, Z, NC, H);
+  add(e->off_ln2b, H);
+  add(e->off_ln2s, H);
+  for (int s = 0; s < 3; ++s)
+    for (int q = 0; q < 5; ++q) {
+      const Stack& k = e->stk[s];
+      add(k.cb[q], k.co);
+      add(k.cw[q], 9LL * (q == 0 ? k.ci : k.co) * k.co);
+    }
+  add(e->off_ln1b, F);
+  add(e->off_ln1s, F);
+  add(e->off_emb, (long long)e->T * e->D);
+  e->n_flax = f;
+  int rc;
+  for (float** q : {&e->p, &e->g, &e->mu, &e->nu, &e->tgt})
+    if ((rc = e->alloc(q, e->n_int))) return bad(rc);
+  const long long img = (long long)B * c->in_ch * c->hw * c->hw;
+  if ((rc = e->alloc(&e->obs_u8, img)) || (rc = e->alloc(&e->nobs_u8, img)) || (rc = e->alloc(&e->nobs, img)))
+    return bad(rc);
+  for (int** q : {&e->act, &e->task, &e->a_next})
+    if ((rc = e->alloc(q, B))) return bad(rc);
+  if ((rc = e->alloc(&e->crop_o, 2 * B)) || (rc = e->alloc(&e->crop_n, 2 * B))) return bad(rc);
+  for (float** q : {&e->rew, &e->done, &e->noise_o, &e->noise_n, &e->rstd1, &e->rstd2, &e->loss_b, &e->logit_b})
+    if ((rc = e->alloc(q, B))) return bad(rc);
+  long long maxact = 0;
+  for (int s = 0; s < 3; ++s) {
+    Stack& k = e->stk[s];
+    const long long big = (long long)B * k.hin * k.hin * k.co, sm = (long long)B * k.ho * k.ho * k.co;
+    maxact = std::max({maxact, big, (long long)B * k.hin * k.hin * k.ci});
+    if ((rc = e->alloc(&k.conv0, big)) || (rc = e->alloc(&k.arg, sm))) return bad(rc);
+    for (float** q : {&k.c[0], &k.c[1], &k.c[2], &k.r[0], &k.r[1]})
+      if ((rc = e->alloc(q, sm))) return bad(rc);
+  }
+  if ((rc = e->alloc(&e->stk[0].xin_own, img))) return bad(rc);
+  for (float** q : {&e->ga, &e->gb, &e->gc})
+    if ((rc = e->alloc(q, maxact))) return bad(rc);
+  for (float** q : {&e->feat, &e->xhat1, &e->ln1, &e->dln1, &e->dfeat})
+    if ((rc = e->alloc(q, (long long)B * F))) return bad(rc);
+  for (float** q : {&e->z1, &e->xhat2, &e->h2, &e->dh2, &e->dz1})
+    if ((rc = e->alloc(q, (long long)B * H))) return bad(rc);
+  for (float** q : {&e->hc, &e->hc_on, &e->hc_tg, &e->dhc})
+    if ((rc = e->alloc(q, (long long)B * NC))) return bad(rc);
+  if ((rc = e->alloc(&e->m, (long long)B * Z))) return bad(rc);
+  long long wp = 0;
+  for (int s = 0; s < 3; ++s) {
+    const Stack& k = e->stk[s];
+    const long long np = drq::conv_wgrad_blocks((long long)B * k.hin * k.hin);
+    wp = std::max(wp, np * (9LL * k.co * k.co + k.co));
+    wp = std::max(wp, np * (9LL * k.ci * k.co + k.co));
+  }
+  if ((rc = e->alloc(&e->wpart, wp))) return bad(rc);
+  e->ws_floats = std::max(gemm_ws_floats(H, NC, 1, gemm_splits(H, NC, B, 1)),
+                          gemm_ws_floats(F, H, 1, gemm_splits(F, H, B, 1)));
+  if ((rc = e->alloc(&e->ws, e->ws_floats))) return bad(rc);
+  if ((rc = e->alloc(&e->part, 2 * 1024)) || (rc = e->alloc(&e->logs, DRQ_NUM_LOGS))) return bad(rc);
+  if (hipStreamSynchronize(e->st) != hipSuccess) return bad(fail(-5, "init sync"));
+  *out = e;
+  return 0;
+}
+
+void drq_destroy(drq_engine* e) {
+  if (!e) return;
+  if (e->st) (void)hipStreamSynchronize(e->st);
+  for (void* q : e->allocs) (void)hipFree(q);
+  if (e->st) (void)hipStreamDestroy(e->st);
+  delete e;
+}
+
+long long drq_num_params(const drq_engine* e) { return e ? e->n_flax : -22; }
+
+static float* which_buf(drq_engine* e, int which) {
+  switch (which) {
+    case DRQ_PARAMS: return e->p;
+    case DRQ_TARGET: return e->tgt;
+    case DRQ_ADAM_MU: return e->mu;
+    case DRQ_ADAM_NU: return e->nu;
+    case DRQ_GRAD: return e->g;
+    default: return nullptr;
+  }
+}
+
+int drq_set_params(drq_engine* e, int which, const float* flat, long long n) {
+  if (!e || !flat) return fail(-22, "null argument");
+  float* dst = which == DRQ_GRAD ? nullptr : which_buf(e, which);
+  if (!dst) return fail(-22, "bad buffer id");
+  if (n != e->n_flax) return fail(-22, "parameter count mismatch");
+  std::vector<float> host((size_t)e->n_int, 0.f);
+  for (const auto& mp : e->map)
+    for (long long r = 0; r < mp.rows; ++r)
+      std::memcpy(&host[(size_t)(mp.i + r * mp.ld)], flat + mp.f + r * mp.n, sizeof(float) * (size_t)mp.n);
+  if (hipMemcpyAsync(dst, host.data(), sizeof(float) * host.size(), hipMemcpyHostToDevice, e->st) != hipSuccess ||
+      hipStreamSynchronize(e->st) != hipSuccess)
+    return fail(-5, "upload failed");
+  return 0;
+}
+
+int drq_get_params(drq_engine* e, int which, float* flat, long long n) {
+  if (!e || !flat) return fail(-22, "null argument");
+  float* src = which_buf(e, which);
+  if (!src) return fail(-22, "bad buffer id");
+  if (n != e->n_flax) return fail(-22, "parameter count mismatch");
+  std::vector<float> host((size_t)e->n_int);
+  if (hipMemcpyAsync(host.data(), src, sizeof(float) * host.size(), hipMemcpyDeviceToHost, e->st) != hipSuccess ||
+      hipStreamSynchronize(e->st) != hipSuccess)
+    return fail(-5, "download failed");
+  for (const auto& mp : e->map)
+    for (long long r = 0; r < mp.rows; ++r)
+      std::memcpy(flat + mp.f + r * mp.n, &host[(size_t)(mp.i + r * mp.ld)], sizeof(float) * (size_t)mp.n);
+  return 0;
+}
+
+int drq_set_step(drq_engine* e, int adam_count) {
+  if (!e || adam_count < 0) return fail(-22, "bad argument");
+  e->count = adam_count;
+  return 0;
+}
+
+int drq_update(drq_engine* e, const drq_batch* b) {
+  if (!e || !b) return fail(-22, "null argument");
+  const int B = e->B;
+  const size_t img = (size_t)B * e->cfg.in_ch * e->cfg.hw * e->cfg.hw;
+  int rc;
+  if ((rc = copy_in(e->obs_u8, b->obs, img, e->st)) || (rc = copy_in(e->nobs_u8, b->next_obs, img, e->st)) ||
+      (rc = copy_in(e->act, b->actions, sizeof(int) * B, e->st)) ||
+      (rc = copy_in(e->task, b->task_ids, sizeof(int) * B, e->st)) ||
+      (rc = copy_in(e->rew, b->rewards, sizeof(float) * B, e->st)) ||
+      (rc = copy_in(e->done, b->dones, sizeof(float) * B, e->st)) ||
+      (rc = copy_in(e->crop_o, b->crop_obs, sizeof(int) * 2 * B, e->st)) ||
+      (rc = copy_in(e->crop_n, b->crop_next, sizeof(int) * 2 * B, e->st)) ||
+      (rc = copy_in(e->noise_o, b->noise_obs, sizeof(float) * B, e->st)) ||
+      (rc = copy_in(e->noise_n, b->noise_next, sizeof(float) * B, e->st)))
+    return rc;
+  e->step();
+  return hipGetLastError() == hipSuccess ? 0 : fail(-5, "kernel launch failed");
+}
+
+int drq_update_resident(drq_engine* e, int steps) {
+  if (!e || steps < 0) return fail(-22, "bad argument");
+  for (int i = 0; i < steps; ++i) e->step();
+  return hipGetLastError() == hipSuccess ? 0 : fail(-5, "kernel launch failed");
+}
+
+int drq_get_logs(drq_engine* e, float* out) {
+  if (!e || !out) return fail(-22, "null argument");
+  if (hipMemcpyAsync(out, e->logs, sizeof(float) * DRQ_NUM_LOGS, hipMemcpyDeviceToHost, e->st) != hipSuccess ||
+      hipStreamSynchronize(e->st) != hipSuccess)
+    return fail(-5, "log download failed");
+  return 0;
+}
+
+int drq_synchronize(drq_engine* e) {
+  if (!e) return fail(-22, "null argument");
+  return hipStreamSynchronize(e->st) == hipSuccess ? 0 : fail(-5, "stream sync failed");
+}
+
+}  // extern "C"

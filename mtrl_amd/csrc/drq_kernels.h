@@ -1,0 +1,55 @@
+// drq_kernels.h -- launch wrappers of the DrQ-eps device kernels (drq.hip), internal to libmtsac.so.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace mtsac {
+namespace drq {
+
+// augment (augmentation.py:101-117), draws given: uint8 [B][C][H][W] -> NHWC [-1, 1] * noise[b],
+// edge pad `pad`, crop offsets crop[b] = (along H, along W) in [0, 2 pad]
+void augment(const unsigned char* obs, const int* crop, const float* noise, float* out, int B, int C, int H, int W,
+             int pad, hipStream_t st);
+bool conv_supported(int ci, int co);
+// 3x3 / stride 1 / SAME on NHWC, kernel [3][3][ci][co]; relu_in applies ReLU to the input, res
+// (nullable) is added to the output
+void conv_fwd(const float* in, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
+              int ci, int co, bool relu_in, hipStream_t st);
+// din = conv^T(dout) * [mask > 0] (mask nullable) + dres (nullable)
+void conv_bwd_data(const float* dout, const float* w, const float* mask, const float* dres, float* din, int B, int H,
+                   int W, int ci, int co, hipStream_t st);
+int conv_wgrad_blocks(long long npix);
+// dw [3][3][ci][co], db [co] of a conv whose input is act(in); part: conv_wgrad_blocks(B H W) x
+// (9 ci co + co) floats
+void conv_wgrad(const float* in, const float* dout, float* part, float* dw, float* db, int B, int H, int W, int ci,
+                int co, bool relu_in, hipStream_t st);
+// max pool 3x3 / stride 2 / SAME (out (H + 1) / 2), argmax tap per output
+void maxpool_fwd(const float* in, float* out, unsigned char* arg, int B, int H, int W, int C, hipStream_t st);
+void maxpool_bwd(const float* dout, const unsigned char* arg, float* din, int B, int H, int W, int C, hipStream_t st);
+// feat[b] = [relu(enc[b]) | normalised emb[task[b]]]
+void concat_feat(const float* enc, int nenc, const float* emb, int D, const int* task, float* feat, int ldf, int B,
+                 hipStream_t st);
+// LayerNorm over F columns of (x + xb) (xb nullable), y = ln * scale + bias (ReLU when relu)
+void ln_fwd(const float* x, const float* xb, int ldx, int F, const float* scale, const float* bias, float eps,
+            float* y, int ldy, float* xhat, float* rstd, int B, bool relu, hipStream_t st);
+void ln_bwd(const float* dy, int lddy, const float* y, int ldy, const float* xhat, const float* rstd,
+            const float* scale, int F, float* dx, int lddx, float* dscale, float* dbias, int B, bool relu,
+            hipStream_t st);
+void colsum_rows(const float* x, int ld, int F, int B, float* out, hipStream_t st);
+// head output hc[b][ldh] = [adv (A Z) | val (Z)] before bias (hb): C51 target m[b][Z]
+void c51_target(const float* hc_on, const float* hc_tg, int ldh, const float* hb_on, const float* hb_tg, int A, int Z,
+                const float* rew, const float* done, float gamma_n, float vmin, float vmax, float* m, int* a_next,
+                int B, hipStream_t st);
+void c51_loss(const float* hc, int ldh, const float* hb, int A, int Z, const int* act, const float* m, float* dh,
+              float* loss_b, float* logit_b, int B, hipStream_t st);
+void embed_bwd(const float* dfeat, int ldf, int off, const float* emb, int D, const int* task, int B, int T,
+               float* demb, hipStream_t st);
+void enc_grad(const float* dfeat, int ldf, const float* enc, int nenc, float* denc, int B, hipStream_t st);
+// optax.adamw + Polyak over a flat buffer; part[2 G]: sum g^2, sum p_pre^2 per block; returns G
+int adamw(float* p, float* mu, float* nu, const float* g, float* tgt, long long n, float lr, float b1, float b2,
+          float eps, float wd, float tau, int count, float* part, int max_blocks, hipStream_t st);
+// logs = [mean online logit, |g|, |p_pre|, mean loss]
+void drq_logs(const float* part, int G, const float* loss_b, const float* logit_b, int B, int Z, float* logs,
+              hipStream_t st);
+
+}  // namespace drq
+}  // namespace mtsac

@@ -1,0 +1,113 @@
+"""Host mirror of the DrQ-eps update (experiments/atari.py, mtrl/rl/algorithms/drqeps.py) on the
+HIP engine of include/drq.h.  The product path: there is no CPU fallback (the library must load).
+
+``DrQEngine.update(batch, aug)`` runs DrQ.update (drqeps.py:337-343): augmentation of obs and
+next_obs with the given draws, then _update_inner (drqeps.py:268-335) -- C51 target from the online
+greedy action and the target network at s', cross entropy at the taken action, optax.adamw, Polyak.
+Parameters are flat float32 vectors in flax ravel order (oracle/drq.py:param_spec)."""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+
+
+@dataclass(frozen=True)
+class DrQSettings:
+    num_tasks: int = 26
+    n_actions: int = 18
+    n_atoms: int = 51
+    in_ch: int = 4
+    hw: int = 84
+    scale: int = 1
+    embed_dim: int = 32
+    n_hidden: int = 512
+    batch: int = 256
+    nstep: int = 3
+    gamma: float = 0.99
+    v_min: float = -10.0
+    v_max: float = 10.0
+    tau: float = 0.005
+    lr: float = 1e-4
+    b1: float = 0.9
+    b2: float = 0.999
+    eps: float = 1.5e-4
+    weight_decay: float = 0.05
+    ln_eps: float = 1e-6
+
+
+def _ptr(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def _drq_check(rc: int) -> int:
+    if rc < 0:
+        msg = L.load().drq_last_error()
+        raise L.MTSACError(f"libmtsac drq error {rc}: {msg.decode() if msg else ''}")
+    return rc
+
+
+class DrQEngine:
+    def __init__(self, s: DrQSettings = DrQSettings(), device: int = 0):
+        self.lib = L.load()
+        self.s = s
+        c = L.DrqConfig(**{k: getattr(s, k) for k, _ in L.DrqConfig._fields_})
+        h = ctypes.c_void_p()
+        _drq_check(self.lib.drq_create(ctypes.byref(c), device, ctypes.byref(h)))
+        self.h = h
+        self.n = int(self.lib.drq_num_params(h))
+        self._keep = []
+
+    def close(self):
+        if self.h:
+            self.lib.drq_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_params(self, which: int, flat):
+        a = np.ascontiguousarray(flat, np.float32)
+        assert a.size == self.n, (a.size, self.n)
+        _drq_check(self.lib.drq_set_params(self.h, which, _ptr(a), self.n))
+
+    def get_params(self, which: int = L.DRQ_PARAMS) -> np.ndarray:
+        out = np.empty(self.n, np.float32)
+        _drq_check(self.lib.drq_get_params(self.h, which, _ptr(out), self.n))
+        return out
+
+    def set_step(self, count: int):
+        _drq_check(self.lib.drq_set_step(self.h, int(count)))
+
+    def update(self, batch, aug) -> None:
+        """batch = (obs u8 [B][C][H][W], actions, next_obs u8, dones, rewards, task_ids);
+        aug = (crop_obs int [B][2], noise_obs [B], crop_next, noise_next)."""
+        obs, act, nobs, done, rew, task = batch
+        co, no, cn, nn = aug
+        arrs = [np.ascontiguousarray(obs, np.uint8), np.ascontiguousarray(act, np.int32),
+                np.ascontiguousarray(nobs, np.uint8), np.ascontiguousarray(done, np.float32),
+                np.ascontiguousarray(rew, np.float32), np.ascontiguousarray(task, np.int32),
+                np.ascontiguousarray(co, np.int32), np.ascontiguousarray(no, np.float32),
+                np.ascontiguousarray(cn, np.int32), np.ascontiguousarray(nn, np.float32)]
+        b = L.DrqBatch(*[a.ctypes.data for a in arrs])
+        _drq_check(self.lib.drq_update(self.h, ctypes.byref(b)))
+        self._keep = arrs  # alive until the copies on the engine's stream have run
+        self.synchronize()
+
+    def update_resident(self, steps: int):
+        _drq_check(self.lib.drq_update_resident(self.h, int(steps)))
+
+    def logs(self) -> dict:
+        out = np.zeros(L.DRQ_NUM_LOGS, np.float32)
+        _drq_check(self.lib.drq_get_logs(self.h, _ptr(out)))
+        return dict(zip(L.DRQ_LOG_KEYS, (float(v) for v in out)))
+
+    def synchronize(self):
+        _drq_check(self.lib.drq_synchronize(self.h))

@@ -11,7 +11,7 @@ def _declared():
     names = set()
     for h in (ROOT / "include").glob("*.h"):
         text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
-        names |= set(re.findall(r"\b(mtsac_[a-z0-9_]+)\s*\(", text))
+        names |= set(re.findall(r"\b((?:mtsac|drq)_[a-z0-9_]+)\s*\(", text))
     return names
 
 
