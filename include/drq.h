@@ -44,7 +44,7 @@ typedef struct drq_engine drq_engine;
 /* One update's inputs (host or device pointers): observations uint8 [batch][in_ch][hw][hw]
  * (NCHW, as the Atari buffer stores them), actions int [batch], rewards / dones float [batch]
  * (n-step returns and terminal flags), task ids int [batch], and the augmentation draws:
- * crop offsets int [batch][2] in [0, 8] and intensity factors float [batch] for obs and next_obs. */
+ * crop offsets int [batch][2] in [0, 8) and intensity factors float [batch] for obs and next_obs. */
 typedef struct drq_batch {
   const unsigned char* obs;
   const int* actions;

@@ -166,13 +166,14 @@ __global__ __launch_bounds__(256) void conv_bwd_data_kernel(const float* __restr
 
 // Weight gradient partials: block g takes 64-pixel tiles g, g + G, ... (G = gridDim.x); the
 // tile's im2col rows (act applied, zero outside the image) and dout go through LDS; lane t owns
-// taps (tap * CI + ci, co) t, t + 256, ... and the bias entries co = t (< CO), summed over the
-// tile's pixels in order.  part[g][9 CI CO + CO], summed over g in order by sum_parts_kernel.
+// column co = t % CO of rows tc = t / CO + (256 / CO) j of dW ([tap * CI + ci][co]) and the bias
+// entry co = t (< CO), summed over the tile's pixels in order.  part[g][9 CI CO + CO], summed over g in order by sum_parts_kernel.
 template <int CI, int CO, bool RELU_IN>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict__ in, const float* __restrict__ dout,
                                                          float* __restrict__ part, int B, int H, int W) {
   constexpr int NW = 9 * CI * CO;
-  constexpr int PER = (NW + 255) / 256;
+  constexpr int NG = 256 / CO;                 // lane groups; lane t: co = t % CO, tap-channel rows
+  constexpr int PER = (9 * CI + NG - 1) / NG;  // tc = t / CO + NG j (one dout read per NG-row sweep)
   constexpr int TP = 64;
   __shared__ float sin_[TP][9 * CI];
   __shared__ float sg[TP][CO];
@@ -212,14 +213,15 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
       sg[q][co] = pix < npix ? dout[pix * CO + co] : 0.f;
     }
     __syncthreads();
+    {
+      const int co = t % CO, tg = t / CO;
+      for (int q = 0; q < TP; ++q) {
+        const float gq = sg[q][co];
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int e = t + 256 * k;
-      if (e < NW) {
-        const int tc = e / CO, co = e - tc * CO;  // tc = tap * CI + ci
-        float s = acc[k];
-        for (int q = 0; q < TP; ++q) s = fmaf(sin_[q][tc], sg[q][co], s);
-        acc[k] = s;
+        for (int k = 0; k < PER; ++k) {
+          const int tc = tg + NG * k;  // tc = tap * CI + ci
+          if (tc < 9 * CI) acc[k] = fmaf(sin_[q][tc], gq, acc[k]);
+        }
       }
     }
     if (t < CO) {
@@ -230,20 +232,39 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
   }
   float* pp = part + (long long)blockIdx.x * (NW + CO);
 #pragma unroll
-  for (int k = 0; k < PER; ++k)
-    if (t + 256 * k < NW) pp[t + 256 * k] = acc[k];
+  for (int k = 0; k < PER; ++k) {
+    const int tc = t / CO + NG * k;
+    if (tc < 9 * CI) pp[tc * CO + t % CO] = acc[k];
+  }
   if (t < CO) pp[NW + t] = bacc;
 }
 
-// dw[e] / db[e - nw] = sum_g part[g][e] in g order (e < n)
-__global__ void sum_parts_kernel(const float* __restrict__ part, int G, int n, float* __restrict__ dst_w,
-                                 float* __restrict__ dst_b, int nw) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  double s = 0.0;  // the partials of up to ~10^5 pixels x 9 taps: no further fp32 rounding here
-  for (int g = 0; g < G; ++g) s += (double)part[(long long)g * n + e];
-  if (e < nw) dst_w[e] = (float)s;
-  else dst_b[e - nw] = (float)s;
+// dw[e] / db[e - nw] = sum_g part[g][e] (e < n): block of 64 entries x 4 lanes of g (g = lane
+// group + 4 j, 8 loads in flight), double accumulation, the 4 groups added in order
+__global__ __launch_bounds__(256) void sum_parts_kernel(const float* __restrict__ part, int G, int n,
+                                                        float* __restrict__ dst_w, float* __restrict__ dst_b, int nw) {
+  __shared__ double red[4][64];
+  const int el = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + el;
+  double s = 0.0;
+  if (e < n) {
+    int g = grp;
+    for (; g + 28 < G; g += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(long long)(g + 4 * u) * n + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += (double)v[u];
+    }
+    for (; g < G; g += 4) s += (double)part[(long long)g * n + e];
+  }
+  red[grp][el] = s;
+  __syncthreads();
+  if (grp == 0 && e < n) {
+    const float r = (float)(((red[0][el] + red[1][el]) + red[2][el]) + red[3][el]);
+    if (e < nw) dst_w[e] = r;
+    else dst_b[e - nw] = r;
+  }
 }
 
 // ------------------------------------------------------------------ max pool 3x3 / 2 / SAME
@@ -680,7 +701,7 @@ void conv_wgrad(const float* in, const float* dout, float* part, float* dw, floa
   CONV_CASES(C_WG)
 #undef C_WG
   const int nw = 9 * ci * co, n = nw + co;
-  hipLaunchKernelGGL(sum_parts_kernel, dim3(blocks(n)), dim3(256), 0, st, part, G, n, dw, db, nw);
+  hipLaunchKernelGGL(sum_parts_kernel, dim3((n + 63) / 64), dim3(256), 0, st, part, G, n, dw, db, nw);
 }
 
 void maxpool_fwd(const float* in, float* out, unsigned char* arg, int B, int H, int W, int C, hipStream_t st) {

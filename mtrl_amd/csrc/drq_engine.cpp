@@ -106,21 +106,24 @@ struct drq_engine {
     }
     drq::concat_feat(stk[2].c[2], NENC, P + off_emb, D, task, feat, F, B, st);
     drq::ln_fwd(feat, nullptr, F, F, P + off_ln1s, P + off_ln1b, cfg.ln_eps, ln1, F, xhat1, rstd1, B, false, st);
-    GemmParams gp{};
-    gp.A = ln1; gp.lda = F;
-    gp.B = P + off_w0; gp.ldb = H;
-    gp.C = z1; gp.ldc = H;
-    gp.M = B; gp.N = H; gp.K = F;
-    gemm_f32(gp, GEMM_NN, EPI_STORE, 1, st);
+    gemm_store(ln1, F, P + off_w0, H, z1, H, B, H, F, GEMM_NN);
     drq::ln_fwd(z1, P + off_b0, H, H, P + off_ln2s, P + off_ln2b, cfg.ln_eps, h2, H, xhat2, rstd2, B, true, st);
-    GemmParams gh{};
-    gh.A = h2; gh.lda = H;
-    gh.B = P + off_wc; gh.ldb = NC;
-    gh.C = out; gh.ldc = NC;
-    gh.M = B; gh.N = NC; gh.K = H;
-    gemm_f32(gh, GEMM_NN, EPI_STORE, 1, st);
+    gemm_store(h2, H, P + off_wc, NC, out, NC, B, NC, H, GEMM_NN);
   }
   int cfg_blocks() const { return 2; }
+
+  // C[M][N] = A . op(B) with split-K over the few row tiles a batch of 256 gives (EPI_STORE)
+  void gemm_store(const float* Aop, int lda, const float* Bop, int ldb, float* C, int ldc, int M, int N, int K,
+                  GemmKind kind) {
+    GemmParams gp{};
+    gp.A = Aop; gp.lda = lda;
+    gp.B = Bop; gp.ldb = ldb;
+    gp.C = C; gp.ldc = ldc;
+    gp.M = M; gp.N = N; gp.K = K;
+    gp.splits = gemm_splits(M, N, K, 1);
+    gp.ws = ws;
+    gemm_f32(gp, kind, EPI_STORE, 1, st);
+  }
 
   void wgrad_gemm(const float* Aop, int lda, const float* Bop, int ldb, float* C, float* db, int M, int N) {
     GemmParams gp{};
@@ -147,25 +150,11 @@ struct drq_engine {
     drq::c51_loss(hc, NC, p + off_bc, A, Z, act, m, dhc, loss_b, logit_b, B, st);
     // ---- head backward
     wgrad_gemm(h2, H, dhc, NC, g + off_wc, g + off_bc, H, NC);
-    {
-      GemmParams gp{};
-      gp.A = dhc; gp.lda = NC;
-      gp.B = p + off_wc; gp.ldb = NC;  // [N = H][K = NC]
-      gp.C = dh2; gp.ldc = H;
-      gp.M = B; gp.N = H; gp.K = NC;
-      gemm_f32(gp, GEMM_NT, EPI_STORE, 1, st);
-    }
+    gemm_store(dhc, NC, p + off_wc, NC, dh2, H, B, H, NC, GEMM_NT);  // Wc as [N = H][K = NC]
     drq::ln_bwd(dh2, H, h2, H, xhat2, rstd2, p + off_ln2s, H, dz1, H, g + off_ln2s, g + off_ln2b, B, true, st);
     drq::colsum_rows(dz1, H, H, B, g + off_b0, st);
     wgrad_gemm(ln1, F, dz1, H, g + off_w0, nullptr, F, H);
-    {
-      GemmParams gp{};
-      gp.A = dz1; gp.lda = H;
-      gp.B = p + off_w0; gp.ldb = H;  // [N = F][K = H]
-      gp.C = dln1; gp.ldc = F;
-      gp.M = B; gp.N = F; gp.K = H;
-      gemm_f32(gp, GEMM_NT, EPI_STORE, 1, st);
-    }
+    gemm_store(dz1, H, p + off_w0, H, dln1, F, B, F, H, GEMM_NT);  // W0 as [N = F][K = H]
     drq::ln_bwd(dln1, F, nullptr, 0, xhat1, rstd1, p + off_ln1s, F, dfeat, F, g + off_ln1s, g + off_ln1b, B, false, st);
     drq::embed_bwd(dfeat, F, NENC, p + off_emb, D, task, B, T, g + off_emb, st);
     // ---- encoder backward, stacks in reverse
@@ -333,8 +322,12 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
     wp = std::max(wp, np * (9LL * k.ci * k.co + k.co));
   }
   if ((rc = e->alloc(&e->wpart, wp))) return bad(rc);
-  e->ws_floats = std::max(gemm_ws_floats(H, NC, 1, gemm_splits(H, NC, B, 1)),
-                          gemm_ws_floats(F, H, 1, gemm_splits(F, H, B, 1)));
+  e->ws_floats = std::max({gemm_ws_floats(H, NC, 1, gemm_splits(H, NC, B, 1)),
+                           gemm_ws_floats(F, H, 1, gemm_splits(F, H, B, 1)),
+                           gemm_ws_floats(B, H, 1, gemm_splits(B, H, F, 1)),
+                           gemm_ws_floats(B, NC, 1, gemm_splits(B, NC, H, 1)),
+                           gemm_ws_floats(B, H, 1, gemm_splits(B, H, NC, 1)),
+                           gemm_ws_floats(B, F, 1, gemm_splits(B, F, H, 1))});
   if ((rc = e->alloc(&e->ws, e->ws_floats))) return bad(rc);
   if ((rc = e->alloc(&e->part, 2 * 1024)) || (rc = e->alloc(&e->logs, DRQ_NUM_LOGS))) return bad(rc);
   if (hipStreamSynchronize(e->st) != hipSuccess) return bad(fail(-5, "init sync"));

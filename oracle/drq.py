@@ -205,7 +205,7 @@ def c51_target(logits_next_online, logits_next_target, rewards, dones, cfg: DrQC
     distribution at that action, projected onto the support (the l == u case drops its mass, as
     the reference's two scatter-adds do)."""
     B = logits_next_online.shape[0]
-    support = torch.linspace(cfg.v_min, cfg.v_max, cfg.n_atoms, dtype=torch.float64)
+    support = torch.linspace(cfg.v_min, cfg.v_max, cfg.n_atoms, dtype=logits_next_online.dtype)
     q_next = (torch.softmax(logits_next_online, -1) * support).sum(-1)
     a_next = q_next.argmax(-1)
     target_dist = torch.softmax(logits_next_target, -1)[torch.arange(B), a_next]
@@ -213,9 +213,9 @@ def c51_target(logits_next_online, logits_next_target, rewards, dones, cfg: DrQC
     dz = (cfg.v_max - cfg.v_min) / (cfg.n_atoms - 1)
     b = (tz - cfg.v_min) / dz
     l, u = torch.floor(b).long(), torch.ceil(b).long()
-    m = torch.zeros(B, cfg.n_atoms, dtype=torch.float64)
-    m.scatter_add_(1, l, target_dist * (u.double() - b))
-    m.scatter_add_(1, u, target_dist * (b - l.double()))
+    m = torch.zeros(B, cfg.n_atoms, dtype=b.dtype)
+    m.scatter_add_(1, l, target_dist * (u.to(b.dtype) - b))
+    m.scatter_add_(1, u, target_dist * (b - l.to(b.dtype)))
     return m, a_next
 
 
@@ -233,12 +233,13 @@ def init_state(cfg: DrQConfig, seed: int = 0) -> DrQState:
     return DrQState(p.copy(), p.copy(), np.zeros_like(p), np.zeros_like(p), 0)
 
 
-def update(cfg: DrQConfig, st: DrQState, batch, return_internals: bool = False):
+def update(cfg: DrQConfig, st: DrQState, batch, return_internals: bool = False, dtype=torch.float64):
     """One DrQ._update_inner step (drqeps.py:268-335) on an augmented batch
     (obs NHWC float, actions int, next_obs NHWC float, dones, rewards, task_ids).
-    Returns the new state and the LogDict (mean online logit, loss, grad / pre-update param norms)."""
+    Returns the new state and the LogDict (mean online logit, loss, grad / pre-update param norms).
+    dtype=torch.float32 only for the bench's CPU baseline (the reference computes in fp32)."""
     obs, actions, next_obs, dones, rewards, task_ids = batch
-    t = lambda a: torch.as_tensor(np.asarray(a, np.float64))
+    t = lambda a: torch.as_tensor(np.asarray(a)).to(dtype)
     ti = torch.as_tensor(np.asarray(task_ids, np.int64))
     pt = t(st.params).clone().requires_grad_(True)
     with torch.no_grad():
@@ -251,7 +252,7 @@ def update(cfg: DrQConfig, st: DrQState, batch, return_internals: bool = False):
     logits = forward(unflatten(pt, cfg), t(obs), ti, cfg)[torch.arange(B), torch.as_tensor(np.asarray(actions, np.int64))]
     loss = -(m * torch.log_softmax(logits, -1)).sum(-1).mean()
     loss.backward()
-    g = pt.grad.detach().numpy()
+    g = pt.grad.detach().numpy().astype(np.float64)
     # optax.adamw: mu, nu, bias correction, u = -lr (mu_hat / (sqrt(nu_hat) + eps) + wd p)
     count = st.count + 1
     mu = (1 - cfg.b1) * g + cfg.b1 * st.mu
@@ -268,5 +269,5 @@ def update(cfg: DrQConfig, st: DrQState, batch, return_internals: bool = False):
     }
     new = DrQState(p_new, tgt, mu, nu, count)
     if return_internals:
-        return new, logs, {"grad": g, "m": m.numpy(), "a_next": a_next.numpy()}
+        return new, logs, {"grad": g, "m": m.double().numpy(), "a_next": a_next.numpy()}
     return new, logs

@@ -22,7 +22,7 @@ def _batch(cfg, B, seed):
     done = (rng.random(B) < 0.2).astype(np.float32)
     rew = np.round(rng.standard_normal(B) * 2, 3).astype(np.float32)
     task = rng.integers(0, cfg.num_tasks, B).astype(np.int32)
-    co, cn = rng.integers(0, 9, (B, 2)).astype(np.int32), rng.integers(0, 9, (B, 2)).astype(np.int32)
+    co, cn = rng.integers(0, 8, (B, 2)).astype(np.int32), rng.integers(0, 8, (B, 2)).astype(np.int32)
     no = (1 + 0.05 * np.clip(rng.standard_normal(B), -2, 2)).astype(np.float32)
     nn = (1 + 0.05 * np.clip(rng.standard_normal(B), -2, 2)).astype(np.float32)
     return (obs, act, nobs, done, rew, task), (co, no, cn, nn)
@@ -71,9 +71,9 @@ def test_update_matches_oracle(hw, hidden, B):
         n = int(np.prod(shape))
         a, b = g_gpu[o:o + n], g_ref[o:o + n]
         scale = np.abs(b).max() + 1e-12
-        # conv kernels sum B x H x W pixels x 9 taps (1.1e5 terms at 84 x 84) in fp32 with heavy
+        # conv leaves sum B x H x W pixels (x 9 taps; 1.1e5 terms at 84 x 84) in fp32 with heavy
         # cancellation: held to 5e-4 of the leaf's largest entry; everything else to 1e-4
-        tol = 5e-4 if ("Conv_" in path and path.endswith("kernel")) else 1e-4
+        tol = 5e-4 if "Conv_" in path else 1e-4
         assert np.abs(a - b).max() <= tol * scale + 1e-9, (path, float(np.abs(a - b).max()), float(scale))
         o += n
     mu = e.get_params(L.DRQ_ADAM_MU).astype(np.float64)
