@@ -77,6 +77,11 @@ int drq_set_step(drq_engine* e, int adam_count);
 int drq_update(drq_engine* e, const drq_batch* batch);
 /* run `steps` more updates on the batch already resident on the device (benchmarks) */
 int drq_update_resident(drq_engine* e, int steps);
+/* expected Q [n][n_actions] of the online network on n <= batch observations (uint8 NCHW), after
+ * the augmentation with the given draws: the quantity _sample_action / _eval_action take the argmax
+ * of (drqeps.py:56-97); epsilon-greedy stays with the caller's RNG.  Synchronous. */
+int drq_q_values(drq_engine* e, const unsigned char* obs, const int* task_ids, const int* crop, const float* noise,
+                 int n, float* q);
 int drq_get_logs(drq_engine* e, float* out /* DRQ_NUM_LOGS */);
 int drq_synchronize(drq_engine* e);
 const char* drq_last_error(void);

@@ -185,6 +185,7 @@ SIGNATURES.update({
     "drq_update": (ctypes.c_int, [P, ctypes.POINTER(DrqBatch)]),
     "drq_update_resident": (ctypes.c_int, [P, ctypes.c_int]),
     "drq_get_logs": (ctypes.c_int, [P, P]),
+    "drq_q_values": (ctypes.c_int, [P, P, P, P, P, ctypes.c_int, P]),
     "drq_synchronize": (ctypes.c_int, [P]),
 })
 

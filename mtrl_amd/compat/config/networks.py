@@ -2,7 +2,7 @@
 
 from dataclasses import dataclass
 
-from .nn import NeuralNetworkConfig, VanillaNetworkConfig
+from .nn import ImpalaEncoderConfig, NeuralNetworkConfig, TaskEmbeddingConfig, VanillaNetworkConfig
 
 
 @dataclass(frozen=True)
@@ -19,3 +19,11 @@ class QValueFunctionConfig:
     use_classification: bool = False
     num_atoms: int | None = None
     dueling: bool = False
+
+
+@dataclass(frozen=True)
+class ImpalaDQNConfig:  # mtrl/config/networks.py:37-42
+    impala_config: ImpalaEncoderConfig = ImpalaEncoderConfig()
+    q_function_config: QValueFunctionConfig = QValueFunctionConfig(use_classification=True, num_atoms=101)
+    task_embed_config: TaskEmbeddingConfig = TaskEmbeddingConfig()
+    use_layer_norm: bool = True

@@ -26,3 +26,18 @@ class VanillaNetworkConfig(NeuralNetworkConfig):
 @dataclass(frozen=True, kw_only=True)
 class MultiHeadConfig(NeuralNetworkConfig):
     num_tasks: int
+
+
+@dataclass(frozen=True, kw_only=True)
+class ImpalaEncoderConfig(NeuralNetworkConfig):  # mtrl/config/nn.py:47-52
+    use_layer_norm: bool = False
+    scale: int = 1
+    blocks: int = 2
+    stacks: tuple[int, ...] = (8, 16, 16)
+    num_critics: int = 1
+
+
+@dataclass(frozen=True, kw_only=True)
+class TaskEmbeddingConfig:  # mtrl/config/nn.py:54-59
+    num_tasks: int = 26
+    embed_dim: int = 32

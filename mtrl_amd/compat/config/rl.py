@@ -40,3 +40,22 @@ class OffPolicyTrainingConfig(TrainingConfig):
     warmstart_steps: int = int(4e3)
     buffer_size: int = int(1e6)
     batch_size: int = 1280
+
+
+@dataclass(frozen=True)
+class DrQTrainingConfig(OffPolicyTrainingConfig):  # mtrl/config/rl.py:53-79 (the fields the DrQ path reads)
+    warmstart_steps: int = 1_000
+    buffer_size: int = 100_000
+    batch_size: int = 256
+    num_critics: int = 2
+    tau: float = 0.005
+    eps_start: float = 1.0
+    eps_end: float = 0.01
+    eps_decay_steps: int = 5_000
+    v_min: float = -10.0
+    v_max: float = 10.0
+    num_tasks: int = 26
+    normalize_rewards: bool = True
+    nstep: int = 3
+    replay_ratio: int = 2
+    eval_step_frequency: int = 10_000

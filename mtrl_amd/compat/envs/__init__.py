@@ -1,4 +1,5 @@
+from .atari import AtariConfig
 from .base import EnvConfig
 from .metaworld import MetaworldConfig
 
-__all__ = ["EnvConfig", "MetaworldConfig"]
+__all__ = ["AtariConfig", "EnvConfig", "MetaworldConfig"]

@@ -26,3 +26,17 @@ except ImportError:  # gymnasium is not part of this image
 
         def seed(self, seed=None):
             self._rng = np.random.default_rng(seed)
+
+
+try:  # pragma: no cover - depends on the environment
+    from gymnasium.spaces import Discrete  # noqa: F401
+except ImportError:
+
+    class Discrete:  # type: ignore[no-redef]
+        def __init__(self, n, seed=None):
+            self.n = int(n)
+            self.shape = ()
+            self._rng = np.random.default_rng(seed)
+
+        def sample(self):
+            return int(self._rng.integers(0, self.n))

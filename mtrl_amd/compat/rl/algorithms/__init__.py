@@ -2,13 +2,16 @@
 
 from ...config.rl import AlgorithmConfig
 from .base import Algorithm, OffPolicyAlgorithm
+from .drqeps import DrQ, DrQConfig
 from .mtsac import MTSAC, MTSACConfig
 
 
 def get_algorithm_for_config(config: AlgorithmConfig) -> type[Algorithm]:
     if type(config) is MTSACConfig:
         return MTSAC
-    raise ValueError(f"Invalid config type: {type(config)} (only MTSACConfig runs on the MI355X engine)")
+    if type(config) is DrQConfig:
+        return DrQ
+    raise ValueError(f"Invalid config type: {type(config)} (MTSACConfig and DrQConfig run on the MI355X engines)")
 
 
-__all__ = ["Algorithm", "OffPolicyAlgorithm", "MTSAC", "MTSACConfig", "get_algorithm_for_config"]
+__all__ = ["Algorithm", "OffPolicyAlgorithm", "DrQ", "DrQConfig", "MTSAC", "MTSACConfig", "get_algorithm_for_config"]

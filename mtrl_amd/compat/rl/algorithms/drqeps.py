@@ -1,0 +1,109 @@
+"""DrQConfig / DrQ (mtrl/rl/algorithms/drqeps.py:98-343) on the MI355X DrQ-eps engine.
+
+The API surface the Atari experiment uses: DrQ.initialize(config, env_config, seed),
+update(data) -> (self, logs), sample_action(obs, task_ids) -> (self, actions),
+eval_action(obs, task_ids), get_num_params().  The device does the augmentation, the three
+ImpalaDQN passes, the C51 loss, its backward, AdamW and Polyak (include/drq.h).  The random draws
+the reference takes from jax.random (augmentation crops and intensities, epsilon-greedy coins and
+random actions) come from a numpy Generator seeded by `seed` here: JAX's threefry is not
+reproduced, so trajectories match the reference in distribution, not draw for draw."""
+
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+
+from ....drq import DrQEngine, DrQSettings
+from ....drq_init import init_drq
+from ... import types as T
+from ...config.networks import ImpalaDQNConfig
+from ...config.rl import AlgorithmConfig
+
+_PAD = 4  # augmentation.py:75 (img_pad)
+
+
+@dataclasses.dataclass(frozen=True)
+class DrQConfig(AlgorithmConfig):  # drqeps.py:98-109
+    critic_config: ImpalaDQNConfig = ImpalaDQNConfig()
+    tau: float = 0.005
+    v_min: float = -10.0
+    v_max: float = 10.0
+    n_atoms: int = 51
+    eps_start: float = 1.0
+    eps_end: float = 0.01
+    eps_decay_steps: int = 5_000
+    num_tasks: int = 26
+
+
+class DrQ:
+    def __init__(self, engine: DrQEngine, config: DrQConfig, seed: int, batch: int):
+        self.engine = engine
+        self.config = config
+        self.rng = np.random.default_rng(seed)
+        self.step = 0
+        self.batch = batch
+
+    @staticmethod
+    def initialize(config: DrQConfig, env_config, seed: int = 1, batch_size: int = 256, nstep: int = 3) -> "DrQ":
+        obs_shape = tuple(getattr(env_config, "observation_space").shape)  # (C, H, W) uint8
+        n_actions = int(getattr(env_config, "action_space").n)
+        enc = config.critic_config.impala_config
+        opt = config.critic_config.q_function_config.network_config.optimizer
+        s = DrQSettings(num_tasks=config.num_tasks, n_actions=n_actions, n_atoms=config.n_atoms, in_ch=obs_shape[0],
+                        hw=obs_shape[1], scale=enc.scale, embed_dim=config.critic_config.task_embed_config.embed_dim,
+                        batch=batch_size, nstep=nstep, gamma=config.gamma, v_min=config.v_min, v_max=config.v_max,
+                        tau=config.tau, lr=opt.lr, eps=opt.eps if opt.eps is not None else 1e-8,
+                        weight_decay=opt.weight_decay if opt.weight_decay is not None else 1e-4)
+        eng = DrQEngine(s)
+        p = init_drq(seed, num_tasks=config.num_tasks, n_actions=n_actions, n_atoms=config.n_atoms,
+                     in_ch=obs_shape[0], hw=obs_shape[1], scale=enc.scale,
+                     embed_dim=config.critic_config.task_embed_config.embed_dim)
+        eng.set_params(0, p)
+        eng.set_params(1, p)  # target = the shrink-and-perturbed params (drqeps.py:196)
+        return DrQ(eng, config, seed, batch_size)
+
+    def get_num_params(self) -> dict[str, int]:
+        return {"critic_num_params": self.engine.n}
+
+    def _aug_draws(self, n):
+        crop = self.rng.integers(0, 2 * _PAD, (n, 2)).astype(np.int32)
+        noise = (1.0 + 0.05 * np.clip(self.rng.standard_normal(n), -2.0, 2.0)).astype(np.float32)
+        return crop, noise
+
+    def update(self, data: T.AtariReplayBufferSamples):
+        """DrQ.update (drqeps.py:337-343): augment both observation batches, _update_inner."""
+        B = data.observations.shape[0]
+        if B != self.batch:
+            raise ValueError(f"batch of {B} rows; the engine was built for {self.batch}")
+        co, no = self._aug_draws(B)
+        cn, nn = self._aug_draws(B)
+        self.engine.update((data.observations, np.asarray(data.actions).reshape(B), data.next_observations,
+                            np.asarray(data.dones).reshape(B), np.asarray(data.rewards).reshape(B),
+                            np.asarray(data.task_ids).reshape(B)), (co, no, cn, nn))
+        return self, self.engine.logs()
+
+    def _q(self, observation, task_ids):
+        n = observation.shape[0]
+        crop, noise = self._aug_draws(n)
+        return self.engine.q_values(observation, task_ids, crop, noise)
+
+    def sample_action(self, observation, task_ids):
+        """_sample_action (drqeps.py:49-79): epsilon decays linearly over eps_decay_steps env steps."""
+        c = self.config
+        q = self._q(observation, task_ids)
+        t = min(self.step / c.eps_decay_steps, 1.0)
+        eps = c.eps_start + t * (c.eps_end - c.eps_start)
+        n = q.shape[0]
+        greedy = q.argmax(-1)
+        coins = self.rng.uniform(size=n)
+        rand = self.rng.integers(0, 18, n)  # hardcoded for Atari in the reference (drqeps.py:75)
+        self.step += c.num_tasks
+        return self, np.where(coins < eps, rand, greedy)
+
+    def eval_action(self, observation, task_ids):
+        """_eval_action (drqeps.py:81-97): greedy on the augmented observation."""
+        return self._q(observation, task_ids).argmax(-1)
+
+    def close(self):
+        self.engine.close()

@@ -15,6 +15,16 @@ class ReplayBufferSamples(NamedTuple):
     rewards: np.ndarray
 
 
+class AtariReplayBufferSamples(NamedTuple):  # mtrl/types.py:38-45
+    observations: np.ndarray  # uint8 [B][C][H][W]
+    actions: np.ndarray
+    next_observations: np.ndarray
+    truncations: np.ndarray
+    dones: np.ndarray
+    rewards: np.ndarray
+    task_ids: np.ndarray
+
+
 class CheckpointMetadata(TypedDict):
     timestamp: str
     step: int

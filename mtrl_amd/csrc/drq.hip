@@ -492,6 +492,29 @@ __global__ void c51_target_kernel(const float* __restrict__ hc_on, const float* 
   if (lane == 0) a_next[b] = besta;
 }
 
+// expected Q per action (drqeps.py:80-84: softmax over atoms . support), one wave per sample
+__global__ void q_values_kernel(const float* __restrict__ hc, int ldh, const float* __restrict__ hb, int A, int Z,
+                                float vmin, float vmax, float* __restrict__ q, int B) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= B) return;
+  const float* h = hc + (long long)b * ldh;
+  const bool zl = lane < Z;
+  const float sup = vmin + (vmax - vmin) / (float)(Z - 1) * (float)lane;
+  float madv = 0.f;
+  if (zl) {
+    for (int a = 0; a < A; ++a) madv += h[a * Z + lane] + hb[a * Z + lane];
+    madv /= (float)A;
+  }
+  for (int a = 0; a < A; ++a) {
+    const float l = zl ? head_logit(h, hb, A, Z, a, lane, madv) : -INFINITY;
+    const float mx = wmax(l);
+    const float e = zl ? expf(l - mx) : 0.f;
+    const float se = wsum(e);
+    const float qa = wsum(zl ? (e / se) * sup : 0.f);
+    if (lane == 0) q[(long long)b * A + a] = qa;
+  }
+}
+
 // Cross entropy at the taken action and its gradient (drqeps.py:300-309): per sample
 // loss_b = -sum_z m log_softmax(logit[act]); d logit[act] = (softmax sum(m) - m) / B, then through
 // the dueling combination: d val = d logit[act], d adv[a] = d logit[act] (delta(a, act) - 1 / A).
@@ -758,6 +781,11 @@ void c51_target(const float* hc_on, const float* hc_tg, int ldh, const float* hb
                 int B, hipStream_t st) {
   hipLaunchKernelGGL(c51_target_kernel, dim3((B + 3) / 4), dim3(256), 0, st, hc_on, hc_tg, ldh, hb_on, hb_tg, A, Z, rew,
                      done, gamma_n, vmin, vmax, m, a_next, B);
+}
+
+void q_values(const float* hc, int ldh, const float* hb, int A, int Z, float vmin, float vmax, float* q, int B,
+              hipStream_t st) {
+  hipLaunchKernelGGL(q_values_kernel, dim3((B + 3) / 4), dim3(256), 0, st, hc, ldh, hb, A, Z, vmin, vmax, q, B);
 }
 
 void c51_loss(const float* hc, int ldh, const float* hb, int A, int Z, const int* act, const float* m, float* dh,

@@ -90,7 +90,8 @@ struct drq_engine {
   // ------------------------------------------------------------------ forward
   // ImpalaDQN at params P on augmented images X -> combined head output out[B][NC] (no bias);
   // the saved activations of the backward are written in every pass (the s pass runs last)
-  void forward(const float* P, const float* X, float* out) {
+  void forward(const float* P, const float* X, float* out) { forward_rows(P, X, out, B); }
+  void forward_rows(const float* P, const float* X, float* out, int B) {  // B: rows (<= the batch)
     const float* x = X;
     for (int s = 0; s < 3; ++s) {
       Stack& k = stk[s];
@@ -111,6 +112,13 @@ struct drq_engine {
     gemm_store(h2, H, P + off_wc, NC, out, NC, B, NC, H, GEMM_NN);
   }
   int cfg_blocks() const { return 2; }
+
+  // expected Q of the online network on n (<= batch) staged observations (rollout actions)
+  void q_values(int n, float* q) {
+    drq::augment(obs_u8, crop_o, noise_o, stk[0].xin_own, n, cfg.in_ch, cfg.hw, cfg.hw, 4, st);
+    forward_rows(p, stk[0].xin_own, hc_on, n);
+    drq::q_values(hc_on, NC, p + off_bc, A, Z, cfg.v_min, cfg.v_max, q, n, st);
+  }
 
   // C[M][N] = A . op(B) with split-K over the few row tiles a batch of 256 gives (EPI_STORE)
   void gemm_store(const float* Aop, int lda, const float* Bop, int ldb, float* C, int ldc, int M, int N, int K,
@@ -415,6 +423,23 @@ int drq_update_resident(drq_engine* e, int steps) {
   if (!e || steps < 0) return fail(-22, "bad argument");
   for (int i = 0; i < steps; ++i) e->step();
   return hipGetLastError() == hipSuccess ? 0 : fail(-5, "kernel launch failed");
+}
+
+int drq_q_values(drq_engine* e, const unsigned char* obs, const int* task_ids, const int* crop, const float* noise,
+                 int n, float* q) {
+  if (!e || !q) return fail(-22, "null argument");
+  if (n < 1 || n > e->B) return fail(-22, "n must be in [1, batch]");
+  const size_t img = (size_t)n * e->cfg.in_ch * e->cfg.hw * e->cfg.hw;
+  int rc;
+  if ((rc = copy_in(e->obs_u8, obs, img, e->st)) || (rc = copy_in(e->task, task_ids, sizeof(int) * n, e->st)) ||
+      (rc = copy_in(e->crop_o, crop, sizeof(int) * 2 * n, e->st)) ||
+      (rc = copy_in(e->noise_o, noise, sizeof(float) * n, e->st)))
+    return rc;
+  e->q_values(n, e->m);  // m (B x Z floats) as scratch for the n x A values
+  if (hipMemcpyAsync(q, e->m, sizeof(float) * (size_t)n * e->A, hipMemcpyDefault, e->st) != hipSuccess ||
+      hipStreamSynchronize(e->st) != hipSuccess)
+    return fail(-5, "q download failed");
+  return 0;
 }
 
 int drq_get_logs(drq_engine* e, float* out) {

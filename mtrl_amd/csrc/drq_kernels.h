@@ -39,6 +39,9 @@ void colsum_rows(const float* x, int ld, int F, int B, float* out, hipStream_t s
 void c51_target(const float* hc_on, const float* hc_tg, int ldh, const float* hb_on, const float* hb_tg, int A, int Z,
                 const float* rew, const float* done, float gamma_n, float vmin, float vmax, float* m, int* a_next,
                 int B, hipStream_t st);
+// expected Q per action: q[b][a] = softmax_z(logit[b][a]) . support
+void q_values(const float* hc, int ldh, const float* hb, int A, int Z, float vmin, float vmax, float* q, int B,
+              hipStream_t st);
 void c51_loss(const float* hc, int ldh, const float* hb, int A, int Z, const int* act, const float* m, float* dh,
               float* loss_b, float* logit_b, int B, hipStream_t st);
 void embed_bwd(const float* dfeat, int ldf, int off, const float* emb, int D, const int* task, int B, int T,

@@ -101,6 +101,17 @@ class DrQEngine:
         self._keep = arrs  # alive until the copies on the engine's stream have run
         self.synchronize()
 
+    def q_values(self, obs, task_ids, crop, noise) -> np.ndarray:
+        """Expected Q [n][A] of the online network on augmented observations (n <= batch)."""
+        o = np.ascontiguousarray(obs, np.uint8)
+        t = np.ascontiguousarray(task_ids, np.int32)
+        c = np.ascontiguousarray(crop, np.int32)
+        z = np.ascontiguousarray(noise, np.float32)
+        n = o.shape[0]
+        q = np.empty((n, self.s.n_actions), np.float32)
+        _drq_check(self.lib.drq_q_values(self.h, _ptr(o), _ptr(t), _ptr(c), _ptr(z), n, _ptr(q)))
+        return q
+
     def update_resident(self, steps: int):
         _drq_check(self.lib.drq_update_resident(self.h, int(steps)))
 

@@ -1,0 +1,71 @@
+"""DrQ-eps path on CPU: the oracle's pieces against independent restatements (max-pool SAME
+padding, C51 projection mass, LayerNorm), the product-side parameter layout (mtrl_amd/drq_init.py)
+against the oracle's flax ravel order, and the compat API surface (mtrl.rl.algorithms.DrQConfig,
+experiments/atari.py's config tree)."""
+
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from oracle import drq as od
+
+
+def test_param_layout_matches_oracle():
+    from mtrl_amd.drq_init import init_drq, param_spec
+
+    cfg = od.DrQConfig()
+    assert param_spec() == od.param_spec(cfg)
+    assert od.n_params(cfg) == 1535697 == init_drq(3).size
+    small = od.DrQConfig(hw=20, n_hidden=64, scale=1)
+    assert param_spec(hw=20, n_hidden=64) == od.param_spec(small)
+
+
+def test_max_pool_same_padding():
+    x = torch.arange(2 * 5 * 5 * 3, dtype=torch.float64).reshape(2, 5, 5, 3) * ((-1) ** torch.arange(150).reshape(2, 5, 5, 3))
+    y = od._max_pool(x)
+    assert y.shape == (2, 3, 3, 3)
+    # SAME for 5 -> 3 with k 3 / s 2: total pad 2, lo 1: window rows of output 0 are -1..1
+    xn = x.numpy()
+    for b in range(2):
+        for oy in range(3):
+            for ox in range(3):
+                ys, xs = slice(max(2 * oy - 1, 0), 2 * oy + 2), slice(max(2 * ox - 1, 0), 2 * ox + 2)
+                np.testing.assert_array_equal(y[b, oy, ox].numpy(), xn[b, ys, xs].reshape(-1, 3).max(0))
+
+
+def test_c51_projection_conserves_mass_off_the_grid():
+    cfg = od.DrQConfig()
+    B = 6
+    lo = torch.randn(B, cfg.n_actions, cfg.n_atoms, dtype=torch.float64)
+    lt = torch.randn(B, cfg.n_actions, cfg.n_atoms, dtype=torch.float64)
+    rew = torch.tensor([0.013, -0.37, 1.21, 0.5, 0.0, 0.2], dtype=torch.float64)
+    done = torch.tensor([0.0, 0.0, 0.0, 1.0, 1.0, 0.0], dtype=torch.float64)
+    m, _ = od.c51_target(lo, lt, rew, done, cfg)
+    s = m.sum(-1).numpy()
+    # off-grid targets keep their mass; a terminal reward on an atom (0.0 -> b = 25 exactly) drops it,
+    # as the reference's two scatter-adds do (l == u contributes (u - b) = (b - l) = 0)
+    np.testing.assert_allclose(s[[0, 1, 2, 5]], 1.0, rtol=1e-12)
+    assert abs(s[4]) < 1e-15
+
+
+def test_compat_config_tree():
+    import mtrl  # noqa: F401
+    from mtrl.config.networks import ImpalaDQNConfig, QValueFunctionConfig
+    from mtrl.config.nn import ImpalaEncoderConfig, VanillaNetworkConfig
+    from mtrl.config.optim import OptimizerConfig
+    from mtrl.config.rl import DrQTrainingConfig
+    from mtrl.config.utils import Optimizer
+    from mtrl.envs import AtariConfig
+    from mtrl.rl.algorithms import DrQ, DrQConfig, get_algorithm_for_config
+
+    c = DrQConfig(num_tasks=26, gamma=0.99, critic_config=ImpalaDQNConfig(
+        impala_config=ImpalaEncoderConfig(scale=1),
+        q_function_config=QValueFunctionConfig(use_classification=True, num_atoms=101, network_config=VanillaNetworkConfig(
+            optimizer=OptimizerConfig(lr=1e-4, optimizer=Optimizer.AdamW, eps=1.5e-4, weight_decay=0.05)))))
+    assert get_algorithm_for_config(c) is DrQ
+    assert (c.n_atoms, c.v_min, c.v_max, c.tau, c.eps_decay_steps) == (51, -10.0, 10.0, 0.005, 5000)
+    t = DrQTrainingConfig(total_steps=26 * 100_000, normalize_rewards=True, buffer_size=26 * 100_000)
+    assert (t.batch_size, t.nstep, t.replay_ratio) == (256, 3, 2)
+    env = AtariConfig()
+    assert env.observation_space.shape == (4, 84, 84) and env.action_space.n == 18

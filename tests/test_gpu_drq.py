@@ -104,3 +104,47 @@ def test_deterministic():
         e.close()
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     assert outs[0][1] == outs[1][1]
+
+
+def test_q_values_match_oracle():
+    import torch
+
+    from mtrl_amd import _lib as L
+
+    cfg = od.DrQConfig(hw=84, n_hidden=512)
+    st = od.init_state(cfg, 5)
+    e = _engine(cfg, 16)
+    e.set_params(L.DRQ_PARAMS, st.params)
+    (obs, _, _, _, _, task), (co, no, _, _) = _batch(cfg, 11, 6)
+    q = e.q_values(obs, task, co, no)
+    with torch.no_grad():
+        lg = od.forward(od.unflatten(torch.as_tensor(st.params.astype(np.float32).astype(np.float64)), cfg),
+                        torch.as_tensor(od.augment(obs, co, no).astype(np.float64)), torch.as_tensor(task.astype(np.int64)), cfg)
+        sup = torch.linspace(cfg.v_min, cfg.v_max, cfg.n_atoms, dtype=torch.float64)
+        want = (torch.softmax(lg, -1) * sup).sum(-1).numpy()
+    np.testing.assert_allclose(q, want, rtol=1e-5, atol=1e-5)
+    e.close()
+
+
+def test_compat_drq_api():
+    import mtrl  # noqa: F401
+    from mtrl.envs import AtariConfig
+    from mtrl.rl.algorithms import DrQ, DrQConfig
+    from mtrl_amd.compat.types import AtariReplayBufferSamples
+
+    agent = DrQ.initialize(DrQConfig(num_tasks=26), AtariConfig(), seed=1, batch_size=32)
+    assert agent.get_num_params()["critic_num_params"] == 1535697
+    rng = np.random.default_rng(0)
+    obs = rng.integers(0, 256, (26, 4, 84, 84), dtype=np.uint8)
+    agent, a = agent.sample_action(obs, np.arange(26))
+    assert a.shape == (26,) and a.min() >= 0 and a.max() < 18 and agent.step == 26
+    g = agent.eval_action(obs, np.arange(26))
+    assert g.shape == (26,)
+    data = AtariReplayBufferSamples(rng.integers(0, 256, (32, 4, 84, 84), dtype=np.uint8), rng.integers(0, 18, (32, 1)),
+                                    rng.integers(0, 256, (32, 4, 84, 84), dtype=np.uint8), np.zeros((32, 1)),
+                                    np.zeros((32, 1)), rng.standard_normal((32, 1)), np.arange(32) % 26)
+    agent, logs = agent.update(data)
+    assert set(logs) == {"losses/online_logits", "metrics/critic_grad_magnitude", "metrics/critic_params_norm",
+                         "losses/critic_loss"}
+    assert all(np.isfinite(v) for v in logs.values())
+    agent.close()
