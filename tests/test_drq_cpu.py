@@ -39,13 +39,13 @@ def test_c51_projection_conserves_mass_off_the_grid():
     B = 6
     lo = torch.randn(B, cfg.n_actions, cfg.n_atoms, dtype=torch.float64)
     lt = torch.randn(B, cfg.n_actions, cfg.n_atoms, dtype=torch.float64)
-    rew = torch.tensor([0.013, -0.37, 1.21, 0.5, 0.0, 0.2], dtype=torch.float64)
+    rew = torch.tensor([0.013, -0.17, 0.21, 0.5, 0.0, 0.05], dtype=torch.float64)
     done = torch.tensor([0.0, 0.0, 0.0, 1.0, 1.0, 0.0], dtype=torch.float64)
     m, _ = od.c51_target(lo, lt, rew, done, cfg)
     s = m.sum(-1).numpy()
-    # off-grid targets keep their mass; a terminal reward on an atom (0.0 -> b = 25 exactly) drops it,
-    # as the reference's two scatter-adds do (l == u contributes (u - b) = (b - l) = 0)
-    np.testing.assert_allclose(s[[0, 1, 2, 5]], 1.0, rtol=1e-12)
+    # unclipped off-grid targets keep their mass; a terminal reward on an atom (0.0 -> b = 25
+    # exactly) drops it, as the reference's two scatter-adds do (l == u: (u - b) = (b - l) = 0)
+    np.testing.assert_allclose(s[[0, 1, 2, 3, 5]], 1.0, rtol=1e-12)
     assert abs(s[4]) < 1e-15
 
 
