@@ -239,31 +239,32 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
   if (t < CO) pp[NW + t] = bacc;
 }
 
-// dw[e] / db[e - nw] = sum_g part[g][e] (e < n): block of 64 entries x 4 lanes of g (g = lane
-// group + 4 j, 8 loads in flight), double accumulation, the 4 groups added in order
+// dw[e] / db[e - nw] = sum_g part[g][e] (e < n): block of 16 entries x 16 lane groups over g
+// (g = group + 16 j, 8 loads in flight), double accumulation, the groups added in order
 __global__ __launch_bounds__(256) void sum_parts_kernel(const float* __restrict__ part, int G, int n,
                                                         float* __restrict__ dst_w, float* __restrict__ dst_b, int nw) {
-  __shared__ double red[4][64];
-  const int el = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int e = blockIdx.x * 64 + el;
+  __shared__ double red[16][16];
+  const int el = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int e = blockIdx.x * 16 + el;
   double s = 0.0;
   if (e < n) {
     int g = grp;
-    for (; g + 28 < G; g += 32) {
+    for (; g + 112 < G; g += 128) {
       float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(long long)(g + 4 * u) * n + e];
+      for (int u = 0; u < 8; ++u) v[u] = part[(long long)(g + 16 * u) * n + e];
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += (double)v[u];
     }
-    for (; g < G; g += 4) s += (double)part[(long long)g * n + e];
+    for (; g < G; g += 16) s += (double)part[(long long)g * n + e];
   }
   red[grp][el] = s;
   __syncthreads();
   if (grp == 0 && e < n) {
-    const float r = (float)(((red[0][el] + red[1][el]) + red[2][el]) + red[3][el]);
-    if (e < nw) dst_w[e] = r;
-    else dst_b[e - nw] = r;
+    double t = red[0][el];
+    for (int k = 1; k < 16; ++k) t += red[k][el];
+    if (e < nw) dst_w[e] = (float)t;
+    else dst_b[e - nw] = (float)t;
   }
 }
 
@@ -400,32 +401,46 @@ __global__ void ln_bwd_kernel(const float* __restrict__ dy, int lddy, const floa
   }
 }
 
-// dscale[i] = sum_b dy xhat, dbias[i] = sum_b dy (masked like ln_bwd), rows in order per column
+// dscale[i] = sum_b dy xhat, dbias[i] = sum_b dy (masked like ln_bwd): block of 64 columns x 4 row
+// groups (rows g, g + 4, ...), the groups added in order
 template <bool RELU>
-__global__ void ln_param_grad_kernel(const float* __restrict__ dy, int lddy, const float* __restrict__ y, int ldy,
-                                     const float* __restrict__ xhat, int F, int B, float* __restrict__ dscale,
-                                     float* __restrict__ dbias, float* __restrict__ dxb) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= F) return;
+__global__ __launch_bounds__(256) void ln_param_grad_kernel(const float* __restrict__ dy, int lddy,
+                                                            const float* __restrict__ y, int ldy,
+                                                            const float* __restrict__ xhat, int F, int B,
+                                                            float* __restrict__ dscale, float* __restrict__ dbias) {
+  __shared__ float red[2][4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + cl;
   float a = 0.f, c = 0.f;
-  for (int b = 0; b < B; ++b) {
-    float d = dy[(long long)b * lddy + i];
-    if (RELU && !(y[(long long)b * ldy + i] > 0.f)) d = 0.f;
-    a += d * xhat[(long long)b * F + i];
-    c += d;
+  if (i < F) {
+    for (int b = grp; b < B; b += 4) {
+      float d = dy[(long long)b * lddy + i];
+      if (RELU && !(y[(long long)b * ldy + i] > 0.f)) d = 0.f;
+      a += d * xhat[(long long)b * F + i];
+      c += d;
+    }
   }
-  dscale[i] = a;
-  dbias[i] = c;
-  (void)dxb;
+  red[0][grp][cl] = a;
+  red[1][grp][cl] = c;
+  __syncthreads();
+  if (grp == 0 && i < F) {
+    dscale[i] = ((red[0][0][cl] + red[0][1][cl]) + red[0][2][cl]) + red[0][3][cl];
+    dbias[i] = ((red[1][0][cl] + red[1][1][cl]) + red[1][2][cl]) + red[1][3][cl];
+  }
 }
 
-// column sums (the Dense_0 bias grad) of x[B][ld] over F columns
-__global__ void colsum_rows_kernel(const float* __restrict__ x, int ld, int F, int B, float* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= F) return;
+// column sums (the Dense_0 bias grad) of x[B][ld] over F columns, 4 row groups added in order
+__global__ __launch_bounds__(256) void colsum_rows_kernel(const float* __restrict__ x, int ld, int F, int B,
+                                                          float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (int b = 0; b < B; ++b) s += x[(long long)b * ld + i];
-  out[i] = s;
+  if (i < F)
+    for (int b = grp; b < B; b += 4) s += x[(long long)b * ld + i];
+  red[grp][cl] = s;
+  __syncthreads();
+  if (grp == 0 && i < F) out[i] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
 }
 
 // ------------------------------------------------------------------ dueling head + C51
@@ -711,7 +726,9 @@ void conv_bwd_data(const float* dout, const float* w, const float* mask, const f
 #undef C_BD
 }
 
-int conv_wgrad_blocks(long long npix) { return (int)std::min<long long>(512, std::max<long long>(1, (npix + 63) / 64)); }
+// enough 64-pixel tiles in flight per CU to cover the staging loads' latency (the partials'
+// reduction is cheap next to them)
+int conv_wgrad_blocks(long long npix) { return (int)std::min<long long>(2048, std::max<long long>(1, (npix + 63) / 64)); }
 
 void conv_wgrad(const float* in, const float* dout, float* part, float* dw, float* db, int B, int H, int W, int ci,
                 int co, bool relu_in, hipStream_t st) {
@@ -724,7 +741,7 @@ void conv_wgrad(const float* in, const float* dout, float* part, float* dw, floa
   CONV_CASES(C_WG)
 #undef C_WG
   const int nw = 9 * ci * co, n = nw + co;
-  hipLaunchKernelGGL(sum_parts_kernel, dim3((n + 63) / 64), dim3(256), 0, st, part, G, n, dw, db, nw);
+  hipLaunchKernelGGL(sum_parts_kernel, dim3((n + 15) / 16), dim3(256), 0, st, part, G, n, dw, db, nw);
 }
 
 void maxpool_fwd(const float* in, float* out, unsigned char* arg, int B, int H, int W, int C, hipStream_t st) {
@@ -762,18 +779,18 @@ void ln_bwd(const float* dy, int lddy, const float* y, int ldy, const float* xha
   if (relu) {
     hipLaunchKernelGGL(ln_bwd_kernel<true>, dim3((B + 3) / 4), dim3(256), 0, st, dy, lddy, y, ldy, xhat, rstd, scale, F,
                        dx, lddx, B);
-    hipLaunchKernelGGL(ln_param_grad_kernel<true>, dim3(blocks(F)), dim3(256), 0, st, dy, lddy, y, ldy, xhat, F, B,
-                       dscale, dbias, nullptr);
+    hipLaunchKernelGGL(ln_param_grad_kernel<true>, dim3((F + 63) / 64), dim3(256), 0, st, dy, lddy, y, ldy, xhat, F,
+                       B, dscale, dbias);
   } else {
     hipLaunchKernelGGL(ln_bwd_kernel<false>, dim3((B + 3) / 4), dim3(256), 0, st, dy, lddy, y, ldy, xhat, rstd, scale,
                        F, dx, lddx, B);
-    hipLaunchKernelGGL(ln_param_grad_kernel<false>, dim3(blocks(F)), dim3(256), 0, st, dy, lddy, y, ldy, xhat, F, B,
-                       dscale, dbias, nullptr);
+    hipLaunchKernelGGL(ln_param_grad_kernel<false>, dim3((F + 63) / 64), dim3(256), 0, st, dy, lddy, y, ldy, xhat, F,
+                       B, dscale, dbias);
   }
 }
 
 void colsum_rows(const float* x, int ld, int F, int B, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(colsum_rows_kernel, dim3(blocks(F)), dim3(256), 0, st, x, ld, F, B, out);
+  hipLaunchKernelGGL(colsum_rows_kernel, dim3((F + 63) / 64), dim3(256), 0, st, x, ld, F, B, out);
 }
 
 void c51_target(const float* hc_on, const float* hc_tg, int ldh, const float* hb_on, const float* hb_tg, int A, int Z,
