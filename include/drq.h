@@ -37,6 +37,9 @@ typedef struct drq_config {
   int nstep;        /* 3 */
   float gamma, v_min, v_max, tau;                 /* 0.99, -10, 10, 0.005 */
   float lr, b1, b2, eps, weight_decay, ln_eps;    /* 1e-4, 0.9, 0.999, 1.5e-4, 0.05, 1e-6 */
+  long long capacity;     /* replay slots per task (0: no device buffer; buffer_size / num_tasks) */
+  int normalize_rewards;  /* per-task min-max reward normalisation at sample time */
+  int reserved;
 } drq_config;
 
 typedef struct drq_engine drq_engine;
@@ -82,6 +85,23 @@ int drq_update_resident(drq_engine* e, int steps);
  * of (drqeps.py:56-97); epsilon-greedy stays with the caller's RNG.  Synchronous. */
 int drq_q_values(drq_engine* e, const unsigned char* obs, const int* task_ids, const int* crop, const float* noise,
                  int n, float* q);
+/* The device replay buffer, MemoryEfficientAtariMultiTaskReplayBuffer (mtrl/rl/buffers.py:949-1229):
+ * one uint8 frame-stack array [capacity][num_tasks][in_ch][hw][hw] holds obs and next_obs (nstep
+ * slots ahead).  add: one env step of all tasks (host pointers; the n-step ring runs on the host
+ * exactly as buffers.py:1048-1186 does).  The index stream is numpy's Generator (PCG64) whose state
+ * drq_rng_set takes (bit_generator.state), reproduced bit for bit on the device. */
+int drq_buffer_add(drq_engine* e, const unsigned char* obs, const unsigned char* next_obs, const int* action,
+                   const float* reward, const float* truncate, const float* done);
+int drq_buffer_state(drq_engine* e, long long* pos, int* full);
+int drq_rng_set(drq_engine* e, unsigned long long state_hi, unsigned long long state_lo, unsigned long long inc_hi,
+                unsigned long long inc_lo, int has_uint32, unsigned int uinteger);
+/* sample(batch) from the device buffer into the engine's staged batch (batch % num_tasks == 0) */
+int drq_sample(drq_engine* e);
+/* `steps` x (sample + update): DrQ's training step with the batch drawn on the device */
+int drq_sample_update(drq_engine* e, int steps);
+/* the staged batch (tests): uint8 obs / next_obs, actions, rewards, dones, truncations, task ids */
+int drq_read_batch(drq_engine* e, unsigned char* obs, unsigned char* next_obs, int* actions, float* rewards,
+                   float* dones, float* truncations, int* task_ids);
 int drq_get_logs(drq_engine* e, float* out /* DRQ_NUM_LOGS */);
 int drq_synchronize(drq_engine* e);
 const char* drq_last_error(void);

@@ -162,7 +162,8 @@ class DrqConfig(ctypes.Structure):  # include/drq.h
     _fields_ = [(n, ctypes.c_int32) for n in ("num_tasks", "n_actions", "n_atoms", "in_ch", "hw", "scale",
                                               "embed_dim", "n_hidden", "batch", "nstep")] + \
                [(n, ctypes.c_float) for n in ("gamma", "v_min", "v_max", "tau", "lr", "b1", "b2", "eps",
-                                              "weight_decay", "ln_eps")]
+                                              "weight_decay", "ln_eps")] + \
+               [("capacity", ctypes.c_int64), ("normalize_rewards", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class DrqBatch(ctypes.Structure):
@@ -186,6 +187,12 @@ SIGNATURES.update({
     "drq_update_resident": (ctypes.c_int, [P, ctypes.c_int]),
     "drq_get_logs": (ctypes.c_int, [P, P]),
     "drq_q_values": (ctypes.c_int, [P, P, P, P, P, ctypes.c_int, P]),
+    "drq_buffer_add": (ctypes.c_int, [P, P, P, P, P, P, P]),
+    "drq_buffer_state": (ctypes.c_int, [P, PI64, PI32]),
+    "drq_rng_set": (ctypes.c_int, [P, U64, U64, U64, U64, ctypes.c_int, U32]),
+    "drq_sample": (ctypes.c_int, [P]),
+    "drq_sample_update": (ctypes.c_int, [P, ctypes.c_int]),
+    "drq_read_batch": (ctypes.c_int, [P, P, P, P, P, P, P, P]),
     "drq_synchronize": (ctypes.c_int, [P]),
 })
 

@@ -51,6 +51,59 @@ __global__ void augment_kernel(const unsigned char* __restrict__ obs, const int*
   out[i] = ((v / 255.0f - 0.5f) * 2.0f) * noise[b];
 }
 
+// ------------------------------------------------------------------ Atari replay sample
+// MemoryEfficientAtariMultiTaskReplayBuffer.sample (buffers.py:1188-1227) from the device store:
+// row b = (sample i = b / T, task t = b % T); draw k = idx[i] -> slot via the guard window
+// (_sample_indices, buffers.py:1082-1105); next_obs = the frame stack nstep slots ahead; rewards
+// min-max normalised in double per task; task_ids as the reference lists them (b / n).
+struct AtariSampleParams {
+  const unsigned char* store;  // [cap][T][img]
+  const int* act;
+  const float *rew, *done, *trunc;  // [cap][T]
+  const double* minmax;        // [2][T] (normalize) or null
+  const int* idx;
+  long long cap;
+  int T, n, img16, nstep, full, pos, guard;
+  double eps;
+  unsigned char *obs, *nobs;
+  int *act_out, *task_out;
+  float *rew_out, *done_out, *trunc_out;
+};
+
+__global__ void atari_sample_kernel(AtariSampleParams p) {
+  const int b = blockIdx.y;
+  const int i = b / p.T, t = b - i * p.T;
+  const long long k = p.idx[i];
+  long long slot = k;
+  if (p.full) {
+    if (p.pos + p.guard <= p.cap) slot = k < p.pos ? k : k + p.guard;
+    else slot = k + (p.pos + p.guard - p.cap);
+  }
+  const long long nslot = (slot + p.nstep) % p.cap;
+  const uint4* src = reinterpret_cast<const uint4*>(p.store) + (slot * p.T + t) * p.img16;
+  const uint4* nsrc = reinterpret_cast<const uint4*>(p.store) + (nslot * p.T + t) * p.img16;
+  uint4* dst = reinterpret_cast<uint4*>(p.obs) + (long long)b * p.img16;
+  uint4* ndst = reinterpret_cast<uint4*>(p.nobs) + (long long)b * p.img16;
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < p.img16; c += gridDim.x * blockDim.x) {
+    dst[c] = src[c];
+    ndst[c] = nsrc[c];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const long long r = slot * p.T + t;
+    p.act_out[b] = p.act[r];
+    float rw = p.rew[r];
+    if (p.minmax) {  // rewards -= mn; rewards /= (mx - mn + eps): float64 ops, float32 storage
+      const double mn = p.minmax[t], mx = p.minmax[p.T + t];
+      rw = (float)((double)rw - mn);
+      rw = (float)((double)rw / (mx - mn + p.eps));
+    }
+    p.rew_out[b] = rw;
+    p.done_out[b] = p.done[r];
+    p.trunc_out[b] = p.trunc[r];
+    p.task_out[b] = b / p.n;  // np.repeat(np.arange(T), n)
+  }
+}
+
 // ------------------------------------------------------------------ convolutions
 // out[b][y][x][:] = bias + sum_{dy,dx,ci} act(in[b][y+dy-1][x+dx-1][ci]) w[dy][dx][ci][:]
 // (+ res[b][y][x][:]); act = relu when RELU_IN.  One lane per output pixel.
@@ -679,6 +732,15 @@ __global__ void drq_logs_kernel(const float* __restrict__ part, int G, const flo
 
 // ------------------------------------------------------------------ launchers
 static unsigned blocks(long long n, int t = 256) { return (unsigned)((n + t - 1) / t); }
+
+void atari_sample(const unsigned char* store, const int* act, const float* rew, const float* done, const float* trunc,
+                  const double* minmax, const int* idx, long long cap, int T, int n, int img_bytes, int nstep,
+                  int full, int pos, int guard, double eps, unsigned char* obs, unsigned char* nobs, int* act_out,
+                  float* rew_out, float* done_out, float* trunc_out, int* task_out, hipStream_t st) {
+  AtariSampleParams p{store, act, rew, done, trunc, minmax, idx, cap, T, n, img_bytes / 16, nstep, full, pos, guard,
+                      eps, obs, nobs, act_out, task_out, rew_out, done_out, trunc_out};
+  hipLaunchKernelGGL(atari_sample_kernel, dim3(4, n * T), dim3(256), 0, st, p);
+}
 
 void augment(const unsigned char* obs, const int* crop, const float* noise, float* out, int B, int C, int H, int W,
              int pad, hipStream_t st) {

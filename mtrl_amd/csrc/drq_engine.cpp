@@ -23,6 +23,8 @@
 
 using namespace mtsac;
 
+extern "C" int pcg_jump_table(unsigned long long* out);  // engine.cpp: numpy PCG64 jumps
+
 namespace {
 
 thread_local std::string g_err;
@@ -76,6 +78,20 @@ struct drq_engine {
   float *wpart = nullptr, *ws = nullptr, *part = nullptr, *loss_b = nullptr, *logit_b = nullptr, *logs = nullptr;
   long long ws_floats = 0;
   std::vector<void*> allocs;
+  // ---- device replay buffer (MemoryEfficientAtariMultiTaskReplayBuffer)
+  long long cap = 0, img = 0, pos = 0;
+  int full = 0, ns_pos = 0, ns_count = 0, n_per_task = 0;
+  unsigned char* store = nullptr;
+  int* b_act = nullptr;
+  float *b_rew = nullptr, *b_done = nullptr, *b_trunc = nullptr, *trunc = nullptr;
+  double* d_minmax = nullptr;
+  PcgDev* rng = nullptr;
+  unsigned long long* jump = nullptr;
+  int* idx = nullptr;
+  std::vector<unsigned char> ns_obs, ns_next;  // [nstep][T][img]
+  std::vector<int> ns_act;
+  std::vector<float> ns_rew, ns_trunc, ns_done;  // [nstep][T]
+  std::vector<double> minmax;                    // [2][T]: min, max
 
   template <class T_>
   int alloc(T_** ptr, long long n) {
@@ -143,6 +159,77 @@ struct drq_engine {
     gp.splits = gemm_splits(M, N, B, 1);
     gp.ws = ws;
     gemm_f32(gp, GEMM_TN, EPI_STORE, 1, st);
+  }
+
+  // ------------------------------------------------------------------ replay
+  // add (buffers.py:1138-1186): n-step ring on the host, the aggregated transition to the device
+  int buffer_add(const unsigned char* o, const unsigned char* no, const int* a, const float* r, const float* tr,
+                 const float* d) {
+    const int n = cfg.nstep;
+    const size_t row = (size_t)T * img;
+    const int sl = ns_pos;
+    std::memcpy(&ns_obs[sl * row], o, row);
+    std::memcpy(&ns_next[sl * row], no, row);
+    for (int t = 0; t < T; ++t) {
+      ns_act[sl * T + t] = a[t];
+      ns_rew[sl * T + t] = r[t];
+      ns_trunc[sl * T + t] = tr[t];
+      ns_done[sl * T + t] = d[t];
+    }
+    ns_pos = (sl + 1) % n;
+    ns_count = std::min(ns_count + 1, n);
+    if (ns_count < n) return 0;
+    // _get_nstep_info (buffers.py:1048-1080): float32 arithmetic in the reference's order
+    const int oldest = ns_pos, newest = (ns_pos - 1 + n) % n;
+    std::vector<float> rw(&ns_rew[newest * T], &ns_rew[newest * T] + T), dn(&ns_done[newest * T], &ns_done[newest * T] + T);
+    std::vector<int> src(T, newest);  // which ring slot's next_obs each task takes
+    const float g = cfg.gamma;
+    for (int k = 1; k < n; ++k) {
+      const int i = ((ns_pos - 1 - k) % n + n) % n;
+      for (int t = 0; t < T; ++t) {
+        float v = rw[t] * g;
+        v = v * (1.0f - ns_done[i * T + t]);
+        rw[t] = v + ns_rew[i * T + t];
+        if (ns_done[i * T + t] > 0.0f) {
+          src[t] = i;
+          dn[t] = ns_done[i * T + t];
+        }
+      }
+    }
+    const long long p = pos, pn = (pos + n) % cap;
+    std::vector<unsigned char> nxt(row);
+    for (int t = 0; t < T; ++t) std::memcpy(&nxt[(size_t)t * img], &ns_next[(size_t)src[t] * row + (size_t)t * img], img);
+    if (hipMemcpyAsync(store + (size_t)p * row, &ns_obs[(size_t)oldest * row], row, hipMemcpyHostToDevice, st) !=
+            hipSuccess ||
+        hipMemcpyAsync(store + (size_t)pn * row, nxt.data(), row, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(b_act + p * T, &ns_act[oldest * T], sizeof(int) * T, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(b_rew + p * T, rw.data(), sizeof(float) * T, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(b_done + p * T, dn.data(), sizeof(float) * T, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(b_trunc + p * T, &ns_trunc[oldest * T], sizeof(float) * T, hipMemcpyHostToDevice, st) !=
+            hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)  // the host staging above is stack / ring memory
+      return fail(-5, "buffer upload failed");
+    if (cfg.normalize_rewards)
+      for (int t = 0; t < T; ++t) {
+        minmax[t] = std::min(minmax[t], (double)rw[t]);
+        minmax[T + t] = std::max(minmax[T + t], (double)rw[t]);
+      }
+    pos = (p + 1) % cap;
+    if (pos == 0) full = 1;
+    return 0;
+  }
+
+  // sample (buffers.py:1188-1227) into the staged batch
+  int sample() {
+    const int n = n_per_task, guard = cfg.nstep + 6;
+    const long long high = full ? cap - guard : std::max(pos - cfg.nstep, 1LL);
+    replay_indices_high(rng, jump, high, n, idx, st);
+    if (cfg.normalize_rewards &&
+        hipMemcpyAsync(d_minmax, minmax.data(), sizeof(double) * 2 * T, hipMemcpyHostToDevice, st) != hipSuccess)
+      return fail(-5, "reward stats upload failed");
+    drq::atari_sample(store, b_act, b_rew, b_done, b_trunc, cfg.normalize_rewards ? d_minmax : nullptr, idx, cap, T, n,
+                      (int)img, cfg.nstep, full, (int)pos, guard, 1e-8, obs_u8, nobs_u8, act, rew, done, trunc, task, st);
+    return 0;
   }
 
   // ------------------------------------------------------------------ one update on the staged batch
@@ -338,6 +425,36 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
                            gemm_ws_floats(B, F, 1, gemm_splits(B, F, H, 1))});
   if ((rc = e->alloc(&e->ws, e->ws_floats))) return bad(rc);
   if ((rc = e->alloc(&e->part, 2 * 1024)) || (rc = e->alloc(&e->logs, DRQ_NUM_LOGS))) return bad(rc);
+  if ((rc = e->alloc(&e->trunc, B))) return bad(rc);
+  e->img = (long long)c->in_ch * c->hw * c->hw;
+  if (c->capacity > 0) {
+    if (c->capacity <= c->nstep + 6 || c->nstep < 1 || B % e->T != 0 || e->img % 16 != 0 || c->capacity > (1LL << 30))
+      return bad(fail(-22, "buffer: capacity > nstep + 6, batch % num_tasks == 0, frames of 16-B multiples"));
+    e->cap = c->capacity;
+    e->n_per_task = B / e->T;
+    if ((rc = e->alloc(&e->store, e->cap * e->T * e->img))) return bad(rc);
+    if ((rc = e->alloc(&e->b_act, e->cap * e->T))) return bad(rc);
+    for (float** q : {&e->b_rew, &e->b_done, &e->b_trunc})
+      if ((rc = e->alloc(q, e->cap * e->T))) return bad(rc);
+    if ((rc = e->alloc(&e->d_minmax, 2 * e->T)) || (rc = e->alloc(&e->rng, 1)) || (rc = e->alloc(&e->jump, 65 * 4)) ||
+        (rc = e->alloc(&e->idx, e->n_per_task)))
+      return bad(rc);
+    unsigned long long jt[65 * 4];
+    pcg_jump_table(jt);
+    if (hipMemcpy(e->jump, jt, sizeof(jt), hipMemcpyHostToDevice) != hipSuccess) return bad(fail(-5, "jump table"));
+    const size_t ring = (size_t)c->nstep * e->T;
+    e->ns_obs.assign(ring * e->img, 0);
+    e->ns_next.assign(ring * e->img, 0);
+    e->ns_act.assign(ring, 0);
+    e->ns_rew.assign(ring, 0.f);
+    e->ns_trunc.assign(ring, 0.f);
+    e->ns_done.assign(ring, 0.f);
+    e->minmax.assign(2 * e->T, 0.0);
+    for (int t = 0; t < e->T; ++t) {
+      e->minmax[t] = INFINITY;
+      e->minmax[e->T + t] = -INFINITY;
+    }
+  }
   if (hipStreamSynchronize(e->st) != hipSuccess) return bad(fail(-5, "init sync"));
   *out = e;
   return 0;
@@ -440,6 +557,74 @@ int drq_q_values(drq_engine* e, const unsigned char* obs, const int* task_ids, c
       hipStreamSynchronize(e->st) != hipSuccess)
     return fail(-5, "q download failed");
   return 0;
+}
+
+int drq_buffer_add(drq_engine* e, const unsigned char* obs, const unsigned char* next_obs, const int* action,
+                   const float* reward, const float* truncate, const float* done) {
+  if (!e || !obs || !next_obs || !action || !reward || !truncate || !done) return fail(-22, "null argument");
+  if (!e->store) return fail(-95, "engine created without a buffer (capacity 0)");
+  return e->buffer_add(obs, next_obs, action, reward, truncate, done);
+}
+
+int drq_buffer_state(drq_engine* e, long long* pos, int* full) {
+  if (!e || !pos || !full) return fail(-22, "null argument");
+  *pos = e->pos;
+  *full = e->full;
+  return 0;
+}
+
+int drq_rng_set(drq_engine* e, unsigned long long shi, unsigned long long slo, unsigned long long ihi,
+                unsigned long long ilo, int has32, unsigned int u) {
+  if (!e) return fail(-22, "null argument");
+  if (!e->rng) return fail(-95, "engine created without a buffer (capacity 0)");
+  PcgDev h{shi, slo, ihi, ilo, has32, u};
+  if (hipMemcpyAsync(e->rng, &h, sizeof(h), hipMemcpyHostToDevice, e->st) != hipSuccess ||
+      hipStreamSynchronize(e->st) != hipSuccess)
+    return fail(-5, "rng upload failed");
+  return 0;
+}
+
+int drq_sample(drq_engine* e) {
+  if (!e) return fail(-22, "null argument");
+  if (!e->store) return fail(-95, "engine created without a buffer (capacity 0)");
+  if (!e->full && e->pos == 0) return fail(-22, "empty buffer");
+  int rc = e->sample();
+  if (rc) return rc;
+  return hipGetLastError() == hipSuccess ? 0 : fail(-5, "kernel launch failed");
+}
+
+int drq_sample_update(drq_engine* e, int steps) {
+  if (!e || steps < 0) return fail(-22, "bad argument");
+  if (!e->store) return fail(-95, "engine created without a buffer (capacity 0)");
+  if (!e->full && e->pos == 0) return fail(-22, "empty buffer");
+  for (int i = 0; i < steps; ++i) {
+    int rc = e->sample();
+    if (rc) return rc;
+    e->step();
+  }
+  return hipGetLastError() == hipSuccess ? 0 : fail(-5, "kernel launch failed");
+}
+
+int drq_read_batch(drq_engine* e, unsigned char* obs, unsigned char* next_obs, int* actions, float* rewards,
+                   float* dones, float* truncations, int* task_ids) {
+  if (!e) return fail(-22, "null argument");
+  const int B = e->B;
+  const size_t img = (size_t)B * e->img;
+  struct {
+    void* dst;
+    const void* src;
+    size_t n;
+  } cp[7] = {{obs, e->obs_u8, img},
+             {next_obs, e->nobs_u8, img},
+             {actions, e->act, sizeof(int) * B},
+             {rewards, e->rew, sizeof(float) * B},
+             {dones, e->done, sizeof(float) * B},
+             {truncations, e->trunc, sizeof(float) * B},
+             {task_ids, e->task, sizeof(int) * B}};
+  for (auto& c : cp)
+    if (c.dst && hipMemcpyAsync(c.dst, c.src, c.n, hipMemcpyDeviceToHost, e->st) != hipSuccess)
+      return fail(-5, "batch download failed");
+  return hipStreamSynchronize(e->st) == hipSuccess ? 0 : fail(-5, "stream sync failed");
 }
 
 int drq_get_logs(drq_engine* e, float* out) {

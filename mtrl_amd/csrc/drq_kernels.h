@@ -9,6 +9,11 @@ namespace drq {
 // edge pad `pad`, crop offsets crop[b] = (along H, along W) in [0, 2 pad]
 void augment(const unsigned char* obs, const int* crop, const float* noise, float* out, int B, int C, int H, int W,
              int pad, hipStream_t st);
+// MemoryEfficientAtariMultiTaskReplayBuffer.sample rows from the device store (img_bytes % 16 == 0)
+void atari_sample(const unsigned char* store, const int* act, const float* rew, const float* done, const float* trunc,
+                  const double* minmax, const int* idx, long long cap, int T, int n, int img_bytes, int nstep,
+                  int full, int pos, int guard, double eps, unsigned char* obs, unsigned char* nobs, int* act_out,
+                  float* rew_out, float* done_out, float* trunc_out, int* task_out, hipStream_t st);
 bool conv_supported(int ci, int co);
 // 3x3 / stride 1 / SAME on NHWC, kernel [3][3][ci][co]; relu_in applies ReLU to the input, res
 // (nullable) is added to the output

@@ -1355,7 +1355,7 @@ void mtsac_default_config(mtsac_config* c, int32_t T) {
   c->noise_seed = 2;
 }
 
-static int pcg_jump_table(unsigned long long* out /* 65*4 */) {
+int pcg_jump_table(unsigned long long* out /* 65*4 */) {
   // state_{j} = A_j s + C_j inc;  A_0 = 1, C_0 = 0;  A_{j+1} = M A_j, C_{j+1} = M C_j + 1
   typedef unsigned __int128 u128h;
   const u128h M = ((u128h)0x2360ED051FC65DA4ull << 64) | (u128h)0x4385DF649FCCF645ull;

@@ -135,6 +135,9 @@ struct PcgDev {  // device-resident numpy PCG64 state (buffers.py:260)
 // n indices in [0, max(size, n)) with numpy's Generator.integers stream; size read from *buf_size
 void replay_indices(PcgDev* rng, const unsigned long long* jump /*65 x (A_hi,A_lo,C_hi,C_lo)*/,
                     const long long* buf_size, int n, int* idx_out, hipStream_t st);
+// the same stream for integers(0, high) with high given (>= 1; high == 1 draws nothing)
+void replay_indices_high(PcgDev* rng, const unsigned long long* jump, long long high, int n, int* idx_out,
+                         hipStream_t st);
 
 struct GatherParams {
   const float* store;   // [cap][T_l][R] transition records

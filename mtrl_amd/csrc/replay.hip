@@ -23,10 +23,11 @@ namespace mtsac {
 // offers two candidates (lo, hi); a ballot prefix count places the accepted ones.
 __global__ __launch_bounds__(64) void replay_indices_kernel(PcgDev* rng, const unsigned long long* __restrict__ jump,
                                                             const long long* __restrict__ buf_size, int n,
-                                                            int* __restrict__ idx) {
+                                                            int* __restrict__ idx, long long exact_high) {
   const int lane = threadIdx.x;
-  const long long size = *buf_size;
-  const long long high = size > n ? size : (long long)n;  // max(pos or cap, n)   buffers.py:525
+  const long long size = exact_high > 0 ? exact_high : *buf_size;
+  // max(pos or cap, n) (buffers.py:525); exact_high > 0: integers(0, exact_high) as given
+  const long long high = exact_high > 0 ? exact_high : (size > n ? size : (long long)n);
   if (high <= 1) {
     for (int i = lane; i < n; i += 64) idx[i] = 0;  // rng == 0: no stream consumption
     return;
@@ -97,7 +98,12 @@ __global__ __launch_bounds__(64) void replay_indices_kernel(PcgDev* rng, const u
 
 void replay_indices(PcgDev* rng, const unsigned long long* jump, const long long* buf_size, int n, int* idx_out,
                     hipStream_t st) {
-  hipLaunchKernelGGL(replay_indices_kernel, dim3(1), dim3(64), 0, st, rng, jump, buf_size, n, idx_out);
+  hipLaunchKernelGGL(replay_indices_kernel, dim3(1), dim3(64), 0, st, rng, jump, buf_size, n, idx_out, 0LL);
+}
+
+void replay_indices_high(PcgDev* rng, const unsigned long long* jump, long long high, int n, int* idx_out,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(replay_indices_kernel, dim3(1), dim3(64), 0, st, rng, jump, nullptr, n, idx_out, high);
 }
 
 // ------------------------------------------------------------------ gather

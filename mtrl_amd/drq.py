@@ -38,6 +38,8 @@ class DrQSettings:
     eps: float = 1.5e-4
     weight_decay: float = 0.05
     ln_eps: float = 1e-6
+    capacity: int = 0  # device replay slots per task (0: none)
+    normalize_rewards: int = 0
 
 
 def _ptr(a):
@@ -55,7 +57,7 @@ class DrQEngine:
     def __init__(self, s: DrQSettings = DrQSettings(), device: int = 0):
         self.lib = L.load()
         self.s = s
-        c = L.DrqConfig(**{k: getattr(s, k) for k, _ in L.DrqConfig._fields_})
+        c = L.DrqConfig(**{k: getattr(s, k) for k, _ in L.DrqConfig._fields_ if k != "reserved"})
         h = ctypes.c_void_p()
         _drq_check(self.lib.drq_create(ctypes.byref(c), device, ctypes.byref(h)))
         self.h = h
@@ -111,6 +113,46 @@ class DrQEngine:
         q = np.empty((n, self.s.n_actions), np.float32)
         _drq_check(self.lib.drq_q_values(self.h, _ptr(o), _ptr(t), _ptr(c), _ptr(z), n, _ptr(q)))
         return q
+
+    # ---- device replay buffer (MemoryEfficientAtariMultiTaskReplayBuffer)
+    def buffer_add(self, obs, next_obs, action, reward, truncate, done):
+        arrs = [np.ascontiguousarray(obs, np.uint8), np.ascontiguousarray(next_obs, np.uint8),
+                np.ascontiguousarray(action, np.int32).reshape(-1), np.ascontiguousarray(reward, np.float32).reshape(-1),
+                np.ascontiguousarray(truncate, np.float32).reshape(-1), np.ascontiguousarray(done, np.float32).reshape(-1)]
+        _drq_check(self.lib.drq_buffer_add(self.h, *[_ptr(a) for a in arrs]))
+
+    def buffer_state(self):
+        pos, full = ctypes.c_int64(), ctypes.c_int32()
+        _drq_check(self.lib.drq_buffer_state(self.h, ctypes.byref(pos), ctypes.byref(full)))
+        return int(pos.value), bool(full.value)
+
+    def seed_rng(self, seed: int):
+        """numpy.random.default_rng(seed)'s PCG64 state (buffers.py:981), drawn on the device."""
+        st = np.random.default_rng(seed).bit_generator.state
+        self.set_rng_state(st)
+
+    def set_rng_state(self, st: dict):
+        s_, inc = st["state"]["state"], st["state"]["inc"]
+        m = (1 << 64) - 1
+        _drq_check(self.lib.drq_rng_set(self.h, s_ >> 64, s_ & m, inc >> 64, inc & m, int(st["has_uint32"]),
+                                        int(st["uinteger"])))
+
+    def sample(self):
+        _drq_check(self.lib.drq_sample(self.h))
+
+    def sample_update(self, steps: int = 1):
+        _drq_check(self.lib.drq_sample_update(self.h, int(steps)))
+
+    def read_batch(self):
+        B, C, H = self.s.batch, self.s.in_ch, self.s.hw
+        obs = np.empty((B, C, H, H), np.uint8)
+        nobs = np.empty_like(obs)
+        act = np.empty(B, np.int32)
+        rew, done, trunc = (np.empty(B, np.float32) for _ in range(3))
+        task = np.empty(B, np.int32)
+        _drq_check(self.lib.drq_read_batch(self.h, _ptr(obs), _ptr(nobs), _ptr(act), _ptr(rew), _ptr(done),
+                                           _ptr(trunc), _ptr(task)))
+        return obs, act, nobs, trunc, done, rew, task
 
     def update_resident(self, steps: int):
         _drq_check(self.lib.drq_update_resident(self.h, int(steps)))

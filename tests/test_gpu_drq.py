@@ -148,3 +148,63 @@ def test_compat_drq_api():
                          "losses/critic_loss"}
     assert all(np.isfinite(v) for v in logs.values())
     agent.close()
+
+
+@pytest.mark.parametrize("normalize", [False, True], ids=["raw", "normalized"])
+def test_device_buffer_matches_reference_buffer(normalize):
+    """MemoryEfficientAtariMultiTaskReplayBuffer (buffers.py:949-1229) on the device against its
+    numpy restatement: n-step aggregation with episode ends, the guard window once full (both the
+    plain and the wrapping case), the PCG64 index stream, reward normalisation -- bit for bit."""
+    from mtrl_amd.drq import DrQEngine, DrQSettings
+    from oracle.atari_buffer import AtariBuffer
+
+    T, n, cap, hw = 4, 3, 23, 20
+    B = T * n
+    ref = AtariBuffer(cap, T, (4, hw, hw), seed=11, nstep=3, gamma=0.99, normalize_rewards=normalize)
+    e = DrQEngine(DrQSettings(num_tasks=T, hw=hw, n_hidden=64, batch=B, capacity=cap, normalize_rewards=int(normalize)))
+    e.seed_rng(11)
+    rng = np.random.default_rng(5)
+    checks = 0
+    for step in range(70):
+        o = rng.integers(0, 256, (T, 4, hw, hw), dtype=np.uint8)
+        no = rng.integers(0, 256, (T, 4, hw, hw), dtype=np.uint8)
+        a = rng.integers(0, 18, T).astype(np.int32)
+        r = np.round(rng.standard_normal(T) * 3, 2).astype(np.float32)
+        tr = (rng.random(T) < 0.05).astype(np.float32)
+        d = (rng.random(T) < 0.15).astype(np.float32)
+        ref.add(o, no, a, r, tr, d)
+        e.buffer_add(o, no, a, r, tr, d)
+        assert e.buffer_state() == (ref.pos, ref.full)
+        if ref.pos > 0 or ref.full:
+            if step % 3 == 0:
+                want = ref.sample(B)
+                e.sample()
+                got = e.read_batch()
+                names = ("obs", "actions", "next_obs", "truncations", "dones", "rewards", "task_ids")
+                for nm, g, w in zip(names, got, want):
+                    np.testing.assert_array_equal(np.asarray(g).reshape(np.shape(w)).astype(np.asarray(w).dtype), w,
+                                                  err_msg=f"{nm} at step {step}")
+                checks += 1
+    assert ref.full and checks > 15
+    e.close()
+
+
+def test_sample_update_runs():
+    from mtrl_amd import _lib as L
+    from mtrl_amd.drq import DrQEngine, DrQSettings
+
+    cfg = od.DrQConfig(hw=20, n_hidden=64)
+    T, B = 26, 26 * 2
+    e = DrQEngine(DrQSettings(hw=20, n_hidden=64, batch=B, capacity=40))
+    e.set_params(L.DRQ_PARAMS, od.initialize(cfg, 1))
+    e.set_params(L.DRQ_TARGET, od.initialize(cfg, 1))
+    e.seed_rng(3)
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        o = rng.integers(0, 256, (T, 4, 20, 20), dtype=np.uint8)
+        e.buffer_add(o, o, rng.integers(0, 18, T), rng.standard_normal(T), np.zeros(T), np.zeros(T))
+    e.sample_update(3)
+    e.synchronize()
+    logs = e.logs()
+    assert all(np.isfinite(v) for v in logs.values())
+    e.close()
