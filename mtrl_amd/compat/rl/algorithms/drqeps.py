@@ -63,6 +63,28 @@ class DrQ:
         eng.set_params(1, p)  # target = the shrink-and-perturbed params (drqeps.py:196)
         return DrQ(eng, config, seed, batch_size)
 
+    def spawn_replay_buffer(self, env_config, config, seed: int = 1) -> "DeviceAtariReplayBuffer":
+        """drqeps.py:124-137: the buffer lives on the device inside the engine (rebuilt here with
+        buffer_size / num_tasks slots per task, the current parameters and optimizer state carried
+        over)."""
+        from mtrl_amd import _lib as L
+
+        cap = config.buffer_size // self.config.num_tasks
+        s = dataclasses.replace(self.engine.s, capacity=cap, normalize_rewards=int(config.normalize_rewards),
+                                nstep=getattr(config, "nstep", self.engine.s.nstep))
+        state = {w: self.engine.get_params(w) for w in (L.DRQ_PARAMS, L.DRQ_TARGET, L.DRQ_ADAM_MU, L.DRQ_ADAM_NU)}
+        self.engine.close()
+        self.engine = DrQEngine(s)
+        for w, v in state.items():
+            self.engine.set_params(w, v)
+        self.engine.seed_rng(seed)
+        return DeviceAtariReplayBuffer(self.engine)
+
+    def update_from_buffer(self, steps: int = 1):
+        """sample + update on the device (the training loop's fast path: no host batch)."""
+        self.engine.sample_update(steps)
+        return self, self.engine.logs()
+
     def get_num_params(self) -> dict[str, int]:
         return {"critic_num_params": self.engine.n}
 
@@ -107,3 +129,32 @@ class DrQ:
 
     def close(self):
         self.engine.close()
+
+
+class DeviceAtariReplayBuffer:
+    """MemoryEfficientAtariMultiTaskReplayBuffer's API (buffers.py:949-1229) over the engine's
+    device store: add(obs, next_obs, action, reward, truncate, done) per env step of all tasks,
+    sample(batch_size) -> AtariReplayBufferSamples (a host copy of the staged batch)."""
+
+    def __init__(self, engine: DrQEngine):
+        self.engine = engine
+        self.num_tasks = engine.s.num_tasks
+        self.capacity = engine.s.capacity
+
+    @property
+    def pos(self) -> int:
+        return self.engine.buffer_state()[0]
+
+    @property
+    def full(self) -> bool:
+        return self.engine.buffer_state()[1]
+
+    def add(self, obs, next_obs, action, reward, truncate, done) -> None:
+        self.engine.buffer_add(obs, next_obs, action, reward, truncate, done)
+
+    def sample(self, batch_size: int) -> T.AtariReplayBufferSamples:
+        if batch_size != self.engine.s.batch:
+            raise ValueError(f"batch_size {batch_size}: the engine samples {self.engine.s.batch}")
+        self.engine.sample()
+        o, a, no, tr, d, r, t = self.engine.read_batch()
+        return T.AtariReplayBufferSamples(o, a, no, tr[:, None], d[:, None], r[:, None], t)

@@ -208,3 +208,24 @@ def test_sample_update_runs():
     logs = e.logs()
     assert all(np.isfinite(v) for v in logs.values())
     e.close()
+
+
+def test_compat_device_buffer_and_fast_path():
+    import mtrl  # noqa: F401
+    from mtrl.config.rl import DrQTrainingConfig
+    from mtrl.envs import AtariConfig
+    from mtrl.rl.algorithms import DrQ, DrQConfig
+
+    agent = DrQ.initialize(DrQConfig(num_tasks=26), AtariConfig(), seed=1, batch_size=52)
+    buf = agent.spawn_replay_buffer(AtariConfig(), DrQTrainingConfig(total_steps=100, buffer_size=26 * 30), seed=1)
+    rng = np.random.default_rng(0)
+    for _ in range(12):
+        o = rng.integers(0, 256, (26, 4, 84, 84), dtype=np.uint8)
+        buf.add(o, o, rng.integers(0, 18, 26), rng.standard_normal(26), np.zeros(26), np.zeros(26))
+    assert buf.pos == 10 and not buf.full  # 12 steps, 3-step returns
+    data = buf.sample(52)
+    assert data.observations.shape == (52, 4, 84, 84) and data.rewards.shape == (52, 1)
+    agent, logs = agent.update(data)
+    agent, logs2 = agent.update_from_buffer(2)
+    assert all(np.isfinite(v) for v in list(logs.values()) + list(logs2.values()))
+    agent.close()
