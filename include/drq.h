@@ -78,7 +78,8 @@ int drq_get_params(drq_engine* e, int which, float* flat, long long n);
 int drq_set_step(drq_engine* e, int adam_count);
 /* stage one batch and run one update on it (asynchronous on the engine's stream) */
 int drq_update(drq_engine* e, const drq_batch* batch);
-/* run `steps` more updates on the batch already resident on the device (benchmarks) */
+/* run `steps` more updates on the batch already resident on the device (benchmarks), each with
+ * fresh device augmentation draws */
 int drq_update_resident(drq_engine* e, int steps);
 /* expected Q [n][n_actions] of the online network on n <= batch observations (uint8 NCHW), after
  * the augmentation with the given draws: the quantity _sample_action / _eval_action take the argmax
@@ -97,8 +98,19 @@ int drq_rng_set(drq_engine* e, unsigned long long state_hi, unsigned long long s
                 unsigned long long inc_lo, int has_uint32, unsigned int uinteger);
 /* sample(batch) from the device buffer into the engine's staged batch (batch % num_tasks == 0) */
 int drq_sample(drq_engine* e);
-/* `steps` x (sample + update): DrQ's training step with the batch drawn on the device */
+/* `steps` x (sample + update): DrQ's training step with the batch drawn on the device (the
+ * augmentation crops / intensities from the device counter hash seeded by drq_seed_augment) */
 int drq_sample_update(drq_engine* e, int steps);
+/* sample_unbalanced (buffers.py:1230-1279, what OffPolicyAlgorithm.train calls for this buffer,
+ * base.py:217-218): the caller draws the Dirichlet task sizes and the per-task slots with its own
+ * Generator and passes `batch` rows (slot in [0, capacity), task id in [0, num_tasks)); the gather,
+ * next_obs nstep ahead and the reward normalisation run on the device. */
+int drq_sample_rows(drq_engine* e, const long long* slots, const int* task_ids);
+/* `steps` x (sample_rows + update) on [steps][batch] host-drawn rows */
+int drq_sample_rows_update(drq_engine* e, const long long* slots, const int* task_ids, int steps);
+/* the device PCG64 state after drq_sample: state_hi, state_lo, inc_hi, inc_lo, has_uint32, uinteger */
+int drq_rng_get(drq_engine* e, unsigned long long* out6);
+int drq_seed_augment(drq_engine* e, unsigned long long seed);
 /* the staged batch (tests): uint8 obs / next_obs, actions, rewards, dones, truncations, task ids */
 int drq_read_batch(drq_engine* e, unsigned char* obs, unsigned char* next_obs, int* actions, float* rewards,
                    float* dones, float* truncations, int* task_ids);

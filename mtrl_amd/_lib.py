@@ -192,6 +192,10 @@ SIGNATURES.update({
     "drq_rng_set": (ctypes.c_int, [P, U64, U64, U64, U64, ctypes.c_int, U32]),
     "drq_sample": (ctypes.c_int, [P]),
     "drq_sample_update": (ctypes.c_int, [P, ctypes.c_int]),
+    "drq_sample_rows": (ctypes.c_int, [P, P, P]),
+    "drq_sample_rows_update": (ctypes.c_int, [P, P, P, ctypes.c_int]),
+    "drq_rng_get": (ctypes.c_int, [P, P]),
+    "drq_seed_augment": (ctypes.c_int, [P, ctypes.c_uint64]),
     "drq_read_batch": (ctypes.c_int, [P, P, P, P, P, P, P, P]),
     "drq_synchronize": (ctypes.c_int, [P]),
 })

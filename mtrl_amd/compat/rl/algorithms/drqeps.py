@@ -78,11 +78,14 @@ class DrQ:
         for w, v in state.items():
             self.engine.set_params(w, v)
         self.engine.seed_rng(seed)
+        self.engine.seed_augment(int(self.rng.integers(0, 2**63)))
         return DeviceAtariReplayBuffer(self.engine)
 
     def update_from_buffer(self, steps: int = 1):
-        """sample + update on the device (the training loop's fast path: no host batch)."""
-        self.engine.sample_update(steps)
+        """OffPolicyAlgorithm.train's update loop (base.py:213-221) for this buffer:
+        `steps` x (sample_unbalanced(batch_size) + update), rows drawn with the buffer's Generator,
+        gather, augmentation and update on the device (no host batch)."""
+        self.engine.sample_unbalanced_update(steps)
         return self, self.engine.logs()
 
     def get_num_params(self) -> dict[str, int]:
@@ -152,9 +155,22 @@ class DeviceAtariReplayBuffer:
     def add(self, obs, next_obs, action, reward, truncate, done) -> None:
         self.engine.buffer_add(obs, next_obs, action, reward, truncate, done)
 
-    def sample(self, batch_size: int) -> T.AtariReplayBufferSamples:
+    def _check(self, batch_size):
         if batch_size != self.engine.s.batch:
             raise ValueError(f"batch_size {batch_size}: the engine samples {self.engine.s.batch}")
-        self.engine.sample()
+
+    def _read(self) -> T.AtariReplayBufferSamples:
         o, a, no, tr, d, r, t = self.engine.read_batch()
         return T.AtariReplayBufferSamples(o, a, no, tr[:, None], d[:, None], r[:, None], t)
+
+    def sample(self, batch_size: int) -> T.AtariReplayBufferSamples:
+        """buffers.py:1188-1227 (batch_size % num_tasks == 0)."""
+        self._check(batch_size)
+        self.engine.sample()
+        return self._read()
+
+    def sample_unbalanced(self, batch_size: int) -> T.AtariReplayBufferSamples:
+        """buffers.py:1230-1279: Dirichlet task proportions (what the training loop calls)."""
+        self._check(batch_size)
+        self.engine.sample_unbalanced()
+        return self._read()

@@ -56,6 +56,8 @@ __global__ void augment_kernel(const unsigned char* __restrict__ obs, const int*
 // row b = (sample i = b / T, task t = b % T); draw k = idx[i] -> slot via the guard window
 // (_sample_indices, buffers.py:1082-1105); next_obs = the frame stack nstep slots ahead; rewards
 // min-max normalised in double per task; task_ids as the reference lists them (b / n).
+// Row mode (rslot != null, sample_unbalanced, buffers.py:1230-1279): row b reads slot rslot[b] of
+// task rtask[b], both drawn on the host, and task_ids = rtask[b].
 struct AtariSampleParams {
   const unsigned char* store;  // [cap][T][img]
   const int* act;
@@ -68,14 +70,17 @@ struct AtariSampleParams {
   unsigned char *obs, *nobs;
   int *act_out, *task_out;
   float *rew_out, *done_out, *trunc_out;
+  const long long* rslot;
+  const int* rtask;
 };
 
 __global__ void atari_sample_kernel(AtariSampleParams p) {
   const int b = blockIdx.y;
-  const int i = b / p.T, t = b - i * p.T;
-  const long long k = p.idx[i];
-  long long slot = k;
-  if (p.full) {
+  int i = b / p.T, t = b - i * p.T;
+  long long slot = p.rslot ? p.rslot[b] : p.idx[i];
+  if (p.rslot) t = p.rtask[b];
+  else if (p.full) {
+    const long long k = slot;
     if (p.pos + p.guard <= p.cap) slot = k < p.pos ? k : k + p.guard;
     else slot = k + (p.pos + p.guard - p.cap);
   }
@@ -100,8 +105,36 @@ __global__ void atari_sample_kernel(AtariSampleParams p) {
     p.rew_out[b] = rw;
     p.done_out[b] = p.done[r];
     p.trunc_out[b] = p.trunc[r];
-    p.task_out[b] = b / p.n;  // np.repeat(np.arange(T), n)
+    p.task_out[b] = p.rslot ? t : b / p.n;  // np.repeat(np.arange(T), n)
   }
+}
+
+// ------------------------------------------------------------------ augmentation draws
+// The device-side draws of the sample+update entries (the reference takes them from jax.random,
+// augmentation.py:75-117; threefry is not reproduced): per row two crop offsets in [0, 2 pad) and
+// an intensity factor 1 + 0.05 clip(N(0, 1), -2, 2), for obs and next_obs, from a counter hash.
+__device__ inline unsigned long long mix64(unsigned long long z) {
+  z += 0x9e3779b97f4a7c15ULL;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+__global__ void aug_draw_kernel(unsigned long long seed, unsigned long long ctr, int B, int span, int* crop_o,
+                                float* noise_o, int* crop_n, float* noise_n) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= 2 * B) return;
+  const unsigned long long h0 = mix64(seed ^ mix64(ctr * 0x100000001b3ULL + (unsigned long long)b));
+  const unsigned long long h1 = mix64(h0 ^ 0x5851f42d4c957f2dULL);
+  const int r = b < B ? b : b - B;
+  int* crop = b < B ? crop_o : crop_n;
+  float* noise = b < B ? noise_o : noise_n;
+  crop[2 * r] = (int)((h0 & 0xffffffffULL) % (unsigned)span);
+  crop[2 * r + 1] = (int)((h0 >> 32) % (unsigned)span);
+  const float u1 = ((float)(h1 >> 40) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
+  const float u2 = (float)((h1 >> 16) & 0xffffffULL) * (1.0f / 16777216.0f);
+  const float z = sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
+  noise[r] = 1.0f + 0.05f * fminf(fmaxf(z, -2.0f), 2.0f);
 }
 
 // ------------------------------------------------------------------ convolutions
@@ -738,8 +771,24 @@ void atari_sample(const unsigned char* store, const int* act, const float* rew, 
                   int full, int pos, int guard, double eps, unsigned char* obs, unsigned char* nobs, int* act_out,
                   float* rew_out, float* done_out, float* trunc_out, int* task_out, hipStream_t st) {
   AtariSampleParams p{store, act, rew, done, trunc, minmax, idx, cap, T, n, img_bytes / 16, nstep, full, pos, guard,
-                      eps, obs, nobs, act_out, task_out, rew_out, done_out, trunc_out};
+                      eps, obs, nobs, act_out, task_out, rew_out, done_out, trunc_out, nullptr, nullptr};
   hipLaunchKernelGGL(atari_sample_kernel, dim3(4, n * T), dim3(256), 0, st, p);
+}
+
+void atari_sample_rows(const unsigned char* store, const int* act, const float* rew, const float* done,
+                       const float* trunc, const double* minmax, const long long* slots, const int* tasks, int rows,
+                       long long cap, int T, int img_bytes, int nstep, double eps, unsigned char* obs,
+                       unsigned char* nobs, int* act_out, float* rew_out, float* done_out, float* trunc_out,
+                       int* task_out, hipStream_t st) {
+  AtariSampleParams p{store, act, rew, done, trunc, minmax, nullptr, cap, T, 1, img_bytes / 16, nstep, 0, 0, 0,
+                      eps, obs, nobs, act_out, task_out, rew_out, done_out, trunc_out, slots, tasks};
+  hipLaunchKernelGGL(atari_sample_kernel, dim3(4, rows), dim3(256), 0, st, p);
+}
+
+void aug_draw(unsigned long long seed, unsigned long long ctr, int B, int pad, int* crop_o, float* noise_o,
+              int* crop_n, float* noise_n, hipStream_t st) {
+  hipLaunchKernelGGL(aug_draw_kernel, dim3(blocks(2LL * B)), dim3(256), 0, st, seed, ctr, B, 2 * pad, crop_o, noise_o,
+                     crop_n, noise_n);
 }
 
 void augment(const unsigned char* obs, const int* crop, const float* noise, float* out, int B, int C, int H, int W,

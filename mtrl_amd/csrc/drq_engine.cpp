@@ -88,6 +88,10 @@ struct drq_engine {
   PcgDev* rng = nullptr;
   unsigned long long* jump = nullptr;
   int* idx = nullptr;
+  static constexpr int ROWS_STEPS = 64;  // host-drawn rows staged per upload (sample_rows_update)
+  long long* r_slot = nullptr;           // [ROWS_STEPS][B]
+  int* r_task = nullptr;
+  unsigned long long aug_seed = 0, aug_ctr = 0;
   std::vector<unsigned char> ns_obs, ns_next;  // [nstep][T][img]
   std::vector<int> ns_act;
   std::vector<float> ns_rew, ns_trunc, ns_done;  // [nstep][T]
@@ -221,6 +225,7 @@ struct drq_engine {
 
   // sample (buffers.py:1188-1227) into the staged batch
   int sample() {
+    if (n_per_task < 1 || B % T != 0) return fail(-22, "balanced sample: batch % num_tasks must be 0");
     const int n = n_per_task, guard = cfg.nstep + 6;
     const long long high = full ? cap - guard : std::max(pos - cfg.nstep, 1LL);
     replay_indices_high(rng, jump, high, n, idx, st);
@@ -231,6 +236,33 @@ struct drq_engine {
                       (int)img, cfg.nstep, full, (int)pos, guard, 1e-8, obs_u8, nobs_u8, act, rew, done, trunc, task, st);
     return 0;
   }
+
+  // sample_unbalanced (buffers.py:1230-1279) with the rows drawn by the caller: rows [s][B] at
+  // slots / tasks already on the device
+  int sample_rows(const long long* slots, const int* tasks) {
+    if (cfg.normalize_rewards &&
+        hipMemcpyAsync(d_minmax, minmax.data(), sizeof(double) * 2 * T, hipMemcpyHostToDevice, st) != hipSuccess)
+      return fail(-5, "reward stats upload failed");
+    drq::atari_sample_rows(store, b_act, b_rew, b_done, b_trunc, cfg.normalize_rewards ? d_minmax : nullptr, slots,
+                           tasks, B, cap, T, (int)img, cfg.nstep, 1e-8, obs_u8, nobs_u8, act, rew, done, trunc, task,
+                           st);
+    return 0;
+  }
+
+  // checked upload of `steps` host-drawn row sets into r_slot / r_task (stream ordered)
+  int upload_rows(const long long* slots, const int* tasks, int steps) {
+    const long long n = (long long)steps * B;
+    for (long long i = 0; i < n; ++i)
+      if (slots[i] < 0 || slots[i] >= cap || tasks[i] < 0 || tasks[i] >= T)
+        return fail(-22, "row " + std::to_string(i) + ": slot or task out of range");
+    if (hipMemcpyAsync(r_slot, slots, sizeof(long long) * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(r_task, tasks, sizeof(int) * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)  // the caller's arrays may go away on return
+      return fail(-5, "row upload failed");
+    return 0;
+  }
+
+  void draw_aug() { drq::aug_draw(aug_seed, aug_ctr++, B, 4, crop_o, noise_o, crop_n, noise_n, st); }
 
   // ------------------------------------------------------------------ one update on the staged batch
   void step() {
@@ -428,8 +460,8 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
   if ((rc = e->alloc(&e->trunc, B))) return bad(rc);
   e->img = (long long)c->in_ch * c->hw * c->hw;
   if (c->capacity > 0) {
-    if (c->capacity <= c->nstep + 6 || c->nstep < 1 || B % e->T != 0 || e->img % 16 != 0 || c->capacity > (1LL << 30))
-      return bad(fail(-22, "buffer: capacity > nstep + 6, batch % num_tasks == 0, frames of 16-B multiples"));
+    if (c->capacity <= c->nstep + 6 || c->nstep < 1 || e->img % 16 != 0 || c->capacity > (1LL << 30))
+      return bad(fail(-22, "buffer: capacity > nstep + 6, frames of 16-B multiples"));
     e->cap = c->capacity;
     e->n_per_task = B / e->T;
     if ((rc = e->alloc(&e->store, e->cap * e->T * e->img))) return bad(rc);
@@ -437,7 +469,8 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
     for (float** q : {&e->b_rew, &e->b_done, &e->b_trunc})
       if ((rc = e->alloc(q, e->cap * e->T))) return bad(rc);
     if ((rc = e->alloc(&e->d_minmax, 2 * e->T)) || (rc = e->alloc(&e->rng, 1)) || (rc = e->alloc(&e->jump, 65 * 4)) ||
-        (rc = e->alloc(&e->idx, e->n_per_task)))
+        (rc = e->alloc(&e->idx, e->n_per_task)) || (rc = e->alloc(&e->r_slot, (long long)drq_engine::ROWS_STEPS * B)) ||
+        (rc = e->alloc(&e->r_task, (long long)drq_engine::ROWS_STEPS * B)))
       return bad(rc);
     unsigned long long jt[65 * 4];
     pcg_jump_table(jt);
@@ -538,7 +571,10 @@ int drq_update(drq_engine* e, const drq_batch* b) {
 
 int drq_update_resident(drq_engine* e, int steps) {
   if (!e || steps < 0) return fail(-22, "bad argument");
-  for (int i = 0; i < steps; ++i) e->step();
+  for (int i = 0; i < steps; ++i) {
+    e->draw_aug();
+    e->step();
+  }
   return hipGetLastError() == hipSuccess ? 0 : fail(-5, "kernel launch failed");
 }
 
@@ -600,9 +636,58 @@ int drq_sample_update(drq_engine* e, int steps) {
   for (int i = 0; i < steps; ++i) {
     int rc = e->sample();
     if (rc) return rc;
+    e->draw_aug();
     e->step();
   }
   return hipGetLastError() == hipSuccess ? 0 : fail(-5, "kernel launch failed");
+}
+
+int drq_sample_rows(drq_engine* e, const long long* slots, const int* task_ids) {
+  if (!e || !slots || !task_ids) return fail(-22, "null argument");
+  if (!e->store) return fail(-95, "engine created without a buffer (capacity 0)");
+  int rc;
+  if ((rc = e->upload_rows(slots, task_ids, 1)) || (rc = e->sample_rows(e->r_slot, e->r_task))) return rc;
+  return hipGetLastError() == hipSuccess ? 0 : fail(-5, "kernel launch failed");
+}
+
+int drq_sample_rows_update(drq_engine* e, const long long* slots, const int* task_ids, int steps) {
+  if (!e || !slots || !task_ids || steps < 0) return fail(-22, "bad argument");
+  if (!e->store) return fail(-95, "engine created without a buffer (capacity 0)");
+  const long long B = e->B;
+  for (int s0 = 0; s0 < steps; s0 += drq_engine::ROWS_STEPS) {
+    const int k = std::min(steps - s0, drq_engine::ROWS_STEPS);
+    int rc = e->upload_rows(slots + s0 * B, task_ids + s0 * B, k);
+    if (rc) return rc;
+    for (int i = 0; i < k; ++i) {
+      if ((rc = e->sample_rows(e->r_slot + i * B, e->r_task + i * B))) return rc;
+      e->draw_aug();
+      e->step();
+    }
+  }
+  return hipGetLastError() == hipSuccess ? 0 : fail(-5, "kernel launch failed");
+}
+
+int drq_rng_get(drq_engine* e, unsigned long long* out6) {
+  if (!e || !out6) return fail(-22, "null argument");
+  if (!e->rng) return fail(-95, "engine created without a buffer (capacity 0)");
+  PcgDev h{};
+  if (hipMemcpyAsync(&h, e->rng, sizeof(h), hipMemcpyDeviceToHost, e->st) != hipSuccess ||
+      hipStreamSynchronize(e->st) != hipSuccess)
+    return fail(-5, "rng download failed");
+  out6[0] = h.state_hi;
+  out6[1] = h.state_lo;
+  out6[2] = h.inc_hi;
+  out6[3] = h.inc_lo;
+  out6[4] = (unsigned long long)h.has_uint32;
+  out6[5] = h.uinteger;
+  return 0;
+}
+
+int drq_seed_augment(drq_engine* e, unsigned long long seed) {
+  if (!e) return fail(-22, "null argument");
+  e->aug_seed = seed;
+  e->aug_ctr = 0;
+  return 0;
 }
 
 int drq_read_batch(drq_engine* e, unsigned char* obs, unsigned char* next_obs, int* actions, float* rewards,

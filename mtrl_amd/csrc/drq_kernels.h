@@ -14,6 +14,16 @@ void atari_sample(const unsigned char* store, const int* act, const float* rew, 
                   const double* minmax, const int* idx, long long cap, int T, int n, int img_bytes, int nstep,
                   int full, int pos, int guard, double eps, unsigned char* obs, unsigned char* nobs, int* act_out,
                   float* rew_out, float* done_out, float* trunc_out, int* task_out, hipStream_t st);
+// sample_unbalanced rows: row b = (slot slots[b], task tasks[b]), both drawn on the host
+void atari_sample_rows(const unsigned char* store, const int* act, const float* rew, const float* done,
+                       const float* trunc, const double* minmax, const long long* slots, const int* tasks, int rows,
+                       long long cap, int T, int img_bytes, int nstep, double eps, unsigned char* obs,
+                       unsigned char* nobs, int* act_out, float* rew_out, float* done_out, float* trunc_out,
+                       int* task_out, hipStream_t st);
+// fresh augmentation draws for obs and next_obs from (seed, ctr): crops in [0, 2 pad), intensity
+// 1 + 0.05 clip(N(0, 1), -2, 2)
+void aug_draw(unsigned long long seed, unsigned long long ctr, int B, int pad, int* crop_o, float* noise_o,
+              int* crop_n, float* noise_n, hipStream_t st);
 bool conv_supported(int ci, int co);
 // 3x3 / stride 1 / SAME on NHWC, kernel [3][3][ci][co]; relu_in applies ReLU to the input, res
 // (nullable) is added to the output

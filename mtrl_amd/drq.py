@@ -53,6 +53,37 @@ def _drq_check(rc: int) -> int:
     return rc
 
 
+def unbalanced_rows(rng: np.random.Generator, num_tasks: int, batch: int, pos: int, full: bool, capacity: int,
+                    nstep: int):
+    """The host draws of sample_unbalanced (buffers.py:1235-1257) with _sample_indices
+    (buffers.py:1082-1100): Dirichlet(1, ..., 1) task weights, floor(w * batch) rows per task plus
+    the remainder to the largest weights, then each task's slots from the same Generator.  The
+    guard window's valid[k] is computed arithmetically (no list of the capacity).
+    Returns (slots int64 [batch], task ids int32 [batch]) in the reference's row order."""
+    weights = rng.dirichlet([1] * num_tasks)
+    sizes = np.floor(weights * batch).astype(np.int32)
+    rem = batch - sizes.sum()
+    if rem > 0:
+        sizes[np.argsort(-weights)[:rem]] += 1
+    slots = np.empty(batch, np.int64)
+    tasks = np.empty(batch, np.int32)
+    guard = nstep + 6
+    c = 0
+    for i in range(num_tasks):
+        n = int(sizes[i])
+        if n == 0:
+            continue
+        if not full:
+            idx = rng.integers(0, max(pos - nstep, 1), size=(n,))
+        else:
+            k = rng.integers(0, capacity - guard, size=(n,))
+            idx = np.where(k < pos, k, k + guard) if pos + guard <= capacity else k + (pos + guard - capacity)
+        slots[c:c + n] = idx
+        tasks[c:c + n] = i
+        c += n
+    return slots, tasks
+
+
 class DrQEngine:
     def __init__(self, s: DrQSettings = DrQSettings(), device: int = 0):
         self.lib = L.load()
@@ -63,6 +94,10 @@ class DrQEngine:
         self.h = h
         self.n = int(self.lib.drq_num_params(h))
         self._keep = []
+        # the buffer's Generator: drawn on the device by sample(), on the host by sample_unbalanced();
+        # one stream either way (the side that draws next first takes the other's state)
+        self._rng = np.random.Generator(np.random.PCG64())
+        self._rng_on_device = True
 
     def close(self):
         if self.h:
@@ -127,7 +162,7 @@ class DrQEngine:
         return int(pos.value), bool(full.value)
 
     def seed_rng(self, seed: int):
-        """numpy.random.default_rng(seed)'s PCG64 state (buffers.py:981), drawn on the device."""
+        """numpy.random.default_rng(seed)'s PCG64 state (buffers.py:981)."""
         st = np.random.default_rng(seed).bit_generator.state
         self.set_rng_state(st)
 
@@ -136,12 +171,63 @@ class DrQEngine:
         m = (1 << 64) - 1
         _drq_check(self.lib.drq_rng_set(self.h, s_ >> 64, s_ & m, inc >> 64, inc & m, int(st["has_uint32"]),
                                         int(st["uinteger"])))
+        self._rng.bit_generator.state = st
+        self._rng_on_device = False
+
+    def get_rng_state(self) -> dict:
+        if not self._rng_on_device:
+            return self._rng.bit_generator.state
+        o = np.zeros(6, np.uint64)
+        _drq_check(self.lib.drq_rng_get(self.h, _ptr(o)))
+        v = [int(x) for x in o]
+        return {"bit_generator": "PCG64", "state": {"state": (v[0] << 64) | v[1], "inc": (v[2] << 64) | v[3]},
+                "has_uint32": v[4], "uinteger": v[5]}
+
+    def _host_rng(self) -> np.random.Generator:
+        if self._rng_on_device:
+            self._rng.bit_generator.state = self.get_rng_state()
+            self._rng_on_device = False
+        return self._rng
+
+    def _push_rng(self):
+        self.set_rng_state(self._rng.bit_generator.state)
+
+    def seed_augment(self, seed: int):
+        """seed of the device augmentation draws of sample_update / sample_unbalanced_update."""
+        _drq_check(self.lib.drq_seed_augment(self.h, int(seed) & ((1 << 64) - 1)))
 
     def sample(self):
+        """sample(batch) (buffers.py:1188-1227), indices drawn on the device."""
         _drq_check(self.lib.drq_sample(self.h))
+        self._rng_on_device = True
 
     def sample_update(self, steps: int = 1):
         _drq_check(self.lib.drq_sample_update(self.h, int(steps)))
+        self._rng_on_device = True
+
+    def _rows(self, steps):
+        pos, full = self.buffer_state()
+        if pos == 0 and not full:
+            raise L.MTSACError("libmtsac drq error -22: empty buffer")
+        rng = self._host_rng()
+        s = self.s
+        rows = [unbalanced_rows(rng, s.num_tasks, s.batch, pos, full, s.capacity, s.nstep) for _ in range(steps)]
+        slots = np.ascontiguousarray(np.concatenate([r[0] for r in rows]))
+        tasks = np.ascontiguousarray(np.concatenate([r[1] for r in rows]))
+        self._push_rng()
+        return slots, tasks
+
+    def sample_unbalanced(self):
+        """sample_unbalanced(batch) (buffers.py:1230-1279): rows drawn on the host, gathered on the device."""
+        slots, tasks = self._rows(1)
+        _drq_check(self.lib.drq_sample_rows(self.h, _ptr(slots), _ptr(tasks)))
+
+    def sample_unbalanced_update(self, steps: int = 1):
+        """`steps` x (sample_unbalanced + update): OffPolicyAlgorithm.train's inner loop (base.py:213-221)."""
+        if steps <= 0:
+            return
+        slots, tasks = self._rows(steps)
+        _drq_check(self.lib.drq_sample_rows_update(self.h, _ptr(slots), _ptr(tasks), int(steps)))
 
     def read_batch(self):
         B, C, H = self.s.batch, self.s.in_ch, self.s.hw

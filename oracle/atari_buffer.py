@@ -4,6 +4,8 @@ the n-step ring and _get_nstep_info, _sample_indices with the guard window, samp
 min-max reward normalisation).  numpy, same dtypes and operation order as the reference, so the
 device path is compared bit for bit (indices from numpy's own Generator).
 
+sample_unbalanced restates buffers.py:1230-1279 (Dirichlet task sizes, per-task gathers).
+
 Kept from the reference: the sampled rows are (sample i, task t) in i-major order (obs[idx] of shape
 [n][T] flattened), while task_ids = repeat(arange(T), n) lists tasks in task-major order
 (buffers.py:1213-1227) -- the two orders differ whenever n > 1."""
@@ -103,3 +105,40 @@ class AtariBuffer:
         f = lambda a: a.reshape(batch_size, *a.shape[2:])
         return (f(self.obs[idx]), f(self.actions[idx]), f(self.obs[nidx]), f(self.truncations[idx]),
                 f(self.dones[idx]), f(rewards), task_ids)
+
+    def sample_unbalanced(self, batch_size):  # buffers.py:1230-1279
+        weights = self.rng.dirichlet([1] * self.T)
+        task_sizes = np.floor(weights * batch_size).astype(np.int32)
+        remainder = batch_size - task_sizes.sum()
+        if remainder > 0:
+            task_sizes[np.argsort(-weights)[:remainder]] += 1
+        shp = self.obs.shape[2:]
+        out_obs = np.empty((batch_size, *shp), np.uint8)
+        out_next = np.empty((batch_size, *shp), np.uint8)
+        out_act = np.empty((batch_size,), np.int32)
+        out_tr = np.empty((batch_size, 1), np.float32)
+        out_d = np.empty((batch_size, 1), np.float32)
+        out_r = np.empty((batch_size, 1), np.float32)
+        out_t = np.empty((batch_size,), np.int32)
+        cursor = 0
+        for i in range(self.T):
+            n = task_sizes[i]
+            if n == 0:
+                continue
+            sl = slice(cursor, cursor + n)
+            idx = self.sample_indices(n)
+            nxt = (idx + self.nstep) % self.capacity
+            out_obs[sl] = self.obs[idx, i]
+            out_next[sl] = self.obs[nxt, i]
+            out_act[sl] = self.actions[idx, i]
+            out_tr[sl] = self.truncations[idx, i]
+            out_d[sl] = self.dones[idx, i]
+            out_t[sl] = i
+            r = self.rewards[idx, i]
+            if self.normalize_rewards:
+                r = r.copy()
+                r -= self.min_r[i]
+                r /= (self.max_r[i] - self.min_r[i] + self.eps)
+            out_r[sl] = r
+            cursor += n
+        return out_obs, out_act, out_next, out_tr, out_d, out_r, out_t

@@ -189,6 +189,70 @@ def test_device_buffer_matches_reference_buffer(normalize):
     e.close()
 
 
+@pytest.mark.parametrize("normalize", [False, True], ids=["raw", "normalized"])
+def test_unbalanced_sample_matches_reference_buffer(normalize):
+    """sample_unbalanced (buffers.py:1230-1279, the one OffPolicyAlgorithm.train calls) against the
+    numpy restatement bit for bit, batch not a multiple of the task count, interleaved with the
+    balanced device sampler on the same Generator stream (host <-> device hand-over of the state)."""
+    from mtrl_amd.drq import DrQEngine, DrQSettings
+    from oracle.atari_buffer import AtariBuffer
+
+    T, cap, hw, B = 5, 29, 20, 23
+    ref = AtariBuffer(cap, T, (4, hw, hw), seed=7, nstep=3, gamma=0.99, normalize_rewards=normalize)
+    e = DrQEngine(DrQSettings(num_tasks=T, hw=hw, n_hidden=64, batch=B, capacity=cap, normalize_rewards=int(normalize)))
+    e.seed_rng(7)
+    rng = np.random.default_rng(9)
+    names = ("obs", "actions", "next_obs", "truncations", "dones", "rewards", "task_ids")
+    checks = 0
+    for step in range(80):
+        o = rng.integers(0, 256, (T, 4, hw, hw), dtype=np.uint8)
+        no = rng.integers(0, 256, (T, 4, hw, hw), dtype=np.uint8)
+        a = rng.integers(0, 18, T).astype(np.int32)
+        r = np.round(rng.standard_normal(T) * 3, 2).astype(np.float32)
+        tr = (rng.random(T) < 0.05).astype(np.float32)
+        d = (rng.random(T) < 0.15).astype(np.float32)
+        ref.add(o, no, a, r, tr, d)
+        e.buffer_add(o, no, a, r, tr, d)
+        if ref.pos > 0 or ref.full:
+            if step % 2 == 0:
+                want = ref.sample_unbalanced(B)
+                e.sample_unbalanced()
+            elif step % 7 == 1:  # the balanced sampler needs batch % T == 0: draw its indices only
+                want = None
+                ref.sample_indices(3)
+                e2 = e.get_rng_state()
+                g = np.random.Generator(np.random.PCG64())
+                g.bit_generator.state = e2
+                g.integers(0, max(ref.pos - 3, 1) if not ref.full else cap - 9, size=(3,))
+                e.set_rng_state(g.bit_generator.state)
+            else:
+                continue
+            if want is not None:
+                got = e.read_batch()
+                for nm, gv, w in zip(names, got, want):
+                    np.testing.assert_array_equal(np.asarray(gv).reshape(np.shape(w)).astype(np.asarray(w).dtype), w,
+                                                  err_msg=f"{nm} at step {step}")
+                checks += 1
+    assert ref.full and checks > 25
+    assert e.get_rng_state() == ref.rng.bit_generator.state
+    e.close()
+
+
+def test_sample_rows_rejects_out_of_range():
+    from mtrl_amd import _lib as L
+    from mtrl_amd.drq import DrQEngine, DrQSettings
+
+    e = DrQEngine(DrQSettings(num_tasks=2, hw=20, n_hidden=64, batch=4, capacity=12))
+    tasks = np.zeros(4, np.int32)
+    for slots, tk in ((np.array([0, 1, 12, 2], np.int64), tasks), (np.array([0, 1, -1, 2], np.int64), tasks),
+                      (np.zeros(4, np.int64), np.array([0, 2, 0, 0], np.int32))):
+        assert e.lib.drq_sample_rows(e.h, slots.ctypes.data, tk.ctypes.data) == -22
+        assert b"out of range" in e.lib.drq_last_error()
+    with pytest.raises(L.MTSACError, match="empty buffer"):
+        e.sample_unbalanced()
+    e.close()
+
+
 def test_sample_update_runs():
     from mtrl_amd import _lib as L
     from mtrl_amd.drq import DrQEngine, DrQSettings
@@ -207,6 +271,10 @@ def test_sample_update_runs():
     e.synchronize()
     logs = e.logs()
     assert all(np.isfinite(v) for v in logs.values())
+    e.seed_augment(5)
+    e.sample_unbalanced_update(70)  # > one 64-step row upload
+    e.synchronize()
+    assert all(np.isfinite(v) for v in e.logs().values())
     e.close()
 
 
@@ -226,6 +294,8 @@ def test_compat_device_buffer_and_fast_path():
     data = buf.sample(52)
     assert data.observations.shape == (52, 4, 84, 84) and data.rewards.shape == (52, 1)
     agent, logs = agent.update(data)
+    ub = buf.sample_unbalanced(52)
+    assert ub.observations.shape == (52, 4, 84, 84) and np.all(np.diff(ub.task_ids) >= 0)
     agent, logs2 = agent.update_from_buffer(2)
     assert all(np.isfinite(v) for v in list(logs.values()) + list(logs2.values()))
     agent.close()

@@ -16,6 +16,7 @@ ap.add_argument("--steps", type=int, default=200)
 ap.add_argument("--warmup", type=int, default=20)
 ap.add_argument("--batch", type=int, default=256)
 ap.add_argument("--cpu-steps", type=int, default=3)
+ap.add_argument("--capacity", type=int, default=1000, help="device buffer slots per task for the sample+update leg")
 args = ap.parse_args()
 
 from mtrl_amd import _lib as L  # noqa: E402
@@ -49,6 +50,31 @@ dt = time.perf_counter() - t0
 logs = e.logs()
 e.close()
 
+# sample_unbalanced + update from the device Atari buffer (MemoryEfficientAtariMultiTaskReplayBuffer,
+# what OffPolicyAlgorithm.train calls), filled past capacity so the guard window is in play; the
+# Dirichlet / index draws on the host are inside the timed region
+import dataclasses  # noqa: E402
+
+eb = DrQEngine(dataclasses.replace(DrQSettings(batch=B), capacity=args.capacity))
+eb.set_params(L.DRQ_PARAMS, p0)
+eb.set_params(L.DRQ_TARGET, p0)
+eb.seed_rng(1)
+T = 26
+a0 = time.perf_counter()
+for i in range(args.capacity + 8):
+    o = np.roll(obs[:T], i, axis=-1)
+    eb.buffer_add(o, o, act[:T], rew[:T], np.zeros(T, np.float32), done[:T])
+eb.synchronize()
+add_dt = time.perf_counter() - a0
+eb.seed_augment(2)
+eb.sample_unbalanced_update(args.warmup)
+eb.synchronize()
+t0 = time.perf_counter()
+eb.sample_unbalanced_update(args.steps)
+eb.synchronize()
+sdt = time.perf_counter() - t0
+eb.close()
+
 import torch  # noqa: E402
 
 threads = torch.get_num_threads()
@@ -65,6 +91,10 @@ print(json.dumps({
     "value": args.steps / dt, "unit": "gradient steps/sec", "ms_per_step": 1e3 * dt / args.steps,
     "steps": args.steps, "warmup": args.warmup, "dtype": "fp32", "data": "synthetic uint8 frames, resident batch",
     "logs": logs,
+    "sample_update": {"value": args.steps / sdt, "unit": "gradient steps/sec", "ms_per_step": 1e3 * sdt / args.steps,
+                      "sampler": "sample_unbalanced (host draws, device gather + augmentation draws)",
+                      "capacity_per_task": args.capacity, "buffer_full": True,
+                      "add_ms_per_env_step": 1e3 * add_dt / (args.capacity + 8)},
     "cpu_baseline": {"value": args.cpu_steps / cdt, "unit": "gradient steps/sec", "cores": threads, "kind": "port",
                      "sample": f"{args.cpu_steps} steps of the PyTorch-CPU fp32 restatement (oracle/drq.py), batch {B}"},
 }), flush=True)
