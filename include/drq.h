@@ -39,8 +39,15 @@ typedef struct drq_config {
   float lr, b1, b2, eps, weight_decay, ln_eps;    /* 1e-4, 0.9, 0.999, 1.5e-4, 0.05, 1e-6 */
   long long capacity;     /* replay slots per task (0: no device buffer; buffer_size / num_tasks) */
   int normalize_rewards;  /* per-task min-max reward normalisation at sample time */
-  int reserved;
+  int buffer_kind;        /* DRQ_BUFFER_MEMORY_EFFICIENT (0) or DRQ_BUFFER_ATARI (1) */
 } drq_config;
+
+/* MemoryEfficientAtariMultiTaskReplayBuffer (buffers.py:949-1279): next_obs is the slot nstep
+ * ahead in the one frame array, indices avoid the guard window [pos, pos + nstep + 6). */
+#define DRQ_BUFFER_MEMORY_EFFICIENT 0
+/* AtariMultiTaskReplayBuffer (buffers.py:710-947): a second frame array for next_obs, indices in
+ * [0, max(pos or capacity, n)) with no guard window. */
+#define DRQ_BUFFER_ATARI 1
 
 typedef struct drq_engine drq_engine;
 

@@ -163,7 +163,7 @@ class DrqConfig(ctypes.Structure):  # include/drq.h
                                               "embed_dim", "n_hidden", "batch", "nstep")] + \
                [(n, ctypes.c_float) for n in ("gamma", "v_min", "v_max", "tau", "lr", "b1", "b2", "eps",
                                               "weight_decay", "ln_eps")] + \
-               [("capacity", ctypes.c_int64), ("normalize_rewards", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+               [("capacity", ctypes.c_int64), ("normalize_rewards", ctypes.c_int32), ("buffer_kind", ctypes.c_int32)]
 
 
 class DrqBatch(ctypes.Structure):

@@ -88,6 +88,26 @@ class DrQ:
         self.engine.sample_unbalanced_update(steps)
         return self, self.engine.logs()
 
+    def shrink_and_perturb(self, dummy_obs=None, critic_config=None, action_dim=None, shrink_rate: float = 0.5) -> "DrQ":
+        """drqeps.py:212-245: encoder leaves pulled halfway to a fresh init, the rest re-initialised,
+        target = the new parameters, a fresh AdamW state.  The geometry is the engine's (the
+        reference's dummy_obs / critic_config / action_dim arguments rebuild the same network)."""
+        from mtrl_amd import _lib as L
+
+        from ....drq_init import shrink_and_perturb
+
+        s = self.engine.s
+        geo = dict(num_tasks=s.num_tasks, n_actions=s.n_actions, n_atoms=s.n_atoms, in_ch=s.in_ch, hw=s.hw,
+                   scale=s.scale, embed_dim=s.embed_dim, n_hidden=s.n_hidden)
+        p = shrink_and_perturb(self.engine.get_params(L.DRQ_PARAMS), self.rng, shrink_rate, **geo)
+        self.engine.set_params(L.DRQ_PARAMS, p)
+        self.engine.set_params(L.DRQ_TARGET, p)
+        zero = np.zeros_like(p)
+        self.engine.set_params(L.DRQ_ADAM_MU, zero)
+        self.engine.set_params(L.DRQ_ADAM_NU, zero)
+        self.engine.set_step(0)
+        return self
+
     def get_num_params(self) -> dict[str, int]:
         return {"critic_num_params": self.engine.n}
 

@@ -58,8 +58,10 @@ __global__ void augment_kernel(const unsigned char* __restrict__ obs, const int*
 // min-max normalised in double per task; task_ids as the reference lists them (b / n).
 // Row mode (rslot != null, sample_unbalanced, buffers.py:1230-1279): row b reads slot rslot[b] of
 // task rtask[b], both drawn on the host, and task_ids = rtask[b].
+// AtariMultiTaskReplayBuffer (nstore != null): next_obs from its own array at the same slot.
 struct AtariSampleParams {
   const unsigned char* store;  // [cap][T][img]
+  const unsigned char* nstore; // [cap][T][img] next_obs (buffer kind 1) or null
   const int* act;
   const float *rew, *done, *trunc;  // [cap][T]
   const double* minmax;        // [2][T] (normalize) or null
@@ -84,9 +86,9 @@ __global__ void atari_sample_kernel(AtariSampleParams p) {
     if (p.pos + p.guard <= p.cap) slot = k < p.pos ? k : k + p.guard;
     else slot = k + (p.pos + p.guard - p.cap);
   }
-  const long long nslot = (slot + p.nstep) % p.cap;
+  const long long nslot = p.nstore ? slot : (slot + p.nstep) % p.cap;
   const uint4* src = reinterpret_cast<const uint4*>(p.store) + (slot * p.T + t) * p.img16;
-  const uint4* nsrc = reinterpret_cast<const uint4*>(p.store) + (nslot * p.T + t) * p.img16;
+  const uint4* nsrc = reinterpret_cast<const uint4*>(p.nstore ? p.nstore : p.store) + (nslot * p.T + t) * p.img16;
   uint4* dst = reinterpret_cast<uint4*>(p.obs) + (long long)b * p.img16;
   uint4* ndst = reinterpret_cast<uint4*>(p.nobs) + (long long)b * p.img16;
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < p.img16; c += gridDim.x * blockDim.x) {
@@ -97,10 +99,14 @@ __global__ void atari_sample_kernel(AtariSampleParams p) {
     const long long r = slot * p.T + t;
     p.act_out[b] = p.act[r];
     float rw = p.rew[r];
-    if (p.minmax) {  // rewards -= mn; rewards /= (mx - mn + eps): float64 ops, float32 storage
+    if (p.minmax) {
       const double mn = p.minmax[t], mx = p.minmax[p.T + t];
-      rw = (float)((double)rw - mn);
-      rw = (float)((double)rw / (mx - mn + p.eps));
+      if (p.nstore) {  // (rewards - mn) / (mx - mn + eps) in float64, one rounding (buffers.py:877)
+        rw = (float)(((double)rw - mn) / (mx - mn + p.eps));
+      } else {  // rewards -= mn; rewards /= (...): in place on float32 (buffers.py:1207-1212)
+        rw = (float)((double)rw - mn);
+        rw = (float)((double)rw / (mx - mn + p.eps));
+      }
     }
     p.rew_out[b] = rw;
     p.done_out[b] = p.done[r];
@@ -766,22 +772,23 @@ __global__ void drq_logs_kernel(const float* __restrict__ part, int G, const flo
 // ------------------------------------------------------------------ launchers
 static unsigned blocks(long long n, int t = 256) { return (unsigned)((n + t - 1) / t); }
 
-void atari_sample(const unsigned char* store, const int* act, const float* rew, const float* done, const float* trunc,
-                  const double* minmax, const int* idx, long long cap, int T, int n, int img_bytes, int nstep,
-                  int full, int pos, int guard, double eps, unsigned char* obs, unsigned char* nobs, int* act_out,
-                  float* rew_out, float* done_out, float* trunc_out, int* task_out, hipStream_t st) {
-  AtariSampleParams p{store, act, rew, done, trunc, minmax, idx, cap, T, n, img_bytes / 16, nstep, full, pos, guard,
-                      eps, obs, nobs, act_out, task_out, rew_out, done_out, trunc_out, nullptr, nullptr};
+void atari_sample(const unsigned char* store, const unsigned char* nstore, const int* act, const float* rew,
+                  const float* done, const float* trunc, const double* minmax, const int* idx, long long cap, int T,
+                  int n, int img_bytes, int nstep, int full, int pos, int guard, double eps, unsigned char* obs,
+                  unsigned char* nobs, int* act_out, float* rew_out, float* done_out, float* trunc_out, int* task_out,
+                  hipStream_t st) {
+  AtariSampleParams p{store, nstore, act, rew, done, trunc, minmax, idx, cap, T, n, img_bytes / 16, nstep, full, pos,
+                      guard, eps, obs, nobs, act_out, task_out, rew_out, done_out, trunc_out, nullptr, nullptr};
   hipLaunchKernelGGL(atari_sample_kernel, dim3(4, n * T), dim3(256), 0, st, p);
 }
 
-void atari_sample_rows(const unsigned char* store, const int* act, const float* rew, const float* done,
-                       const float* trunc, const double* minmax, const long long* slots, const int* tasks, int rows,
-                       long long cap, int T, int img_bytes, int nstep, double eps, unsigned char* obs,
+void atari_sample_rows(const unsigned char* store, const unsigned char* nstore, const int* act, const float* rew,
+                       const float* done, const float* trunc, const double* minmax, const long long* slots,
+                       const int* tasks, int rows, long long cap, int T, int img_bytes, int nstep, double eps, unsigned char* obs,
                        unsigned char* nobs, int* act_out, float* rew_out, float* done_out, float* trunc_out,
                        int* task_out, hipStream_t st) {
-  AtariSampleParams p{store, act, rew, done, trunc, minmax, nullptr, cap, T, 1, img_bytes / 16, nstep, 0, 0, 0,
-                      eps, obs, nobs, act_out, task_out, rew_out, done_out, trunc_out, slots, tasks};
+  AtariSampleParams p{store, nstore, act, rew, done, trunc, minmax, nullptr, cap, T, 1, img_bytes / 16, nstep, 0, 0,
+                      0, eps, obs, nobs, act_out, task_out, rew_out, done_out, trunc_out, slots, tasks};
   hipLaunchKernelGGL(atari_sample_kernel, dim3(4, rows), dim3(256), 0, st, p);
 }
 

@@ -82,6 +82,7 @@ struct drq_engine {
   long long cap = 0, img = 0, pos = 0;
   int full = 0, ns_pos = 0, ns_count = 0, n_per_task = 0;
   unsigned char* store = nullptr;
+  unsigned char* nstore = nullptr;  // buffer kind 1: next_obs [cap][T][img]
   int* b_act = nullptr;
   float *b_rew = nullptr, *b_done = nullptr, *b_trunc = nullptr, *trunc = nullptr;
   double* d_minmax = nullptr;
@@ -200,12 +201,13 @@ struct drq_engine {
         }
       }
     }
-    const long long p = pos, pn = (pos + n) % cap;
+    const long long p = pos, pn = nstore ? pos : (pos + n) % cap;
     std::vector<unsigned char> nxt(row);
     for (int t = 0; t < T; ++t) std::memcpy(&nxt[(size_t)t * img], &ns_next[(size_t)src[t] * row + (size_t)t * img], img);
     if (hipMemcpyAsync(store + (size_t)p * row, &ns_obs[(size_t)oldest * row], row, hipMemcpyHostToDevice, st) !=
             hipSuccess ||
-        hipMemcpyAsync(store + (size_t)pn * row, nxt.data(), row, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync((nstore ? nstore : store) + (size_t)pn * row, nxt.data(), row, hipMemcpyHostToDevice, st) !=
+            hipSuccess ||
         hipMemcpyAsync(b_act + p * T, &ns_act[oldest * T], sizeof(int) * T, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(b_rew + p * T, rw.data(), sizeof(float) * T, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(b_done + p * T, dn.data(), sizeof(float) * T, hipMemcpyHostToDevice, st) != hipSuccess ||
@@ -227,13 +229,16 @@ struct drq_engine {
   int sample() {
     if (n_per_task < 1 || B % T != 0) return fail(-22, "balanced sample: batch % num_tasks must be 0");
     const int n = n_per_task, guard = cfg.nstep + 6;
-    const long long high = full ? cap - guard : std::max(pos - cfg.nstep, 1LL);
+    // kind 1: integers(0, max(pos or capacity, n)) (buffers.py:863-869)
+    const long long high = nstore ? std::max(full ? cap : pos, (long long)n)
+                                  : full ? cap - guard : std::max(pos - cfg.nstep, 1LL);
     replay_indices_high(rng, jump, high, n, idx, st);
     if (cfg.normalize_rewards &&
         hipMemcpyAsync(d_minmax, minmax.data(), sizeof(double) * 2 * T, hipMemcpyHostToDevice, st) != hipSuccess)
       return fail(-5, "reward stats upload failed");
-    drq::atari_sample(store, b_act, b_rew, b_done, b_trunc, cfg.normalize_rewards ? d_minmax : nullptr, idx, cap, T, n,
-                      (int)img, cfg.nstep, full, (int)pos, guard, 1e-8, obs_u8, nobs_u8, act, rew, done, trunc, task, st);
+    drq::atari_sample(store, nstore, b_act, b_rew, b_done, b_trunc, cfg.normalize_rewards ? d_minmax : nullptr, idx,
+                      cap, T, n, (int)img, cfg.nstep, nstore ? 0 : full, (int)pos, guard, 1e-8, obs_u8, nobs_u8, act,
+                      rew, done, trunc, task, st);
     return 0;
   }
 
@@ -243,9 +248,9 @@ struct drq_engine {
     if (cfg.normalize_rewards &&
         hipMemcpyAsync(d_minmax, minmax.data(), sizeof(double) * 2 * T, hipMemcpyHostToDevice, st) != hipSuccess)
       return fail(-5, "reward stats upload failed");
-    drq::atari_sample_rows(store, b_act, b_rew, b_done, b_trunc, cfg.normalize_rewards ? d_minmax : nullptr, slots,
-                           tasks, B, cap, T, (int)img, cfg.nstep, 1e-8, obs_u8, nobs_u8, act, rew, done, trunc, task,
-                           st);
+    drq::atari_sample_rows(store, nstore, b_act, b_rew, b_done, b_trunc, cfg.normalize_rewards ? d_minmax : nullptr,
+                           slots, tasks, B, cap, T, (int)img, cfg.nstep, 1e-8, obs_u8, nobs_u8, act, rew, done, trunc,
+                           task, st);
     return 0;
   }
 
@@ -464,7 +469,10 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
       return bad(fail(-22, "buffer: capacity > nstep + 6, frames of 16-B multiples"));
     e->cap = c->capacity;
     e->n_per_task = B / e->T;
+    if (c->buffer_kind != DRQ_BUFFER_MEMORY_EFFICIENT && c->buffer_kind != DRQ_BUFFER_ATARI)
+      return bad(fail(-22, "buffer_kind"));
     if ((rc = e->alloc(&e->store, e->cap * e->T * e->img))) return bad(rc);
+    if (c->buffer_kind == DRQ_BUFFER_ATARI && (rc = e->alloc(&e->nstore, e->cap * e->T * e->img))) return bad(rc);
     if ((rc = e->alloc(&e->b_act, e->cap * e->T))) return bad(rc);
     for (float** q : {&e->b_rew, &e->b_done, &e->b_trunc})
       if ((rc = e->alloc(q, e->cap * e->T))) return bad(rc);

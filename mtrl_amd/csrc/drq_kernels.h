@@ -9,15 +9,17 @@ namespace drq {
 // edge pad `pad`, crop offsets crop[b] = (along H, along W) in [0, 2 pad]
 void augment(const unsigned char* obs, const int* crop, const float* noise, float* out, int B, int C, int H, int W,
              int pad, hipStream_t st);
-// MemoryEfficientAtariMultiTaskReplayBuffer.sample rows from the device store (img_bytes % 16 == 0)
-void atari_sample(const unsigned char* store, const int* act, const float* rew, const float* done, const float* trunc,
-                  const double* minmax, const int* idx, long long cap, int T, int n, int img_bytes, int nstep,
-                  int full, int pos, int guard, double eps, unsigned char* obs, unsigned char* nobs, int* act_out,
-                  float* rew_out, float* done_out, float* trunc_out, int* task_out, hipStream_t st);
+// MemoryEfficientAtariMultiTaskReplayBuffer.sample rows from the device store (img_bytes % 16 == 0);
+// nstore != null: AtariMultiTaskReplayBuffer's separate next_obs array (no guard: pass full = 0)
+void atari_sample(const unsigned char* store, const unsigned char* nstore, const int* act, const float* rew,
+                  const float* done, const float* trunc, const double* minmax, const int* idx, long long cap, int T,
+                  int n, int img_bytes, int nstep, int full, int pos, int guard, double eps, unsigned char* obs,
+                  unsigned char* nobs, int* act_out, float* rew_out, float* done_out, float* trunc_out, int* task_out,
+                  hipStream_t st);
 // sample_unbalanced rows: row b = (slot slots[b], task tasks[b]), both drawn on the host
-void atari_sample_rows(const unsigned char* store, const int* act, const float* rew, const float* done,
-                       const float* trunc, const double* minmax, const long long* slots, const int* tasks, int rows,
-                       long long cap, int T, int img_bytes, int nstep, double eps, unsigned char* obs,
+void atari_sample_rows(const unsigned char* store, const unsigned char* nstore, const int* act, const float* rew,
+                       const float* done, const float* trunc, const double* minmax, const long long* slots,
+                       const int* tasks, int rows, long long cap, int T, int img_bytes, int nstep, double eps, unsigned char* obs,
                        unsigned char* nobs, int* act_out, float* rew_out, float* done_out, float* trunc_out,
                        int* task_out, hipStream_t st);
 // fresh augmentation draws for obs and next_obs from (seed, ctr): crops in [0, 2 pad), intensity

@@ -40,6 +40,7 @@ class DrQSettings:
     ln_eps: float = 1e-6
     capacity: int = 0  # device replay slots per task (0: none)
     normalize_rewards: int = 0
+    buffer_kind: int = 0  # 0: MemoryEfficientAtariMultiTaskReplayBuffer, 1: AtariMultiTaskReplayBuffer
 
 
 def _ptr(a):
@@ -54,11 +55,12 @@ def _drq_check(rc: int) -> int:
 
 
 def unbalanced_rows(rng: np.random.Generator, num_tasks: int, batch: int, pos: int, full: bool, capacity: int,
-                    nstep: int):
+                    nstep: int, kind: int = 0):
     """The host draws of sample_unbalanced (buffers.py:1235-1257) with _sample_indices
     (buffers.py:1082-1100): Dirichlet(1, ..., 1) task weights, floor(w * batch) rows per task plus
     the remainder to the largest weights, then each task's slots from the same Generator.  The
-    guard window's valid[k] is computed arithmetically (no list of the capacity).
+    guard window's valid[k] is computed arithmetically (no list of the capacity).  kind 1
+    (AtariMultiTaskReplayBuffer.sample_unbalanced, buffers.py:896-947): slots in [0, pos or capacity).
     Returns (slots int64 [batch], task ids int32 [batch]) in the reference's row order."""
     weights = rng.dirichlet([1] * num_tasks)
     sizes = np.floor(weights * batch).astype(np.int32)
@@ -73,7 +75,9 @@ def unbalanced_rows(rng: np.random.Generator, num_tasks: int, batch: int, pos: i
         n = int(sizes[i])
         if n == 0:
             continue
-        if not full:
+        if kind == 1:
+            idx = rng.integers(0, capacity if full else pos, size=(n,))
+        elif not full:
             idx = rng.integers(0, max(pos - nstep, 1), size=(n,))
         else:
             k = rng.integers(0, capacity - guard, size=(n,))
@@ -88,7 +92,7 @@ class DrQEngine:
     def __init__(self, s: DrQSettings = DrQSettings(), device: int = 0):
         self.lib = L.load()
         self.s = s
-        c = L.DrqConfig(**{k: getattr(s, k) for k, _ in L.DrqConfig._fields_ if k != "reserved"})
+        c = L.DrqConfig(**{k: getattr(s, k) for k, _ in L.DrqConfig._fields_})
         h = ctypes.c_void_p()
         _drq_check(self.lib.drq_create(ctypes.byref(c), device, ctypes.byref(h)))
         self.h = h
@@ -211,7 +215,8 @@ class DrQEngine:
             raise L.MTSACError("libmtsac drq error -22: empty buffer")
         rng = self._host_rng()
         s = self.s
-        rows = [unbalanced_rows(rng, s.num_tasks, s.batch, pos, full, s.capacity, s.nstep) for _ in range(steps)]
+        rows = [unbalanced_rows(rng, s.num_tasks, s.batch, pos, full, s.capacity, s.nstep, s.buffer_kind)
+                for _ in range(steps)]
         slots = np.ascontiguousarray(np.concatenate([r[0] for r in rows]))
         tasks = np.ascontiguousarray(np.concatenate([r[1] for r in rows]))
         self._push_rng()

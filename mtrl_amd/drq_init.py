@@ -65,3 +65,22 @@ def init_drq(seed: int = 1, shrink_rate: float = 0.5, **geometry) -> np.ndarray:
     parts = [(a * (1 - shrink_rate) + b * shrink_rate) if p.startswith("ImpalaEncoder_0") else b
              for (p, _), a, b in zip(spec, first, fresh)]
     return np.concatenate(parts).astype(np.float32)
+
+
+def shrink_and_perturb(params: np.ndarray, rng: np.random.Generator, shrink_rate: float = 0.5,
+                       **geometry) -> np.ndarray:
+    """DrQ.shrink_and_perturb (drqeps.py:212-245) on a flat parameter vector: one fresh draw; the
+    ImpalaEncoder leaves become old (1 - rate) + fresh rate (float32, as jax computes them), every
+    other leaf the fresh draw."""
+    spec = param_spec(**geometry)
+    fresh = _draw(spec, rng)
+    old = np.asarray(params, np.float32)
+    out, o = [], 0
+    r = np.float32(shrink_rate)
+    for (path, shape), new in zip(spec, fresh):
+        n = int(np.prod(shape))
+        new = new.astype(np.float32)
+        out.append(old[o:o + n] * (np.float32(1) - r) + new * r if path.startswith("ImpalaEncoder_0") else new)
+        o += n
+    assert o == old.size, (o, old.size)
+    return np.concatenate(out)

@@ -5,6 +5,9 @@ min-max reward normalisation).  numpy, same dtypes and operation order as the re
 device path is compared bit for bit (indices from numpy's own Generator).
 
 sample_unbalanced restates buffers.py:1230-1279 (Dirichlet task sizes, per-task gathers).
+kind=1 restates AtariMultiTaskReplayBuffer (buffers.py:710-947) instead: its own next_obs array,
+indices in [0, max(pos or capacity, n)) with no guard window, and the reward normalisation as one
+float64 expression (no in-place float32 rounding in between).
 
 Kept from the reference: the sampled rows are (sample i, task t) in i-major order (obs[idx] of shape
 [n][T] flattened), while task_ids = repeat(arange(T), n) lists tasks in task-major order
@@ -17,7 +20,8 @@ import numpy as np
 
 class AtariBuffer:
     def __init__(self, capacity: int, num_tasks: int, obs_shape, seed: int, nstep: int = 3, gamma: float = 0.99,
-                 normalize_rewards: bool = False, reward_norm_eps: float = 1e-8):
+                 normalize_rewards: bool = False, reward_norm_eps: float = 1e-8, kind: int = 0):
+        self.kind = kind
         self.capacity, self.T, self.nstep, self.gamma = capacity, num_tasks, nstep, gamma
         self.normalize_rewards, self.eps = normalize_rewards, reward_norm_eps
         self.rng = np.random.default_rng(seed)
@@ -32,6 +36,8 @@ class AtariBuffer:
         self.min_r = np.full(T, np.inf)
         self.max_r = np.full(T, -np.inf)
         self.obs = np.zeros((capacity, T, *obs_shape), np.uint8)
+        if kind == 1:
+            self.next_obs = np.zeros((capacity, T, *obs_shape), np.uint8)
         self.actions = np.zeros((capacity, T), np.int32)
         self.rewards = np.zeros((capacity, T, 1), np.float32)
         self.dones = np.zeros((capacity, T, 1), np.float32)
@@ -71,7 +77,10 @@ class AtariBuffer:
         o, a, r, tr, d, nxt = self._nstep_info()
         p = self.pos
         self.obs[p] = o
-        self.obs[(p + self.nstep) % self.capacity] = nxt
+        if self.kind == 1:
+            self.next_obs[p] = nxt  # buffers.py:836
+        else:
+            self.obs[(p + self.nstep) % self.capacity] = nxt
         self.actions[p] = a
         self.rewards[p] = r.reshape(-1, 1)
         self.dones[p] = d.reshape(-1, 1)
@@ -84,6 +93,8 @@ class AtariBuffer:
             self.full = True
 
     def sample_indices(self, n):  # buffers.py:1082-1105
+        if self.kind == 1:  # buffers.py:863-869
+            return self.rng.integers(0, max(self.pos if not self.full else self.capacity, n), size=(n,))
         if not self.full:
             return self.rng.integers(0, max(self.pos - self.nstep, 1), size=(n,))
         guard = self.nstep + 6
@@ -96,6 +107,15 @@ class AtariBuffer:
         idx = self.sample_indices(n)
         nidx = (idx + self.nstep) % self.capacity
         rewards = self.rewards[idx].copy()
+        if self.kind == 1:  # buffers.py:872-892
+            if self.normalize_rewards:
+                mn = self.min_r[None, :, None]
+                mx = self.max_r[None, :, None]
+                rewards = (rewards - mn) / (mx - mn + self.eps)
+            task_ids = np.repeat(np.arange(self.T), n)
+            f = lambda a: a.reshape(batch_size, *a.shape[2:])
+            return (f(self.obs[idx]), f(self.actions[idx]), f(self.next_obs[idx]), f(self.truncations[idx]),
+                    f(self.dones[idx]), f(rewards), task_ids)
         if self.normalize_rewards:
             mn = self.min_r[None, :, None]
             mx = self.max_r[None, :, None]
@@ -126,16 +146,21 @@ class AtariBuffer:
             if n == 0:
                 continue
             sl = slice(cursor, cursor + n)
-            idx = self.sample_indices(n)
-            nxt = (idx + self.nstep) % self.capacity
+            if self.kind == 1:  # buffers.py:922-937
+                idx = self.rng.integers(0, self.pos if not self.full else self.capacity, size=(n,))
+                out_next[sl] = self.next_obs[idx, i]
+            else:
+                idx = self.sample_indices(n)
+                out_next[sl] = self.obs[(idx + self.nstep) % self.capacity, i]
             out_obs[sl] = self.obs[idx, i]
-            out_next[sl] = self.obs[nxt, i]
             out_act[sl] = self.actions[idx, i]
             out_tr[sl] = self.truncations[idx, i]
             out_d[sl] = self.dones[idx, i]
             out_t[sl] = i
             r = self.rewards[idx, i]
-            if self.normalize_rewards:
+            if self.normalize_rewards and self.kind == 1:
+                r = (r - self.min_r[i]) / (self.max_r[i] - self.min_r[i] + self.eps)
+            elif self.normalize_rewards:
                 r = r.copy()
                 r -= self.min_r[i]
                 r /= (self.max_r[i] - self.min_r[i] + self.eps)

@@ -6,6 +6,7 @@ experiments/atari.py's config tree)."""
 from __future__ import annotations
 
 import numpy as np
+import pytest
 import torch
 
 from oracle import drq as od
@@ -69,3 +70,50 @@ def test_compat_config_tree():
     assert (t.batch_size, t.nstep, t.replay_ratio) == (256, 3, 2)
     env = AtariConfig()
     assert env.observation_space.shape == (4, 84, 84) and env.action_space.n == 18
+
+
+@pytest.mark.parametrize("kind", [0, 1], ids=["memory_efficient", "atari"])
+def test_unbalanced_rows_reproduce_reference_draws(kind):
+    """The host half of sample_unbalanced (mtrl_amd.drq.unbalanced_rows): the same Generator calls
+    as buffers.py:1235-1257 / 906-925, so gathering the restated buffer at its (slot, task) rows
+    gives the restatement's own batch, through the fill and the (wrapping) guard window."""
+    from mtrl_amd.drq import unbalanced_rows
+    from oracle.atari_buffer import AtariBuffer
+
+    T, cap, B = 6, 17, 31
+    ref = AtariBuffer(cap, T, (4, 4, 4), seed=3, kind=kind)
+    rng = np.random.default_rng(1)
+    host = np.random.default_rng(3)
+    for step in range(50):
+        o = rng.integers(0, 256, (T, 4, 4, 4), dtype=np.uint8)
+        ref.add(o, rng.integers(0, 256, (T, 4, 4, 4), dtype=np.uint8), rng.integers(0, 18, T), rng.standard_normal(T),
+                np.zeros(T), (rng.random(T) < 0.1) * 1.0)
+        if ref.pos == 0 and not ref.full:
+            continue
+        slots, tasks = unbalanced_rows(host, T, B, ref.pos, ref.full, cap, 3, kind)
+        want = ref.sample_unbalanced(B)
+        np.testing.assert_array_equal(ref.obs[slots, tasks], want[0])
+        nxt = ref.next_obs[slots, tasks] if kind == 1 else ref.obs[(slots + 3) % cap, tasks]
+        np.testing.assert_array_equal(nxt, want[2])
+        np.testing.assert_array_equal(tasks, want[6])
+        assert host.bit_generator.state == ref.rng.bit_generator.state
+    assert ref.full
+
+
+def test_shrink_and_perturb_mixes_only_the_encoder():
+    from mtrl_amd.drq_init import init_drq, param_spec, shrink_and_perturb
+
+    geo = dict(num_tasks=3, hw=20, n_hidden=64)
+    p = init_drq(1, **geo)
+    q = shrink_and_perturb(p, np.random.default_rng(5), 0.5, **geo)
+    fresh = shrink_and_perturb(np.zeros_like(p), np.random.default_rng(5), 0.5, **geo)
+    assert q.dtype == np.float32 and q.shape == p.shape
+    o = 0
+    for path, shape in param_spec(**geo):
+        n = int(np.prod(shape))
+        a, b, f = p[o:o + n], q[o:o + n], fresh[o:o + n]
+        if path.startswith("ImpalaEncoder_0"):
+            np.testing.assert_array_equal(b, a * np.float32(0.5) + (f * 2) * np.float32(0.5))
+        else:
+            np.testing.assert_array_equal(b, f)
+        o += n

@@ -150,18 +150,33 @@ def test_compat_drq_api():
     agent.close()
 
 
+def _same_batch(got, want, where):
+    names = ("obs", "actions", "next_obs", "truncations", "dones", "rewards", "task_ids")
+    for nm, g, w in zip(names, got, want):
+        w = np.asarray(w)
+        if w.dtype == np.float64:  # AtariMultiTaskReplayBuffer returns float64 rewards; the update takes float32
+            w = w.astype(np.float32)
+        np.testing.assert_array_equal(np.asarray(g).reshape(w.shape).astype(w.dtype), w, err_msg=f"{nm} at {where}")
+
+
+_KINDS = pytest.mark.parametrize("kind", [0, 1], ids=["memory_efficient", "atari"])
+
+
+@_KINDS
 @pytest.mark.parametrize("normalize", [False, True], ids=["raw", "normalized"])
-def test_device_buffer_matches_reference_buffer(normalize):
-    """MemoryEfficientAtariMultiTaskReplayBuffer (buffers.py:949-1229) on the device against its
-    numpy restatement: n-step aggregation with episode ends, the guard window once full (both the
-    plain and the wrapping case), the PCG64 index stream, reward normalisation -- bit for bit."""
+def test_device_buffer_matches_reference_buffer(normalize, kind):
+    """MemoryEfficientAtariMultiTaskReplayBuffer (buffers.py:949-1229, kind 0) and
+    AtariMultiTaskReplayBuffer (buffers.py:710-947, kind 1) on the device against their numpy
+    restatement: n-step aggregation with episode ends, the guard window once full (both the plain
+    and the wrapping case), the PCG64 index stream, reward normalisation -- bit for bit."""
     from mtrl_amd.drq import DrQEngine, DrQSettings
     from oracle.atari_buffer import AtariBuffer
 
     T, n, cap, hw = 4, 3, 23, 20
     B = T * n
-    ref = AtariBuffer(cap, T, (4, hw, hw), seed=11, nstep=3, gamma=0.99, normalize_rewards=normalize)
-    e = DrQEngine(DrQSettings(num_tasks=T, hw=hw, n_hidden=64, batch=B, capacity=cap, normalize_rewards=int(normalize)))
+    ref = AtariBuffer(cap, T, (4, hw, hw), seed=11, nstep=3, gamma=0.99, normalize_rewards=normalize, kind=kind)
+    e = DrQEngine(DrQSettings(num_tasks=T, hw=hw, n_hidden=64, batch=B, capacity=cap, normalize_rewards=int(normalize),
+                              buffer_kind=kind))
     e.seed_rng(11)
     rng = np.random.default_rng(5)
     checks = 0
@@ -179,18 +194,15 @@ def test_device_buffer_matches_reference_buffer(normalize):
             if step % 3 == 0:
                 want = ref.sample(B)
                 e.sample()
-                got = e.read_batch()
-                names = ("obs", "actions", "next_obs", "truncations", "dones", "rewards", "task_ids")
-                for nm, g, w in zip(names, got, want):
-                    np.testing.assert_array_equal(np.asarray(g).reshape(np.shape(w)).astype(np.asarray(w).dtype), w,
-                                                  err_msg=f"{nm} at step {step}")
+                _same_batch(e.read_batch(), want, f"step {step}")
                 checks += 1
     assert ref.full and checks > 15
     e.close()
 
 
+@_KINDS
 @pytest.mark.parametrize("normalize", [False, True], ids=["raw", "normalized"])
-def test_unbalanced_sample_matches_reference_buffer(normalize):
+def test_unbalanced_sample_matches_reference_buffer(normalize, kind):
     """sample_unbalanced (buffers.py:1230-1279, the one OffPolicyAlgorithm.train calls) against the
     numpy restatement bit for bit, batch not a multiple of the task count, interleaved with the
     balanced device sampler on the same Generator stream (host <-> device hand-over of the state)."""
@@ -198,11 +210,11 @@ def test_unbalanced_sample_matches_reference_buffer(normalize):
     from oracle.atari_buffer import AtariBuffer
 
     T, cap, hw, B = 5, 29, 20, 23
-    ref = AtariBuffer(cap, T, (4, hw, hw), seed=7, nstep=3, gamma=0.99, normalize_rewards=normalize)
-    e = DrQEngine(DrQSettings(num_tasks=T, hw=hw, n_hidden=64, batch=B, capacity=cap, normalize_rewards=int(normalize)))
+    ref = AtariBuffer(cap, T, (4, hw, hw), seed=7, nstep=3, gamma=0.99, normalize_rewards=normalize, kind=kind)
+    e = DrQEngine(DrQSettings(num_tasks=T, hw=hw, n_hidden=64, batch=B, capacity=cap, normalize_rewards=int(normalize),
+                              buffer_kind=kind))
     e.seed_rng(7)
     rng = np.random.default_rng(9)
-    names = ("obs", "actions", "next_obs", "truncations", "dones", "rewards", "task_ids")
     checks = 0
     for step in range(80):
         o = rng.integers(0, 256, (T, 4, hw, hw), dtype=np.uint8)
@@ -223,15 +235,15 @@ def test_unbalanced_sample_matches_reference_buffer(normalize):
                 e2 = e.get_rng_state()
                 g = np.random.Generator(np.random.PCG64())
                 g.bit_generator.state = e2
-                g.integers(0, max(ref.pos - 3, 1) if not ref.full else cap - 9, size=(3,))
+                if kind == 1:
+                    g.integers(0, max(ref.pos if not ref.full else cap, 3), size=(3,))
+                else:
+                    g.integers(0, max(ref.pos - 3, 1) if not ref.full else cap - 9, size=(3,))
                 e.set_rng_state(g.bit_generator.state)
             else:
                 continue
             if want is not None:
-                got = e.read_batch()
-                for nm, gv, w in zip(names, got, want):
-                    np.testing.assert_array_equal(np.asarray(gv).reshape(np.shape(w)).astype(np.asarray(w).dtype), w,
-                                                  err_msg=f"{nm} at step {step}")
+                _same_batch(e.read_batch(), want, f"step {step}")
                 checks += 1
     assert ref.full and checks > 25
     assert e.get_rng_state() == ref.rng.bit_generator.state
@@ -298,4 +310,32 @@ def test_compat_device_buffer_and_fast_path():
     assert ub.observations.shape == (52, 4, 84, 84) and np.all(np.diff(ub.task_ids) >= 0)
     agent, logs2 = agent.update_from_buffer(2)
     assert all(np.isfinite(v) for v in list(logs.values()) + list(logs2.values()))
+    agent.close()
+
+
+def test_compat_shrink_and_perturb():
+    """drqeps.py:212-245 through the engine: encoder leaves halfway to a fresh draw, the rest fresh,
+    target = params, AdamW state reset (the next update's moments are those of a first step)."""
+    import mtrl  # noqa: F401
+    from mtrl.envs import AtariConfig
+    from mtrl.rl.algorithms import DrQ, DrQConfig
+    from mtrl_amd import _lib as L
+    from mtrl_amd.compat.types import AtariReplayBufferSamples
+
+    agent = DrQ.initialize(DrQConfig(num_tasks=26), AtariConfig(), seed=2, batch_size=26)
+    rng = np.random.default_rng(0)
+    data = AtariReplayBufferSamples(rng.integers(0, 256, (26, 4, 84, 84), dtype=np.uint8), rng.integers(0, 18, (26, 1)),
+                                    rng.integers(0, 256, (26, 4, 84, 84), dtype=np.uint8), np.zeros((26, 1)),
+                                    np.zeros((26, 1)), rng.standard_normal((26, 1)), np.arange(26))
+    agent, _ = agent.update(data)
+    before = agent.engine.get_params(L.DRQ_PARAMS)
+    agent = agent.shrink_and_perturb()
+    p = agent.engine.get_params(L.DRQ_PARAMS)
+    assert not np.array_equal(p, before)
+    np.testing.assert_array_equal(agent.engine.get_params(L.DRQ_TARGET), p)
+    assert not agent.engine.get_params(L.DRQ_ADAM_MU).any() and not agent.engine.get_params(L.DRQ_ADAM_NU).any()
+    agent, logs = agent.update(data)
+    g = agent.engine.get_params(L.DRQ_GRAD)
+    np.testing.assert_allclose(agent.engine.get_params(L.DRQ_ADAM_MU), 0.1 * g, rtol=1e-6, atol=1e-12)
+    assert all(np.isfinite(v) for v in logs.values())
     agent.close()
