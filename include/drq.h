@@ -122,6 +122,16 @@ int drq_seed_augment(drq_engine* e, unsigned long long seed);
 int drq_read_batch(drq_engine* e, unsigned char* obs, unsigned char* next_obs, int* actions, float* rewards,
                    float* dones, float* truncations, int* task_ids);
 int drq_get_logs(drq_engine* e, float* out /* DRQ_NUM_LOGS */);
+/* compute_weights (drqeps.py:353-482).  drq_task_gradient: the loss gradient (no optimizer step)
+ * of one task group's `batch` rows, stored in flax ravel order as row `slot` of the engine's
+ * per-task gradient matrix [num_slots][drq_num_params] (grown on demand).
+ * drq_project_task_gradients: project_grad (drqeps.py:428-448) of the first num_slots rows,
+ * out[t][j] = sum_k g_t[k] N(k, j) / sqrt(proj_dim), N the (chunk x proj_dim) blocks of
+ * jax.random.normal(PRNGKey(seed + block)) regenerated on the device (threefry2x32, jax 0.5.3
+ * partitionable bits); out is host or device, [num_slots][proj_dim].  Synchronous. */
+int drq_task_gradient(drq_engine* e, const drq_batch* batch, int slot, int num_slots);
+int drq_get_task_gradient(drq_engine* e, int slot, float* flat, long long n);
+int drq_project_task_gradients(drq_engine* e, int num_slots, int proj_dim, long long chunk, int seed, float* out);
 int drq_synchronize(drq_engine* e);
 const char* drq_last_error(void);
 

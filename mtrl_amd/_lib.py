@@ -196,6 +196,9 @@ SIGNATURES.update({
     "drq_sample_rows_update": (ctypes.c_int, [P, P, P, ctypes.c_int]),
     "drq_rng_get": (ctypes.c_int, [P, P]),
     "drq_seed_augment": (ctypes.c_int, [P, ctypes.c_uint64]),
+    "drq_task_gradient": (ctypes.c_int, [P, ctypes.POINTER(DrqBatch), ctypes.c_int, ctypes.c_int]),
+    "drq_get_task_gradient": (ctypes.c_int, [P, ctypes.c_int, P, I64]),
+    "drq_project_task_gradients": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, I64, ctypes.c_int, P]),
     "drq_read_batch": (ctypes.c_int, [P, P, P, P, P, P, P, P]),
     "drq_synchronize": (ctypes.c_int, [P]),
 })

@@ -21,6 +21,12 @@ from ...config.networks import ImpalaDQNConfig
 from ...config.rl import AlgorithmConfig
 
 _PAD = 4  # augmentation.py:75 (img_pad)
+# compute_conflict_metrics' keys (utils.py:155-174), unprefixed in DrQ.compute_weights' dict
+_CONFLICT_KEYS = ("conflict_rate", "mean_conflict_magnitude", "mean_conflict_angle", "per_task_conflict_rate",
+                  "per_task_grad_magnitude", "pairwise_conflict", "pairwise_cos_sim", "pairwise_angle",
+                  "avg_interference_rate", "interference_asymmetry", "per_task_interference_in",
+                  "per_task_interference_out", "pairwise_interference_rate", "avg_participation_ratio",
+                  "per_task_participation_ratio", "effective_rank")
 
 
 @dataclasses.dataclass(frozen=True)
@@ -108,6 +114,51 @@ class DrQ:
         self.engine.set_step(0)
         return self
 
+    def _metrics_engine(self, n: int) -> DrQEngine:
+        """An engine of batch n (one task group) sharing the current parameters and target."""
+        from mtrl_amd import _lib as L
+
+        e = getattr(self, "_meng", None)
+        if e is None or e.s.batch != n:
+            if e is not None:
+                e.close()
+            e = self._meng = DrQEngine(dataclasses.replace(self.engine.s, batch=n, capacity=0))
+        for w in (L.DRQ_PARAMS, L.DRQ_TARGET):
+            e.set_params(w, self.engine.get_params(w))
+        return e
+
+    def compute_weights(self, data: T.AtariReplayBufferSamples, proj_dim: int = 10_000, chunk: int = 500_000,
+                        proj_seed: int = 42):
+        """drqeps.py:353-482: both observation batches augmented, rows grouped by task id (stable
+        argsort), each group's C51 loss gradient on the device, project_grad's JL projection of
+        every task gradient to proj_dim (the Gaussian matrix regenerated on the device from
+        jax.random's threefry stream, PRNGKey(42 + block)), then vmap_cos_sim and
+        compute_conflict_metrics (utils.py:49-174) on the T x proj_dim matrix."""
+        from ....conflict import conflict_metrics_from_stats, matrix_stats
+
+        c = self.config
+        Tn = c.num_tasks
+        obs, nobs = np.asarray(data.observations), np.asarray(data.next_observations)
+        B = obs.shape[0]
+        if B % Tn:
+            raise ValueError(f"batch of {B} rows is not a multiple of num_tasks {Tn}")
+        n = B // Tn
+        co, no = self._aug_draws(B)
+        cn, nn = self._aug_draws(B)
+        task = np.asarray(data.task_ids).reshape(B)
+        act, rew = np.asarray(data.actions).reshape(B), np.asarray(data.rewards).reshape(B)
+        done = np.asarray(data.dones).reshape(B)
+        order = np.argsort(task, kind="stable")
+        eng = self._metrics_engine(n)
+        for t in range(Tn):
+            r = order[t * n:(t + 1) * n]
+            eng.task_gradient((obs[r], act[r], nobs[r], done[r], rew[r], task[r]), (co[r], no[r], cn[r], nn[r]), t, Tn)
+        proj = eng.project_task_gradients(Tn, proj_dim, chunk, proj_seed)
+        m = conflict_metrics_from_stats(matrix_stats(proj))
+        logs = {"critic_avg_cos_sim": m["avg_cos_sim"], "critic_avg_grad_magnitude": m["avg_grad_magnitude"]}
+        logs.update({k: m[k] for k in _CONFLICT_KEYS})
+        return self, logs
+
     def get_num_params(self) -> dict[str, int]:
         return {"critic_num_params": self.engine.n}
 
@@ -152,6 +203,8 @@ class DrQ:
 
     def close(self):
         self.engine.close()
+        if getattr(self, "_meng", None) is not None:
+            self._meng.close()
 
 
 class DeviceAtariReplayBuffer:
@@ -184,8 +237,11 @@ class DeviceAtariReplayBuffer:
         return T.AtariReplayBufferSamples(o, a, no, tr[:, None], d[:, None], r[:, None], t)
 
     def sample(self, batch_size: int) -> T.AtariReplayBufferSamples:
-        """buffers.py:1188-1227 (batch_size % num_tasks == 0)."""
-        self._check(batch_size)
+        """buffers.py:1188-1227 (batch_size % num_tasks == 0); batches other than the engine's
+        (the evaluation-time metrics batch) draw their indices on the host."""
+        if batch_size != self.engine.s.batch:
+            o, a, no, tr, d, r, t = self.engine.sample_balanced_host(batch_size)
+            return T.AtariReplayBufferSamples(o, a, no, tr[:, None], d[:, None], r[:, None], t)
         self.engine.sample()
         return self._read()
 

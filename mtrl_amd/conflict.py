@@ -45,8 +45,9 @@ def network_stats(engine, which: int, support_percentile: float = 0.8, eps: floa
     return st
 
 
-def metrics_from_stats(st: dict) -> dict:
-    """The reference's per-network metrics from the device statistics."""
+def conflict_metrics_from_stats(st: dict) -> dict:
+    """vmap_cos_sim + compute_conflict_metrics (utils.py:49-174) from the Gram matrix, L1 norms,
+    near-zero counts and sparsity-mismatch counts of a [T][P] gradient matrix (float64)."""
     gram = np.asarray(st["gram"], np.float64)
     T = gram.shape[0]
     P = int(st["P"])
@@ -81,23 +82,6 @@ def metrics_from_stats(st: dict) -> dict:
     sv = np.linalg.svd(gram, compute_uv=False)
     sv_dist = sv / max(sv.sum(), 1e-10)
     effective_rank = float(np.exp(-(sv_dist * np.log(sv_dist + 1e-10)).sum()))
-
-    # compute_gram_metrics (mtsac.py:733-771)
-    cosine_from_gram = gram / (np.outer(norms, norms) + 1e-8)
-    avg_cosine_gram = (cosine_from_gram * off).sum() / n_pairs
-    gram_off_mean = (gram * off).sum() / n_pairs
-    gram_off_std = np.sqrt((((gram - gram_off_mean) ** 2) * off).sum() / n_pairs)
-
-    # compute_support_metrics (mtsac.py:774-867)
-    inter = np.asarray(st["intersection"], np.float64)
-    size = np.diag(inter).copy()
-    union = size[:, None] + size[None, :] - inter
-    jaccard = inter / (union + 1e-8)
-    avg_jaccard = (jaccard * off).sum() / n_pairs
-    genuine = np.asarray(st["genuine"], np.float64)
-    ghost = np.asarray(st["conflict"], np.float64) - genuine
-    total = genuine + ghost + 1e-8
-    genuine_rate, ghost_rate = genuine / total, ghost / total
     f = np.float32
     return {
         "avg_cos_sim": f(avg_cos_sim),
@@ -118,6 +102,48 @@ def metrics_from_stats(st: dict) -> dict:
         "avg_participation_ratio": f(participation.mean()),
         "per_task_participation_ratio": participation.astype(f),
         "effective_rank": f(effective_rank),
+    }
+
+
+def matrix_stats(flat: np.ndarray, eps: float = 1e-3, tau: float = 1.0) -> dict:
+    """The statistics conflict_metrics_from_stats takes, from a small [T][P] matrix on the host
+    (DrQ's projected gradients, T x 10 000)."""
+    g = np.asarray(flat, np.float64)
+    a = np.abs(np.asarray(flat, np.float32))
+    near = (a < np.float32(eps)).astype(np.float64)
+    large = (a > np.float32(tau)).astype(np.float64)
+    return {"gram": g @ g.T, "l1": a.astype(np.float64).sum(1), "near_zero": near.sum(1), "mismatch": near @ large.T,
+            "P": g.shape[1]}
+
+
+def metrics_from_stats(st: dict) -> dict:
+    """The reference's per-network metrics from the device statistics."""
+    out = conflict_metrics_from_stats(st)
+    gram = np.asarray(st["gram"], np.float64)
+    T = gram.shape[0]
+    off = 1.0 - np.eye(T)
+    n_pairs = T * (T - 1)
+    norms = np.sqrt(np.maximum(np.diag(gram), 0.0))
+
+    # compute_gram_metrics (mtsac.py:733-771)
+    cosine_from_gram = gram / (np.outer(norms, norms) + 1e-8)
+    avg_cosine_gram = (cosine_from_gram * off).sum() / n_pairs
+    gram_off_mean = (gram * off).sum() / n_pairs
+    gram_off_std = np.sqrt((((gram - gram_off_mean) ** 2) * off).sum() / n_pairs)
+
+    # compute_support_metrics (mtsac.py:774-867)
+    inter = np.asarray(st["intersection"], np.float64)
+    size = np.diag(inter).copy()
+    union = size[:, None] + size[None, :] - inter
+    jaccard = inter / (union + 1e-8)
+    avg_jaccard = (jaccard * off).sum() / n_pairs
+    genuine = np.asarray(st["genuine"], np.float64)
+    ghost = np.asarray(st["conflict"], np.float64) - genuine
+    total = genuine + ghost + 1e-8
+    genuine_rate, ghost_rate = genuine / total, ghost / total
+    f = np.float32
+    return {
+        **out,
         "avg_cosine_gram": f(avg_cosine_gram),
         "gram_diag": np.diag(gram).astype(f),
         "gram_off_diag_mean": f(gram_off_mean),

@@ -767,6 +767,122 @@ __global__ void drq_logs_kernel(const float* __restrict__ part, int G, const flo
   }
 }
 
+// ------------------------------------------------------------------ compute_weights (drqeps.py:353-482)
+// Internal layout -> flax ravel order of one gradient (a row of the per-task matrix).  Segment
+// table entries: (flax offset, internal offset, count, internal row stride, rows).
+__global__ void flax_gather_kernel(const float* __restrict__ g, const long long* __restrict__ map,
+                                   float* __restrict__ out) {
+  const long long* m = map + 5 * blockIdx.y;
+  const long long f = m[0], i0 = m[1], n = m[2], ld = m[3], rows = m[4];
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n * rows; e += (long long)gridDim.x * 256) {
+    const long long r = e / n, c = e - r * n;
+    out[f + e] = g[i0 + r * (ld ? ld : n) + c];
+  }
+}
+
+// jax.random.normal(PRNGKey(seed), shape) element at linear index `lin` (jax 0.5.3 defaults:
+// threefry2x32 with jax_threefry_partitionable = True, so the element's bits are
+// threefry2x32(key = (0, seed), counter = (lin >> 32, lin & 0xffffffff)) as out0 ^ out1; then
+// _uniform on [nextafter(-1, 0), 1) and sqrt(2) * erf_inv with XLA's single-precision erf_inv
+// (Giles' polynomial, w = -log1p(-x^2)).
+__device__ inline unsigned rotl32(unsigned x, int r) { return (x << r) | (x >> (32 - r)); }
+
+__device__ inline unsigned threefry_bits(unsigned k0, unsigned k1, unsigned c0, unsigned c1) {
+  const unsigned k2 = k0 ^ k1 ^ 0x1BD11BDAu;
+  unsigned x0 = c0 + k0, x1 = c1 + k1;
+#define TF_ROUND(r) \
+  x0 += x1;         \
+  x1 = rotl32(x1, r); \
+  x1 ^= x0;
+#define TF_A TF_ROUND(13) TF_ROUND(15) TF_ROUND(26) TF_ROUND(6)
+#define TF_B TF_ROUND(17) TF_ROUND(29) TF_ROUND(16) TF_ROUND(24)
+  TF_A x0 += k1; x1 += k2 + 1u;
+  TF_B x0 += k2; x1 += k0 + 2u;
+  TF_A x0 += k0; x1 += k1 + 3u;
+  TF_B x0 += k1; x1 += k2 + 4u;
+  TF_A x0 += k2; x1 += k0 + 5u;
+#undef TF_A
+#undef TF_B
+#undef TF_ROUND
+  return x0 ^ x1;
+}
+
+__device__ inline float jax_normal(unsigned seed, unsigned long long lin) {
+  const unsigned bits = threefry_bits(0u, seed, (unsigned)(lin >> 32), (unsigned)lin);
+  const float f = __uint_as_float((bits >> 9) | 0x3f800000u) - 1.0f;
+  const float lo = -0.99999994f;  // nextafter(-1, 0)
+  const float x = fmaxf(lo, f * 2.0f + lo);  // (maxval - minval) rounds to 2 in float32
+  float w = -log1pf(-x * x);
+  const bool lt = w < 5.0f;
+  w = lt ? w - 2.5f : sqrtf(w) - 3.0f;
+  float p = lt ? 2.81022636e-08f : -0.000200214257f;
+  p = (lt ? 3.43273939e-07f : 0.000100950558f) + p * w;
+  p = (lt ? -3.5233877e-06f : 0.00134934322f) + p * w;
+  p = (lt ? -4.39150654e-06f : -0.00367342844f) + p * w;
+  p = (lt ? 0.00021858087f : 0.00573950773f) + p * w;
+  p = (lt ? -0.00125372503f : -0.0076224613f) + p * w;
+  p = (lt ? -0.00417768164f : 0.00943887047f) + p * w;
+  p = (lt ? 0.246640727f : 1.00167406f) + p * w;
+  p = (lt ? 1.50140941f : 2.83297682f) + p * w;
+  return 1.41421354f * (p * x);
+}
+
+// project_grad (drqeps.py:428-448) for up to JL_T task rows at once, each random matrix element
+// generated once and used for every task: part[ks][t][j] = sum_{k in split ks} G[t][k] N(k, j) with
+// N(k, j) = normal(PRNGKey(seed + k / chunk))[(k % chunk) * D + j].  One lane per output column j;
+// the G tile [JL_K][JL_T] in LDS (broadcast reads).
+constexpr int JL_T = 32, JL_K = 64;
+
+__global__ __launch_bounds__(256) void jl_project_kernel(const float* __restrict__ G, long long ldg, int T,
+                                                         long long P, int D, long long chunk, int seed,
+                                                         long long kper, float* __restrict__ part) {
+  __shared__ float gs[JL_K][JL_T];
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const long long k0 = (long long)blockIdx.y * kper, k1 = k0 + kper < P ? k0 + kper : P;
+  float acc[JL_T];
+#pragma unroll
+  for (int t = 0; t < JL_T; ++t) acc[t] = 0.f;
+  for (long long kb = k0; kb < k1; kb += JL_K) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < JL_K * JL_T; e += 256) {
+      const int kk = e / JL_T, t = e - kk * JL_T;
+      const long long k = kb + kk;
+      gs[kk][t] = (t < T && k < k1) ? G[(long long)t * ldg + k] : 0.f;
+    }
+    __syncthreads();
+    if (j < D) {
+      const int kn = (int)(k1 - kb < JL_K ? k1 - kb : JL_K);
+      for (int kk = 0; kk < kn; ++kk) {
+        const long long k = kb + kk;
+        const long long c = k / chunk;
+        const float n = jax_normal((unsigned)(seed + c), (unsigned long long)(k - c * chunk) * D + j);
+        const float4* row = reinterpret_cast<const float4*>(&gs[kk][0]);
+#pragma unroll
+        for (int q = 0; q < JL_T / 4; ++q) {
+          const float4 g4 = row[q];
+          acc[4 * q] += g4.x * n;
+          acc[4 * q + 1] += g4.y * n;
+          acc[4 * q + 2] += g4.z * n;
+          acc[4 * q + 3] += g4.w * n;
+        }
+      }
+    }
+  }
+  if (j < D)
+    for (int t = 0; t < T && t < JL_T; ++t) part[((long long)blockIdx.y * JL_T + t) * D + j] = acc[t];
+}
+
+// out[t][j] = (sum over splits, in order, in double) / sqrt(D)
+__global__ void jl_reduce_kernel(const float* __restrict__ part, int splits, int T, int D, float div,
+                                 float* __restrict__ out, long long ldo) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long long)T * D) return;
+  const int t = (int)(e / D), j = (int)(e - (long long)t * D);
+  double s = 0.0;
+  for (int k = 0; k < splits; ++k) s += part[((long long)k * JL_T + t) * D + j];
+  out[(long long)t * ldo + j] = (float)(s / div);
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
@@ -950,6 +1066,37 @@ int adamw(float* p, float* mu, float* nu, const float* g, float* tgt, long long 
 void drq_logs(const float* part, int G, const float* loss_b, const float* logit_b, int B, int Z, float* logs,
               hipStream_t st) {
   hipLaunchKernelGGL(drq_logs_kernel, dim3(1), dim3(256), 0, st, part, G, loss_b, logit_b, B, Z, logs);
+}
+
+
+// ------------------------------------------------------------------ compute_weights launchers
+void flax_gather(const float* g, const long long* map, int entries, long long max_n, float* out, hipStream_t st) {
+  const unsigned gx = (unsigned)std::min<long long>((max_n + 255) / 256, 4096);
+  hipLaunchKernelGGL(flax_gather_kernel, dim3(gx, entries), dim3(256), 0, st, g, map, out);
+}
+
+int jl_splits(long long P, int D) {
+  const long long jb = (D + 255) / 256;
+  long long s = (2048 + jb - 1) / jb;  // >= 2048 workgroups over the 256 CUs
+  s = std::min<long long>(s, (P + JL_K - 1) / JL_K);
+  return (int)std::max<long long>(s, 1);
+}
+
+long long jl_part_floats(long long P, int D) { return (long long)jl_splits(P, D) * JL_T * D; }
+
+int jl_max_tasks() { return JL_T; }
+
+void jl_project(const float* G, long long ldg, int T, long long P, int D, long long chunk, int seed, float* part,
+                float* out, long long ldo, hipStream_t st) {
+  const int splits = jl_splits(P, D);
+  long long kper = (P + splits - 1) / splits;
+  kper = (kper + JL_K - 1) / JL_K * JL_K;
+  const int used = (int)((P + kper - 1) / kper);
+  hipLaunchKernelGGL(jl_project_kernel, dim3((D + 255) / 256, used), dim3(256), 0, st, G, ldg, T, P, D, chunk, seed,
+                     kper, part);
+  const long long n = (long long)T * D;
+  hipLaunchKernelGGL(jl_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, used, T, D,
+                     sqrtf((float)D), out, ldo);
 }
 
 }  // namespace drq

@@ -93,10 +93,34 @@ struct drq_engine {
   long long* r_slot = nullptr;           // [ROWS_STEPS][B]
   int* r_task = nullptr;
   unsigned long long aug_seed = 0, aug_ctr = 0;
+  // ---- compute_weights: per-task gradients in flax order [slots][n_flax], the segment table
+  long long* d_map = nullptr;
+  long long map_max = 0;
+  float* tg = nullptr;
+  int tg_slots = 0;
+  float* jl_part = nullptr;
+  long long jl_part_n = 0;
+  float* jl_out = nullptr;
+  long long jl_out_n = 0;
   std::vector<unsigned char> ns_obs, ns_next;  // [nstep][T][img]
   std::vector<int> ns_act;
   std::vector<float> ns_rew, ns_trunc, ns_done;  // [nstep][T]
   std::vector<double> minmax;                    // [2][T]: min, max
+
+  // (re)allocate a lazily sized buffer
+  template <class T_>
+  int realloc_buf(T_** ptr, long long& have, long long n) {
+    if (n <= have) return 0;
+    if (*ptr) {
+      if (hipStreamSynchronize(st) != hipSuccess) return fail(-5, "stream sync failed");
+      allocs.erase(std::remove(allocs.begin(), allocs.end(), (void*)*ptr), allocs.end());
+      (void)hipFree(*ptr);
+      *ptr = nullptr;
+    }
+    int rc = alloc(ptr, n);
+    if (!rc) have = n;
+    return rc;
+  }
 
   template <class T_>
   int alloc(T_** ptr, long long n) {
@@ -271,6 +295,15 @@ struct drq_engine {
 
   // ------------------------------------------------------------------ one update on the staged batch
   void step() {
+    grad_pass();
+    ++count;
+    const int G = drq::adamw(p, mu, nu, g, tgt, n_int, cfg.lr, cfg.b1, cfg.b2, cfg.eps, cfg.weight_decay, cfg.tau,
+                             count, part, 1024, st);
+    drq::drq_logs(part, G, loss_b, logit_b, B, Z, logs, st);
+  }
+
+  // the loss gradient of the staged batch into g (drqeps.py:268-308 up to the optimizer)
+  void grad_pass() {
     const int C0 = cfg.in_ch;
     drq::augment(nobs_u8, crop_n, noise_n, nobs, B, C0, cfg.hw, cfg.hw, 4, st);
     drq::augment(obs_u8, crop_o, noise_o, stk[0].xin_own, B, C0, cfg.hw, cfg.hw, 4, st);
@@ -308,11 +341,6 @@ struct drq_engine {
       drq::conv_wgrad(xin, dn, wpart, g + k.cw[0], g + k.cb[0], B, k.hin, k.hin, k.ci, k.co, false, st);
       if (s > 0) drq::conv_bwd_data(dn, p + k.cw[0], nullptr, nullptr, dc, B, k.hin, k.hin, k.ci, k.co, st);
     }
-    // ---- optimizer
-    ++count;
-    const int G = drq::adamw(p, mu, nu, g, tgt, n_int, cfg.lr, cfg.b1, cfg.b2, cfg.eps, cfg.weight_decay, cfg.tau,
-                             count, part, 1024, st);
-    drq::drq_logs(part, G, loss_b, logit_b, B, Z, logs, st);
   }
 };
 
@@ -417,6 +445,16 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
   add(e->off_emb, (long long)e->T * e->D);
   e->n_flax = f;
   int rc;
+  {
+    std::vector<long long> tab;
+    for (const auto& mp : e->map) {
+      tab.insert(tab.end(), {mp.f, mp.i, mp.n, mp.ld, mp.rows});
+      e->map_max = std::max(e->map_max, mp.n * mp.rows);
+    }
+    if ((rc = e->alloc(&e->d_map, (long long)tab.size())) ||
+        hipMemcpy(e->d_map, tab.data(), sizeof(long long) * tab.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return bad(rc ? rc : fail(-5, "segment table upload"));
+  }
   for (float** q : {&e->p, &e->g, &e->mu, &e->nu, &e->tgt})
     if ((rc = e->alloc(q, e->n_int))) return bad(rc);
   const long long img = (long long)B * c->in_ch * c->hw * c->hw;
@@ -731,6 +769,62 @@ int drq_get_logs(drq_engine* e, float* out) {
 int drq_synchronize(drq_engine* e) {
   if (!e) return fail(-22, "null argument");
   return hipStreamSynchronize(e->st) == hipSuccess ? 0 : fail(-5, "stream sync failed");
+}
+
+int drq_task_gradient(drq_engine* e, const drq_batch* b, int slot, int num_slots) {
+  if (!e || !b) return fail(-22, "null argument");
+  if (num_slots < 1 || slot < 0 || slot >= num_slots) return fail(-22, "slot out of range");
+  const int B = e->B;
+  const size_t img = (size_t)B * e->cfg.in_ch * e->cfg.hw * e->cfg.hw;
+  int rc;
+  long long have = (long long)e->tg_slots * e->n_flax;
+  if ((rc = e->realloc_buf(&e->tg, have, (long long)num_slots * e->n_flax))) return rc;
+  e->tg_slots = (int)(have / e->n_flax);
+  if ((rc = copy_in(e->obs_u8, b->obs, img, e->st)) || (rc = copy_in(e->nobs_u8, b->next_obs, img, e->st)) ||
+      (rc = copy_in(e->act, b->actions, sizeof(int) * B, e->st)) ||
+      (rc = copy_in(e->task, b->task_ids, sizeof(int) * B, e->st)) ||
+      (rc = copy_in(e->rew, b->rewards, sizeof(float) * B, e->st)) ||
+      (rc = copy_in(e->done, b->dones, sizeof(float) * B, e->st)) ||
+      (rc = copy_in(e->crop_o, b->crop_obs, sizeof(int) * 2 * B, e->st)) ||
+      (rc = copy_in(e->crop_n, b->crop_next, sizeof(int) * 2 * B, e->st)) ||
+      (rc = copy_in(e->noise_o, b->noise_obs, sizeof(float) * B, e->st)) ||
+      (rc = copy_in(e->noise_n, b->noise_next, sizeof(float) * B, e->st)))
+    return rc;
+  e->grad_pass();
+  drq::flax_gather(e->g, e->d_map, (int)e->map.size(), e->map_max, e->tg + (long long)slot * e->n_flax, e->st);
+  return hipGetLastError() == hipSuccess ? 0 : fail(-5, "kernel launch failed");
+}
+
+int drq_get_task_gradient(drq_engine* e, int slot, float* flat, long long n) {
+  if (!e || !flat) return fail(-22, "null argument");
+  if (slot < 0 || slot >= e->tg_slots) return fail(-22, "slot out of range");
+  if (n != e->n_flax) return fail(-22, "parameter count mismatch");
+  if (hipMemcpyAsync(flat, e->tg + (long long)slot * e->n_flax, sizeof(float) * n, hipMemcpyDefault, e->st) !=
+          hipSuccess ||
+      hipStreamSynchronize(e->st) != hipSuccess)
+    return fail(-5, "download failed");
+  return 0;
+}
+
+int drq_project_task_gradients(drq_engine* e, int num_slots, int proj_dim, long long chunk, int seed, float* out) {
+  if (!e || !out) return fail(-22, "null argument");
+  if (num_slots < 1 || num_slots > e->tg_slots) return fail(-22, "num_slots exceeds the stored task gradients");
+  if (proj_dim < 1 || chunk < 1) return fail(-22, "proj_dim and chunk must be positive");
+  const long long P = e->n_flax;
+  int rc;
+  if ((rc = e->realloc_buf(&e->jl_part, e->jl_part_n, drq::jl_part_floats(P, proj_dim))) ||
+      (rc = e->realloc_buf(&e->jl_out, e->jl_out_n, (long long)num_slots * proj_dim)))
+    return rc;
+  const int TM = drq::jl_max_tasks();
+  for (int t0 = 0; t0 < num_slots; t0 += TM)
+    drq::jl_project(e->tg + (long long)t0 * P, P, std::min(TM, num_slots - t0), P, proj_dim, chunk, seed, e->jl_part,
+                    e->jl_out + (long long)t0 * proj_dim, proj_dim, e->st);
+  if (hipGetLastError() != hipSuccess) return fail(-5, "kernel launch failed");
+  if (hipMemcpyAsync(out, e->jl_out, sizeof(float) * (size_t)num_slots * proj_dim, hipMemcpyDefault, e->st) !=
+          hipSuccess ||
+      hipStreamSynchronize(e->st) != hipSuccess)
+    return fail(-5, "download failed");
+  return 0;
 }
 
 }  // extern "C"

@@ -71,5 +71,16 @@ int adamw(float* p, float* mu, float* nu, const float* g, float* tgt, long long 
 void drq_logs(const float* part, int G, const float* loss_b, const float* logit_b, int B, int Z, float* logs,
               hipStream_t st);
 
+// compute_weights (drqeps.py:353-482): one gradient from the internal layout to flax ravel order
+// through the (f, i, n, ld, rows) segment table (entries x 5 int64 on the device)
+void flax_gather(const float* g, const long long* map, int entries, long long max_n, float* out, hipStream_t st);
+// project_grad (drqeps.py:428-448) of T <= jl_max_tasks() rows of G [T][ldg] at once:
+// out[t][j] = sum_k G[t][k] N(k, j) / sqrt(D), N = jax.random.normal(PRNGKey(seed + k / chunk),
+// (chunk, D))[k % chunk][j] regenerated on the fly (threefry2x32, partitionable); part holds
+// jl_part_floats(P, D) floats
+int jl_max_tasks();
+long long jl_part_floats(long long P, int D);
+void jl_project(const float* G, long long ldg, int T, long long P, int D, long long chunk, int seed, float* part,
+                float* out, long long ldo, hipStream_t st);
 }  // namespace drq
 }  // namespace mtsac

@@ -127,6 +127,38 @@ class DrQEngine:
     def set_step(self, count: int):
         _drq_check(self.lib.drq_set_step(self.h, int(count)))
 
+    @staticmethod
+    def _batch_arrays(batch, aug):
+        obs, act, nobs, done, rew, task = batch
+        co, no, cn, nn = aug
+        return [np.ascontiguousarray(obs, np.uint8), np.ascontiguousarray(act, np.int32),
+                np.ascontiguousarray(nobs, np.uint8), np.ascontiguousarray(done, np.float32),
+                np.ascontiguousarray(rew, np.float32), np.ascontiguousarray(task, np.int32),
+                np.ascontiguousarray(co, np.int32), np.ascontiguousarray(no, np.float32),
+                np.ascontiguousarray(cn, np.int32), np.ascontiguousarray(nn, np.float32)]
+
+    def task_gradient(self, batch, aug, slot: int, num_slots: int) -> None:
+        """compute_weights' per_task_loss gradient (drqeps.py:385-410, 454-460) of one task group
+        (this engine's `batch` rows), kept on the device as row `slot` in flax ravel order."""
+        arrs = self._batch_arrays(batch, aug)
+        b = L.DrqBatch(*[a.ctypes.data for a in arrs])
+        _drq_check(self.lib.drq_task_gradient(self.h, ctypes.byref(b), int(slot), int(num_slots)))
+        self._keep = arrs
+        self.synchronize()
+
+    def get_task_gradient(self, slot: int) -> np.ndarray:
+        out = np.empty(self.n, np.float32)
+        _drq_check(self.lib.drq_get_task_gradient(self.h, int(slot), _ptr(out), self.n))
+        return out
+
+    def project_task_gradients(self, num_slots: int, proj_dim: int = 10_000, chunk: int = 500_000,
+                               seed: int = 42) -> np.ndarray:
+        """project_grad (drqeps.py:428-448) of the stored task gradients -> [num_slots][proj_dim]."""
+        out = np.empty((num_slots, proj_dim), np.float32)
+        _drq_check(self.lib.drq_project_task_gradients(self.h, int(num_slots), int(proj_dim), int(chunk), int(seed),
+                                                       _ptr(out)))
+        return out
+
     def update(self, batch, aug) -> None:
         """batch = (obs u8 [B][C][H][W], actions, next_obs u8, dones, rewards, task_ids);
         aug = (crop_obs int [B][2], noise_obs [B], crop_next, noise_next)."""
@@ -221,6 +253,47 @@ class DrQEngine:
         tasks = np.ascontiguousarray(np.concatenate([r[1] for r in rows]))
         self._push_rng()
         return slots, tasks
+
+    def gather_rows(self, slots, tasks):
+        """Rows (slot, task) of the device buffer in batches of this engine's size -> host arrays
+        (obs, actions, next_obs, truncations, dones, rewards, task ids), any number of rows."""
+        slots = np.asarray(slots, np.int64)
+        tasks = np.asarray(tasks, np.int32)
+        R, B = slots.size, self.s.batch
+        parts = []
+        for r0 in range(0, R, B):
+            k = min(B, R - r0)
+            s_ = np.zeros(B, np.int64)
+            t_ = np.zeros(B, np.int32)
+            s_[:k], t_[:k] = slots[r0:r0 + k], tasks[r0:r0 + k]
+            _drq_check(self.lib.drq_sample_rows(self.h, _ptr(s_), _ptr(t_)))
+            parts.append([a[:k] for a in self.read_batch()])
+        return tuple(np.concatenate([p[i] for p in parts]) for i in range(7))
+
+    def sample_balanced_host(self, batch_size: int):
+        """sample(batch_size) (buffers.py:1188-1227) for any multiple of num_tasks (compute_weights'
+        metrics batch, base.py:280): the indices from the buffer's Generator on the host (same
+        stream as the device draws), the rows gathered on the device."""
+        s = self.s
+        T = s.num_tasks
+        if batch_size % T:
+            raise ValueError("batch_size must be a multiple of num_tasks")
+        n = batch_size // T
+        pos, full = self.buffer_state()
+        rng = self._host_rng()
+        guard = s.nstep + 6
+        if s.buffer_kind == 1:
+            idx = rng.integers(0, max(pos if not full else s.capacity, n), size=(n,))
+        elif not full:
+            idx = rng.integers(0, max(pos - s.nstep, 1), size=(n,))
+        else:
+            k = rng.integers(0, s.capacity - guard, size=(n,))
+            idx = np.where(k < pos, k, k + guard) if pos + guard <= s.capacity else k + (pos + guard - s.capacity)
+        self._push_rng()
+        slots = np.repeat(idx, T)  # row i * T + t
+        tasks = np.tile(np.arange(T, dtype=np.int32), n)
+        o, a, no, tr, d, r, _ = self.gather_rows(slots, tasks)
+        return o, a, no, tr, d, r, np.repeat(np.arange(T, dtype=np.int32), n)  # task ids as the reference lists them
 
     def sample_unbalanced(self):
         """sample_unbalanced(batch) (buffers.py:1230-1279): rows drawn on the host, gathered on the device."""

@@ -117,3 +117,31 @@ def test_shrink_and_perturb_mixes_only_the_encoder():
         else:
             np.testing.assert_array_equal(b, f)
         o += n
+
+
+def test_threefry_known_answers():
+    """threefry2x32_20 against the Random123 known-answer vectors (the ones jax's own random tests
+    use): this pins the bit stream of the compute_weights projection (oracle/jl_projection.py)."""
+    from oracle.jl_projection import normal, threefry2x32
+
+    for key, ctr, want in (((0, 0), (0, 0), (0x6B200159, 0x99BA4EFE)),
+                           ((0xFFFFFFFF, 0xFFFFFFFF), (0xFFFFFFFF, 0xFFFFFFFF), (0x1CB996FC, 0xBB002BE7)),
+                           ((0x13198A2E, 0x03707344), (0x243F6A88, 0x85A308D3), (0xC4923A9C, 0x483DF7A0))):
+        x0, x1 = threefry2x32(key[0], key[1], np.array([ctr[0]], np.uint32), np.array([ctr[1]], np.uint32))
+        assert (int(x0[0]), int(x1[0])) == want
+    z = normal(42, np.arange(400_000)).astype(np.float64)
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1) < 0.01 and np.abs(z).max() < 6
+
+
+def test_matrix_stats_match_their_definitions():
+    """The host statistics of DrQ's projected gradients against utils.py:73-113's broadcast forms."""
+    from mtrl_amd.conflict import matrix_stats
+
+    rng = np.random.default_rng(0)
+    g = (rng.standard_normal((5, 300)) * rng.choice([1e-4, 1e-2, 3.0], (5, 300))).astype(np.float32)
+    st = matrix_stats(g)
+    near, large = np.abs(g) < 1e-3, np.abs(g) > 1.0
+    np.testing.assert_array_equal(st["mismatch"], (near[:, None, :] & large[None, :, :]).sum(-1))
+    np.testing.assert_array_equal(st["near_zero"], near.sum(1))
+    np.testing.assert_allclose(st["gram"], g.astype(np.float64) @ g.T.astype(np.float64))
+    np.testing.assert_allclose(st["l1"], np.abs(g).sum(1), rtol=1e-6)

@@ -196,6 +196,8 @@ def test_device_buffer_matches_reference_buffer(normalize, kind):
                 e.sample()
                 _same_batch(e.read_batch(), want, f"step {step}")
                 checks += 1
+            elif step % 3 == 1:  # another batch size: indices on the host, same stream (base.py:280)
+                _same_batch(e.sample_balanced_host(T * 5), ref.sample(T * 5), f"step {step} (host indices)")
     assert ref.full and checks > 15
     e.close()
 
@@ -338,4 +340,70 @@ def test_compat_shrink_and_perturb():
     g = agent.engine.get_params(L.DRQ_GRAD)
     np.testing.assert_allclose(agent.engine.get_params(L.DRQ_ADAM_MU), 0.1 * g, rtol=1e-6, atol=1e-12)
     assert all(np.isfinite(v) for v in logs.values())
+    agent.close()
+
+
+def test_task_gradients_and_projection_match_oracle():
+    """compute_weights' device half (drqeps.py:385-460): each group's gradient lands in flax order
+    (== the update path's gradient of the same rows), and project_grad's JL projection with the
+    Gaussian blocks regenerated from threefry matches the numpy restatement (several blocks + a
+    remainder, float64 reference; tolerance 1e-5 of each row's scale: fp32 sums of 1e5 terms)."""
+    from mtrl_amd import _lib as L
+    from oracle import jl_projection as jl
+
+    cfg = od.DrQConfig(hw=20, n_hidden=64)
+    st = od.init_state(cfg, 4)
+    n, T = 6, 3
+    e = _engine(cfg, n)
+    e.set_params(L.DRQ_PARAMS, st.params)
+    e.set_params(L.DRQ_TARGET, st.params)
+    grads = []
+    for t in range(T):
+        batch, aug = _batch(cfg, n, 20 + t)
+        e.task_gradient(batch, aug, t, T)
+        grads.append(e.get_task_gradient(t))
+    # the same rows through the update path give the same gradient (DRQ_GRAD, host-side reorder)
+    e2 = _engine(cfg, n)
+    e2.set_params(L.DRQ_PARAMS, st.params)
+    e2.set_params(L.DRQ_TARGET, st.params)
+    batch, aug = _batch(cfg, n, 22)
+    e2.update(batch, aug)
+    np.testing.assert_array_equal(e2.get_params(L.DRQ_GRAD), grads[2])
+    e2.close()
+    G = np.stack(grads)
+    P = G.shape[1]
+    for D, chunk, seed in ((64, 20_000, 42), (37, P // 2 + 5, 7)):
+        got = e.project_task_gradients(T, D, chunk, seed)
+        want = jl.project(G, D, chunk, seed)
+        scale = np.linalg.norm(G, axis=1, keepdims=True) / np.sqrt(D)
+        assert np.max(np.abs(got - want) / scale) < 1e-5, (D, chunk)
+    e.close()
+
+
+def test_compat_compute_weights():
+    """DrQ.compute_weights at the reference geometry (26 tasks, 1.5 M parameters, proj_dim 10 000):
+    the reference's 18 keys, shapes, and the T x T algebra consistent with the pairwise matrices."""
+    import mtrl  # noqa: F401
+    from mtrl.config.rl import DrQTrainingConfig
+    from mtrl.envs import AtariConfig
+    from mtrl.rl.algorithms import DrQ, DrQConfig
+
+    agent = DrQ.initialize(DrQConfig(num_tasks=26), AtariConfig(), seed=1, batch_size=52)
+    buf = agent.spawn_replay_buffer(AtariConfig(), DrQTrainingConfig(total_steps=100, buffer_size=26 * 40), seed=1)
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        o = rng.integers(0, 256, (26, 4, 84, 84), dtype=np.uint8)
+        buf.add(o, o, rng.integers(0, 18, 26), rng.standard_normal(26), np.zeros(26), (rng.random(26) < 0.1) * 1.0)
+    data = buf.sample(26 * 4)  # the metrics batch (base.py:280), 4 rows per task
+    assert data.observations.shape == (104, 4, 84, 84)
+    agent, logs = agent.compute_weights(data)
+    assert len(logs) == 18 and logs["pairwise_cos_sim"].shape == (1, 26, 26)  # vmap_cos_sim's leading axis
+    cos = logs["pairwise_cos_sim"][0].astype(np.float64)
+    np.testing.assert_allclose(cos, cos.T, atol=1e-6)
+    np.testing.assert_allclose(np.diag(cos), 1.0, atol=1e-5)
+    triu = np.triu(np.ones((26, 26)), 1)
+    np.testing.assert_allclose(logs["critic_avg_cos_sim"], (triu * cos).sum() / triu.sum(), rtol=1e-5)
+    assert abs(logs["critic_avg_grad_magnitude"] - logs["per_task_grad_magnitude"].mean()) < 1e-5 * \
+        logs["critic_avg_grad_magnitude"]
+    assert all(np.all(np.isfinite(v)) for v in logs.values())
     agent.close()
