@@ -112,7 +112,10 @@ typedef struct mtsac_config {
   float log_std_min, log_std_max;
   int32_t clip;             /* clip y and Q to +-5000 (mtsac.py:557-560)        */
   int32_t use_task_weights; /* mtsac.py:103-113                                 */
-  int32_t normalize_rewards;/* per-task min/max (buffers.py:534-538)            */
+  int32_t normalize_rewards;/* 0 off, 1 per-task min/max (buffers.py:534-538), 2 return
+                               normalisation (buffers.py:392-422, 531-533): rewards divided
+                               by the per-task denominator the host sets through
+                               mtsac_buffer_set_reward_stats(min = 0, max = denominator) */
   int32_t precision;        /* enum mtsac_precision                             */
   uint64_t noise_seed;      /* device N(0,1) stream used when no eps is injected */
 } mtsac_config;
@@ -160,6 +163,7 @@ int mtsac_buffer_read(mtsac_engine* h, int64_t slot_begin, int64_t n_slots, floa
 int mtsac_buffer_fill_synthetic(mtsac_engine* h, uint64_t seed);
 int mtsac_buffer_set_state(mtsac_engine* h, int64_t pos, int32_t full);
 int mtsac_buffer_get_state(mtsac_engine* h, int64_t* pos, int32_t* full);
+/* normalize_rewards 1: the running per-task reward min / max; 2: (0, denominator) */
 int mtsac_buffer_set_reward_stats(mtsac_engine* h, const double* min_r, const double* max_r);
 int mtsac_buffer_get_reward_stats(mtsac_engine* h, double* min_r, double* max_r);
 int mtsac_rng_set(mtsac_engine* h, uint64_t state_hi, uint64_t state_lo, uint64_t inc_hi,

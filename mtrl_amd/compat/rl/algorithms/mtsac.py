@@ -158,13 +158,15 @@ class MTSAC(OffPolicyAlgorithm):
         T = self.num_tasks
         cap, n = config.buffer_size // T, config.batch_size // T
         assert config.batch_size % T == 0
-        if (cap, n, bool(config.normalize_rewards)) != (self._cfg_kwargs["capacity"],
-                                                        self._cfg_kwargs["batch_per_task"],
-                                                        bool(self._cfg_kwargs.get("normalize_rewards", 0))):
-            self._rebuild(capacity=cap, batch_per_task=n, normalize_rewards=int(config.normalize_rewards))
+        returns = bool(getattr(config, "returns_normalization", False))
+        mode = 2 if returns else int(config.normalize_rewards)  # returns first, as buffers.py:531-538
+        if (cap, n, mode) != (self._cfg_kwargs["capacity"], self._cfg_kwargs["batch_per_task"],
+                              int(self._cfg_kwargs.get("normalize_rewards", 0))):
+            self._rebuild(capacity=cap, batch_per_task=n, normalize_rewards=mode)
         self._buffer = MultiTaskReplayBuffer(config.buffer_size, T, env_config.observation_space,
                                              env_config.action_space, seed=seed,
-                                             normalize_rewards=config.normalize_rewards, engine=self.engine)
+                                             normalize_rewards=config.normalize_rewards,
+                                             returns_normalization=returns, engine=self.engine)
         return self._buffer
 
     # ------------------------------------------------------------------ algorithm API

@@ -1,6 +1,11 @@
 """MultiTaskReplayBuffer (mtrl/rl/buffers.py:221-549) backed by the engine's
 device-resident buffer: same add / sample / checkpoint / load_checkpoint API, same
-index stream (numpy PCG64 reproduced on the device), same row layout (row = i*T + t)."""
+index stream (numpy PCG64 reproduced on the device), same row layout (row = i*T + t).
+
+Return normalisation (``returns_normalization=True``, buffers.py:347-422) keeps the reference's
+per-episode bookkeeping here on the host (float64, the reward values as passed to ``add``); the
+per-task denominator goes to the engine (normalize_rewards mode 2) whenever an episode end moves
+it, and the device gather divides the sampled rewards by it."""
 
 from __future__ import annotations
 
@@ -12,10 +17,12 @@ from ..types import ReplayBufferSamples
 class MultiTaskReplayBuffer:
     def __init__(self, total_capacity: int, num_tasks: int, env_obs_space=None, env_action_space=None,
                  seed: int | None = None, max_steps: int = 500, normalize_rewards: bool = False,
-                 reward_norm_eps: float = 1e-8, *, engine=None, **unsupported):
+                 reward_norm_eps: float = 1e-8, reward_filter=None, sigma=None, alpha=None, delta=None,
+                 filter_mode=None, returns_normalization: bool = False, discount: float = 0.99, v_max: float = 10.0,
+                 *, engine=None):
         assert total_capacity % num_tasks == 0, "Total capacity must be divisible by the number of tasks."
-        if unsupported.get("returns_normalization") or unsupported.get("reward_filter"):
-            raise NotImplementedError("return-based normalization / reward filters are not on the MTSAC path")
+        # buffers.py:245-249 accepts the filter arguments but never reads them
+        del reward_filter, sigma, alpha, delta, filter_mode
         if engine is None:
             raise ValueError("the device buffer lives in an MTSAC engine: use MTSAC.spawn_replay_buffer")
         self.engine = engine
@@ -24,6 +31,15 @@ class MultiTaskReplayBuffer:
         self.normalize_rewards = normalize_rewards
         self._min_rewards = np.full(num_tasks, np.inf)
         self._max_rewards = np.full(num_tasks, -np.inf)
+        self.reward_norm_eps = reward_norm_eps
+        self.use_return_normalization = returns_normalization
+        self.discount, self.v_max = discount, v_max
+        self.effective_horizon = 1.0 / (1.0 - discount)
+        self._returns_min = np.full(num_tasks, np.inf, dtype=np.float64)
+        self._returns_max = np.full(num_tasks, -np.inf, dtype=np.float64)
+        self._episode_rewards: list[list[float]] = [[] for _ in range(num_tasks)]
+        if returns_normalization and engine.config.normalize_rewards != 2:
+            raise ValueError("return normalisation needs an engine created with normalize_rewards = 2")
         self.engine.seed_rng(seed)  # np.random.default_rng(seed), buffers.py:260
 
     # pos / full mirror buffers.py:306,337-343 (kept on the host, size uploaded to HBM)
@@ -38,15 +54,54 @@ class MultiTaskReplayBuffer:
     def reset(self) -> None:
         self.engine.set_buffer_state(0, False)
 
+    # ---- return normalisation (buffers.py:347-422), host bookkeeping
+    def _compute_discounted_returns(self, rewards: np.ndarray, truncated: bool) -> tuple[float, float]:
+        values = np.zeros(len(rewards), dtype=np.float64)
+        bootstrap = float(rewards.mean()) * self.effective_horizon if truncated else 0.0
+        for i in reversed(range(len(rewards))):
+            values[i] = rewards[i] + self.discount * bootstrap
+            bootstrap = values[i]
+        return float(values.min()), float(values.max())
+
+    def _update_return_stats(self, rewards, terminal, truncated) -> bool:
+        moved = False
+        for t in range(self.num_tasks):
+            self._episode_rewards[t].append(float(rewards[t]))
+            if bool(terminal[t]) or bool(truncated[t]):
+                lo, hi = self._compute_discounted_returns(np.array(self._episode_rewards[t], dtype=np.float64),
+                                                          truncated=bool(truncated[t]))
+                self._returns_min[t] = min(self._returns_min[t], lo)
+                self._returns_max[t] = max(self._returns_max[t], hi)
+                self._episode_rewards[t] = []
+                moved = True
+        return moved
+
+    def return_denominator(self) -> np.ndarray:
+        """_normalize_rewards_by_return's per-task denominator (buffers.py:406-418)."""
+        no_data = np.isinf(self._returns_min) | np.isinf(self._returns_max)
+        den = np.where(self._returns_max >= np.abs(self._returns_min), self._returns_max, np.abs(self._returns_min))
+        den = den / self.v_max
+        return np.where(no_data | (den < self.reward_norm_eps), 1.0, den)
+
+    def _push_denominator(self) -> None:
+        self.engine.set_reward_stats(np.zeros(self.num_tasks), self.return_denominator())
+
     def add(self, obs, next_obs, action, reward, done, terminal=None, truncated=None) -> None:
         obs = np.asarray(obs, np.float32)
         assert obs.ndim == 2 and obs.shape[0] == self.num_tasks
+        raw_reward = np.asarray(reward).reshape(-1)
         reward = np.asarray(reward, np.float32).reshape(-1)
         self.engine.buffer_add(obs, np.asarray(next_obs, np.float32), np.asarray(action, np.float32), reward,
                                np.asarray(done, np.float32).reshape(-1))
         if self.normalize_rewards:
             self._min_rewards = np.minimum(self._min_rewards, reward)
             self._max_rewards = np.maximum(self._max_rewards, reward)
+        if self.use_return_normalization:  # buffers.py:465-472
+            d = np.asarray(done).reshape(-1)
+            term = np.asarray(terminal).reshape(-1) if terminal is not None else d
+            trunc = np.asarray(truncated).reshape(-1) if truncated is not None else np.zeros_like(d)
+            if self._update_return_stats(raw_reward, term.astype(bool), trunc.astype(bool)):
+                self._push_denominator()
 
     def sample(self, batch_size: int) -> ReplayBufferSamples:
         assert batch_size % self.num_tasks == 0
@@ -60,9 +115,7 @@ class MultiTaskReplayBuffer:
         return {
             "data": {"obs": obs, "actions": act, "rewards": rew[..., None], "next_obs": nobs,
                      "dones": done[..., None], "pos": pos, "full": full,
-                     # return-normalisation statistics (buffers.py:319-321); return normalisation
-                     # is not on the MTSAC path, so they keep their initial values (:281-282)
-                     "returns_min": np.full(self.num_tasks, np.inf), "returns_max": np.full(self.num_tasks, -np.inf)},
+                     "returns_min": self._returns_min.copy(), "returns_max": self._returns_max.copy()},
             "rng_state": self.engine.get_rng_state(),
         }
 
@@ -73,10 +126,11 @@ class MultiTaskReplayBuffer:
         for key in ["obs", "actions", "rewards", "next_obs", "dones", "pos", "full"]:
             assert key in d
         T = self.num_tasks
-        for key, init in (("returns_min", np.inf), ("returns_max", -np.inf)):  # buffers.py:333-334
-            if key in d and not np.all(np.asarray(d[key]) == init):
-                raise NotImplementedError(f"checkpoint carries {key} statistics: return normalisation is not "
-                                          "on the MTSAC path")
+        # buffers.py:333-334 (backwards-compatible: absent keys keep the current statistics)
+        self._returns_min = np.asarray(d.get("returns_min", self._returns_min), np.float64).copy()
+        self._returns_max = np.asarray(d.get("returns_max", self._returns_max), np.float64).copy()
+        if self.use_return_normalization:
+            self._push_denominator()
         self.engine.buffer_write(0, np.asarray(d["obs"]).reshape(-1, d["obs"].shape[-1]),
                                  np.asarray(d["next_obs"]).reshape(-1, d["next_obs"].shape[-1]),
                                  np.asarray(d["actions"]).reshape(-1, d["actions"].shape[-1]),

@@ -1295,7 +1295,9 @@ struct mtsac_engine {
     gp.task = task;
     gp.rmin = cfg.normalize_rewards ? rmin : nullptr;
     gp.rmax = cfg.normalize_rewards ? rmax : nullptr;
-    gp.norm_eps = 1e-8;
+    // mode 2 (return normalisation, buffers.py:392-422): rmin = 0, rmax = the per-task denominator
+    // set by the host, so (r - 0) / (den - 0 + 0) = r / den in float64
+    gp.norm_eps = cfg.normalize_rewards == 2 ? 0.0 : 1e-8;
     gp.err = err;
     return gp;
   }
@@ -1387,6 +1389,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     return fail(-22, "depth must be in [1, 8]");
   if (c.num_critics < 1 || c.num_critics > 4) return fail(-22, "num_critics must be in [1, 4]");
   if (c.batch_per_task < 1) return fail(-22, "batch_per_task must be positive");
+  if (c.normalize_rewards < 0 || c.normalize_rewards > 2) return fail(-22, "normalize_rewards must be 0, 1 or 2");
   if (c.capacity < c.batch_per_task || c.capacity >= (1ll << 31))
     return fail(-22, "capacity must be in [batch_per_task, 2^31)");
   if (c.precision != MTSAC_FP32 && c.precision != MTSAC_FP32_SPLIT3 && c.precision != MTSAC_BF16)
@@ -1570,6 +1573,10 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     return bad(fail(-5, "log_alpha"));
   {
     std::vector<double> mn(e->T_l, INFINITY), mx(e->T_l, -INFINITY);  // buffers.py:266-267
+    if (c.normalize_rewards == 2) {  // no completed episode yet: denominator 1 (buffers.py:417-418)
+      std::fill(mn.begin(), mn.end(), 0.0);
+      std::fill(mx.begin(), mx.end(), 1.0);
+    }
     if (hipMemcpy(e->rmin, mn.data(), sizeof(double) * e->T_l, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(e->rmax, mx.data(), sizeof(double) * e->T_l, hipMemcpyHostToDevice) != hipSuccess)
       return bad(fail(-5, "reward stats"));
@@ -1758,7 +1765,7 @@ int mtsac_buffer_add(mtsac_engine* h, const float* obs, const float* next_obs, c
   const long long np = h->h_pos + 1;
   if (np >= h->cfg.capacity) h->h_full = 1;
   h->h_pos = np % h->cfg.capacity;
-  buffer_commit_slot(slot, T, R, D + A, h->cfg.normalize_rewards ? h->rmin : nullptr, h->rmax, h->buf_size,
+  buffer_commit_slot(slot, T, R, D + A, h->cfg.normalize_rewards == 1 ? h->rmin : nullptr, h->rmax, h->buf_size,
                      h->h_full ? h->cfg.capacity : h->h_pos, h->st);
   HIP_TRY(hipGetLastError());
   return 0;

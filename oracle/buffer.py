@@ -14,6 +14,9 @@ Follows ``mtrl/rl/buffers.py``:
 * ``sample(int)``: ``buffers.py:494-549`` int branch ``520-549``: one shared
   index vector of length ``B // T``; rows come out ``row = i*T + t``.
 * ``checkpoint`` / ``load_checkpoint``: ``buffers.py:308-335``.
+* return normalisation (``returns_normalization=True``): ``_compute_discounted_returns``,
+  ``_update_return_stats``, ``_normalize_rewards_by_return`` (``buffers.py:347-422``), called from
+  ``add`` (``:464-472``) and ``sample`` (``:531-533``, before the min-max branch).
 
 The index stream is drawn through :mod:`oracle.pcg64` (pinned bit-exact against
 ``numpy.random.default_rng`` by ``tests/test_oracle_pcg64.py``).
@@ -28,7 +31,8 @@ from .pcg64 import PCG64State
 
 class MultiTaskReplayBufferOracle:
     def __init__(self, total_capacity: int, num_tasks: int, obs_dim: int, action_dim: int,
-                 seed=None, normalize_rewards: bool = False, reward_norm_eps: float = 1e-8):
+                 seed=None, normalize_rewards: bool = False, reward_norm_eps: float = 1e-8,
+                 returns_normalization: bool = False, discount: float = 0.99, v_max: float = 10.0):
         assert total_capacity % num_tasks == 0, "Total capacity must be divisible by the number of tasks."
         self.capacity = total_capacity // num_tasks
         self.num_tasks = num_tasks
@@ -40,6 +44,12 @@ class MultiTaskReplayBufferOracle:
         self.reward_norm_eps = reward_norm_eps
         self._min_rewards = np.full(num_tasks, np.inf, dtype=np.float64)
         self._max_rewards = np.full(num_tasks, -np.inf, dtype=np.float64)
+        self.use_return_normalization = returns_normalization
+        self.discount, self.v_max = discount, v_max
+        self.effective_horizon = 1.0 / (1.0 - discount)
+        self._returns_min = np.full(num_tasks, np.inf, dtype=np.float64)
+        self._returns_max = np.full(num_tasks, -np.inf, dtype=np.float64)
+        self._episode_rewards = [[] for _ in range(num_tasks)]
         self.reset()
 
     def reset(self) -> None:
@@ -59,7 +69,31 @@ class MultiTaskReplayBufferOracle:
             self.full = True
         self.pos = new_pos % self.capacity
 
-    def add(self, obs, next_obs, action, reward, done) -> None:
+    def _compute_discounted_returns(self, rewards, truncated):  # buffers.py:347-366
+        values = np.zeros(len(rewards), dtype=np.float64)
+        bootstrap = float(rewards.mean()) * self.effective_horizon if truncated else 0.0
+        for i in reversed(range(len(rewards))):
+            values[i] = rewards[i] + self.discount * bootstrap
+            bootstrap = values[i]
+        return float(values.min()), float(values.max())
+
+    def _update_return_stats(self, rewards, terminal, truncated):  # buffers.py:368-390
+        for t in range(self.num_tasks):
+            self._episode_rewards[t].append(float(rewards[t]))
+            if bool(terminal[t]) or bool(truncated[t]):
+                lo, hi = self._compute_discounted_returns(np.array(self._episode_rewards[t], dtype=np.float64),
+                                                          truncated=bool(truncated[t]))
+                self._returns_min[t] = min(self._returns_min[t], lo)
+                self._returns_max[t] = max(self._returns_max[t], hi)
+                self._episode_rewards[t] = []
+
+    def return_denominator(self):  # buffers.py:406-418
+        no_data = np.isinf(self._returns_min) | np.isinf(self._returns_max)
+        den = np.where(self._returns_max >= np.abs(self._returns_min), self._returns_max, np.abs(self._returns_min))
+        den = den / self.v_max
+        return np.where(no_data | (den < self.reward_norm_eps), 1.0, den)
+
+    def add(self, obs, next_obs, action, reward, done, terminal=None, truncated=None) -> None:
         obs, next_obs, action = np.asarray(obs), np.asarray(next_obs), np.asarray(action)
         reward, done = np.asarray(reward), np.asarray(done)
         assert obs.ndim == 2 and action.ndim == 2 and reward.ndim <= 2 and done.ndim <= 2
@@ -72,6 +106,11 @@ class MultiTaskReplayBufferOracle:
         if self.normalize_rewards:
             self._min_rewards = np.minimum(self._min_rewards, reward.reshape(-1))
             self._max_rewards = np.maximum(self._max_rewards, reward.reshape(-1))
+        if self.use_return_normalization:
+            term = terminal if terminal is not None else done
+            trunc = truncated if truncated is not None else np.zeros_like(done)
+            self._update_return_stats(reward.flatten(), np.asarray(term).flatten().astype(bool),
+                                      np.asarray(trunc).flatten().astype(bool))
         self._advance_position(1)
 
     def sample_indices(self, batch_size: int) -> np.ndarray:
@@ -83,7 +122,9 @@ class MultiTaskReplayBufferOracle:
     def gather(self, idx: np.ndarray):
         n = idx.shape[0]
         rewards = self.rewards[idx]
-        if self.normalize_rewards:
+        if self.use_return_normalization:
+            rewards = rewards / self.return_denominator()[np.newaxis, :, np.newaxis]
+        elif self.normalize_rewards:
             mn = self._min_rewards[np.newaxis, :, np.newaxis]
             mx = self._max_rewards[np.newaxis, :, np.newaxis]
             rewards = (rewards - mn) / (mx - mn + self.reward_norm_eps)
@@ -99,6 +140,7 @@ class MultiTaskReplayBufferOracle:
             "data": {
                 "obs": self.obs, "actions": self.actions, "rewards": self.rewards,
                 "next_obs": self.next_obs, "dones": self.dones, "pos": self.pos, "full": self.full,
+                "returns_min": self._returns_min, "returns_max": self._returns_max,
             },
             "rng_state": self.rng.to_numpy_state(),
         }

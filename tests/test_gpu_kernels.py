@@ -233,3 +233,42 @@ def test_bad_one_hot_is_reported():
     with pytest.raises(MTSACError):
         eng.sample()
     eng.close()
+
+
+def test_return_normalisation_matches_reference():
+    """returns_normalization=True (buffers.py:347-422, 531-533): per-episode discounted returns
+    (terminal, and truncated with the mean-reward bootstrap) tracked on the host, the per-task
+    denominator applied in the device gather; batches bit for bit against the restatement, the
+    checkpoint carrying returns_min / returns_max."""
+    from mtrl_amd.compat.rl.buffers import MultiTaskReplayBuffer
+    from mtrl_amd.engine import MTSACEngine, make_config
+
+    T, n, cap, A = 3, 8, 64, 4
+    D = 39 + T
+    eng = MTSACEngine(make_config(num_tasks=T, task_count=T, obs_dim=D, batch_per_task=n, capacity=cap,
+                                  actor_width=16, critic_width=16, normalize_rewards=2))
+    buf = MultiTaskReplayBuffer(cap * T, T, seed=7, returns_normalization=True, engine=eng)
+    orc = MultiTaskReplayBufferOracle(cap * T, T, D, A, seed=7, returns_normalization=True)
+    obs, nobs, act, _, _ = _fill(None, cap, T, D, A, slots=60)
+    rng = np.random.default_rng(3)
+    checks = 0
+    for s in range(60):
+        rew = rng.normal(2.0, 3.0, T)  # float64, as an env hands them over
+        term = rng.uniform(size=T) < 0.08
+        trunc = (rng.uniform(size=T) < 0.05) & ~term
+        done = (term | trunc).astype(np.float32)
+        kw = {"terminal": term, "truncated": trunc} if s % 2 else {}
+        buf.add(obs[s], nobs[s], act[s], rew, done, **kw)
+        orc.add(obs[s], nobs[s], act[s], rew, done, **kw)
+        if s % 5 == 4 and s >= n:  # only written slots (the engine rejects rows without a task one-hot)
+            got = buf.sample(n * T)
+            want = orc.sample(n * T)
+            for g, w in zip(got, want):
+                np.testing.assert_array_equal(np.asarray(g).reshape(w.shape), w.astype(np.float32))
+            checks += 1
+    assert checks == 11 and np.isfinite(orc._returns_max).all()
+    np.testing.assert_array_equal(buf.return_denominator(), orc.return_denominator())
+    ck = buf.checkpoint()
+    np.testing.assert_array_equal(ck["data"]["returns_min"], orc._returns_min)
+    np.testing.assert_array_equal(ck["data"]["returns_max"], orc._returns_max)
+    eng.close()
