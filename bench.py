@@ -60,6 +60,11 @@ GEMM_FAMILIES = {
     },
 }
 METRIC = "SAC gradient-steps/sec, MT50 width-2048 batch=128/task, 1/2/4/8 MI355X"
+# BASELINE.json configs[4] (experiments/atari.py): the reference's Atari agent is DrQ-eps, not PPO
+# 
+DRQ_WORKLOAD = "atari_drq"
+DRQ_METRIC = "DrQ-eps gradient-steps/sec, experiments/atari.py (26 games, IMPALA scale 1, dueling C51, batch 256), 1 MI355X"
+FP32_VALU_PEAK_TF = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector)
 
 
 def pmc_traffic(precision, family):
@@ -142,6 +147,115 @@ def cpu_baseline(T, W, clip, steps, c0_steps):
     return out
 
 
+def bench_drq(args, world, rank, local_rank, dist):
+    """configs[4]: one DrQ-eps training step = sample_unbalanced(256) from a full device Atari
+    buffer (host Dirichlet / index draws included) + augmentation + the three ImpalaDQN passes,
+    C51 loss, backward, AdamW, Polyak (mtrl/rl/algorithms/drqeps.py:268-351, base.py:213-221).
+    The agent does not shard: with --gpus N every rank runs its own replica ("replicas only")."""
+    import dataclasses
+
+    import torch
+
+    from mtrl_amd import _lib as L
+    from mtrl_amd.drq import DrQEngine, DrQSettings
+    from mtrl_amd.drq_init import init_drq
+
+    s = dataclasses.replace(DrQSettings(batch=256), capacity=args.drq_capacity, normalize_rewards=1)
+    e = DrQEngine(s, device=local_rank)
+    p = init_drq(1)
+    e.set_params(L.DRQ_PARAMS, p)
+    e.set_params(L.DRQ_TARGET, p)
+    e.seed_rng(1 + rank)
+    e.seed_augment(2 + rank)
+    rng = np.random.default_rng(rank)
+    T = s.num_tasks
+    frames = rng.integers(0, 256, (T, 4, 84, 84), dtype=np.uint8)
+    for i in range(s.capacity + s.nstep + 8):  # past capacity: the guard window is in play
+        o = np.roll(frames, i, axis=-1)
+        e.buffer_add(o, np.roll(o, 1, axis=-1), rng.integers(0, 18, T), rng.standard_normal(T).astype(np.float32),
+                     np.zeros(T, np.float32), (rng.random(T) < 0.01).astype(np.float32))
+    e.sample_unbalanced_update(args.warmup)
+    e.synchronize()
+    settle = 0
+    if args.settle_s > 0:
+        a = time.perf_counter()
+        e.sample_unbalanced_update(20)
+        e.synchronize()
+        settle = [int(args.settle_s / max((time.perf_counter() - a) / 20, 1e-4))]
+        if dist:
+            dist.broadcast_object_list(settle, src=0)
+        settle = settle[0]
+        e.sample_unbalanced_update(settle)
+        e.synchronize()
+    e.set_timing(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(local_rank)
+    t0 = time.perf_counter()
+    e.sample_unbalanced_update(args.steps)
+    e.synchronize()
+    torch.cuda.synchronize(local_rank)
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms, nl, fl = e.timing()
+    e.set_timing(False)
+    logs = e.logs()
+    e.close()
+    assert all(math.isfinite(v) for v in logs.values()), logs
+    achieved = (fl / nl) / (ms / nl * 1e-3) / 1e12 if nl else 0.0
+    out = {
+        "metric": DRQ_METRIC, "value": world * args.steps / elapsed, "unit": "DrQ gradient-steps/sec",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+        "settle_steps": settle, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": f"synthetic uint8 frame stacks in a full device MemoryEfficientAtariMultiTaskReplayBuffer "
+                f"({s.capacity} slots/task), random-init ImpalaDQN",
+        "config": {"workload": "experiments/atari.py DrQ-eps: 26 games, 4x84x84 uint8, IMPALA 8/16/16 scale 1, "
+                               "task embedding 32, dense 512, 18 actions x 51 atoms, 3-step returns",
+                   "global_batch": 256 * world, "batch_per_replica": 256, "sampler": "sample_unbalanced",
+                   "parallelism": f"replicas{world}" if world > 1 else "single"},
+        "roofline": {"bound": "valu", "kernel": "conv_fwd_kernel<ci, co, *, *> (IMPALA 3x3 convs, fp32 FMA on the "
+                                                "vector ALUs: Cout <= 16 leaves MFMA tiles empty)",
+                     "achieved": achieved, "peak": FP32_VALU_PEAK_TF, "peak_basis": "FP32 vector peak",
+                     "unit": "TFLOP/s", "frac": achieved / FP32_VALU_PEAK_TF, "traffic": None,
+                     "launches": nl, "avg_launch_us": 1e3 * ms / max(nl, 1),
+                     "algorithmic_flops_per_launch": fl / max(nl, 1),
+                     "timing": "HIP events per launch on the engine stream, every 8th update of the timed steps"},
+        "logs": logs,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import drq as od  # the cpu_baseline leg only
+
+        threads, affinity, quota = available_cores()
+        torch.set_num_threads(threads)
+        cfg = od.DrQConfig()
+        st = od.init_state(cfg, 0)
+        B = 256
+        obs = rng.integers(0, 256, (B, 4, 84, 84), dtype=np.uint8)
+        crop = rng.integers(0, 8, (B, 2)).astype(np.int32)
+        noise = (1 + 0.05 * np.clip(rng.standard_normal(B), -2, 2)).astype(np.float32)
+        batch = (od.augment(obs, crop, noise), rng.integers(0, 18, B).astype(np.int32),
+                 od.augment(np.roll(obs, 1, -1), crop, noise), np.zeros(B, np.float32),
+                 rng.standard_normal(B).astype(np.float32), (np.arange(B) % 26).astype(np.int32))
+        st, _ = od.update(cfg, st, batch, dtype=torch.float32)
+        a = time.perf_counter()
+        for _ in range(args.cpu_steps):
+            st, _ = od.update(cfg, st, batch, dtype=torch.float32)
+        dt = time.perf_counter() - a
+        out["cpu_baseline"] = {"value": args.cpu_steps / dt, "unit": "DrQ gradient-steps/sec", "cores": threads,
+                               "kind": "port",
+                               "sample": f"{args.cpu_steps} DrQ updates at batch {B} (augmentation, 3 ImpalaDQN passes, "
+                                         f"C51, autograd backward, AdamW) of the PyTorch-CPU fp32 restatement "
+                                         f"oracle/drq.py, {dt:.1f}s on {threads} threads; {cpu_model()}"}
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def _free_port():
     import socket
 
@@ -174,7 +288,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="mt50_w2048", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="mt50_w2048", choices=sorted(WORKLOADS) + [DRQ_WORKLOAD])
+    ap.add_argument("--drq-capacity", type=int, default=2000, help="atari_drq: device buffer slots per task")
     ap.add_argument("--no-graph", action="store_true", help="same as --exec eager")
     ap.add_argument("--exec", default="auto", choices=["auto", "graph", "eager"],
                     help="hipGraph replay or eager multi-stream DAG; auto = faster of the two")
@@ -203,6 +318,13 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group("gloo")  # host-side control plane only; gradients go over RCCL
+
+    if args.workload == DRQ_WORKLOAD:
+        if not args.dry_run:
+            bench_drq(args, world, rank, local_rank, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
 
     from mtrl_amd.shard import allreduce_floats_per_step, shard_tasks
 

@@ -133,6 +133,10 @@ int drq_task_gradient(drq_engine* e, const drq_batch* batch, int slot, int num_s
 int drq_get_task_gradient(drq_engine* e, int slot, float* flat, long long n);
 int drq_project_task_gradients(drq_engine* e, int num_slots, int proj_dim, long long chunk, int seed, float* out);
 int drq_synchronize(drq_engine* e);
+/* bench.py's roofline: HIP events around the IMPALA conv forward launches of every 8th update on
+ * the engine stream while on; drq_timing sums them (ms), with the launch count and algorithmic flops 2 B H W 9 ci co */
+int drq_set_timing(drq_engine* e, int on);
+int drq_timing(drq_engine* e, double* ms, long long* launches, double* flops);
 const char* drq_last_error(void);
 
 #ifdef __cplusplus

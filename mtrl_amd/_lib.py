@@ -199,6 +199,8 @@ SIGNATURES.update({
     "drq_task_gradient": (ctypes.c_int, [P, ctypes.POINTER(DrqBatch), ctypes.c_int, ctypes.c_int]),
     "drq_get_task_gradient": (ctypes.c_int, [P, ctypes.c_int, P, I64]),
     "drq_project_task_gradients": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, I64, ctypes.c_int, P]),
+    "drq_set_timing": (ctypes.c_int, [P, ctypes.c_int]),
+    "drq_timing": (ctypes.c_int, [P, P, P, P]),
     "drq_read_batch": (ctypes.c_int, [P, P, P, P, P, P, P, P]),
     "drq_synchronize": (ctypes.c_int, [P]),
 })

@@ -145,21 +145,22 @@ __global__ void aug_draw_kernel(unsigned long long seed, unsigned long long ctr,
 
 // ------------------------------------------------------------------ convolutions
 // out[b][y][x][:] = bias + sum_{dy,dx,ci} act(in[b][y+dy-1][x+dx-1][ci]) w[dy][dx][ci][:]
-// (+ res[b][y][x][:]); act = relu when RELU_IN.  One lane per output pixel.
-template <int CI, int CO, bool RELU_IN, bool ADD_RES>
+// (+ res[b][y][x][:]); act = relu when RELU_IN.  One lane per (output pixel, group of CG output
+// channels), the group uniform over the block (blockIdx.y).  The weights are read straight from
+// global memory with wave-uniform addresses, so they arrive by scalar loads as SGPR operands of
+// packed FMAs (an LDS copy put a broadcast read in front of every four FMAs).  The per-output
+// summation order (taps, then input channels) does not depend on CG.
+template <int CI, int CO, int CG, bool RELU_IN, bool ADD_RES>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ in, const float* __restrict__ w,
                                                        const float* __restrict__ bias, const float* __restrict__ res,
                                                        float* __restrict__ out, int B, int H, int W) {
-  __shared__ float ws[9 * CI * CO];
-  for (int i = threadIdx.x; i < 9 * CI * CO; i += 256) ws[i] = w[i];
-  __syncthreads();
-  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (pix >= (long long)B * H * W) return;
-  const int x = (int)(pix % W), y = (int)((pix / W) % H);
-  const long long b = pix / ((long long)H * W);
-  float acc[CO];
+  const int cg = blockIdx.y * CG;
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  if (pix >= B * H * W) return;
+  const int x = pix % W, y = (pix / W) % H;
+  float acc[CG];
 #pragma unroll
-  for (int co = 0; co < CO; ++co) acc[co] = bias[co];
+  for (int c = 0; c < CG; ++c) acc[c] = bias[cg + c];
 #pragma unroll
   for (int dy = 0; dy < 3; ++dy) {
     const int yy = y + dy - 1;
@@ -168,29 +169,28 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
     for (int dx = 0; dx < 3; ++dx) {
       const int xx = x + dx - 1;
       if (xx < 0 || xx >= W) continue;
-      const float* ip = in + ((b * H + yy) * W + xx) * CI;
+      const float* ip = in + (long long)(pix + (dy - 1) * W + (dx - 1)) * CI;
       float v[CI];
 #pragma unroll
       for (int c4 = 0; c4 < CI; c4 += 4) {
         const float4 q = *reinterpret_cast<const float4*>(ip + c4);
         v[c4] = q.x; v[c4 + 1] = q.y; v[c4 + 2] = q.z; v[c4 + 3] = q.w;
       }
-      const float* wt = ws + (dy * 3 + dx) * CI * CO;
+      const float* wt = w + (dy * 3 + dx) * CI * CO + cg;
 #pragma unroll
       for (int ci = 0; ci < CI; ++ci) {
         const float a = RELU_IN ? fmaxf(v[ci], 0.f) : v[ci];
 #pragma unroll
-        for (int co = 0; co < CO; ++co) acc[co] = fmaf(a, wt[ci * CO + co], acc[co]);
+        for (int c = 0; c < CG; ++c) acc[c] = fmaf(a, wt[ci * CO + c], acc[c]);
       }
     }
   }
-  float* op = out + pix * CO;
-  const float* rp = ADD_RES ? res + pix * CO : nullptr;
+  float* op = out + (long long)pix * CO + cg;
 #pragma unroll
-  for (int c4 = 0; c4 < CO; c4 += 4) {
+  for (int c4 = 0; c4 < CG; c4 += 4) {
     float4 o = make_float4(acc[c4], acc[c4 + 1], acc[c4 + 2], acc[c4 + 3]);
     if (ADD_RES) {
-      const float4 r = *reinterpret_cast<const float4*>(rp + c4);
+      const float4 r = *reinterpret_cast<const float4*>(res + (long long)pix * CO + cg + c4);
       o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
     }
     *reinterpret_cast<float4*>(op + c4) = o;
@@ -198,22 +198,20 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
 }
 
 // din[b][y][x][ci] = (sum_{dy,dx,co} dout[b][y-dy+1][x-dx+1][co] w[dy][dx][ci][co]) * [mask > 0]
-// (MASK: the ReLU in front of the conv) (+ dres[b][y][x][ci]).  One lane per input pixel.
-template <int CI, int CO, bool MASK, bool ADD_RES>
+// (MASK: the ReLU in front of the conv) (+ dres[b][y][x][ci]).  One lane per (input pixel, group
+// of CG input channels), weights by scalar loads as above.
+template <int CI, int CO, int CG, bool MASK, bool ADD_RES>
 __global__ __launch_bounds__(256) void conv_bwd_data_kernel(const float* __restrict__ dout, const float* __restrict__ w,
                                                             const float* __restrict__ mask,
                                                             const float* __restrict__ dres, float* __restrict__ din,
                                                             int B, int H, int W) {
-  __shared__ float ws[9 * CI * CO];
-  for (int i = threadIdx.x; i < 9 * CI * CO; i += 256) ws[i] = w[i];
-  __syncthreads();
-  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (pix >= (long long)B * H * W) return;
-  const int x = (int)(pix % W), y = (int)((pix / W) % H);
-  const long long b = pix / ((long long)H * W);
-  float acc[CI];
+  const int cg = blockIdx.y * CG;
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  if (pix >= B * H * W) return;
+  const int x = pix % W, y = (pix / W) % H;
+  float acc[CG];
 #pragma unroll
-  for (int ci = 0; ci < CI; ++ci) acc[ci] = 0.f;
+  for (int c = 0; c < CG; ++c) acc[c] = 0.f;
 #pragma unroll
   for (int dy = 0; dy < 3; ++dy) {
     const int yy = y - dy + 1;
@@ -222,37 +220,37 @@ __global__ __launch_bounds__(256) void conv_bwd_data_kernel(const float* __restr
     for (int dx = 0; dx < 3; ++dx) {
       const int xx = x - dx + 1;
       if (xx < 0 || xx >= W) continue;
-      const float* gp = dout + ((b * H + yy) * W + xx) * CO;
+      const float* gp = dout + (long long)(pix + (1 - dy) * W + (1 - dx)) * CO;
       float g[CO];
 #pragma unroll
       for (int c4 = 0; c4 < CO; c4 += 4) {
         const float4 q = *reinterpret_cast<const float4*>(gp + c4);
         g[c4] = q.x; g[c4 + 1] = q.y; g[c4 + 2] = q.z; g[c4 + 3] = q.w;
       }
-      const float* wt = ws + (dy * 3 + dx) * CI * CO;
+      const float* wt = w + (dy * 3 + dx) * CI * CO + cg * CO;
 #pragma unroll
-      for (int ci = 0; ci < CI; ++ci) {
-        float s = acc[ci];
+      for (int c = 0; c < CG; ++c) {
+        float s = acc[c];
 #pragma unroll
-        for (int co = 0; co < CO; ++co) s = fmaf(g[co], wt[ci * CO + co], s);
-        acc[ci] = s;
+        for (int co = 0; co < CO; ++co) s = fmaf(g[co], wt[c * CO + co], s);
+        acc[c] = s;
       }
     }
   }
-  float* op = din + pix * CI;
 #pragma unroll
-  for (int c4 = 0; c4 < CI; c4 += 4) {
-    float4 o = make_float4(acc[c4], acc[c4 + 1], acc[c4 + 2], acc[c4 + 3]);
+  for (int c4 = 0; c4 < CG; c4 += 4) {
+    const long long o = (long long)pix * CI + cg + c4;
+    float4 r4 = make_float4(acc[c4], acc[c4 + 1], acc[c4 + 2], acc[c4 + 3]);
     if (MASK) {
-      const float4 m = *reinterpret_cast<const float4*>(mask + pix * CI + c4);
-      o.x = m.x > 0.f ? o.x : 0.f; o.y = m.y > 0.f ? o.y : 0.f;
-      o.z = m.z > 0.f ? o.z : 0.f; o.w = m.w > 0.f ? o.w : 0.f;
+      const float4 m = *reinterpret_cast<const float4*>(mask + o);
+      r4.x = m.x > 0.f ? r4.x : 0.f; r4.y = m.y > 0.f ? r4.y : 0.f;
+      r4.z = m.z > 0.f ? r4.z : 0.f; r4.w = m.w > 0.f ? r4.w : 0.f;
     }
     if (ADD_RES) {
-      const float4 r = *reinterpret_cast<const float4*>(dres + pix * CI + c4);
-      o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+      const float4 r = *reinterpret_cast<const float4*>(dres + o);
+      r4.x += r.x; r4.y += r.y; r4.z += r.z; r4.w += r.w;
     }
-    *reinterpret_cast<float4*>(op + c4) = o;
+    *reinterpret_cast<float4*>(din + o) = r4;
   }
 }
 
@@ -366,41 +364,47 @@ __global__ __launch_bounds__(256) void sum_parts_kernel(const float* __restrict_
 // gradient; jax's select-and-scatter takes the first maximum, as here)
 __global__ void maxpool_fwd_kernel(const float* __restrict__ in, float* __restrict__ out,
                                    unsigned char* __restrict__ arg, int B, int H, int W, int C, int Ho, int Wo, int lo) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long long)B * Ho * Wo * C) return;
-  const int c = (int)(i % C);
-  long long r = i / C;
-  const int ox = (int)(r % Wo);
+  // one lane per 4 channels of one output pixel: float4 loads / stores, 32-bit index math
+  const int C4 = C >> 2;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * Ho * Wo * C4) return;
+  const int c = (i % C4) * 4;
+  int r = i / C4;
+  const int ox = r % Wo;
   r /= Wo;
-  const int oy = (int)(r % Ho);
-  const long long b = r / Ho;
-  float best = -INFINITY;
-  int bi = 0;
+  const int oy = r % Ho;
+  const int b = r / Ho;
+  float4 best = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+  uchar4 bi = make_uchar4(0, 0, 0, 0);
   for (int tap = 0; tap < 9; ++tap) {
     const int y = 2 * oy - lo + tap / 3, x = 2 * ox - lo + tap % 3;
     if (y < 0 || y >= H || x < 0 || x >= W) continue;
-    const float v = in[((b * H + y) * W + x) * C + c];
-    if (v > best) {
-      best = v;
-      bi = tap;
-    }
+    const float4 v = *reinterpret_cast<const float4*>(in + ((b * H + y) * W + x) * C + c);
+    const unsigned char t = (unsigned char)tap;
+    if (v.x > best.x) { best.x = v.x; bi.x = t; }
+    if (v.y > best.y) { best.y = v.y; bi.y = t; }
+    if (v.z > best.z) { best.z = v.z; bi.z = t; }
+    if (v.w > best.w) { best.w = v.w; bi.w = t; }
   }
-  out[i] = best;
-  arg[i] = (unsigned char)bi;
+  const int o = ((b * Ho + oy) * Wo + ox) * C + c;
+  *reinterpret_cast<float4*>(out + o) = best;
+  *reinterpret_cast<uchar4*>(arg + o) = bi;
 }
 
-// din[b][y][x][c] = sum over the windows whose argmax is (y, x) of dout (a gather: deterministic)
+// din[b][y][x][c] = sum over the windows whose argmax is (y, x) of dout (a gather: deterministic),
+// one lane per 4 channels of one input pixel
 __global__ void maxpool_bwd_kernel(const float* __restrict__ dout, const unsigned char* __restrict__ arg,
                                    float* __restrict__ din, int B, int H, int W, int C, int Ho, int Wo, int lo) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long long)B * H * W * C) return;
-  const int c = (int)(i % C);
-  long long r = i / C;
-  const int x = (int)(r % W);
+  const int C4 = C >> 2;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * H * W * C4) return;
+  const int c = (i % C4) * 4;
+  int r = i / C4;
+  const int x = r % W;
   r /= W;
-  const int y = (int)(r % H);
-  const long long b = r / H;
-  float s = 0.f;
+  const int y = r % H;
+  const int b = r / H;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   // windows o with 2 o - lo <= y <= 2 o - lo + 2, in order
   const int oy0 = y + lo - 2 <= 0 ? 0 : (y + lo - 1) / 2, oy1 = min((y + lo) / 2, Ho - 1);
   const int ox0 = x + lo - 2 <= 0 ? 0 : (x + lo - 1) / 2, ox1 = min((x + lo) / 2, Wo - 1);
@@ -410,11 +414,17 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ dout, const unsigne
     for (int ox = ox0; ox <= ox1; ++ox) {
       const int tx = x - (2 * ox - lo);
       if (tx < 0 || tx > 2) continue;
-      const long long o = ((b * Ho + oy) * Wo + ox) * C + c;
-      if (arg[o] == ty * 3 + tx) s += dout[o];
+      const int o = ((b * Ho + oy) * Wo + ox) * C + c;
+      const uchar4 a = *reinterpret_cast<const uchar4*>(arg + o);
+      const float4 d = *reinterpret_cast<const float4*>(dout + o);
+      const unsigned char t = (unsigned char)(ty * 3 + tx);
+      if (a.x == t) s.x += d.x;
+      if (a.y == t) s.y += d.y;
+      if (a.z == t) s.z += d.z;
+      if (a.w == t) s.w += d.w;
     }
   }
-  din[i] = s;
+  *reinterpret_cast<float4*>(din + ((b * H + y) * W + x) * C + c) = s;
 }
 
 // ------------------------------------------------------------------ encoder output + embedding
@@ -930,34 +940,52 @@ bool conv_supported(int ci, int co) {
   return false;
 }
 
+// channels per lane (measured, rocprofv3 per-kernel sums): the forward keeps every output channel
+// of a pixel in one lane (splitting re-reads the input patch per group); the data gradient splits
+// 16 input channels into groups of 4 (4x the waves for the same dout reads, 1.4x faster there)
+static int conv_fwd_group(int co) { return co; }
+static int conv_bwd_group(int ci) { return ci == 16 ? 4 : ci; }
+
 void conv_fwd(const float* in, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
               int ci, int co, bool relu_in, hipStream_t st) {
-  const dim3 g(blocks((long long)B * H * W)), t(256);
-#define C_FWD(a, b)                                                                                                  \
-  if (ci == a && co == b) {                                                                                          \
-    if (relu_in && res) hipLaunchKernelGGL((conv_fwd_kernel<a, b, true, true>), g, t, 0, st, in, w, bias, res, out, B, H, W); \
-    else if (relu_in) hipLaunchKernelGGL((conv_fwd_kernel<a, b, true, false>), g, t, 0, st, in, w, bias, res, out, B, H, W); \
-    else if (res) hipLaunchKernelGGL((conv_fwd_kernel<a, b, false, true>), g, t, 0, st, in, w, bias, res, out, B, H, W); \
-    else hipLaunchKernelGGL((conv_fwd_kernel<a, b, false, false>), g, t, 0, st, in, w, bias, res, out, B, H, W);        \
-    return;                                                                                                          \
+  const long long npix = (long long)B * H * W;
+  const int G = conv_fwd_group(co);
+  const dim3 g(blocks(npix), co / G), t(256);
+#define C_FWD_G(a, b, cg)                                                                                           \
+  if (relu_in && res) hipLaunchKernelGGL((conv_fwd_kernel<a, b, cg, true, true>), g, t, 0, st, in, w, bias, res, out, B, H, W); \
+  else if (relu_in) hipLaunchKernelGGL((conv_fwd_kernel<a, b, cg, true, false>), g, t, 0, st, in, w, bias, res, out, B, H, W); \
+  else if (res) hipLaunchKernelGGL((conv_fwd_kernel<a, b, cg, false, true>), g, t, 0, st, in, w, bias, res, out, B, H, W); \
+  else hipLaunchKernelGGL((conv_fwd_kernel<a, b, cg, false, false>), g, t, 0, st, in, w, bias, res, out, B, H, W);
+#define C_FWD(a, b)                   \
+  if (ci == a && co == b) {           \
+    if (G == b) { C_FWD_G(a, b, b) }  \
+    else { C_FWD_G(a, b, 4) }         \
+    return;                           \
   }
   CONV_CASES(C_FWD)
 #undef C_FWD
+#undef C_FWD_G
 }
 
 void conv_bwd_data(const float* dout, const float* w, const float* mask, const float* dres, float* din, int B, int H,
                    int W, int ci, int co, hipStream_t st) {
-  const dim3 g(blocks((long long)B * H * W)), t(256);
-#define C_BD(a, b)                                                                                                   \
-  if (ci == a && co == b) {                                                                                          \
-    if (mask && dres) hipLaunchKernelGGL((conv_bwd_data_kernel<a, b, true, true>), g, t, 0, st, dout, w, mask, dres, din, B, H, W); \
-    else if (mask) hipLaunchKernelGGL((conv_bwd_data_kernel<a, b, true, false>), g, t, 0, st, dout, w, mask, dres, din, B, H, W); \
-    else if (dres) hipLaunchKernelGGL((conv_bwd_data_kernel<a, b, false, true>), g, t, 0, st, dout, w, mask, dres, din, B, H, W); \
-    else hipLaunchKernelGGL((conv_bwd_data_kernel<a, b, false, false>), g, t, 0, st, dout, w, mask, dres, din, B, H, W); \
-    return;                                                                                                          \
+  const long long npix = (long long)B * H * W;
+  const int G = conv_bwd_group(ci);
+  const dim3 g(blocks(npix), ci / G), t(256);
+#define C_BD_G(a, b, cg)                                                                                            \
+  if (mask && dres) hipLaunchKernelGGL((conv_bwd_data_kernel<a, b, cg, true, true>), g, t, 0, st, dout, w, mask, dres, din, B, H, W); \
+  else if (mask) hipLaunchKernelGGL((conv_bwd_data_kernel<a, b, cg, true, false>), g, t, 0, st, dout, w, mask, dres, din, B, H, W); \
+  else if (dres) hipLaunchKernelGGL((conv_bwd_data_kernel<a, b, cg, false, true>), g, t, 0, st, dout, w, mask, dres, din, B, H, W); \
+  else hipLaunchKernelGGL((conv_bwd_data_kernel<a, b, cg, false, false>), g, t, 0, st, dout, w, mask, dres, din, B, H, W);
+#define C_BD(a, b)                   \
+  if (ci == a && co == b) {          \
+    if (G == a) { C_BD_G(a, b, a) }  \
+    else { C_BD_G(a, b, 4) }         \
+    return;                          \
   }
   CONV_CASES(C_BD)
 #undef C_BD
+#undef C_BD_G
 }
 
 // enough 64-pixel tiles in flight per CU to cover the staging loads' latency (the partials'
@@ -981,14 +1009,14 @@ void conv_wgrad(const float* in, const float* dout, float* part, float* dw, floa
 void maxpool_fwd(const float* in, float* out, unsigned char* arg, int B, int H, int W, int C, hipStream_t st) {
   const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
   const int lo = std::max((Ho - 1) * 2 + 3 - H, 0) / 2;
-  const long long n = (long long)B * Ho * Wo * C;
+  const long long n = (long long)B * Ho * Wo * (C / 4);  // C % 4 == 0, B H W C < 2^31 (drq_create)
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(blocks(n)), dim3(256), 0, st, in, out, arg, B, H, W, C, Ho, Wo, lo);
 }
 
 void maxpool_bwd(const float* dout, const unsigned char* arg, float* din, int B, int H, int W, int C, hipStream_t st) {
   const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
   const int lo = std::max((Ho - 1) * 2 + 3 - H, 0) / 2;
-  const long long n = (long long)B * H * W * C;
+  const long long n = (long long)B * H * W * (C / 4);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(blocks(n)), dim3(256), 0, st, dout, arg, din, B, H, W, C, Ho, Wo, lo);
 }
 

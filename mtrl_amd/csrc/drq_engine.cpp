@@ -140,13 +140,13 @@ struct drq_engine {
     const float* x = X;
     for (int s = 0; s < 3; ++s) {
       Stack& k = stk[s];
-      drq::conv_fwd(x, P + k.cw[0], P + k.cb[0], nullptr, k.conv0, B, k.hin, k.hin, k.ci, k.co, false, st);
+      conv_fwd_t(x, P + k.cw[0], P + k.cb[0], nullptr, k.conv0, B, k.hin, k.hin, k.ci, k.co, false);
       drq::maxpool_fwd(k.conv0, k.c[0], k.arg, B, k.hin, k.hin, k.co, st);
       for (int b = 0; b < cfg_blocks(); ++b) {
-        drq::conv_fwd(k.c[b], P + k.cw[1 + 2 * b], P + k.cb[1 + 2 * b], nullptr, k.r[b], B, k.ho, k.ho, k.co, k.co,
-                      true, st);
-        drq::conv_fwd(k.r[b], P + k.cw[2 + 2 * b], P + k.cb[2 + 2 * b], k.c[b], k.c[b + 1], B, k.ho, k.ho, k.co, k.co,
-                      true, st);
+        conv_fwd_t(k.c[b], P + k.cw[1 + 2 * b], P + k.cb[1 + 2 * b], nullptr, k.r[b], B, k.ho, k.ho, k.co, k.co,
+                   true);
+        conv_fwd_t(k.r[b], P + k.cw[2 + 2 * b], P + k.cb[2 + 2 * b], k.c[b], k.c[b + 1], B, k.ho, k.ho, k.co, k.co,
+                   true);
       }
       x = k.c[2];
     }
@@ -157,6 +157,38 @@ struct drq_engine {
     gemm_store(h2, H, P + off_wc, NC, out, NC, B, NC, H, GEMM_NN);
   }
   int cfg_blocks() const { return 2; }
+
+  // ---- per-launch timing of the conv forward family (bench.py's roofline): HIP events on the
+  // engine stream around each launch of every 8th update (event records cost host time on a
+  // launch-dense step), algorithmic flops 2 B H W 9 ci co
+  bool timing = false;
+  std::vector<hipEvent_t> ev;
+  size_t ev_used = 0;
+  double t_flops = 0;
+  long long t_launches = 0;
+  void conv_fwd_t(const float* in, const float* w, const float* bias, const float* res, float* out, int Bn, int Hh,
+                  int Ww, int ci, int co, bool relu_in) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (timing && count % 8 == 0) {
+      while (ev.size() < ev_used + 2) {
+        hipEvent_t x;
+        if (hipEventCreate(&x) != hipSuccess) break;
+        ev.push_back(x);
+      }
+      if (ev.size() >= ev_used + 2) {
+        a = ev[ev_used];
+        b = ev[ev_used + 1];
+        ev_used += 2;
+        (void)hipEventRecord(a, st);
+      }
+    }
+    drq::conv_fwd(in, w, bias, res, out, Bn, Hh, Ww, ci, co, relu_in, st);
+    if (a) {
+      (void)hipEventRecord(b, st);
+      t_flops += 2.0 * Bn * Hh * Ww * 9.0 * ci * co;
+      ++t_launches;
+    }
+  }
 
   // expected Q of the online network on n (<= batch) staged observations (rollout actions)
   void q_values(int n, float* q) {
@@ -363,6 +395,8 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
   if (c->num_tasks < 1 || c->n_actions < 1 || c->n_atoms < 2 || c->n_atoms > 64 || c->batch < 1 || c->hw < 4 ||
       c->scale < 1 || c->embed_dim < 1 || c->embed_dim > 64 || c->n_hidden < 4)
     return fail(-22, "bad drq_config");
+  if ((long long)c->batch * c->hw * c->hw * 16 * c->scale >= (1LL << 31))  // 32-bit indices in the pool kernels
+    return fail(-22, "batch x hw x hw x channels must stay below 2^31");
   if (hipSetDevice(device) != hipSuccess) return fail(-19, "hipSetDevice failed");
   drq_engine* e = new drq_engine();
   e->cfg = *c;
@@ -542,6 +576,7 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
 void drq_destroy(drq_engine* e) {
   if (!e) return;
   if (e->st) (void)hipStreamSynchronize(e->st);
+  for (hipEvent_t x : e->ev) (void)hipEventDestroy(x);
   for (void* q : e->allocs) (void)hipFree(q);
   if (e->st) (void)hipStreamDestroy(e->st);
   delete e;
@@ -824,6 +859,31 @@ int drq_project_task_gradients(drq_engine* e, int num_slots, int proj_dim, long 
           hipSuccess ||
       hipStreamSynchronize(e->st) != hipSuccess)
     return fail(-5, "download failed");
+  return 0;
+}
+
+int drq_set_timing(drq_engine* e, int on) {
+  if (!e) return fail(-22, "null argument");
+  if (hipStreamSynchronize(e->st) != hipSuccess) return fail(-5, "stream sync failed");
+  e->timing = on != 0;
+  e->ev_used = 0;
+  e->t_flops = 0;
+  e->t_launches = 0;
+  return 0;
+}
+
+int drq_timing(drq_engine* e, double* ms, long long* launches, double* flops) {
+  if (!e || !ms || !launches || !flops) return fail(-22, "null argument");
+  if (hipStreamSynchronize(e->st) != hipSuccess) return fail(-5, "stream sync failed");
+  double total = 0;
+  for (size_t i = 0; i + 1 < e->ev_used; i += 2) {
+    float x = 0;
+    if (hipEventElapsedTime(&x, e->ev[i], e->ev[i + 1]) != hipSuccess) return fail(-5, "event timing failed");
+    total += x;
+  }
+  *ms = total;
+  *launches = e->t_launches;
+  *flops = e->t_flops;
   return 0;
 }
 

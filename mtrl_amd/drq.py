@@ -326,5 +326,14 @@ class DrQEngine:
         _drq_check(self.lib.drq_get_logs(self.h, _ptr(out)))
         return dict(zip(L.DRQ_LOG_KEYS, (float(v) for v in out)))
 
+    def set_timing(self, on: bool):
+        _drq_check(self.lib.drq_set_timing(self.h, int(on)))
+
+    def timing(self):
+        """(ms, launches, flops) of the conv-forward launches since set_timing(True)."""
+        ms, n, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        _drq_check(self.lib.drq_timing(self.h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl)))
+        return ms.value, n.value, fl.value
+
     def synchronize(self):
         _drq_check(self.lib.drq_synchronize(self.h))
