@@ -255,22 +255,28 @@ __global__ __launch_bounds__(256) void conv_bwd_data_kernel(const float* __restr
 }
 
 // Weight gradient partials: block g takes 64-pixel tiles g, g + G, ... (G = gridDim.x); the
-// tile's im2col rows (act applied, zero outside the image) and dout go through LDS; lane t owns
-// column co = t % CO of rows tc = t / CO + (256 / CO) j of dW ([tap * CI + ci][co]) and the bias
-// entry co = t (< CO), summed over the tile's pixels in order.  part[g][9 CI CO + CO], summed over g in order by sum_parts_kernel.
+// tile's im2col rows (act applied, zero outside the image) and dout go through LDS; lane t owns a
+// 4 x 4 block of dW ([tap * CI + ci][co]) over the pixels q = pg, pg + PG, ... of every tile (PG
+// lane groups when the blocks leave lanes over), the groups' partials summed in group order at
+// the end; lanes t < CO own the bias entries.  part[g][9 CI CO + CO], summed over g in order by
+// sum_parts_kernel.
 template <int CI, int CO, bool RELU_IN>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict__ in, const float* __restrict__ dout,
                                                          float* __restrict__ part, int B, int H, int W) {
   constexpr int NW = 9 * CI * CO;
-  constexpr int NG = 256 / CO;                 // lane groups; lane t: co = t % CO, tap-channel rows
-  constexpr int PER = (9 * CI + NG - 1) / NG;  // tc = t / CO + NG j (one dout read per NG-row sweep)
+  constexpr int NB = (9 * CI / 4) * (CO / 4);  // 4 x 4 blocks of dW ([tap * CI + ci][co])
+  constexpr int PG = 256 / NB;                 // pixel groups: lane t = (pg, blk), q = pg, pg + PG, ...
   constexpr int TP = 64;
   __shared__ float sin_[TP][9 * CI];
   __shared__ float sg[TP][CO];
   const int t = threadIdx.x;
-  float acc[PER];
+  const int blk = t % NB, pg = t / NB;
+  const int rb = blk / (CO / 4), cb = blk % (CO / 4);
+  float acc[4][4];
 #pragma unroll
-  for (int k = 0; k < PER; ++k) acc[k] = 0.f;
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
   float bacc = 0.f;
   const long long npix = (long long)B * H * W;
   for (long long p0 = (long long)blockIdx.x * TP; p0 < npix; p0 += (long long)gridDim.x * TP) {
@@ -303,15 +309,17 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
       sg[q][co] = pix < npix ? dout[pix * CO + co] : 0.f;
     }
     __syncthreads();
-    {
-      const int co = t % CO, tg = t / CO;
-      for (int q = 0; q < TP; ++q) {
-        const float gq = sg[q][co];
+    if (t < NB * PG) {  // 4 x 4 register block: two ds_read_b128 feed sixteen FMAs
+      const float4* ar = reinterpret_cast<const float4*>(&sin_[0][4 * rb]);
+      const float4* gr = reinterpret_cast<const float4*>(&sg[0][4 * cb]);
+      for (int q = pg; q < TP; q += PG) {
+        const float4 a = ar[q * (9 * CI / 4)];
+        const float4 g = gr[q * (CO / 4)];
+        const float av[4] = {a.x, a.y, a.z, a.w}, gv[4] = {g.x, g.y, g.z, g.w};
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-          const int tc = tg + NG * k;  // tc = tap * CI + ci
-          if (tc < 9 * CI) acc[k] = fmaf(sin_[q][tc], gq, acc[k]);
-        }
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(av[r], gv[c], acc[r][c]);
       }
     }
     if (t < CO) {
@@ -320,12 +328,31 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
       bacc = s;
     }
   }
+  // the PG pixel-group partials of each block, summed in group order
+  __shared__ float red[PG > 1 ? NB * PG * 16 : 1];
   float* pp = part + (long long)blockIdx.x * (NW + CO);
+  if (PG > 1) {
+    __syncthreads();
+    if (t < NB * PG)
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int tc = t / CO + NG * k;
-    if (tc < 9 * CI) pp[tc * CO + t % CO] = acc[k];
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) red[(pg * NB + blk) * 16 + r * 4 + c] = acc[r][c];
+    __syncthreads();
+    if (t < NB) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        float v = red[blk * 16 + e];
+        for (int g = 1; g < PG; ++g) v += red[(g * NB + blk) * 16 + e];
+        acc[e >> 2][e & 3] = v;
+      }
+    }
   }
+  if (t < NB)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      *reinterpret_cast<float4*>(pp + (4 * rb + r) * CO + 4 * cb) =
+          make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
   if (t < CO) pp[NW + t] = bacc;
 }
 
