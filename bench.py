@@ -384,6 +384,11 @@ def main():
     import torch
 
     mode = "eager" if args.no_graph else args.exec
+    if mode == "auto" and world > 1:
+        # task shards run faster eager (profiles/r2c_shard_steps.txt: 25 / 13 / 7 tasks 4.83 / 3.21 /
+        # 2.38 ms eager vs 4.88 / 3.38 / 2.60 graph), where the per-layer all-reduce buckets on the
+        # collective stream overlap the rest of the backward; no RCCL collective is captured in a graph
+        mode = "eager"
     eng.enable_graph(mode != "eager")
     eng.update_many(args.warmup)
     eng.synchronize()

@@ -62,6 +62,9 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
 int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int K, int iters, double* ms_per_launch);
 /* Rows per gemm_x3s tile / 16 (TI, 4..8) the cost model picks for an M x N output, batch entries. */
 int mtsac_debug_x3s_ti(int M, int N, int batch);
+// DrQ conv channel groups per lane (fwd: output channels, bwd: input channels; 0 = the engine's
+// choice); returns the previous fwd | bwd << 8.  Experiments only.
+int mtsac_debug_drq_groups(int fwd, int bwd);
 
 /* Per-launch record of the last timed step (mtsac_set_timing): i < 0 returns the number of
  * records; else dims = {family = GEMM kind, M, N, K, batch} and *ms its duration. */

@@ -6,6 +6,7 @@
 
 #include "../../include/mtsac.h"
 #include "../../include/mtsac_debug.h"
+#include "drq_kernels.h"
 #include "kernels.h"
 
 using namespace mtsac;
@@ -344,5 +345,13 @@ int mtsac_debug_x3p_geo(int geo) {
 }
 
 int mtsac_debug_x3s_ti(int M, int N, int batch) { return gemm_x3s_ti(M, N, batch); }
+
+// DrQ conv channel groups per lane (0 = the engine's choice); returns the previous fwd | bwd << 8
+int mtsac_debug_drq_groups(int fwd, int bwd) {
+  const int old = drq::g_drq_fwd_g | (drq::g_drq_bwd_g << 8);
+  drq::g_drq_fwd_g = fwd;
+  drq::g_drq_bwd_g = bwd;
+  return old;
+}
 
 }  // extern "C"

@@ -968,15 +968,24 @@ bool conv_supported(int ci, int co) {
 }
 
 // channels per lane (measured, rocprofv3 per-kernel sums): the forward keeps every output channel
-// of a pixel in one lane (splitting re-reads the input patch per group); the data gradient splits
-// 16 input channels into groups of 4 (4x the waves for the same dout reads, 1.4x faster there)
-static int conv_fwd_group(int co) { return co; }
-static int conv_bwd_group(int ci) { return ci == 16 ? 4 : ci; }
+// of a pixel in one lane (splitting re-reads the input patch per group) while the launch has enough
+// waves to hide its latency; the data gradient splits 16 input channels into groups of 4 (4x the
+// waves for the same dout reads, 1.4x faster there).  g_drq_fwd_g / g_drq_bwd_g > 0 force a group
+// (experiments, mtsac_debug_drq_groups).
+int g_drq_fwd_g = 0, g_drq_bwd_g = 0;
+static int conv_fwd_group(int co, long long npix) {
+  if (g_drq_fwd_g > 0 && co % g_drq_fwd_g == 0) return g_drq_fwd_g;
+  return co;
+}
+static int conv_bwd_group(int ci) {
+  if (g_drq_bwd_g > 0 && ci % g_drq_bwd_g == 0) return g_drq_bwd_g;
+  return ci == 16 ? 4 : ci;
+}
 
 void conv_fwd(const float* in, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
               int ci, int co, bool relu_in, hipStream_t st) {
   const long long npix = (long long)B * H * W;
-  const int G = conv_fwd_group(co);
+  const int G = conv_fwd_group(co, npix);
   const dim3 g(blocks(npix), co / G), t(256);
 #define C_FWD_G(a, b, cg)                                                                                           \
   if (relu_in && res) hipLaunchKernelGGL((conv_fwd_kernel<a, b, cg, true, true>), g, t, 0, st, in, w, bias, res, out, B, H, W); \
@@ -986,6 +995,7 @@ void conv_fwd(const float* in, const float* w, const float* bias, const float* r
 #define C_FWD(a, b)                   \
   if (ci == a && co == b) {           \
     if (G == b) { C_FWD_G(a, b, b) }  \
+    else if (G == 8) { C_FWD_G(a, b, 8) } \
     else { C_FWD_G(a, b, 4) }         \
     return;                           \
   }
@@ -1007,6 +1017,7 @@ void conv_bwd_data(const float* dout, const float* w, const float* mask, const f
 #define C_BD(a, b)                   \
   if (ci == a && co == b) {          \
     if (G == a) { C_BD_G(a, b, a) }  \
+    else if (G == 8) { if constexpr (a >= 8) { C_BD_G(a, b, 8) } } \
     else { C_BD_G(a, b, 4) }         \
     return;                          \
   }

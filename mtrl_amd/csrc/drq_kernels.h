@@ -27,6 +27,7 @@ void atari_sample_rows(const unsigned char* store, const unsigned char* nstore, 
 void aug_draw(unsigned long long seed, unsigned long long ctr, int B, int pad, int* crop_o, float* noise_o,
               int* crop_n, float* noise_n, hipStream_t st);
 bool conv_supported(int ci, int co);
+extern int g_drq_fwd_g, g_drq_bwd_g;  // conv channel groups per lane, 0: the engine's choice (experiments)
 // 3x3 / stride 1 / SAME on NHWC, kernel [3][3][ci][co]; relu_in applies ReLU to the input, res
 // (nullable) is added to the output
 void conv_fwd(const float* in, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
