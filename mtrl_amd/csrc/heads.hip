@@ -157,34 +157,41 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyParams p) {
   policy_finish<HD>(p, b, t, acc, lane);
 }
 
-// Rows grouped by task (task_rows lists): a workgroup takes PH_ROWS rows of one task, PH_RW per
-// wave, so the task's head kernel is fetched (from L2) once per wave for PH_RW rows; no LDS, so
-// it co-resides with the trunk GEMMs running on other streams.
-constexpr int PH_RW = 4;               // rows per wave
-constexpr int PH_ROWS = 4 * PH_RW;     // rows per workgroup
-
-template <int HD>
+// Rows grouped by task (task_rows lists): a workgroup takes 4 RW rows of one task, RW per wave, so
+// the task's head kernel is fetched (from L2) once per wave for RW rows; no LDS, so it co-resides
+// with the trunk GEMMs running on other streams.  RW = 4 when that still gives a workgroup per CU;
+// small task shards take fewer rows per wave (more waves in flight; each row's sums are the same).
+template <int HD, int RW>
 __global__ __launch_bounds__(256) void policy_head_grouped_kernel(PolicyParams p) {
+  constexpr int ROWS = 4 * RW;  // rows per workgroup
   const HeadParams& hp = p.head;
   const int t = blockIdx.x;
   const int n = p.counts[t];
-  const int j0 = blockIdx.y * PH_ROWS;
+  const int j0 = blockIdx.y * ROWS;
   if (j0 >= n) return;  // uniform over the workgroup
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int* rl = p.rows + (long long)t * p.max_rows;
-  int row[PH_RW];
-  const float* hr[PH_RW];
+  int row[RW];
+  const float* hr[RW];
 #pragma unroll
-  for (int r = 0; r < PH_RW; ++r) {
-    const int jj = j0 + wave * PH_RW + r;
+  for (int r = 0; r < RW; ++r) {
+    const int jj = j0 + wave * RW + r;
     row[r] = rl[jj < n ? jj : j0];
     hr[r] = hp.h + (long long)row[r] * hp.W;
   }
-  float acc[PH_RW][HD];
-  rows_dot<HD, PH_RW>(hr, hp.Wh + (long long)t * hp.W * HD, hp.W, acc);
+  float acc[RW][HD];
+  rows_dot<HD, RW>(hr, hp.Wh + (long long)t * hp.W * HD, hp.W, acc);
 #pragma unroll
-  for (int r = 0; r < PH_RW; ++r)
-    if (j0 + wave * PH_RW + r < n) policy_finish<HD>(p, row[r], t, acc[r], lane);
+  for (int r = 0; r < RW; ++r)
+    if (j0 + wave * RW + r < n) policy_finish<HD>(p, row[r], t, acc[r], lane);
+}
+
+// rows per wave for a launch that would have wgs_at_rw1 workgroups at one row per wave: the largest
+// of 4, 2, 1 that still gives >= 256 workgroups (one per CU)
+static int rows_per_wave(long long wgs_at_rw1) {
+  for (int rw = 4; rw > 1; rw >>= 1)
+    if (wgs_at_rw1 / rw >= 256) return rw;
+  return 1;
 }
 
 // ------------------------------------------------------------------ critic heads + losses
@@ -467,11 +474,10 @@ __global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, con
 }
 
 // ------------------------------------------------------------------ critic -> action grad -> policy grad
-// AG_RW rows per wavefront: the critic layer-0 kernel rows (A x Wc) are read once per AG_RW rows.
-// Per row the sums run over the lane's w (16-B chunks 4l + 256i when Wc % 4 == 0, else l + 64i),
-// then over the wave.
-constexpr int AG_RW = 4;
-
+// AG_RW rows per wavefront: the critic layer-0 kernel rows (A x Wc) are read once per AG_RW rows
+// (4, or fewer on small task shards, see rows_per_wave).  Per row the sums run over the lane's w
+// (16-B chunks 4l + 256i when Wc % 4 == 0, else l + 64i), then over the wave.
+template <int AG_RW>
 __global__ __launch_bounds__(256) void action_grad_kernel(ActionGradParams p) {
   const int lane = threadIdx.x & 63;
   const int b0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * AG_RW;
@@ -567,15 +573,17 @@ __global__ __launch_bounds__(256) void row_alpha_kernel(const int* __restrict__ 
 void policy_head(const PolicyParams& p, hipStream_t st) {
   const int hd = p.head.hd;
   if (p.counts != nullptr) {
-    dim3 grid((unsigned)p.T_l, (unsigned)((p.max_count + PH_ROWS - 1) / PH_ROWS));
-    if (hd == 8)
-      hipLaunchKernelGGL(policy_head_grouped_kernel<8>, grid, dim3(256), 0, st, p);
-    else if (hd == 6)
-      hipLaunchKernelGGL(policy_head_grouped_kernel<6>, grid, dim3(256), 0, st, p);
-    else if (hd == 4)
-      hipLaunchKernelGGL(policy_head_grouped_kernel<4>, grid, dim3(256), 0, st, p);
-    else
-      hipLaunchKernelGGL(policy_head_grouped_kernel<2>, grid, dim3(256), 0, st, p);
+    const int rw = rows_per_wave((long long)p.T_l * ((p.max_count + 3) / 4));
+    dim3 grid((unsigned)p.T_l, (unsigned)((p.max_count + 4 * rw - 1) / (4 * rw)));
+#define PHG(HDV)                                                                                          \
+  if (rw == 4) hipLaunchKernelGGL((policy_head_grouped_kernel<HDV, 4>), grid, dim3(256), 0, st, p);        \
+  else if (rw == 2) hipLaunchKernelGGL((policy_head_grouped_kernel<HDV, 2>), grid, dim3(256), 0, st, p);   \
+  else hipLaunchKernelGGL((policy_head_grouped_kernel<HDV, 1>), grid, dim3(256), 0, st, p);
+    if (hd == 8) { PHG(8) }
+    else if (hd == 6) { PHG(6) }
+    else if (hd == 4) { PHG(4) }
+    else { PHG(2) }
+#undef PHG
     return;
   }
   dim3 grid((p.head.B + 3) / 4);
@@ -629,7 +637,11 @@ void head_backward_weight(const HeadParams& hp, const float* dout, long long s_d
 }
 
 void action_grad(const ActionGradParams& p, hipStream_t st) {
-  hipLaunchKernelGGL(action_grad_kernel, dim3((p.B + 4 * AG_RW - 1) / (4 * AG_RW)), dim3(256), 0, st, p);
+  const int rw = rows_per_wave((p.B + 3) / 4);
+  const dim3 grid((unsigned)((p.B + 4 * rw - 1) / (4 * rw)));
+  if (rw == 4) hipLaunchKernelGGL(action_grad_kernel<4>, grid, dim3(256), 0, st, p);
+  else if (rw == 2) hipLaunchKernelGGL(action_grad_kernel<2>, grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL(action_grad_kernel<1>, grid, dim3(256), 0, st, p);
 }
 
 void row_alpha(const int* task, int task_begin, const float* log_alpha, int T_glob, int B, int use_task_weights,
