@@ -317,9 +317,11 @@ struct mtsac_engine {
     if (gemm_x3f_ok(p, epi, batch)) {
       const bool split = gemm_x3f(p, epi, batch, cur) > 1;
       // the rocprof symbol: gemm_x3f_kernel<BM, EPI, C_OUT, P_OUT, MASK16, TAG, NP> (split-K launches
-      // run the raw-slab instance <208, 0, true, false, false, 0, NP> plus a finishing pass)
+      // run the raw-slab instance <208 or 128, 0, true, false, false, 0, NP> plus a finishing pass)
       const bool tagged = epi == EPI_BIAS_RELU && p.tag == 1 && p.Cp && !p.C;
-      fam_kernel[family] = split ? std::string("gemm_x3f_kernel<208, 0, true, false, false, 0, ") +
+      fam_kernel[family] = split ? std::string("gemm_x3f_kernel<") +
+                                       std::to_string(gemm_x3f_split_bm(p.M, p.N, p.K, batch)) +
+                                       ", 0, true, false, false, 0, " +
                                        (p.np == 1 ? "1" : "3") + "> + splitk_epilogue_kernel"
                                  : std::string("gemm_x3f_kernel<208, ") + std::to_string(epi) + ", " +
                                        (p.C ? "true" : "false") + ", " + (p.Cp ? "true" : "false") + ", " +

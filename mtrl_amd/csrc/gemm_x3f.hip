@@ -25,6 +25,7 @@
 //     output row leaves in whole lines (1 KB fp32, 512 B per bf16 plane); bias+ReLU or ReLU mask
 //     (fp32 or the bf16 high plane of the activation: h > 0 <=> h_hi > 0 for every normal h).
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "gemm_x3p_impl.h"
@@ -342,24 +343,46 @@ void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t s
 
 int gemm_x3f_row_tiles(int M) { return (M + x3fk::BM0 - 1) / x3fk::BM0; }
 
-// split-K slices for row counts whose tiles do not fill the chip (task shards): least
-// (rounds of tiles x S workgroups) / S, plus ~4 % of a round per extra slice (its partial slab
-// traffic and the finishing pass); >= 4 64-deep steps per slice
-int gemm_x3f_splits(int M, int N, int K, int batch) {
-  const long long tiles = (long long)gemm_x3f_tiles(M, N, batch);
-  if (tiles >= 192) return 1;
-  const int smax = std::min(8, std::max(1, K / x3fk::KS / 4));
-  int best = 1;
+namespace x3fk {
+constexpr int BMS = 128;  // the split-K row tile alternative for task shards (96 KB of LDS)
+
+struct SplitPlan {
+  int bm, s;
+};
+
+// Row tile and split-K slices for row counts whose 208-row tiles do not fill the chip (task shards):
+// least (rounds of tiles x S workgroups) x (row-tile work relative to 208 rows / its MFMA
+// efficiency) / S, plus ~4 % of a round per extra slice (its partial slab traffic and the finishing
+// pass); >= 4 64-deep steps per slice.  A 128-row tile wins where 208 rows leave a mostly empty last
+// tile (896 rows: 4 x 208 + 64 -> 7 x 128, 2 slices instead of 3).  MTSAC_X3F_SPLIT_BM=208|128 forces
+// the row tile (experiments).
+static SplitPlan split_plan(int M, int N, int K, int batch) {
+  if ((long long)gemm_x3f_tiles(M, N, batch) >= 192) return {BM0, 1};
+  static const int forced = [] {
+    const char* e = getenv("MTSAC_X3F_SPLIT_BM");
+    return e ? atoi(e) : 0;
+  }();
+  const int smax = std::min(8, std::max(1, K / KS / 4));
+  SplitPlan best{BM0, 1};
   double best_cost = 1e30;
-  for (int sp = 1; sp <= smax; ++sp) {
-    const double cost = (double)((tiles * sp + 255) / 256) / sp + 0.04 * (sp - 1);
-    if (cost < best_cost - 1e-9) {
-      best_cost = cost;
-      best = sp;
+  for (int bm : {BM0, BMS}) {
+    if (forced && bm != forced) continue;
+    const long long tiles = (long long)((M + bm - 1) / bm) * ((N + BN - 1) / BN) * batch;
+    const double work = bm == BM0 ? 1.0 : (double)bm / BM0 / 0.9;  // 128-row tiles: ~0.9 of the MFMA rate
+    for (int sp = 1; sp <= smax; ++sp) {
+      const double cost = (double)((tiles * sp + 255) / 256) * work / sp + 0.04 * (sp - 1);
+      if (cost < best_cost - 1e-9) {
+        best_cost = cost;
+        best = {bm, sp};
+      }
     }
   }
   return best;
 }
+}  // namespace x3fk
+
+int gemm_x3f_splits(int M, int N, int K, int batch) { return x3fk::split_plan(M, N, K, batch).s; }
+int gemm_x3f_split_bm(int M, int N, int K, int batch) { return x3fk::split_plan(M, N, K, batch).bm; }
 
 long long gemm_x3f_ws_floats(int M, int N, int K, int batch) {
   const int s = gemm_x3f_splits(M, N, K, batch);
@@ -379,10 +402,18 @@ static int x3f_slices(const SplitGemmParams& p, int epi, int batch) {
   return gemm_x3f_splits(p.M, p.N, p.K, batch);
 }
 
+// workgroups of the launch (all slices)
+static long long x3f_workgroups(const SplitGemmParams& p, int epi, int batch) {
+  const int S = x3f_slices(p, epi, batch);
+  if (S == 1) return gemm_x3f_tiles(p.M, p.N, batch);
+  const int bm = x3fk::split_plan(p.M, p.N, p.K, batch).bm;
+  return (long long)((p.M + bm - 1) / bm) * ((p.N + x3fk::BN - 1) / x3fk::BN) * batch * S;
+}
+
 bool gemm_x3f_ok(const SplitGemmParams& p, int epi, int batch) {
   return !p.a_kmajor && !p.b_kmajor && p.K % x3fk::KS == 0 && p.N % 8 == 0 && p.lda % 8 == 0 && p.ldb % 8 == 0 &&
          (!p.C || p.ldc % 4 == 0) && (!p.Cp || p.ldcp % 8 == 0) && (epi != EPI_RELU_MASK || p.ldm % 8 == 0) &&
-         (epi != EPI_STORE) && (long long)gemm_x3f_tiles(p.M, p.N, batch) * x3f_slices(p, epi, batch) >= 192 &&
+         (epi != EPI_STORE) && x3f_workgroups(p, epi, batch) >= 192 &&
          (p.C || p.Cp) && (long long)p.N * p.ldb * 2 < (1ll << 31);
 }
 
@@ -400,11 +431,18 @@ int gemm_x3f(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
     q.dbp = nullptr;
     const int S_eff = (p0.K + q.kchunk - 1) / q.kchunk;
     q.splits = S_eff;
-    const dim3 grid((unsigned)(gemm_x3f_tiles(p0.M, p0.N, batch) * S_eff));
-    if (p0.np == 1)
+    const int bm = split_plan(p0.M, p0.N, p0.K, batch).bm;
+    const dim3 grid((unsigned)(((p0.M + bm - 1) / bm) * ((p0.N + BN - 1) / BN) * batch * S_eff));
+    if (bm == BMS) {
+      if (p0.np == 1)
+        hipLaunchKernelGGL((gemm_x3f_kernel<BMS, EPI_STORE, true, false, false, 0, 1>), grid, dim3(512), 0, st, q);
+      else
+        hipLaunchKernelGGL((gemm_x3f_kernel<BMS, EPI_STORE, true, false, false, 0, 3>), grid, dim3(512), 0, st, q);
+    } else if (p0.np == 1) {
       hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_STORE, true, false, false, 0, 1>), grid, dim3(512), 0, st, q);
-    else
+    } else {
       hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_STORE, true, false, false, 0, 3>), grid, dim3(512), 0, st, q);
+    }
     SplitGemmParams f = p0;
     f.sC = p0.sC;
     splitk_finish(f, epi, S_eff, batch, st);

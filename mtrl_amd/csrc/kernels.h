@@ -95,6 +95,7 @@ int gemm_x3f_row_tiles(int M);  // row tiles of M (the dbp partials' chunk count
 // split-K for few rows: slices (1 = none) and workspace floats; gemm_x3f splits when the params
 // allow it (splits < 0, ws given, no dbp)
 int gemm_x3f_splits(int M, int N, int K, int batch);
+int gemm_x3f_split_bm(int M, int N, int K, int batch);  // row tile of the split-K launches (208 or 128)
 long long gemm_x3f_ws_floats(int M, int N, int K, int batch);
 void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t st);  // experiments
 // the same contract for small row counts (task shards, MT10): 16 TI x 64 tiles, 4 waves splitting
