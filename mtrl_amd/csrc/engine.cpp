@@ -1454,8 +1454,12 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     // Task shards of wide trunks (B = 768..1280 at W = 2048): gemm_x3f + split-K beats gemm_x3p +
     // split-K for the twin critic (E = 2: 64-80 row x column tiles, 8-20 % per launch,
     // tools/x3f_split_bench.py) but not for the actor (E = 1), which stays on gemm_x3p.
+    static const int x3f_min_tiles = [] {  // MTSAC_X3F_MIN_TILES: experiments
+      const char* v = getenv("MTSAC_X3F_MIN_TILES");
+      return v ? atoi(v) : 64;
+    }();
     net->x3f = e->planes && net->depth > 1 &&
-               ((net->ald % 64 == 0 && gemm_x3f_tiles(e->B, net->width, net->E) >= 64) ||
+               ((net->ald % 64 == 0 && gemm_x3f_tiles(e->B, net->width, net->E) >= x3f_min_tiles) ||
                 (net->ald <= 512 && e->B <= 2048));
     if (net->x3f) net->xld = align_up(net->in_dim, 64);  // gemm_x3f steps K by 64
     for (int w = 0; w < (net == &e->critic ? 2 : 1); ++w)
