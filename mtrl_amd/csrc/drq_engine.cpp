@@ -134,7 +134,8 @@ struct drq_engine {
 
   // ------------------------------------------------------------------ forward
   // ImpalaDQN at params P on augmented images X -> combined head output out[B][NC] (no bias);
-  // the saved activations of the backward are written in every pass (the s pass runs last)
+  // the saved activations of the backward are written in every pass (the s pass runs last; the
+  // activation buffers hold 2B rows: the update's online pass covers s and s' at once)
   void forward(const float* P, const float* X, float* out) { forward_rows(P, X, out, B); }
   void forward_rows(const float* P, const float* X, float* out, int B) {  // B: rows (<= the batch)
     const float* x = X;
@@ -339,11 +340,14 @@ struct drq_engine {
     const int C0 = cfg.in_ch;
     drq::augment(nobs_u8, crop_n, noise_n, nobs, B, C0, cfg.hw, cfg.hw, 4, st);
     drq::augment(obs_u8, crop_o, noise_o, stk[0].xin_own, B, C0, cfg.hw, cfg.hw, 4, st);
-    forward(p, nobs, hc_on);
+    // target at s' first; then ONE online pass over the 2B images [s | s'] (nobs = xin_own + B
+    // images; per-image arithmetic is independent of the batch), whose first B rows are the
+    // activations the backward reads and whose last B rows are the online head at s'
     forward(tgt, nobs, hc_tg);
-    drq::c51_target(hc_on, hc_tg, NC, p + off_bc, tgt + off_bc, A, Z, rew, done, gamma_n, cfg.v_min, cfg.v_max, m,
-                    a_next, B, st);
-    forward(p, stk[0].xin_own, hc);
+    (void)hipMemcpyAsync(task + B, task, sizeof(int) * B, hipMemcpyDeviceToDevice, st);
+    forward_rows(p, stk[0].xin_own, hc, 2 * B);
+    drq::c51_target(hc + (long long)B * NC, hc_tg, NC, p + off_bc, tgt + off_bc, A, Z, rew, done, gamma_n, cfg.v_min,
+                    cfg.v_max, m, a_next, B, st);
     drq::c51_loss(hc, NC, p + off_bc, A, Z, act, m, dhc, loss_b, logit_b, B, st);
     // ---- head backward
     wgrad_gemm(h2, H, dhc, NC, g + off_wc, g + off_bc, H, NC);
@@ -492,30 +496,39 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
   for (float** q : {&e->p, &e->g, &e->mu, &e->nu, &e->tgt})
     if ((rc = e->alloc(q, e->n_int))) return bad(rc);
   const long long img = (long long)B * c->in_ch * c->hw * c->hw;
-  if ((rc = e->alloc(&e->obs_u8, img)) || (rc = e->alloc(&e->nobs_u8, img)) || (rc = e->alloc(&e->nobs, img)))
-    return bad(rc);
-  for (int** q : {&e->act, &e->task, &e->a_next})
+  if ((rc = e->alloc(&e->obs_u8, img)) || (rc = e->alloc(&e->nobs_u8, img))) return bad(rc);
+  for (int** q : {&e->act, &e->a_next})
     if ((rc = e->alloc(q, B))) return bad(rc);
+  if ((rc = e->alloc(&e->task, 2 * B))) return bad(rc);  // [task | task]: the online pass over s and s'
   if ((rc = e->alloc(&e->crop_o, 2 * B)) || (rc = e->alloc(&e->crop_n, 2 * B))) return bad(rc);
-  for (float** q : {&e->rew, &e->done, &e->noise_o, &e->noise_n, &e->rstd1, &e->rstd2, &e->loss_b, &e->logit_b})
+  for (float** q : {&e->rew, &e->done, &e->noise_o, &e->noise_n, &e->loss_b, &e->logit_b})
     if ((rc = e->alloc(q, B))) return bad(rc);
+  const long long B2 = 2LL * B;  // rows of the forward buffers
+  for (float** q : {&e->rstd1, &e->rstd2})
+    if ((rc = e->alloc(q, B2))) return bad(rc);
   long long maxact = 0;
   for (int s = 0; s < 3; ++s) {
     Stack& k = e->stk[s];
     const long long big = (long long)B * k.hin * k.hin * k.co, sm = (long long)B * k.ho * k.ho * k.co;
     maxact = std::max({maxact, big, (long long)B * k.hin * k.hin * k.ci});
-    if ((rc = e->alloc(&k.conv0, big)) || (rc = e->alloc(&k.arg, sm))) return bad(rc);
+    if ((rc = e->alloc(&k.conv0, 2 * big)) || (rc = e->alloc(&k.arg, 2 * sm))) return bad(rc);
     for (float** q : {&k.c[0], &k.c[1], &k.c[2], &k.r[0], &k.r[1]})
-      if ((rc = e->alloc(q, sm))) return bad(rc);
+      if ((rc = e->alloc(q, 2 * sm))) return bad(rc);
   }
-  if ((rc = e->alloc(&e->stk[0].xin_own, img))) return bad(rc);
+  if ((rc = e->alloc(&e->stk[0].xin_own, 2 * img))) return bad(rc);  // [augmented obs | augmented next_obs]
+  e->nobs = e->stk[0].xin_own + img;
   for (float** q : {&e->ga, &e->gb, &e->gc})
     if ((rc = e->alloc(q, maxact))) return bad(rc);
-  for (float** q : {&e->feat, &e->xhat1, &e->ln1, &e->dln1, &e->dfeat})
+  for (float** q : {&e->feat, &e->xhat1, &e->ln1})
+    if ((rc = e->alloc(q, B2 * F))) return bad(rc);
+  for (float** q : {&e->dln1, &e->dfeat})
     if ((rc = e->alloc(q, (long long)B * F))) return bad(rc);
-  for (float** q : {&e->z1, &e->xhat2, &e->h2, &e->dh2, &e->dz1})
+  for (float** q : {&e->z1, &e->xhat2, &e->h2})
+    if ((rc = e->alloc(q, B2 * H))) return bad(rc);
+  for (float** q : {&e->dh2, &e->dz1})
     if ((rc = e->alloc(q, (long long)B * H))) return bad(rc);
-  for (float** q : {&e->hc, &e->hc_on, &e->hc_tg, &e->dhc})
+  if ((rc = e->alloc(&e->hc, B2 * NC))) return bad(rc);
+  for (float** q : {&e->hc_on, &e->hc_tg, &e->dhc})
     if ((rc = e->alloc(q, (long long)B * NC))) return bad(rc);
   if ((rc = e->alloc(&e->m, (long long)B * Z))) return bad(rc);
   long long wp = 0;
@@ -531,7 +544,9 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
                            gemm_ws_floats(B, H, 1, gemm_splits(B, H, F, 1)),
                            gemm_ws_floats(B, NC, 1, gemm_splits(B, NC, H, 1)),
                            gemm_ws_floats(B, H, 1, gemm_splits(B, H, NC, 1)),
-                           gemm_ws_floats(B, F, 1, gemm_splits(B, F, H, 1))});
+                           gemm_ws_floats(B, F, 1, gemm_splits(B, F, H, 1)),
+                           gemm_ws_floats(2 * B, H, 1, gemm_splits(2 * B, H, F, 1)),
+                           gemm_ws_floats(2 * B, NC, 1, gemm_splits(2 * B, NC, H, 1))});
   if ((rc = e->alloc(&e->ws, e->ws_floats))) return bad(rc);
   if ((rc = e->alloc(&e->part, 2 * 1024)) || (rc = e->alloc(&e->logs, DRQ_NUM_LOGS))) return bad(rc);
   if ((rc = e->alloc(&e->trunc, B))) return bad(rc);
