@@ -151,12 +151,20 @@ __global__ void aug_draw_kernel(unsigned long long seed, unsigned long long ctr,
 // packed FMAs (an LDS copy put a broadcast read in front of every four FMAs).  The per-output
 // summation order (taps, then input channels) does not depend on CG.
 template <int CI, int CO, int CG, bool RELU_IN, bool ADD_RES>
-__global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ in, const float* __restrict__ w,
-                                                       const float* __restrict__ bias, const float* __restrict__ res,
-                                                       float* __restrict__ out, int B, int H, int W) {
+__global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ in, const float* __restrict__ w_a,
+                                                       const float* __restrict__ bias_a,
+                                                       const float* __restrict__ w_b,
+                                                       const float* __restrict__ bias_b, const float* __restrict__ res,
+                                                       float* __restrict__ out, int B, int B1, int H, int W) {
+  // images [0, B1) use (w_a, bias_a), [B1, B) (w_b, bias_b): the blocks of the two ranges are
+  // separate, so the weights stay block-uniform (scalar loads)
   const int cg = blockIdx.y * CG;
-  const int pix = blockIdx.x * 256 + threadIdx.x;
-  if (pix >= B * H * W) return;
+  const int n1 = B1 * H * W, nb1 = (n1 + 255) / 256;
+  const bool second = (int)blockIdx.x >= nb1;
+  const int pix = second ? n1 + ((int)blockIdx.x - nb1) * 256 + (int)threadIdx.x : (int)blockIdx.x * 256 + (int)threadIdx.x;
+  if (pix >= (second ? B * H * W : n1)) return;
+  const float* __restrict__ w = second ? w_b : w_a;
+  const float* __restrict__ bias = second ? bias_b : bias_a;
   const int x = pix % W, y = (pix / W) % H;
   float acc[CG];
 #pragma unroll
@@ -983,15 +991,21 @@ static int conv_bwd_group(int ci) {
 }
 
 void conv_fwd(const float* in, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
-              int ci, int co, bool relu_in, hipStream_t st) {
+              int ci, int co, bool relu_in, hipStream_t st, const float* w2, const float* bias2, int B1) {
   const long long npix = (long long)B * H * W;
   const int G = conv_fwd_group(co, npix);
-  const dim3 g(blocks(npix), co / G), t(256);
+  if (w2 == nullptr || B1 < 0 || B1 > B) {  // one parameter set
+    w2 = w;
+    bias2 = bias;
+    B1 = B;
+  }
+  const long long n1 = (long long)B1 * H * W;
+  const dim3 g(blocks(n1) + blocks(npix - n1), co / G), t(256);
 #define C_FWD_G(a, b, cg)                                                                                           \
-  if (relu_in && res) hipLaunchKernelGGL((conv_fwd_kernel<a, b, cg, true, true>), g, t, 0, st, in, w, bias, res, out, B, H, W); \
-  else if (relu_in) hipLaunchKernelGGL((conv_fwd_kernel<a, b, cg, true, false>), g, t, 0, st, in, w, bias, res, out, B, H, W); \
-  else if (res) hipLaunchKernelGGL((conv_fwd_kernel<a, b, cg, false, true>), g, t, 0, st, in, w, bias, res, out, B, H, W); \
-  else hipLaunchKernelGGL((conv_fwd_kernel<a, b, cg, false, false>), g, t, 0, st, in, w, bias, res, out, B, H, W);
+  if (relu_in && res) hipLaunchKernelGGL((conv_fwd_kernel<a, b, cg, true, true>), g, t, 0, st, in, w, bias, w2, bias2, res, out, B, B1, H, W); \
+  else if (relu_in) hipLaunchKernelGGL((conv_fwd_kernel<a, b, cg, true, false>), g, t, 0, st, in, w, bias, w2, bias2, res, out, B, B1, H, W); \
+  else if (res) hipLaunchKernelGGL((conv_fwd_kernel<a, b, cg, false, true>), g, t, 0, st, in, w, bias, w2, bias2, res, out, B, B1, H, W); \
+  else hipLaunchKernelGGL((conv_fwd_kernel<a, b, cg, false, false>), g, t, 0, st, in, w, bias, w2, bias2, res, out, B, B1, H, W);
 #define C_FWD(a, b)                   \
   if (ci == a && co == b) {           \
     if (G == b) { C_FWD_G(a, b, b) }  \

@@ -134,28 +134,36 @@ struct drq_engine {
 
   // ------------------------------------------------------------------ forward
   // ImpalaDQN at params P on augmented images X -> combined head output out[B][NC] (no bias);
-  // the saved activations of the backward are written in every pass (the s pass runs last; the
-  // activation buffers hold 2B rows: the update's online pass covers s and s' at once)
-  void forward(const float* P, const float* X, float* out) { forward_rows(P, X, out, B); }
-  void forward_rows(const float* P, const float* X, float* out, int B) {  // B: rows (<= the batch)
+  // the saved activations of the backward are the first B rows of the pass (the activation buffers
+  // hold 3B rows: the update's pass covers online s, online s' and target s' at once)
+  // rows: B (<= 3 x the batch, see the buffers); P2 (nullable): rows [B1, B) run at params P2
+  void forward_rows(const float* P, const float* X, float* out, int B, const float* P2 = nullptr, int B1 = -1) {
+    if (P2 == nullptr) B1 = B;
+    const float* Q2 = P2 ? P2 : P;
     const float* x = X;
     for (int s = 0; s < 3; ++s) {
       Stack& k = stk[s];
-      conv_fwd_t(x, P + k.cw[0], P + k.cb[0], nullptr, k.conv0, B, k.hin, k.hin, k.ci, k.co, false);
+      conv_fwd_t(x, P, Q2, k.cw[0], k.cb[0], nullptr, k.conv0, B, B1, k.hin, k.ci, k.co, false);
       drq::maxpool_fwd(k.conv0, k.c[0], k.arg, B, k.hin, k.hin, k.co, st);
       for (int b = 0; b < cfg_blocks(); ++b) {
-        conv_fwd_t(k.c[b], P + k.cw[1 + 2 * b], P + k.cb[1 + 2 * b], nullptr, k.r[b], B, k.ho, k.ho, k.co, k.co,
-                   true);
-        conv_fwd_t(k.r[b], P + k.cw[2 + 2 * b], P + k.cb[2 + 2 * b], k.c[b], k.c[b + 1], B, k.ho, k.ho, k.co, k.co,
-                   true);
+        conv_fwd_t(k.c[b], P, Q2, k.cw[1 + 2 * b], k.cb[1 + 2 * b], nullptr, k.r[b], B, B1, k.ho, k.co, k.co, true);
+        conv_fwd_t(k.r[b], P, Q2, k.cw[2 + 2 * b], k.cb[2 + 2 * b], k.c[b], k.c[b + 1], B, B1, k.ho, k.co, k.co, true);
       }
       x = k.c[2];
     }
-    drq::concat_feat(stk[2].c[2], NENC, P + off_emb, D, task, feat, F, B, st);
-    drq::ln_fwd(feat, nullptr, F, F, P + off_ln1s, P + off_ln1b, cfg.ln_eps, ln1, F, xhat1, rstd1, B, false, st);
-    gemm_store(ln1, F, P + off_w0, H, z1, H, B, H, F, GEMM_NN);
-    drq::ln_fwd(z1, P + off_b0, H, H, P + off_ln2s, P + off_ln2b, cfg.ln_eps, h2, H, xhat2, rstd2, B, true, st);
-    gemm_store(h2, H, P + off_wc, NC, out, NC, B, NC, H, GEMM_NN);
+    head_rows(P, 0, B1, out);
+    if (B1 < B) head_rows(Q2, B1, B - B1, out);
+  }
+  // the dense head of rows [r0, r0 + n) at params P
+  void head_rows(const float* P, int r0, int n, float* out) {
+    const long long r = r0;
+    drq::concat_feat(stk[2].c[2] + r * NENC, NENC, P + off_emb, D, task + r0, feat + r * F, F, n, st);
+    drq::ln_fwd(feat + r * F, nullptr, F, F, P + off_ln1s, P + off_ln1b, cfg.ln_eps, ln1 + r * F, F, xhat1 + r * F,
+                rstd1 + r, n, false, st);
+    gemm_store(ln1 + r * F, F, P + off_w0, H, z1 + r * H, H, n, H, F, GEMM_NN);
+    drq::ln_fwd(z1 + r * H, P + off_b0, H, H, P + off_ln2s, P + off_ln2b, cfg.ln_eps, h2 + r * H, H, xhat2 + r * H,
+                rstd2 + r, n, true, st);
+    gemm_store(h2 + r * H, H, P + off_wc, NC, out + r * NC, NC, n, NC, H, GEMM_NN);
   }
   int cfg_blocks() const { return 2; }
 
@@ -167,8 +175,10 @@ struct drq_engine {
   size_t ev_used = 0;
   double t_flops = 0;
   long long t_launches = 0;
-  void conv_fwd_t(const float* in, const float* w, const float* bias, const float* res, float* out, int Bn, int Hh,
-                  int Ww, int ci, int co, bool relu_in) {
+  // conv (weights at offset cw, bias at cb) of images [0, B1) at params P and [B1, Bn) at P2
+  void conv_fwd_t(const float* in, const float* P, const float* P2, long long cw, long long cb, const float* res,
+                  float* out, int Bn, int B1, int Hh, int ci, int co, bool relu_in) {
+    const int Ww = Hh;
     hipEvent_t a = nullptr, b = nullptr;
     if (timing && count % 8 == 0) {
       while (ev.size() < ev_used + 2) {
@@ -183,7 +193,7 @@ struct drq_engine {
         (void)hipEventRecord(a, st);
       }
     }
-    drq::conv_fwd(in, w, bias, res, out, Bn, Hh, Ww, ci, co, relu_in, st);
+    drq::conv_fwd(in, P + cw, P + cb, res, out, Bn, Hh, Ww, ci, co, relu_in, st, P2 + cw, P2 + cb, B1);
     if (a) {
       (void)hipEventRecord(b, st);
       t_flops += 2.0 * Bn * Hh * Ww * 9.0 * ci * co;
@@ -340,14 +350,17 @@ struct drq_engine {
     const int C0 = cfg.in_ch;
     drq::augment(nobs_u8, crop_n, noise_n, nobs, B, C0, cfg.hw, cfg.hw, 4, st);
     drq::augment(obs_u8, crop_o, noise_o, stk[0].xin_own, B, C0, cfg.hw, cfg.hw, 4, st);
-    // target at s' first; then ONE online pass over the 2B images [s | s'] (nobs = xin_own + B
-    // images; per-image arithmetic is independent of the batch), whose first B rows are the
-    // activations the backward reads and whose last B rows are the online head at s'
-    forward(tgt, nobs, hc_tg);
+    // ONE pass over the 3B images [s | s' | s'] (nobs = xin_own + B images): online params for
+    // the first 2B, target params for the last B (per-image arithmetic does not depend on the
+    // batch).  Its first B rows are the activations the backward reads; head rows [B, 2B) are the
+    // online head at s', [2B, 3B) the target's.
+    const size_t img_bytes = sizeof(float) * (size_t)B * C0 * cfg.hw * cfg.hw;
+    (void)hipMemcpyAsync(nobs + (size_t)B * C0 * cfg.hw * cfg.hw, nobs, img_bytes, hipMemcpyDeviceToDevice, st);
     (void)hipMemcpyAsync(task + B, task, sizeof(int) * B, hipMemcpyDeviceToDevice, st);
-    forward_rows(p, stk[0].xin_own, hc, 2 * B);
-    drq::c51_target(hc + (long long)B * NC, hc_tg, NC, p + off_bc, tgt + off_bc, A, Z, rew, done, gamma_n, cfg.v_min,
-                    cfg.v_max, m, a_next, B, st);
+    (void)hipMemcpyAsync(task + 2 * B, task, sizeof(int) * B, hipMemcpyDeviceToDevice, st);
+    forward_rows(p, stk[0].xin_own, hc, 3 * B, tgt, 2 * B);
+    drq::c51_target(hc + (long long)B * NC, hc + 2LL * B * NC, NC, p + off_bc, tgt + off_bc, A, Z, rew, done, gamma_n,
+                    cfg.v_min, cfg.v_max, m, a_next, B, st);
     drq::c51_loss(hc, NC, p + off_bc, A, Z, act, m, dhc, loss_b, logit_b, B, st);
     // ---- head backward
     wgrad_gemm(h2, H, dhc, NC, g + off_wc, g + off_bc, H, NC);
@@ -499,11 +512,11 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
   if ((rc = e->alloc(&e->obs_u8, img)) || (rc = e->alloc(&e->nobs_u8, img))) return bad(rc);
   for (int** q : {&e->act, &e->a_next})
     if ((rc = e->alloc(q, B))) return bad(rc);
-  if ((rc = e->alloc(&e->task, 2 * B))) return bad(rc);  // [task | task]: the online pass over s and s'
+  if ((rc = e->alloc(&e->task, 3 * B))) return bad(rc);  // [task | task | task]: the pass over s, s', s'
   if ((rc = e->alloc(&e->crop_o, 2 * B)) || (rc = e->alloc(&e->crop_n, 2 * B))) return bad(rc);
   for (float** q : {&e->rew, &e->done, &e->noise_o, &e->noise_n, &e->loss_b, &e->logit_b})
     if ((rc = e->alloc(q, B))) return bad(rc);
-  const long long B2 = 2LL * B;  // rows of the forward buffers
+  const long long B2 = 3LL * B;  // rows of the forward buffers (online s, online s', target s')
   for (float** q : {&e->rstd1, &e->rstd2})
     if ((rc = e->alloc(q, B2))) return bad(rc);
   long long maxact = 0;
@@ -511,11 +524,11 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
     Stack& k = e->stk[s];
     const long long big = (long long)B * k.hin * k.hin * k.co, sm = (long long)B * k.ho * k.ho * k.co;
     maxact = std::max({maxact, big, (long long)B * k.hin * k.hin * k.ci});
-    if ((rc = e->alloc(&k.conv0, 2 * big)) || (rc = e->alloc(&k.arg, 2 * sm))) return bad(rc);
+    if ((rc = e->alloc(&k.conv0, 3 * big)) || (rc = e->alloc(&k.arg, 3 * sm))) return bad(rc);
     for (float** q : {&k.c[0], &k.c[1], &k.c[2], &k.r[0], &k.r[1]})
-      if ((rc = e->alloc(q, 2 * sm))) return bad(rc);
+      if ((rc = e->alloc(q, 3 * sm))) return bad(rc);
   }
-  if ((rc = e->alloc(&e->stk[0].xin_own, 2 * img))) return bad(rc);  // [augmented obs | augmented next_obs]
+  if ((rc = e->alloc(&e->stk[0].xin_own, 3 * img))) return bad(rc);  // augmented [obs | next_obs | next_obs]
   e->nobs = e->stk[0].xin_own + img;
   for (float** q : {&e->ga, &e->gb, &e->gc})
     if ((rc = e->alloc(q, maxact))) return bad(rc);

@@ -29,9 +29,11 @@ void aug_draw(unsigned long long seed, unsigned long long ctr, int B, int pad, i
 bool conv_supported(int ci, int co);
 extern int g_drq_fwd_g, g_drq_bwd_g;  // conv channel groups per lane, 0: the engine's choice (experiments)
 // 3x3 / stride 1 / SAME on NHWC, kernel [3][3][ci][co]; relu_in applies ReLU to the input, res
-// (nullable) is added to the output
+// (nullable) is added to the output.  w2 / bias2 (nullable): images [B1, B) use that second
+// parameter set (one launch over the online and the target passes)
 void conv_fwd(const float* in, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
-              int ci, int co, bool relu_in, hipStream_t st);
+              int ci, int co, bool relu_in, hipStream_t st, const float* w2 = nullptr, const float* bias2 = nullptr,
+              int B1 = -1);
 // din = conv^T(dout) * [mask > 0] (mask nullable) + dres (nullable)
 void conv_bwd_data(const float* dout, const float* w, const float* mask, const float* dres, float* din, int B, int H,
                    int W, int ci, int co, hipStream_t st);
