@@ -286,21 +286,24 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
   float bacc = 0.f;
-  const long long npix = (long long)B * H * W;
-  for (long long p0 = (long long)blockIdx.x * TP; p0 < npix; p0 += (long long)gridDim.x * TP) {
+  // 32-bit pixel indexing (B H W < 2^31, checked at drq_create): the tap's input pixel is
+  // pix + dy W + dx inside the image, so only x and y need a division
+  const int npix = B * H * W;
+  for (int p0 = blockIdx.x * TP; p0 < npix; p0 += gridDim.x * TP) {
     __syncthreads();
     for (int pr = t; pr < TP * 9; pr += 256) {
       const int q = pr / 9, tap = pr - 9 * q;
-      const long long pix = p0 + q;
+      const int pix = p0 + q;
       float v[CI];
 #pragma unroll
       for (int ci = 0; ci < CI; ++ci) v[ci] = 0.f;
       if (pix < npix) {
-        const int x = (int)(pix % W), y = (int)((pix / W) % H);
-        const long long b = pix / ((long long)H * W);
-        const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+        const int r = pix / W;
+        const int x = pix - r * W, y = r % H;
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        const int yy = y + dy, xx = x + dx;
         if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
-          const float* ip = in + ((b * H + yy) * W + xx) * CI;
+          const float* ip = in + (long long)(pix + dy * W + dx) * CI;
 #pragma unroll
           for (int c4 = 0; c4 < CI; c4 += 4) {
             const float4 u = *reinterpret_cast<const float4*>(ip + c4);
@@ -313,8 +316,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
     }
     for (int pr = t; pr < TP * CO; pr += 256) {
       const int q = pr / CO, co = pr - CO * q;
-      const long long pix = p0 + q;
-      sg[q][co] = pix < npix ? dout[pix * CO + co] : 0.f;
+      const int pix = p0 + q;
+      sg[q][co] = pix < npix ? dout[(long long)pix * CO + co] : 0.f;
     }
     __syncthreads();
     if (t < NB * PG) {  // 4 x 4 register block: two ds_read_b128 feed sixteen FMAs

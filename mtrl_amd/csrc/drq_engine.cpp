@@ -412,7 +412,8 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
   if (c->num_tasks < 1 || c->n_actions < 1 || c->n_atoms < 2 || c->n_atoms > 64 || c->batch < 1 || c->hw < 4 ||
       c->scale < 1 || c->embed_dim < 1 || c->embed_dim > 64 || c->n_hidden < 4)
     return fail(-22, "bad drq_config");
-  if ((long long)c->batch * c->hw * c->hw * 16 * c->scale >= (1LL << 31))  // 32-bit indices in the pool kernels
+  // 32-bit indices in the conv / pool kernels, over the update's 3B-image forward pass
+  if (3LL * c->batch * c->hw * c->hw * 16 * c->scale >= (1LL << 31))
     return fail(-22, "batch x hw x hw x channels must stay below 2^31");
   if (hipSetDevice(device) != hipSuccess) return fail(-19, "hipSetDevice failed");
   drq_engine* e = new drq_engine();
