@@ -36,15 +36,16 @@ __device__ inline float wmax(float v) {
 __global__ void augment_kernel(const unsigned char* __restrict__ obs, const int* __restrict__ crop,
                                const float* __restrict__ noise, float* __restrict__ out, int B, int C, int H, int W,
                                int pad) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long n = (long long)B * H * W * C;
-  if (i >= n) return;
-  const int c = (int)(i % C);
-  long long r = i / C;
-  const int x = (int)(r % W);
-  r /= W;
-  const int y = (int)(r % H);
-  const int b = (int)(r / H);
+  // 32-bit indexing: B H W C < 2^31 (checked at drq_create)
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * H * W * C) return;
+  int r = i / C;
+  const int c = i - r * C;
+  int r2 = r / W;
+  const int x = r - r2 * W;
+  r = r2 / H;
+  const int y = r2 - r * H;
+  const int b = r;
   const int sy = min(max(y + crop[2 * b] - pad, 0), H - 1);
   const int sx = min(max(x + crop[2 * b + 1] - pad, 0), W - 1);
   const float v = (float)obs[(((long long)b * C + c) * H + sy) * W + sx];
@@ -266,8 +267,8 @@ __global__ __launch_bounds__(256) void conv_bwd_data_kernel(const float* __restr
 // tile's im2col rows (act applied, zero outside the image) and dout go through LDS; lane t owns a
 // 4 x 4 block of dW ([tap * CI + ci][co]) over the pixels q = pg, pg + PG, ... of every tile (PG
 // lane groups when the blocks leave lanes over), the groups' partials summed in group order at
-// the end; lanes t < CO own the bias entries.  part[g][9 CI CO + CO], summed over g in order by
-// sum_parts_kernel.
+// the end; the bias entries are summed by 256 / CO lane groups over interleaved pixels, the groups
+// added in order at the end.  part[g][9 CI CO + CO], summed over g in order by sum_parts_kernel.
 template <int CI, int CO, bool RELU_IN>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict__ in, const float* __restrict__ dout,
                                                          float* __restrict__ part, int B, int H, int W) {
@@ -277,8 +278,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
   constexpr int TP = 64;
   __shared__ float sin_[TP][9 * CI];
   __shared__ float sg[TP][CO];
+  constexpr int BG = 256 / CO;  // bias lane groups
+  static_assert(256 % CO == 0, "bias groups");
   const int t = threadIdx.x;
   const int blk = t % NB, pg = t / NB;
+  const int bco = t % CO, bg = t / CO;
   const int rb = blk / (CO / 4), cb = blk % (CO / 4);
   float acc[4][4];
 #pragma unroll
@@ -333,9 +337,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
           for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(av[r], gv[c], acc[r][c]);
       }
     }
-    if (t < CO) {
+    {  // bias: lane group bg sums pixels q = bg, bg + BG, ... of channel bco (all lanes busy)
       float s = bacc;
-      for (int q = 0; q < TP; ++q) s += sg[q][t];
+      for (int q = bg; q < TP; q += BG) s += sg[q][bco];
       bacc = s;
     }
   }
@@ -364,7 +368,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
     for (int r = 0; r < 4; ++r)
       *reinterpret_cast<float4*>(pp + (4 * rb + r) * CO + 4 * cb) =
           make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
-  if (t < CO) pp[NW + t] = bacc;
+  // the bias groups' partials, summed in group order
+  __shared__ float bred[256];
+  __syncthreads();
+  bred[t] = bacc;
+  __syncthreads();
+  if (t < CO) {
+    float v = bred[t];
+    for (int g = 1; g < BG; ++g) v += bred[g * CO + t];
+    pp[NW + t] = v;
+  }
 }
 
 // dw[e] / db[e - nw] = sum_g part[g][e] (e < n): block of 16 entries x 16 lane groups over g
