@@ -382,11 +382,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
 
 // dw[e] / db[e - nw] = sum_g part[g][e] (e < n): block of 16 entries x 16 lane groups over g
 // (g = group + 16 j, 8 loads in flight), double accumulation, the groups added in order
-__global__ __launch_bounds__(256) void sum_parts_kernel(const float* __restrict__ part, int G, int n,
-                                                        float* __restrict__ dst_w, float* __restrict__ dst_b, int nw) {
+__device__ inline void sum_parts_block(const float* __restrict__ part, int G, int n, float* __restrict__ dst_w,
+                                       float* __restrict__ dst_b, int nw, int bx) {
   __shared__ double red[16][16];
   const int el = threadIdx.x & 15, grp = threadIdx.x >> 4;
-  const int e = blockIdx.x * 16 + el;
+  const int e = bx * 16 + el;
   double s = 0.0;
   if (e < n) {
     int g = grp;
@@ -407,6 +407,19 @@ __global__ __launch_bounds__(256) void sum_parts_kernel(const float* __restrict_
     if (e < nw) dst_w[e] = (float)t;
     else dst_b[e - nw] = (float)t;
   }
+}
+
+__global__ __launch_bounds__(256) void sum_parts_kernel(const float* __restrict__ part, int G, int n,
+                                                        float* __restrict__ dst_w, float* __restrict__ dst_b, int nw) {
+  sum_parts_block(part, G, n, dst_w, dst_b, nw, blockIdx.x);
+}
+
+// every conv's partials of one backward in one launch: block ranges per segment (blk0 ascending)
+__global__ __launch_bounds__(256) void sum_parts_multi_kernel(const SumSeg* __restrict__ segs, int nseg) {
+  int k = 0;
+  while (k + 1 < nseg && (int)blockIdx.x >= segs[k + 1].blk0) ++k;
+  const SumSeg sg = segs[k];
+  sum_parts_block(sg.part, sg.G, sg.n, sg.dw, sg.db, sg.nw, (int)blockIdx.x - sg.blk0);
 }
 
 // ------------------------------------------------------------------ max pool 3x3 / 2 / SAME
@@ -1061,7 +1074,7 @@ void conv_bwd_data(const float* dout, const float* w, const float* mask, const f
 int conv_wgrad_blocks(long long npix) { return (int)std::min<long long>(2048, std::max<long long>(1, (npix + 63) / 64)); }
 
 void conv_wgrad(const float* in, const float* dout, float* part, float* dw, float* db, int B, int H, int W, int ci,
-                int co, bool relu_in, hipStream_t st) {
+                int co, bool relu_in, hipStream_t st, bool defer_sum) {
   const int G = conv_wgrad_blocks((long long)B * H * W);
 #define C_WG(a, b)                                                                                             \
   if (ci == a && co == b) {                                                                                    \
@@ -1070,8 +1083,15 @@ void conv_wgrad(const float* in, const float* dout, float* part, float* dw, floa
   }
   CONV_CASES(C_WG)
 #undef C_WG
+  if (defer_sum) return;  // summed with the other convs' partials by sum_parts_multi
   const int nw = 9 * ci * co, n = nw + co;
   hipLaunchKernelGGL(sum_parts_kernel, dim3((n + 15) / 16), dim3(256), 0, st, part, G, n, dw, db, nw);
+}
+
+int sum_parts_blocks(int ci, int co) { return (9 * ci * co + co + 15) / 16; }
+
+void sum_parts_multi(const SumSeg* segs, int nseg, int blocks, hipStream_t st) {
+  hipLaunchKernelGGL(sum_parts_multi_kernel, dim3(blocks), dim3(256), 0, st, segs, nseg);
 }
 
 void maxpool_fwd(const float* in, float* out, unsigned char* arg, int B, int H, int W, int C, hipStream_t st) {

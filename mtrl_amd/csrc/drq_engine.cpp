@@ -75,7 +75,10 @@ struct drq_engine {
   // backward
   float *dhc = nullptr, *dh2 = nullptr, *dz1 = nullptr, *dln1 = nullptr, *dfeat = nullptr;
   float *ga = nullptr, *gb = nullptr, *gc = nullptr;  // conv activation grads (largest tensor)
-  float *wpart = nullptr, *ws = nullptr, *part = nullptr, *loss_b = nullptr, *logit_b = nullptr, *logs = nullptr;
+  float* wparts[3][5] = {};  // per conv (stack, conv index): its weight-grad partials
+  drq::SumSeg* d_segs = nullptr;
+  int seg_blocks = 0;
+  float *ws = nullptr, *part = nullptr, *loss_b = nullptr, *logit_b = nullptr, *logs = nullptr;
   long long ws_floats = 0;
   std::vector<void*> allocs;
   // ---- device replay buffer (MemoryEfficientAtariMultiTaskReplayBuffer)
@@ -379,17 +382,19 @@ struct drq_engine {
       Stack& k = stk[s];
       for (int b = 1; b >= 0; --b) {  // c[b + 1] = conv_k2(relu(r[b])) + c[b], r[b] = conv_k1(relu(c[b]))
         const int k2 = 2 + 2 * b, k1 = 1 + 2 * b;
-        drq::conv_wgrad(k.r[b], dc, wpart, g + k.cw[k2], g + k.cb[k2], B, k.ho, k.ho, k.co, k.co, true, st);
+        drq::conv_wgrad(k.r[b], dc, wparts[s][k2], g + k.cw[k2], g + k.cb[k2], B, k.ho, k.ho, k.co, k.co, true, st, true);
         drq::conv_bwd_data(dc, p + k.cw[k2], k.r[b], nullptr, dr, B, k.ho, k.ho, k.co, k.co, st);
-        drq::conv_wgrad(k.c[b], dr, wpart, g + k.cw[k1], g + k.cb[k1], B, k.ho, k.ho, k.co, k.co, true, st);
+        drq::conv_wgrad(k.c[b], dr, wparts[s][k1], g + k.cw[k1], g + k.cb[k1], B, k.ho, k.ho, k.co, k.co, true, st, true);
         drq::conv_bwd_data(dr, p + k.cw[k1], k.c[b], dc, dn, B, k.ho, k.ho, k.co, k.co, st);
         std::swap(dc, dn);
       }
       drq::maxpool_bwd(dc, k.arg, dn, B, k.hin, k.hin, k.co, st);  // dn: grad wrt conv0's output
       const float* xin = s == 0 ? stk[0].xin_own : stk[s - 1].c[2];
-      drq::conv_wgrad(xin, dn, wpart, g + k.cw[0], g + k.cb[0], B, k.hin, k.hin, k.ci, k.co, false, st);
+      drq::conv_wgrad(xin, dn, wparts[s][0], g + k.cw[0], g + k.cb[0], B, k.hin, k.hin, k.ci, k.co, false, st, true);
       if (s > 0) drq::conv_bwd_data(dn, p + k.cw[0], nullptr, nullptr, dc, B, k.hin, k.hin, k.ci, k.co, st);
     }
+    // every conv's weight / bias gradient from its partials, one launch (the segment table)
+    drq::sum_parts_multi(d_segs, 15, seg_blocks, st);
   }
 };
 
@@ -545,14 +550,33 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
   for (float** q : {&e->hc_on, &e->hc_tg, &e->dhc})
     if ((rc = e->alloc(q, (long long)B * NC))) return bad(rc);
   if ((rc = e->alloc(&e->m, (long long)B * Z))) return bad(rc);
-  long long wp = 0;
-  for (int s = 0; s < 3; ++s) {
-    const Stack& k = e->stk[s];
-    const long long np = drq::conv_wgrad_blocks((long long)B * k.hin * k.hin);
-    wp = std::max(wp, np * (9LL * k.co * k.co + k.co));
-    wp = std::max(wp, np * (9LL * k.ci * k.co + k.co));
+  {  // per-conv partial regions and the segment table of the one partial-sum launch
+    std::vector<drq::SumSeg> segs;
+    long long total = 0;
+    for (int s = 0; s < 3; ++s)
+      for (int j = 0; j < 5; ++j) {
+        const Stack& k = e->stk[s];
+        const int hh = j == 0 ? k.hin : k.ho, ci = j == 0 ? k.ci : k.co;
+        total += (long long)drq::conv_wgrad_blocks((long long)B * hh * hh) * (9LL * ci * k.co + k.co);
+      }
+    float* all = nullptr;
+    if ((rc = e->alloc(&all, total))) return bad(rc);
+    int blk = 0;
+    for (int s = 0; s < 3; ++s)
+      for (int j = 0; j < 5; ++j) {
+        const Stack& k = e->stk[s];
+        const int hh = j == 0 ? k.hin : k.ho, ci = j == 0 ? k.ci : k.co;
+        const int G = drq::conv_wgrad_blocks((long long)B * hh * hh), n = 9 * ci * k.co + k.co;
+        e->wparts[s][j] = all;
+        segs.push_back({all, e->g + k.cw[j], e->g + k.cb[j], G, n, 9 * ci * k.co, blk});
+        blk += drq::sum_parts_blocks(ci, k.co);
+        all += (long long)G * n;
+      }
+    e->seg_blocks = blk;
+    if ((rc = e->alloc(&e->d_segs, (long long)segs.size())) ||
+        hipMemcpy(e->d_segs, segs.data(), sizeof(drq::SumSeg) * segs.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return bad(rc ? rc : fail(-5, "segment table upload"));
   }
-  if ((rc = e->alloc(&e->wpart, wp))) return bad(rc);
   e->ws_floats = std::max({gemm_ws_floats(H, NC, 1, gemm_splits(H, NC, B, 1)),
                            gemm_ws_floats(F, H, 1, gemm_splits(F, H, B, 1)),
                            gemm_ws_floats(B, H, 1, gemm_splits(B, H, F, 1)),

@@ -40,8 +40,17 @@ void conv_bwd_data(const float* dout, const float* w, const float* mask, const f
 int conv_wgrad_blocks(long long npix);
 // dw [3][3][ci][co], db [co] of a conv whose input is act(in); part: conv_wgrad_blocks(B H W) x
 // (9 ci co + co) floats
+// defer_sum: leave the partials for one sum_parts_multi launch over every conv of the backward
 void conv_wgrad(const float* in, const float* dout, float* part, float* dw, float* db, int B, int H, int W, int ci,
-                int co, bool relu_in, hipStream_t st);
+                int co, bool relu_in, hipStream_t st, bool defer_sum = false);
+// one conv's partial sums: part[G][n] -> dw[0, nw), db[0, n - nw); blocks [blk0, blk0 + sum_parts_blocks)
+struct SumSeg {
+  const float* part;
+  float *dw, *db;
+  int G, n, nw, blk0;
+};
+int sum_parts_blocks(int ci, int co);
+void sum_parts_multi(const SumSeg* segs, int nseg, int blocks, hipStream_t st);
 // max pool 3x3 / stride 2 / SAME (out (H + 1) / 2), argmax tap per output
 void maxpool_fwd(const float* in, float* out, unsigned char* arg, int B, int H, int W, int C, hipStream_t st);
 void maxpool_bwd(const float* dout, const unsigned char* arg, float* din, int B, int H, int W, int C, hipStream_t st);
