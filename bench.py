@@ -378,7 +378,7 @@ def main():
     if world > 1:
         uid = [MTSACEngine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        eng.comm_init(uid[0], world, rank)
+        eng.comm_init(uid[0], world, rank, timeout_s=600.0)  # a rank that never joins ends the run
         nranks = eng.comm_nranks()
 
     import torch

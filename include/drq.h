@@ -83,6 +83,8 @@ long long drq_num_params(const drq_engine* e);
 int drq_set_params(drq_engine* e, int which, const float* flat, long long n);
 int drq_get_params(drq_engine* e, int which, float* flat, long long n);
 int drq_set_step(drq_engine* e, int adam_count);
+/* the AdamW step count (optax ScaleByAdamState.count): bias correction of the next update */
+int drq_get_step(drq_engine* e, int* adam_count);
 /* stage one batch and run one update on it (asynchronous on the engine's stream) */
 int drq_update(drq_engine* e, const drq_batch* batch);
 /* run `steps` more updates on the batch already resident on the device (benchmarks), each with

@@ -9,7 +9,7 @@
  *                                  (device state instead of a flax PyTree)
  *   mtsac_set_params/get_params    TrainState params / opt_state leaves
  *                                  mtrl/rl/algorithms/utils.py:11-46, mtsac.py:197-256
- *   mtsac_buffer_add               MultiTaskReplayBuffer.add        mtrl/rl/buffers.py:426-474
+ *   mtsac_buffer_add[_stream]      MultiTaskReplayBuffer.add        mtrl/rl/buffers.py:426-474
  *   mtsac_buffer_write             MultiTaskReplayBuffer.load_checkpoint data  buffers.py:326-335
  *   mtsac_buffer_read              MultiTaskReplayBuffer.checkpoint data       buffers.py:308-324
  *   mtsac_buffer_set/get_state     pos / full fields                buffers.py:306,337-343
@@ -106,7 +106,8 @@ typedef struct mtsac_config {
   int64_t capacity;         /* slots per task = buffer_size // T               */
   float gamma, tau;
   float actor_lr, critic_lr, alpha_lr;
-  float actor_max_grad_norm, critic_max_grad_norm, alpha_max_grad_norm; /* <=0: no clip */
+  float actor_max_grad_norm, critic_max_grad_norm, alpha_max_grad_norm; /* < 0 (None): no
+                               clip; >= 0: optax clip_by_global_norm, 0 included (config/optim.py:38) */
   float adam_b1, adam_b2, adam_eps;
   float initial_temperature;
   float log_std_min, log_std_max;
@@ -150,11 +151,15 @@ int mtsac_get_adam_count(mtsac_engine* h, int which, int32_t* count);
  * buffer_add (buffers.py:426-474) does not block the host: the T_local rows are staged through
  * a pinned ring and written + committed on the engine stream, ordered after every update issued
  * before it and before every update issued after it.  Pass the five arrays all in host memory
- * or all in device memory; device arrays are read after the work already queued on the legacy
- * default stream (torch's default stream).  Reward min / max (normalize_rewards) are kept on
- * the device. */
+ * or all in device memory.  Device arrays are read after the work already queued on the
+ * producer stream (mtsac_buffer_add: the legacy default stream; mtsac_buffer_add_stream: the
+ * hipStream_t passed as producer_stream, e.g. torch.cuda.current_stream().cuda_stream), and
+ * the producer stream is made to wait for that read, so the caller may free or overwrite the
+ * arrays right after the call.  Reward min / max (normalize_rewards) are kept on the device. */
 int mtsac_buffer_add(mtsac_engine* h, const float* obs, const float* next_obs, const float* actions,
                      const float* rewards, const float* dones);
+int mtsac_buffer_add_stream(mtsac_engine* h, const float* obs, const float* next_obs, const float* actions,
+                            const float* rewards, const float* dones, void* producer_stream);
 int mtsac_buffer_write(mtsac_engine* h, int64_t slot_begin, int64_t n_slots, const float* obs,
                        const float* next_obs, const float* actions, const float* rewards,
                        const float* dones);
@@ -191,7 +196,12 @@ int mtsac_sample_action(mtsac_engine* h, const float* obs, int32_t n, const floa
 /* multi-GPU: RCCL communicator over the shared-trunk gradients */
 int mtsac_comm_unique_id_size(void);
 int mtsac_comm_get_unique_id(void* id_out);
+/* mtsac_comm_init waits for every peer (MTSAC_COMM_INIT_TIMEOUT_S in the environment bounds the
+ * wait); mtsac_comm_init_timeout returns -110 (ETIMEDOUT) when the peers have not joined within
+ * timeout_s seconds (<= 0: wait forever) and leaves the engine without a communicator. */
 int mtsac_comm_init(mtsac_engine* h, const void* unique_id, int32_t nranks, int32_t rank);
+int mtsac_comm_init_timeout(mtsac_engine* h, const void* unique_id, int32_t nranks, int32_t rank,
+                            double timeout_s);
 /* device noise stream (used when no eps is injected): seed and step counter; setting them
  * rebuilds the step graph (checkpoint / resume of the update noise) */
 int mtsac_get_noise_state(mtsac_engine* h, uint64_t* seed, uint64_t* counter);
@@ -200,8 +210,10 @@ int mtsac_set_noise_state(mtsac_engine* h, uint64_t seed, uint64_t counter);
 int mtsac_comm_nranks(mtsac_engine* h, int32_t* nranks);
 /* Bring-your-own collective: when no RCCL communicator is set, the engine calls
  * fn(user, device_buffer, count) at each all-reduce point (after synchronising its
- * stream); fn must leave the element-wise SUM over all shards in the buffer before
- * returning.  Disables hipGraph replay for this engine.  fn == NULL removes it. */
+ * stream), at the same points and in the same order as the RCCL path: one bucket per hidden
+ * layer as its weight gradient completes, then layer 0 and the scalar tail; fn must leave the
+ * element-wise SUM over all shards in the buffer (completed on the device) before returning.
+ * Disables hipGraph replay for this engine.  fn == NULL removes it. */
 typedef int (*mtsac_allreduce_fn)(void* user, float* device_buffer, int64_t count);
 int mtsac_set_allreduce_hook(mtsac_engine* h, mtsac_allreduce_fn fn, void* user);
 /* plain device/host copy helper for hooks written in a host language (hipMemcpyDefault) */

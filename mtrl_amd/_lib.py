@@ -108,6 +108,7 @@ SIGNATURES = {
     "mtsac_set_adam_count": (ctypes.c_int, [P, ctypes.c_int, I32]),
     "mtsac_get_adam_count": (ctypes.c_int, [P, ctypes.c_int, PI32]),
     "mtsac_buffer_add": (ctypes.c_int, [P, P, P, P, P, P]),
+    "mtsac_buffer_add_stream": (ctypes.c_int, [P, P, P, P, P, P, P]),
     "mtsac_buffer_write": (ctypes.c_int, [P, I64, I64, P, P, P, P, P]),
     "mtsac_buffer_read": (ctypes.c_int, [P, I64, I64, P, P, P, P, P]),
     "mtsac_buffer_fill_synthetic": (ctypes.c_int, [P, U64]),
@@ -128,6 +129,7 @@ SIGNATURES = {
     "mtsac_comm_unique_id_size": (ctypes.c_int, []),
     "mtsac_comm_get_unique_id": (ctypes.c_int, [P]),
     "mtsac_comm_init": (ctypes.c_int, [P, P, I32, I32]),
+    "mtsac_comm_init_timeout": (ctypes.c_int, [P, P, I32, I32, ctypes.c_double]),
     "mtsac_comm_nranks": (ctypes.c_int, [P, P]),
     "mtsac_get_noise_state": (ctypes.c_int, [P, P, P]),
     "mtsac_set_noise_state": (ctypes.c_int, [P, ctypes.c_uint64, ctypes.c_uint64]),
@@ -184,6 +186,7 @@ SIGNATURES.update({
     "drq_set_params": (ctypes.c_int, [P, ctypes.c_int, P, I64]),
     "drq_get_params": (ctypes.c_int, [P, ctypes.c_int, P, I64]),
     "drq_set_step": (ctypes.c_int, [P, ctypes.c_int]),
+    "drq_get_step": (ctypes.c_int, [P, P]),
     "drq_update": (ctypes.c_int, [P, ctypes.POINTER(DrqBatch)]),
     "drq_update_resident": (ctypes.c_int, [P, ctypes.c_int]),
     "drq_get_logs": (ctypes.c_int, [P, P]),

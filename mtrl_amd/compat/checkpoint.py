@@ -45,7 +45,7 @@ def opt_prefix(max_grad_norm) -> tuple[str, ...]:
     ``optax.chain(clip_by_global_norm, adam)`` when max_grad_norm is set -> (EmptyState,
     (ScaleByAdamState, EmptyState)) -> ``1/0``; plain ``adam`` (the temperature optimizer,
     max_grad_norm=None, mtsac.py:120) -> (ScaleByAdamState, EmptyState) -> ``0``."""
-    return ("1", "0") if max_grad_norm else ("0",)
+    return ("1", "0") if max_grad_norm is not None else ("0",)
 
 
 def _leaf_path(name: str) -> tuple[str, str]:

@@ -42,6 +42,23 @@ class DrQConfig(AlgorithmConfig):  # drqeps.py:98-109
     num_tasks: int = 26
 
 
+def _adam_settings(opt) -> tuple[float, float]:
+    """(eps, weight_decay) of OptimizerConfig.spawn (config/optim.py:26-43) for the engine's
+    AdamW kernel: eps defaults to 1e-5 for Adam and to optax's 1e-8 for AdamW; weight decay
+    applies to AdamW only (optax.adamw's default 1e-4 when unset) -- Adam is AdamW with decay 0.
+    Anything the kernel does not implement (a clip_by_global_norm link, RMSProp, SGD) raises."""
+    from ...config.utils import Optimizer
+
+    if opt.max_grad_norm is not None:
+        raise NotImplementedError("DrQ engine: clip_by_global_norm (max_grad_norm) is not implemented")
+    if opt.optimizer == Optimizer.Adam:
+        return (opt.eps if opt.eps is not None else 1e-5), 0.0
+    if opt.optimizer == Optimizer.AdamW:
+        return (opt.eps if opt.eps is not None else 1e-8), (opt.weight_decay if opt.weight_decay is not None
+                                                             else 1e-4)
+    raise NotImplementedError(f"DrQ engine: optimizer {opt.optimizer} is not implemented (Adam / AdamW only)")
+
+
 class DrQ:
     def __init__(self, engine: DrQEngine, config: DrQConfig, seed: int, batch: int):
         self.engine = engine
@@ -56,11 +73,11 @@ class DrQ:
         n_actions = int(getattr(env_config, "action_space").n)
         enc = config.critic_config.impala_config
         opt = config.critic_config.q_function_config.network_config.optimizer
+        eps, weight_decay = _adam_settings(opt)
         s = DrQSettings(num_tasks=config.num_tasks, n_actions=n_actions, n_atoms=config.n_atoms, in_ch=obs_shape[0],
                         hw=obs_shape[1], scale=enc.scale, embed_dim=config.critic_config.task_embed_config.embed_dim,
                         batch=batch_size, nstep=nstep, gamma=config.gamma, v_min=config.v_min, v_max=config.v_max,
-                        tau=config.tau, lr=opt.lr, eps=opt.eps if opt.eps is not None else 1e-8,
-                        weight_decay=opt.weight_decay if opt.weight_decay is not None else 1e-4)
+                        tau=config.tau, lr=opt.lr, eps=eps, weight_decay=weight_decay)
         eng = DrQEngine(s)
         p = init_drq(seed, num_tasks=config.num_tasks, n_actions=n_actions, n_atoms=config.n_atoms,
                      in_ch=obs_shape[0], hw=obs_shape[1], scale=enc.scale,
@@ -79,10 +96,12 @@ class DrQ:
         s = dataclasses.replace(self.engine.s, capacity=cap, normalize_rewards=int(config.normalize_rewards),
                                 nstep=getattr(config, "nstep", self.engine.s.nstep))
         state = {w: self.engine.get_params(w) for w in (L.DRQ_PARAMS, L.DRQ_TARGET, L.DRQ_ADAM_MU, L.DRQ_ADAM_NU)}
+        count = self.engine.get_step()  # Adam bias correction continues where it was
         self.engine.close()
         self.engine = DrQEngine(s)
         for w, v in state.items():
             self.engine.set_params(w, v)
+        self.engine.set_step(count)
         self.engine.seed_rng(seed)
         self.engine.seed_augment(int(self.rng.integers(0, 2**63)))
         return DeviceAtariReplayBuffer(self.engine)

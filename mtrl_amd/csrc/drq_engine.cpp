@@ -684,6 +684,12 @@ int drq_set_step(drq_engine* e, int adam_count) {
   return 0;
 }
 
+int drq_get_step(drq_engine* e, int* adam_count) {
+  if (!e || !adam_count) return fail(-22, "null argument");
+  *adam_count = e->count;
+  return 0;
+}
+
 int drq_update(drq_engine* e, const drq_batch* b) {
   if (!e || !b) return fail(-22, "null argument");
   const int B = e->B;

@@ -17,10 +17,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mtsac.h"
@@ -672,6 +674,10 @@ struct mtsac_engine {
   void allreduce(float* buf, size_t count) {
     if (comm != nullptr) {
       ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm, cur);
+      while (r == ncclInProgress) {  // non-blocking communicator: the enqueue completes asynchronously
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+        if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) break;
+      }
       if (r != ncclSuccess) comm_error = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
       return;
     }
@@ -828,7 +834,7 @@ struct mtsac_engine {
   int backward_segs(Net& net, const float* params, const float* X, int ldx, float** acts, __bf16** actp, float** dz,
                     __bf16** dzp, int d_top, int w_prev, int M) {
     int dprev = d_top, wprev = w_prev, rprev = -1;
-    const bool bucket = comm != nullptr && net.depth > 1;
+    const bool bucket = (comm != nullptr || hook != nullptr) && net.depth > 1;
     for (int i = net.depth - 1; i >= 0; --i) {
       wprev = seg({dprev, wprev}, 3, [&, i] { wgrad_layer(net, X, ldx, acts, actp, dz, dzp, i, M); });
       if (bucket && i > 0) {
@@ -845,7 +851,7 @@ struct mtsac_engine {
   // the trunk-gradient all-reduce left after backward_segs: everything, or (buckets) layer 0 and
   // the scalar tail
   void reduce_rest(Net& net) {
-    if (comm != nullptr && net.depth > 1) {
+    if ((comm != nullptr || hook != nullptr) && net.depth > 1) {
       allreduce(net.g + net.trunk_off, (size_t)(net.off_b[1] - net.trunk_off));
       allreduce(net.g + net.n_flat, (size_t)EXTRA);
     } else {
@@ -1348,7 +1354,7 @@ void mtsac_default_config(mtsac_config* c, int32_t T) {
   c->actor_lr = c->critic_lr = c->alpha_lr = 3e-4f;
   c->actor_max_grad_norm = 1.0f;
   c->critic_max_grad_norm = 1.0f;
-  c->alpha_max_grad_norm = 0.0f;
+  c->alpha_max_grad_norm = -1.0f;  // None: no clip (mtsac.py:120)
   c->adam_b1 = 0.9f;
   c->adam_b2 = 0.999f;
   c->adam_eps = 1e-5f;
@@ -1740,6 +1746,11 @@ static int write_slots(mtsac_engine* h, int64_t s0, int64_t ns, const float* obs
 // reward min / max on the device.
 int mtsac_buffer_add(mtsac_engine* h, const float* obs, const float* next_obs, const float* actions,
                      const float* rewards, const float* dones) {
+  return mtsac_buffer_add_stream(h, obs, next_obs, actions, rewards, dones, nullptr);
+}
+
+int mtsac_buffer_add_stream(mtsac_engine* h, const float* obs, const float* next_obs, const float* actions,
+                            const float* rewards, const float* dones, void* producer_stream) {
   if (!h || !obs || !next_obs || !actions || !rewards || !dones) return fail(-22, "null argument");
   const int T = h->T_l, D = h->D, A = h->A, R = h->R;
   const int ndev = (int)on_device(obs) + (int)on_device(next_obs) + (int)on_device(actions) +
@@ -1747,10 +1758,17 @@ int mtsac_buffer_add(mtsac_engine* h, const float* obs, const float* next_obs, c
   if (ndev != 0 && ndev != 5) return fail(-22, "buffer_add: pass all five arrays in host memory or all in device memory");
   float* slot = h->store + (size_t)h->h_pos * T * R;
   if (ndev == 5) {
-    // the producer is assumed on the legacy default stream (torch's default): order after it
-    HIP_TRY(hipEventRecord(h->add_ev, nullptr));
+    // Device arrays: the pack reads them after the producer's queued work, and the producer
+    // stream waits for the pack before anything it issues next (a caching allocator hands a
+    // freed block to the next allocation on that stream), so the caller may drop or overwrite
+    // the arrays as soon as this returns.
+    hipStream_t prod = static_cast<hipStream_t>(producer_stream);
+    HIP_TRY(hipEventRecord(h->add_ev, prod));
     HIP_TRY(hipStreamWaitEvent(h->st, h->add_ev, 0));
     buffer_pack_slot(slot, T, R, D, A, obs, next_obs, actions, rewards, dones, h->st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->add_ev, h->st));
+    HIP_TRY(hipStreamWaitEvent(prod, h->add_ev, 0));
   } else {
     const int k = h->stage_next;
     h->stage_next = (k + 1) % mtsac_engine::NSTAGE;
@@ -2164,14 +2182,48 @@ int mtsac_comm_get_unique_id(void* id_out) {
   return 0;
 }
 int mtsac_comm_init(mtsac_engine* h, const void* unique_id, int32_t nranks, int32_t rank) {
+  const char* v = getenv("MTSAC_COMM_INIT_TIMEOUT_S");
+  return mtsac_comm_init_timeout(h, unique_id, nranks, rank, v ? atof(v) : 0.0);
+}
+
+// The communicator is created non-blocking (ncclConfig_t.blocking = 0) so that a peer that never
+// joins (a dead rank, a wrong unique id) ends in an error after timeout_s instead of a hang:
+// ncclCommInitRankConfig returns at once and the init is polled through ncclCommGetAsyncError;
+// on timeout the half-built communicator is aborted.  Collectives on it may then return
+// ncclInProgress while their connections are set up; allreduce() waits those out.
+int mtsac_comm_init_timeout(mtsac_engine* h, const void* unique_id, int32_t nranks, int32_t rank, double timeout_s) {
   if (!h || !unique_id) return fail(-22, "null argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(-22, "bad rank / nranks");
   if (h->comm) return fail(-16, "communicator already initialised");
   ncclUniqueId id;
   std::memcpy(&id, unique_id, sizeof(id));
   HIP_TRY(hipSetDevice(h->device));
-  ncclResult_t r = ncclCommInitRank(&h->comm, nranks, id, rank);
-  if (r != ncclSuccess) return fail(-5, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
+  config.blocking = 0;
+  ncclComm_t comm = nullptr;
+  ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, id, rank, &config);
+  if (r != ncclSuccess && r != ncclInProgress)
+    return fail(-5, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    ncclResult_t a = ncclInProgress;
+    r = ncclCommGetAsyncError(comm, &a);
+    if (r != ncclSuccess) a = r;
+    if (a == ncclSuccess) break;
+    if (a != ncclInProgress) {
+      (void)ncclCommAbort(comm);
+      return fail(-5, std::string("ncclCommInitRank (rank ") + std::to_string(rank) + " of " +
+                          std::to_string(nranks) + "): " + ncclGetErrorString(a));
+    }
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (timeout_s > 0 && dt > timeout_s) {
+      (void)ncclCommAbort(comm);
+      return fail(-110, "ncclCommInitRank (rank " + std::to_string(rank) + " of " + std::to_string(nranks) +
+                            "): peers did not join within " + std::to_string(timeout_s) + " s");
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+  h->comm = comm;
   h->nranks = nranks;
   h->rank = rank;
   if (h->gexec) {
@@ -2231,6 +2283,9 @@ int mtsac_set_allreduce_hook(mtsac_engine* h, mtsac_allreduce_fn fn, void* user)
 int mtsac_memcpy(void* dst, const void* src, int64_t bytes) {
   if (!dst || !src || bytes < 0) return fail(-22, "bad copy arguments");
   HIP_TRY(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDefault));
+  // a pageable-host -> device copy may still be in flight when hipMemcpy returns; the engine's
+  // streams are non-blocking, so finish it before a hook hands the buffer back
+  HIP_TRY(hipStreamSynchronize(nullptr));
   return 0;
 }
 

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restri
 template <bool POLYAK>
 __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm, long long norm_from4) {
   const OptScalars sc = *a.sc;
-  const bool clip = (max_norm > 0.f) && !(sc.gnorm < max_norm);
+  const bool clip = (max_norm >= 0.f) && !(sc.gnorm < max_norm);
   const float gn = sc.gnorm;
   const float bc1 = 1.0f - powf(a.b1, (float)sc.count);
   const float bc2 = 1.0f - powf(a.b2, (float)sc.count);
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void adam_tiles_kernel(AdamParams a, TileParam
   __shared__ float sp[64][65];
   __shared__ float stg[POLYAK ? 64 : 1][65];
   const OptScalars sc = *a.sc;
-  const bool clip = (max_norm > 0.f) && !(sc.gnorm < max_norm);
+  const bool clip = (max_norm >= 0.f) && !(sc.gnorm < max_norm);
   const float gn = sc.gnorm;
   const float bc1 = 1.0f - powf(a.b1, (float)sc.count);
   const float bc2 = 1.0f - powf(a.b2, (float)sc.count);
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(64) void alpha_adam_kernel(AlphaParams a, float lr,
   float sq = 0.f;
   for (int i = lane; i < a.T_glob; i += 64) sq += a.grad[i] * a.grad[i];
   const float gn = sqrtf(wsumf(sq));
-  const bool clip = (max_norm > 0.f) && !(gn < max_norm);
+  const bool clip = (max_norm >= 0.f) && !(gn < max_norm);
   const int count = a.sc->count + 1;
   const float bc1 = 1.0f - powf(b1, (float)count), bc2 = 1.0f - powf(b2, (float)count);
   float es = 0.f;

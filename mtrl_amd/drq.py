@@ -127,6 +127,11 @@ class DrQEngine:
     def set_step(self, count: int):
         _drq_check(self.lib.drq_set_step(self.h, int(count)))
 
+    def get_step(self) -> int:
+        c = ctypes.c_int()
+        _drq_check(self.lib.drq_get_step(self.h, ctypes.byref(c)))
+        return c.value
+
     @staticmethod
     def _batch_arrays(batch, aug):
         obs, act, nobs, done, rew, task = batch

@@ -5,7 +5,7 @@ level -- DistributionalDense_0 (Dense_0, Dense_1 = advantage, Dense_2 = value, L
 ImpalaEncoder_0 (stack_s / Conv_0..Conv_4, kernel [3][3][Cin][Cout]), LayerNorm_0,
 TaskEmbedding_0/Embed_0/embedding.  Initialisers as the reference's modules: xavier_uniform for
 each stack's first conv and the head's Dense layers (impala.py:17, networks.py:109), flax's
-lecun_normal for the residual convs, zero biases, LayerNorm scale 1, Embed variance_scaling(1,
+lecun_normal (truncated normal) for the residual convs, zero biases, LayerNorm scale 1, Embed variance_scaling(1,
 fan_in, normal).  DrQ.initialize's shrink-and-perturb (drqeps.py:182-197): encoder leaves are the
 mean of two independent draws, everything else the second draw.  The numpy stream replaces JAX's
 threefry (not reproducible)."""
@@ -38,6 +38,19 @@ def param_spec(num_tasks=26, n_actions=18, n_atoms=51, in_ch=4, hw=84, scale=1, 
              ("TaskEmbedding_0/Embed_0/embedding", (num_tasks, embed_dim))])
 
 
+def truncated_lecun_normal(rng: np.random.Generator, shape, fan_in: int) -> np.ndarray:
+    """flax's default kernel init lecun_normal = jax variance_scaling(1, "fan_in",
+    "truncated_normal"): a standard normal truncated to [-2, 2], scaled by
+    sqrt(1 / fan_in) / 0.87962566103423978 (the std of that truncated normal), so the leaf has
+    variance 1 / fan_in.  Rejection sampling on the numpy stream (threefry is not reproduced)."""
+    z = rng.standard_normal(shape)
+    bad = np.abs(z) > 2.0
+    while bad.any():
+        z[bad] = rng.standard_normal(int(bad.sum()))
+        bad = np.abs(z) > 2.0
+    return z * (math.sqrt(1.0 / fan_in) / 0.87962566103423978)
+
+
 def _draw(spec, rng):
     out = []
     for path, shape in spec:
@@ -49,7 +62,7 @@ def _draw(spec, rng):
         elif leaf == "embedding":
             v = rng.normal(0.0, 1.0 / math.sqrt(shape[1]), shape)
         elif "/Conv_" in path and not path.endswith("Conv_0/kernel"):
-            v = rng.normal(0.0, 1.0 / math.sqrt(shape[0] * shape[1] * shape[2]), shape)
+            v = truncated_lecun_normal(rng, shape, shape[0] * shape[1] * shape[2])
         else:
             fi, fo = ((shape[0] * shape[1] * shape[2], shape[0] * shape[1] * shape[3]) if len(shape) == 4 else shape)
             lim = math.sqrt(6.0 / (fi + fo))

@@ -42,7 +42,7 @@ def make_config(**kw) -> Config:
     c = default_config(int(kw["num_tasks"]))
     for k, v in kw.items():
         if k == "actor_max_grad_norm" or k == "critic_max_grad_norm" or k == "alpha_max_grad_norm":
-            v = 0.0 if v is None else v
+            v = -1.0 if v is None else v  # None: no clip_by_global_norm in the chain
         setattr(c, k, v)
     return c
 
@@ -100,8 +100,16 @@ class MTSACEngine:
 
     # ------------------------------------------------------------------ replay buffer
     def buffer_add(self, obs, next_obs, actions, rewards, dones) -> None:
+        """Non-blocking add.  Device (torch) tensors are read in the order of torch's current
+        stream, which then waits for the read (mtsac_buffer_add_stream): they may be reused or
+        freed as soon as this returns."""
         args = [_ptr(x) for x in (obs, next_obs, actions, rewards, dones)]
-        check(self.lib.mtsac_buffer_add(self._h, *[a[0] for a in args]))
+        stream = None
+        if getattr(obs, "is_cuda", False):
+            import torch
+
+            stream = torch.cuda.current_stream(obs.device).cuda_stream
+        check(self.lib.mtsac_buffer_add_stream(self._h, *[a[0] for a in args], stream))
 
     def buffer_write(self, slot_begin: int, obs, next_obs, actions, rewards, dones) -> None:
         n = int(np.asarray(rewards).size) // self.T_l  # slots (rows are slot-major, T_l per slot)
@@ -267,9 +275,11 @@ class MTSACEngine:
         check(lib.mtsac_comm_get_unique_id(buf))
         return buf.raw
 
-    def comm_init(self, unique_id: bytes, nranks: int, rank: int) -> None:
+    def comm_init(self, unique_id: bytes, nranks: int, rank: int, timeout_s: float = 0.0) -> None:
+        """Join the RCCL communicator; timeout_s > 0 raises MTSACError (-110) when the peers have
+        not all joined by then (include/mtsac.h, mtsac_comm_init_timeout)."""
         buf = ctypes.create_string_buffer(bytes(unique_id), len(unique_id))
-        check(self.lib.mtsac_comm_init(self._h, buf, nranks, rank))
+        check(self.lib.mtsac_comm_init_timeout(self._h, buf, nranks, rank, float(timeout_s)))
 
     def noise_state(self) -> tuple[int, int]:
         s, c = ctypes.c_uint64(), ctypes.c_uint64()

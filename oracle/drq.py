@@ -125,8 +125,11 @@ def initialize(cfg: DrQConfig, seed: int = 0) -> np.ndarray:
         elif leaf == "embedding":
             v = rng.normal(0.0, 1.0 / math.sqrt(shape[1]), shape)
         elif "Conv_" in path and not path.endswith("Conv_0/kernel"):  # residual convs: lecun_normal
-            fan_in = shape[0] * shape[1] * shape[2]
-            v = rng.normal(0.0, 1.0 / math.sqrt(fan_in), shape)  # truncated in flax; plain normal here
+            z = rng.standard_normal(shape)  # flax lecun_normal: truncated to [-2, 2], rescaled
+            while (np.abs(z) > 2.0).any():
+                bad = np.abs(z) > 2.0
+                z[bad] = rng.standard_normal(int(bad.sum()))
+            v = z / math.sqrt(shape[0] * shape[1] * shape[2]) / 0.87962566103423978
         else:  # xavier_uniform
             if len(shape) == 4:
                 fan_in, fan_out = shape[0] * shape[1] * shape[2], shape[0] * shape[1] * shape[3]
@@ -219,6 +222,105 @@ def c51_target(logits_next_online, logits_next_target, rewards, dones, cfg: DrQC
     return m, a_next
 
 
+def _ln_abs_back(a_dy, x, scale, eps):
+    """Magnitude rule of the LayerNorm backward: dx = r (g - mean g - xh mean(g xh)), g = dy s,
+    so |terms| propagate as r (|g| + mean|g| + |xh| mean(|g| |xh|))."""
+    mu = x.mean(-1, keepdim=True)
+    r = torch.rsqrt(torch.clamp((x * x).mean(-1, keepdim=True) - mu * mu, min=0.0) + eps)
+    xh = ((x - mu) * r).abs()
+    g = a_dy * scale.abs()
+    return r * (g + g.mean(-1, keepdim=True) + xh * (g * xh).mean(-1, keepdim=True))
+
+
+def conv_error_floors(cfg: DrQConfig, params: np.ndarray, x, task_ids, actions, m) -> dict:
+    """Per conv leaf, the floor an fp32 evaluation of each gradient entry is measured against
+    (test infrastructure for the DrQ parity bound).
+
+    A kernel gradient entry sums x_in[b, h+kh-1, w+kw-1, ci] * dy[b, h, w, co] over images and
+    pixels; both factors carry the fp32 rounding of the step that produced them, and the entries
+    of dy that come out of heavy cancellation carry more error than |dy| suggests.  So the floor
+    is the same correlation of the two one-level magnitudes: A(x_in) = |x| for the image,
+    conv(|x_prev|, |W|) + |b| for a conv output (window max through the pool, |a| + |b| through
+    the residual add), and A(dy) = the |terms| of the step producing dy from the exact upstream
+    gradient -- conv-transpose of |dy_next| with |W| under the real ReLU masks, |dc| added through
+    the residual, the pool's scatter of |dc|, and the LayerNorm magnitude rule at the encoder
+    output.  Deeper rounding is not magnitude-propagated (that bound grows like (sum |W|)^depth);
+    a plain GEMM reduces to the tests' sum |a b| bar.  float64 torch, autograd for the exact
+    upstream gradients."""
+    P = unflatten(torch.as_tensor(params, dtype=torch.float64).clone().requires_grad_(True), cfg)
+    B = x.shape[0]
+    keep, cs = {}, {}  # conv name -> (input, A(input), output); block outputs c
+    with torch.enable_grad():
+        h, ah = x, x.abs()
+        for si in range(len(cfg.stacks)):
+            g = lambda k, leaf: P[f"ImpalaEncoder_0/stack_{si}/Conv_{k}/{leaf}"]
+
+            def conv(xin, axin, k):
+                y = _conv(xin, g(k, "kernel"), g(k, "bias"))
+                y.retain_grad()
+                with torch.no_grad():
+                    ay = _conv(xin.detach().abs(), g(k, "kernel").abs(), g(k, "bias").abs())
+                keep[f"ImpalaEncoder_0/stack_{si}/Conv_{k}"] = (xin.detach(), axin, y)
+                return y, ay
+
+            y, ay = conv(h, ah, 0)
+            c = _max_pool(y)
+            ac = _max_pool(ay).detach()
+            c.retain_grad()
+            cs[(si, -1)] = c
+            for b in range(cfg.blocks):
+                r, ar = conv(torch.relu(c), ac, 1 + 2 * b)
+                y2, ay2 = conv(torch.relu(r), ar, 2 + 2 * b)
+                ac = ay2 + c.detach().abs()
+                c = y2 + c
+                c.retain_grad()
+                cs[(si, b)] = c
+            h, ah = c, ac
+        enc = torch.relu(h).reshape(B, -1)
+        emb = P["TaskEmbedding_0/Embed_0/embedding"][task_ids]
+        emb = emb / (torch.linalg.norm(emb, dim=-1, keepdim=True) + 1e-8)
+        f0 = torch.cat([enc, emb], -1)
+        f1 = _layer_norm(f0, P["LayerNorm_0/scale"], P["LayerNorm_0/bias"], cfg.ln_eps)
+        f1.retain_grad()
+        d = "DistributionalDense_0/"
+        hh = f1 @ P[d + "Dense_0/kernel"] + P[d + "Dense_0/bias"]
+        hh = torch.relu(_layer_norm(hh, P[d + "LayerNorm_0/scale"], P[d + "LayerNorm_0/bias"], cfg.ln_eps))
+        adv = (hh @ P[d + "Dense_1/kernel"] + P[d + "Dense_1/bias"]).reshape(-1, cfg.n_actions, cfg.n_atoms)
+        val = (hh @ P[d + "Dense_2/kernel"] + P[d + "Dense_2/bias"]).reshape(-1, 1, cfg.n_atoms)
+        lg = (val + adv - adv.mean(-2, keepdim=True))[torch.arange(B), actions]
+        (-(m * torch.log_softmax(lg, -1)).sum(-1).mean()).backward()
+    with torch.no_grad():
+        def conv_t(name, a):  # conv-transpose of a magnitude with |W|
+            w = P[name + "/kernel"].detach().abs().permute(3, 2, 0, 1)
+            return torch.nn.grad.conv2d_input((a.shape[0], w.shape[1], a.shape[1], a.shape[2]), w,
+                                              a.permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+
+        a_df0 = _ln_abs_back(f1.grad.abs(), f0.detach(), P["LayerNorm_0/scale"].detach(), cfg.ln_eps)
+        a_dc = a_df0[:, :enc.shape[1]].reshape(h.shape) * (h.detach() > 0)
+        A = {}
+        for si in reversed(range(len(cfg.stacks))):
+            pre = f"ImpalaEncoder_0/stack_{si}/Conv_"
+            for b in reversed(range(cfg.blocks)):
+                A[pre + str(2 + 2 * b)] = a_dc  # the block output's gradient is the conv's
+                dc = cs[(si, b)].grad.abs()
+                A[pre + str(1 + 2 * b)] = conv_t(pre + str(2 + 2 * b), dc) * (keep[pre + str(2 + 2 * b)][0] > 0)
+                dr = keep[pre + str(1 + 2 * b)][2].grad.abs()
+                a_dc = dc + conv_t(pre + str(1 + 2 * b), dr) * (keep[pre + str(1 + 2 * b)][0] > 0)
+            with torch.enable_grad():  # the pool's scatter-add of |dc| (windows overlap)
+                y0 = keep[pre + "0"][2].detach().clone().requires_grad_(True)
+                (_max_pool(y0) * cs[(si, -1)].grad.abs()).sum().backward()
+            A[pre + "0"] = y0.grad
+            if si > 0:
+                a_dc = conv_t(pre + "0", keep[pre + "0"][2].grad.abs())
+        out = {}
+        for name, (_, axin, _) in keep.items():
+            xa, dy = axin.permute(0, 3, 1, 2), A[name].permute(0, 3, 1, 2)
+            w = torch.nn.grad.conv2d_weight(xa, (dy.shape[1], xa.shape[1], 3, 3), dy, padding=1)
+            out[name + "/kernel"] = w.permute(2, 3, 1, 0).reshape(-1).numpy()
+            out[name + "/bias"] = dy.sum((0, 2, 3)).numpy()
+        return out
+
+
 @dataclass
 class DrQState:
     params: np.ndarray
@@ -269,5 +371,8 @@ def update(cfg: DrQConfig, st: DrQState, batch, return_internals: bool = False, 
     }
     new = DrQState(p_new, tgt, mu, nu, count)
     if return_internals:
-        return new, logs, {"grad": g, "m": m.double().numpy(), "a_next": a_next.numpy()}
+        floors = conv_error_floors(cfg, st.params, torch.as_tensor(np.asarray(obs), dtype=torch.float64), ti,
+                                   torch.as_tensor(np.asarray(actions, np.int64)), m.double())
+        return new, logs, {"grad": g, "m": m.double().numpy(), "a_next": a_next.numpy(), "conv_abs": floors,
+                           "batch": batch}
     return new, logs

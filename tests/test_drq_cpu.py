@@ -72,6 +72,35 @@ def test_compat_config_tree():
     assert env.observation_space.shape == (4, 84, 84) and env.action_space.n == 18
 
 
+def test_residual_convs_use_truncated_lecun_normal():
+    """flax Conv's default kernel init (impala.py:27,29): truncated normal on [-2, 2] std units,
+    variance 1 / fan_in."""
+    from mtrl_amd.drq_init import truncated_lecun_normal
+
+    fan = 3 * 3 * 16
+    v = truncated_lecun_normal(np.random.default_rng(0), (200_000,), fan)
+    lim = 2.0 / np.sqrt(fan) / 0.87962566103423978
+    assert np.abs(v).max() <= lim and np.abs(v).max() > 0.99 * lim
+    assert abs(v.var() * fan - 1.0) < 0.01
+
+
+def test_optimizer_settings_follow_optimizer_config_spawn():
+    """config/optim.py:26-43: Adam gets eps 1e-5 and no decay, AdamW optax's defaults unless set;
+    what the AdamW kernel cannot run (a clip link, RMSProp) is refused, not silently replaced."""
+    import mtrl  # noqa: F401
+    from mtrl.config.optim import OptimizerConfig
+    from mtrl.config.utils import Optimizer
+    from mtrl_amd.compat.rl.algorithms.drqeps import _adam_settings
+
+    assert _adam_settings(OptimizerConfig()) == (1e-5, 0.0)
+    assert _adam_settings(OptimizerConfig(eps=1e-3, weight_decay=0.5)) == (1e-3, 0.0)
+    assert _adam_settings(OptimizerConfig(optimizer=Optimizer.AdamW)) == (1e-8, 1e-4)
+    assert _adam_settings(OptimizerConfig(optimizer=Optimizer.AdamW, eps=1.5e-4, weight_decay=0.05)) == (1.5e-4, 0.05)
+    for bad in (OptimizerConfig(max_grad_norm=1.0), OptimizerConfig(optimizer=Optimizer.RMSProp)):
+        with pytest.raises(NotImplementedError):
+            _adam_settings(bad)
+
+
 @pytest.mark.parametrize("kind", [0, 1], ids=["memory_efficient", "atari"])
 def test_unbalanced_rows_reproduce_reference_draws(kind):
     """The host half of sample_unbalanced (mtrl_amd.drq.unbalanced_rows): the same Generator calls

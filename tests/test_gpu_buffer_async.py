@@ -101,6 +101,35 @@ def test_device_array_add_and_reward_stats():
     dev.close()
 
 
+@pytest.mark.parametrize("side_stream", [False, True], ids=["default_stream", "side_stream"])
+def test_device_add_from_one_reused_tensor(side_stream):
+    """The producer overwrites ONE device tensor per field right after every add (and frees
+    temporaries): each add must still store the rows it was given (the pack kernel
+    runs on the engine stream; the producer stream is made to wait for it)."""
+    import torch
+
+    rng = np.random.default_rng(11)
+    host, dev = _engine(), _engine()
+    stream = torch.cuda.Stream() if side_stream else torch.cuda.current_stream()
+    with torch.cuda.stream(stream):
+        bufs = [torch.empty(x.shape, device="cuda") for x in _rows(rng)]
+        for _ in range(50):
+            rows = _rows(rng)
+            host.buffer_add(*rows)
+            for b, x in zip(bufs, rows):
+                b.copy_(torch.from_numpy(x).cuda(non_blocking=True))
+            dev.buffer_add(*bufs)
+            for b in bufs:  # the very next producer work clobbers the arrays
+                b.fill_(-7.0)
+            junk = torch.full((4096,), 3.0, device="cuda")  # reuses freed blocks on this stream
+            del junk
+    torch.cuda.synchronize()
+    for x, y in zip(host.buffer_read(0, CAP), dev.buffer_read(0, CAP)):
+        np.testing.assert_array_equal(x, y)
+    host.close()
+    dev.close()
+
+
 def test_mixed_host_device_add_is_rejected():
     import torch
 

@@ -56,26 +56,54 @@ def _run_both(cfg, B, seed):
     return e, st, new, got, want, internals
 
 
-@pytest.mark.parametrize("hw,hidden,B", [(20, 64, 8), (84, 512, 16)], ids=["small", "reference_geometry"])
+# A conv weight-gradient entry sums B x H x W products (1.8e6 at 84 x 84, batch 256) with heavy
+# cancellation.  Two bars per conv leaf (kernel and bias):
+#  * elementwise against the entry's rounding floor (oracle conv_error_floors: the |terms| of the
+#    sum, each factor at its one-level magnitude), as the GEMM tests hold C to sum |a b|;
+#  * the leaf's error norm against that of a plain PyTorch fp32 evaluation of the same update
+#    (oracle.drq.update in float32): the device is as accurate as an fp32 reference.
+# Calibrated on PyTorch fp32 (CPU) at batch 256 over 4 seeds: elementwise ratios up to 9e-5.
+CONV_FLOOR_TOL = 3e-4
+CONV_VS_FP32_REF = 4.0
+
+
+@pytest.mark.parametrize("hw,hidden,B", [(20, 64, 8), (84, 512, 16), (84, 512, 256)],
+                         ids=["small", "reference_geometry", "reference_geometry_b256"])
 def test_update_matches_oracle(hw, hidden, B):
+    """b256 is the benched configuration (bench.py --workload atari_drq): the single 3B-image
+    encoder pass, the split-K dense layers at M = 256..768 and the segment-table partial sums of
+    all 15 convs run at the bench's own sizes."""
+    import torch
+
     from mtrl_amd import _lib as L
 
     cfg = od.DrQConfig(hw=hw, n_hidden=hidden)
-    e, st, new, got, want, internals = _run_both(cfg, B, seed=hw)
+    e, st, new, got, want, internals = _run_both(cfg, B, seed=hw + B)
     for k, v in want.items():
         assert abs(got[k] - v) <= 1e-5 * max(1.0, abs(v)), (k, got[k], v)
     g_gpu = e.get_params(L.DRQ_GRAD).astype(np.float64)
     g_ref = internals["grad"]
-    o = 0
+    floors = internals["conv_abs"]
+    _, _, ref32 = od.update(cfg, st, internals["batch"], return_internals=True, dtype=torch.float32)
+    g32 = ref32["grad"]
+    o, worst, norm_ratio = 0, {}, {}
     for path, shape in od.param_spec(cfg):
         n = int(np.prod(shape))
-        a, b = g_gpu[o:o + n], g_ref[o:o + n]
-        scale = np.abs(b).max() + 1e-12
-        # conv leaves sum B x H x W pixels (x 9 taps; 1.1e5 terms at 84 x 84) in fp32 with heavy
-        # cancellation: held to 5e-4 of the leaf's largest entry; everything else to 1e-4
-        tol = 5e-4 if "Conv_" in path else 1e-4
-        assert np.abs(a - b).max() <= tol * scale + 1e-9, (path, float(np.abs(a - b).max()), float(scale))
+        a, b, c = g_gpu[o:o + n], g_ref[o:o + n], g32[o:o + n]
         o += n
+        if path in floors:
+            err = np.abs(a - b)
+            worst[path] = float((err / (floors[path] + 1e-30)).max())
+            assert (err <= CONV_FLOOR_TOL * floors[path] + 1e-12).all(), (path, worst[path])
+            e_dev, e_ref = np.linalg.norm(a - b), np.linalg.norm(c - b)
+            norm_ratio[path] = e_dev / max(e_ref, 1e-30)
+            assert e_dev <= CONV_VS_FP32_REF * e_ref + 1e-7 * np.linalg.norm(b), (path, e_dev, e_ref)
+            continue
+        scale = np.abs(b).max() + 1e-12
+        assert np.abs(a - b).max() <= 1e-4 * scale + 1e-9, (path, float(np.abs(a - b).max()), float(scale))
+    assert len(worst) == 2 * 5 * len(cfg.stacks)
+    print(f"conv |err| / floor worst {max(worst.values()):.2e} ({max(worst, key=worst.get)}); "
+          f"|err| vs fp32 reference worst {max(norm_ratio.values()):.2f} ({max(norm_ratio, key=norm_ratio.get)})")
     mu = e.get_params(L.DRQ_ADAM_MU).astype(np.float64)
     np.testing.assert_allclose(mu, new.mu, rtol=1e-4, atol=1e-4 * np.abs(new.mu).max())
     tgt = e.get_params(L.DRQ_TARGET).astype(np.float64)
