@@ -129,7 +129,12 @@ struct drq_engine {
   int alloc(T_** ptr, long long n) {
     void* q = nullptr;
     if (hipMalloc(&q, sizeof(T_) * (size_t)std::max(n, 1LL)) != hipSuccess) return fail(-12, "hipMalloc failed");
-    if (hipMemsetAsync(q, 0, sizeof(T_) * (size_t)std::max(n, 1LL), st) != hipSuccess) return fail(-5, "memset");
+    // zeroed and COMPLETE before returning: callers fill some buffers right away with a plain
+    // hipMemcpy (segment tables), which is not ordered after work on the non-blocking engine
+    // stream -- an asynchronous memset here could land after the copy and zero the table
+    if (hipMemsetAsync(q, 0, sizeof(T_) * (size_t)std::max(n, 1LL), st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return fail(-5, "memset");
     allocs.push_back(q);
     *ptr = static_cast<T_*>(q);
     return 0;

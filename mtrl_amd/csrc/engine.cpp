@@ -71,6 +71,10 @@ struct Net {
   // ald = width rounded up to 32).
   __bf16* wp[2][MAXD] = {};
   long long wld = 0, wrows = 0, arows = 0, ald = 0;
+  // krows: rows of one batch pass rounded up to 32 (the weight grad's K); arows: rows of the
+  // activation planes (= krows, or for the actor, whose forward runs ONCE over [s | s'], krows + B
+  // rounded up: the s rows first, the s' rows from row krows)
+  long long krows = 0;
   // gemm_x3f path (row-major x row-major, gemm_x3f.hip) for the hidden layers' forward and data
   // grad: W_i^T planes ([E][3][width (out)][ald (in)], i >= 1) of p ([0]) and tgt ([1]); hidden
   // activations then keep planes only (their ReLU mask is read from the high plane)
@@ -140,7 +144,9 @@ struct mtsac_engine {
   int stage_next = 0;
   hipEvent_t add_ev = nullptr;  // orders device-pointer adds after the legacy default stream
   // inputs
+  // xa holds [s | s'] for the actor's single forward: xan = xa + krows * ld_a
   float *xa = nullptr, *xan = nullptr, *xc = nullptr, *xcn = nullptr, *xcp = nullptr;
+  int Ma = 0;  // rows of the actor forward over [s | s'] (krows + B; pad rows are zero inputs)
   float *rew = nullptr, *done = nullptr, *tw = nullptr;
   int* task = nullptr;
   int *counts = nullptr, *rows = nullptr;
@@ -148,8 +154,8 @@ struct mtsac_engine {
   float *u_obs = nullptr, *u_act = nullptr, *u_nobs = nullptr, *u_done = nullptr, *u_rew = nullptr;
   float *eps_n = nullptr, *eps_c = nullptr;
   // activations / grads
-  float* ha[MAXD] = {};
-  float* han[MAXD] = {};  // actor(s') activations (concurrent with ha)
+  float* ha[MAXD] = {};   // actor activations over [s | s'] (rows [0, B) and [krows, krows + B))
+  float* han[MAXD] = {};  // = ha[i] + krows * width: the s' rows
   float* hc[MAXD] = {};
   float* hct[MAXD] = {};  // target-critic activations (concurrent with hc)
   float* dza[MAXD] = {};  // per-layer pre-activation grads
@@ -158,7 +164,6 @@ struct mtsac_engine {
   bool planes = false;
   int np = 3;  // operand planes the plane GEMMs read: 3 (split3) or 1 (bf16)
   __bf16* hap[MAXD] = {};
-  __bf16* hanp[MAXD] = {};
   __bf16* hcp[MAXD] = {};
   __bf16* hctp[MAXD] = {};
   __bf16* dzap[MAXD] = {};
@@ -336,6 +341,10 @@ struct mtsac_engine {
                            std::to_string(epi) + ", " + (p.C ? "true" : "false") + ", " + (p.Cp ? "true" : "false") +
                            ", " + (p.mask16 ? "true" : "false") + ", " + (tagged ? "8" : "0") + ", " +
                            (p.np == 1 ? "1" : "3") + ">";
+    } else if ((epi == EPI_RELU_MASK && !p.mask) || (!p.C && !p.Cp)) {
+      // gemm_x3p's direct epilogue reads an fp32 mask and writes through C or Cp: never launch it
+      // on operands it cannot address (a null mask pointer faults the device)
+      comm_error = "no plane GEMM kernel for this launch (mask16-only ReLU mask or no output)";
     } else {
       gemm_x3p(p, epi, batch, cur);
       fam_kernel[family] = "gemm_x3p_kernel";
@@ -549,7 +558,7 @@ struct mtsac_engine {
       g.sC = net.ms_W[i];
       g.M = i == 0 ? net.in_dim : net.width;
       g.N = net.width;
-      g.K = (int)net.arows;
+      g.K = (int)net.krows;  // the s rows (dz is zero past B; the actor's s' rows follow at krows)
       g.tag = i == 0 ? 1 : 0;
       g.splits = -1;  // by tile count (gemm_x3p_splits); the lane workspace is sized for it
       g.ws = ws_lane[cur_lane];
@@ -908,9 +917,11 @@ struct mtsac_engine {
     });
     // critic forward on (s, a) with the current critic (mtsac.py:555)
     const int s_cf = seg({s_in}, 1, [&] { trunk_forward(critic, critic.p, 0, xc, ld_c, hc, hcp, Bl); });
-    // actor forward on s with the pre-update actor (mtsac.py:640-642)
+    // ONE actor forward over [s | s'] with the pre-update actor: update_critic samples a' ~ pi(.|s')
+    // (mtsac.py:525-528) and update_actor a ~ pi(.|s) (:640-642) from the same parameters, so the
+    // two row blocks share every trunk GEMM (rows krows.. are s'; the pad rows between are zeros)
     const int s_af = seg({s_in}, 2, [&] {
-      trunk_forward(actor, actor.p, 0, xa, ld_a, ha, hap, Bl);
+      trunk_forward(actor, actor.p, 0, xa, ld_a, ha, hap, Ma);
       PolicyParams q = pp;
       q.head = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
       q.eps = device_noise ? nullptr : eps_c;
@@ -919,17 +930,16 @@ struct mtsac_engine {
       q.logpi = logpi;
       q.cache = cache;
       policy_head(q, cur);
-    });
-    // a' ~ pi(.|s'), target critic, TD target (mtsac.py:525-553)
-    const int s_tg = seg({s_in}, 0, [&] {
-      trunk_forward(actor, actor.p, 0, xan, ld_a, han, hanp, Bl);
-      PolicyParams q = pp;
+      q = pp;
       q.head = head(actor, actor.p, han[actor.depth - 1], Bl, task);
       q.eps = device_noise ? nullptr : eps_n;
       q.stream_id = 1;
       q.a_out = xcn;
       q.logpi = logpi_n;
       policy_head(q, cur);
+    });
+    // target critic at (s', a'), TD target (mtsac.py:529-553)
+    const int s_tg = seg({s_af}, 0, [&] {
       trunk_forward(critic, critic.tgt, 1, xcn, ld_c, hct, hctp, Bl);
       CriticHeadParams c = ch;
       c.head = head(critic, critic.tgt, hct[critic.depth - 1], Bl, task);
@@ -1450,7 +1460,8 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     net->wrows = align_up(net->width, 32);
     net->ald = align_up(net->width, 32);
     net->xld = align_up(net->in_dim, 32);
-    net->arows = align_up(e->B, 32);
+    net->krows = align_up(e->B, 32);
+    net->arows = net == &e->actor ? align_up(net->krows + e->B, 32) : net->krows;
     // row-major x row-major plane GEMMs for the trunk forward and data grad (hidden activations
     // then keep planes only): gemm_x3f when its 208 x 256 tiles fill the chip (with split-K when
     // they do not), gemm_x3s for narrow trunks (K <= 512: W = 400).  The 16 TI x 64 tiles of
@@ -1464,8 +1475,9 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
       const char* v = getenv("MTSAC_X3F_MIN_TILES");
       return v ? atoi(v) : 64;
     }();
+    const int M_fwd = net == &e->actor ? (int)(net->krows + e->B) : e->B;  // the actor forward's rows
     net->x3f = e->planes && net->depth > 1 &&
-               ((net->ald % 64 == 0 && gemm_x3f_tiles(e->B, net->width, net->E) >= x3f_min_tiles) ||
+               ((net->ald % 64 == 0 && gemm_x3f_tiles(M_fwd, net->width, net->E) >= x3f_min_tiles) ||
                 (net->ald <= 512 && e->B <= 2048));
     if (net->x3f) net->xld = align_up(net->in_dim, 64);  // gemm_x3f steps K by 64
     for (int w = 0; w < (net == &e->critic ? 2 : 1); ++w)
@@ -1485,11 +1497,12 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
         const int M = i == 0 ? net->in_dim : net->width;
         ws = std::max(ws, gemm_ws_floats(M, net->width, net->E, gemm_splits(M, net->width, e->B, net->E)));
         if (e->planes) {
-          ws = std::max(ws, gemm_x3p_ws_floats(M, net->width, (int)net->arows, net->E, true));  // weight grad
-          ws = std::max(ws, gemm_x3p_ws_floats(e->B, net->width, (int)(i == 0 ? net->xld : net->ald), net->E,
-                                               false));  // forward / data grad
-          ws = std::max(ws, gemm_x3f_ws_floats(e->B, net->width, (int)(i == 0 ? align_up(net->in_dim, 64) : net->ald),
-                                               net->E));
+          ws = std::max(ws, gemm_x3p_ws_floats(M, net->width, (int)net->krows, net->E, true));  // weight grad
+          for (int rows : {e->B, net == &e->actor ? (int)(net->krows + e->B) : e->B}) {  // data grad, forward
+            ws = std::max(ws, gemm_x3p_ws_floats(rows, net->width, (int)(i == 0 ? net->xld : net->ald), net->E, false));
+            ws = std::max(ws, gemm_x3f_ws_floats(rows, net->width,
+                                                 (int)(i == 0 ? align_up(net->in_dim, 64) : net->ald), net->E));
+          }
         }
       }
     for (float*& w : e->ws_lane)
@@ -1504,8 +1517,9 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   if ((rc = e->alloc(&e->idx, e->n))) return bad(rc);
   if ((rc = e->alloc(&e->rmin, e->T_l))) return bad(rc);
   if ((rc = e->alloc(&e->rmax, e->T_l))) return bad(rc);
-  if ((rc = e->alloc(&e->xa, (size_t)B * e->ld_a))) return bad(rc);
-  if ((rc = e->alloc(&e->xan, (size_t)B * e->ld_a))) return bad(rc);
+  e->Ma = (int)(e->actor.krows + B);
+  if ((rc = e->alloc(&e->xa, (size_t)e->Ma * e->ld_a))) return bad(rc);  // [s | pad | s'], pad rows stay 0
+  e->xan = e->xa + e->actor.krows * e->ld_a;
   if ((rc = e->alloc(&e->xc, (size_t)B * e->ld_c))) return bad(rc);
   if ((rc = e->alloc(&e->xcn, (size_t)B * e->ld_c))) return bad(rc);
   if ((rc = e->alloc(&e->xcp, (size_t)B * e->ld_c))) return bad(rc);
@@ -1520,9 +1534,11 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   if ((rc = e->alloc(&e->u_act, (size_t)B * e->A))) return bad(rc);
   if ((rc = e->alloc(&e->eps_n, (size_t)B * e->A))) return bad(rc);
   if ((rc = e->alloc(&e->eps_c, (size_t)B * e->A))) return bad(rc);
-  for (int i = 0; i < c.actor_depth; ++i)
-    for (float** p : {&e->ha[i], &e->han[i], &e->dza[i]})
-      if ((rc = e->alloc(p, (size_t)B * c.actor_width))) return bad(rc);
+  for (int i = 0; i < c.actor_depth; ++i) {
+    if ((rc = e->alloc(&e->ha[i], (size_t)e->Ma * c.actor_width))) return bad(rc);
+    e->han[i] = e->ha[i] + e->actor.krows * c.actor_width;
+    if ((rc = e->alloc(&e->dza[i], (size_t)B * c.actor_width))) return bad(rc);
+  }
   for (int i = 0; i < c.critic_depth; ++i)
     for (float** p : {&e->hc[i], &e->hct[i], &e->dzc[i]})
       if ((rc = e->alloc(p, (size_t)c.num_critics * B * c.critic_width))) return bad(rc);
@@ -1530,9 +1546,10 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     for (Net* net : {&e->actor, &e->critic}) {
       const bool cr = net == &e->critic;
       const size_t np = (size_t)net->E * 3 * net->aps();
-      for (int i = 0; i + 1 < net->depth; ++i)
-        for (__bf16** p : {cr ? &e->hcp[i] : &e->hap[i], cr ? &e->hctp[i] : &e->hanp[i]})
-          if ((rc = e->alloc(p, np))) return bad(rc);
+      for (int i = 0; i + 1 < net->depth; ++i) {
+        if ((rc = e->alloc(cr ? &e->hcp[i] : &e->hap[i], np))) return bad(rc);
+        if (cr && (rc = e->alloc(&e->hctp[i], np))) return bad(rc);
+      }
       // dz[0] keeps no planes: its weight grad (K = B, M = in_dim) runs on the on-the-fly split
       // kernel, cheaper than writing the planes in the data-grad epilogue (tools/step_gemms.py)
       for (int i = 1; i < net->depth; ++i)
@@ -1545,6 +1562,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
       const float* xs[5] = {e->xa, e->xan, e->xc, e->xcn, e->xcp};
       for (int k = 0; k < 5; ++k) {
         const Net& net = k < 2 ? e->actor : e->critic;
+        if (k == 1) continue;  // s' rows are part of xa's planes (the merged actor forward)
         e->inp[k].x = xs[k];
         if ((rc = e->alloc(&e->inp[k].p, (size_t)3 * net.arows * net.xld))) return bad(rc);
       }

@@ -104,8 +104,13 @@ def test_update_matches_oracle(hw, hidden, B):
     assert len(worst) == 2 * 5 * len(cfg.stacks)
     print(f"conv |err| / floor worst {max(worst.values()):.2e} ({max(worst, key=worst.get)}); "
           f"|err| vs fp32 reference worst {max(norm_ratio.values()):.2f} ({max(norm_ratio, key=norm_ratio.get)})")
+    # first AdamW step from zero moments: mu = (1 - b1) g, nu = (1 - b2) g^2 of the device's own
+    # gradient (held to the oracle above, leaf by leaf)
     mu = e.get_params(L.DRQ_ADAM_MU).astype(np.float64)
-    np.testing.assert_allclose(mu, new.mu, rtol=1e-4, atol=1e-4 * np.abs(new.mu).max())
+    nu = e.get_params(L.DRQ_ADAM_NU).astype(np.float64)
+    c1, c2 = (float(np.float32(1) - np.float32(b)) for b in (cfg.b1, cfg.b2))  # fp32 constants, as optax
+    np.testing.assert_allclose(mu, c1 * g_gpu, rtol=1e-6, atol=1e-12)
+    np.testing.assert_allclose(nu, c2 * g_gpu * g_gpu, rtol=1e-6, atol=1e-20)
     tgt = e.get_params(L.DRQ_TARGET).astype(np.float64)
     np.testing.assert_allclose(tgt, new.target, rtol=1e-6, atol=1e-6)
     p = e.get_params(L.DRQ_PARAMS).astype(np.float64)

@@ -4,6 +4,6 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r3a
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_multiprocess.py tests/test_gpu_buffer_async.py tests/test_gpu_drq.py tests/test_gpu_shard.py tests/test_gpu_update.py -x -v -s -rf --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_drq.py tests/test_gpu_shard.py tests/test_gpu_update.py tests/test_gpu_fullbatch.py -v -s -rf --timeout 300 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; echo "pytest exit $rc" >> $O/tests.log
 exit $rc
