@@ -330,7 +330,8 @@ struct mtsac_engine {
                                        std::to_string(gemm_x3f_split_bm(p.M, p.N, p.K, batch)) +
                                        ", 0, true, false, false, 0, " +
                                        (p.np == 1 ? "1" : "3") + "> + splitk_epilogue_kernel"
-                                 : std::string("gemm_x3f_kernel<208, ") + std::to_string(epi) + ", " +
+                                 : std::string("gemm_x3f_kernel<") + std::to_string(gemm_x3f_bm(p, batch)) + ", " +
+                                       std::to_string(epi) + ", " +
                                        (p.C ? "true" : "false") + ", " + (p.Cp ? "true" : "false") + ", " +
                                        (p.mask16 ? "true" : "false") + ", " + (tagged ? "8" : "0") + ", " +
                                        (p.np == 1 ? "1" : "3") + ">";

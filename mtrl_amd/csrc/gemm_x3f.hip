@@ -315,11 +315,30 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
 }
 
 constexpr int BM0 = 208;
+// precision bf16 (one plane, one MFMA per product): the operand ingest per CU is (BM + 256) rows
+// of 128 B per 64-deep step against BM x 256 x 64 multiply-adds, so a taller row tile feeds the
+// MFMAs with fewer bytes per flop (BM = 400: 26 B/clk/CU at the MFMA peak, against 36 at 208)
+// and its A planes fit LDS twice (2 x 50 KB).  Used where it does not cost a round of workgroups.
+constexpr int BM_BF16 = 400;
 
 template <int EPI, bool C_OUT, bool P_OUT, bool MASK16, int TAG = 0>
-void launch(const SplitGemmParams& p, dim3 grid, hipStream_t st) {
-  if (p.np == 1) hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, dim3(512), 0, st, p);
+void launch(const SplitGemmParams& p, dim3 grid, hipStream_t st, bool tall = false) {
+  if (p.np == 1 && tall)
+    hipLaunchKernelGGL((gemm_x3f_kernel<BM_BF16, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, dim3(512), 0, st, p);
+  else if (p.np == 1)
+    hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, dim3(512), 0, st, p);
   else hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 3>), grid, dim3(512), 0, st, p);
+}
+
+// the tall bf16 tile when it needs no more rounds of 256 workgroups than 208-row tiles, weighing a
+// tile's work by its rows over its relative MFMA feed (1.2 at 400 rows); not for launches that
+// write per-row-tile column sums (dbp: their chunk count is fixed at 208-row tiles)
+static bool use_tall(const SplitGemmParams& p, int batch) {
+  if (p.np != 1 || p.dbp != nullptr) return false;
+  const long long ny = (p.N + 255) / 256;
+  const long long r0 = ((p.M + BM0 - 1) / BM0 * ny * batch + 255) / 256;
+  const long long r1 = ((p.M + BM_BF16 - 1) / BM_BF16 * ny * batch + 255) / 256;
+  return (double)r1 * BM_BF16 / 1.2 < (double)r0 * BM0;
 }
 
 }  // namespace x3fk
@@ -342,6 +361,8 @@ void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t s
 }
 
 int gemm_x3f_row_tiles(int M) { return (M + x3fk::BM0 - 1) / x3fk::BM0; }
+
+int gemm_x3f_bm(const SplitGemmParams& p, int batch) { return x3fk::use_tall(p, batch) ? x3fk::BM_BF16 : x3fk::BM0; }
 
 namespace x3fk {
 constexpr int BMS = 128;  // the split-K row tile alternative for task shards (96 KB of LDS)
@@ -449,23 +470,25 @@ int gemm_x3f(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
     return S_eff;
   }
   const SplitGemmParams& p = p0;
-  const dim3 grid((unsigned)gemm_x3f_tiles(p.M, p.N, batch));
+  const bool tall = use_tall(p, batch);
+  const int bm = tall ? BM_BF16 : BM0;
+  const dim3 grid((unsigned)(((p.M + bm - 1) / bm) * ((p.N + BN - 1) / BN) * batch));
   const bool c = p.C != nullptr, pl = p.Cp != nullptr, m16 = p.mask16 != nullptr;
   if (epi == EPI_BIAS_RELU && p.tag == 1 && pl && !c) {
-    launch<EPI_BIAS_RELU, false, true, false, TAG_INPUT>(p, grid, st);  // input layer (planes out)
+    launch<EPI_BIAS_RELU, false, true, false, TAG_INPUT>(p, grid, st, tall);  // input layer (planes out)
   } else if (epi == EPI_BIAS_RELU) {
-    if (c && pl) launch<EPI_BIAS_RELU, true, true, false>(p, grid, st);
-    else if (c) launch<EPI_BIAS_RELU, true, false, false>(p, grid, st);
-    else launch<EPI_BIAS_RELU, false, true, false>(p, grid, st);
+    if (c && pl) launch<EPI_BIAS_RELU, true, true, false>(p, grid, st, tall);
+    else if (c) launch<EPI_BIAS_RELU, true, false, false>(p, grid, st, tall);
+    else launch<EPI_BIAS_RELU, false, true, false>(p, grid, st, tall);
   } else {
     if (m16) {
-      if (c && pl) launch<EPI_RELU_MASK, true, true, true>(p, grid, st);
-      else if (c) launch<EPI_RELU_MASK, true, false, true>(p, grid, st);
-      else launch<EPI_RELU_MASK, false, true, true>(p, grid, st);
+      if (c && pl) launch<EPI_RELU_MASK, true, true, true>(p, grid, st, tall);
+      else if (c) launch<EPI_RELU_MASK, true, false, true>(p, grid, st, tall);
+      else launch<EPI_RELU_MASK, false, true, true>(p, grid, st, tall);
     } else {
-      if (c && pl) launch<EPI_RELU_MASK, true, true, false>(p, grid, st);
-      else if (c) launch<EPI_RELU_MASK, true, false, false>(p, grid, st);
-      else launch<EPI_RELU_MASK, false, true, false>(p, grid, st);
+      if (c && pl) launch<EPI_RELU_MASK, true, true, false>(p, grid, st, tall);
+      else if (c) launch<EPI_RELU_MASK, true, false, false>(p, grid, st, tall);
+      else launch<EPI_RELU_MASK, false, true, false>(p, grid, st, tall);
     }
   }
   return 1;

@@ -87,20 +87,31 @@ def test_rejects_small_grids():
 
 
 
-def test_bf16_products():
-    """Precision bf16 on gemm_x3f: exactly the products of the bf16-rounded operands, fp32 sums."""
+@pytest.mark.parametrize("E,M,N,K,epi,m16", [(2, 6400, 2048, 256, 1, False), (2, 6300, 2040, 192, 2, True),
+                                             (1, 12800, 2048, 128, 1, False), (1, 6400, 2048, 128, 2, False)],
+                         ids=["s3_critic_fwd", "ragged_mask16", "merged_actor_fwd", "e1_208rows"])
+def test_bf16_products(E, M, N, K, epi, m16):
+    """Precision bf16 on gemm_x3f: exactly the products of the bf16-rounded operands, fp32 sums.
+    The first three shapes run the 400-row bf16 tile (one round of 256 workgroups), ragged rows
+    and columns included; the last keeps 208 rows (400 would leave half the chip idle)."""
     import torch
 
-    rng = np.random.default_rng(31)
-    A = rng.standard_normal((2, 6400, 256)).astype(np.float32)
-    B = (rng.standard_normal((2, 2048, 256)) / 16).astype(np.float32)
-    bias = rng.standard_normal((2, 2048)).astype(np.float32) * 0.1
-    C, _ = _run(1 | 1024, A, B, bias=bias)
+    rng = np.random.default_rng(31 + M + K)
+    A = rng.standard_normal((E, M, K)).astype(np.float32)
+    B = (rng.standard_normal((E, N, K)) / 16).astype(np.float32)
     Ar = torch.from_numpy(A).to(torch.bfloat16).to(torch.float64).numpy()
     Br = torch.from_numpy(B).to(torch.bfloat16).to(torch.float64).numpy()
     acc, scale = _ref(Ar, Br)
-    want = np.maximum(acc + bias[:, None, :], 0)
-    assert np.all(np.abs(C - want) <= 4e-6 * (scale + np.abs(bias[:, None, :])) + 1e-30)
+    if epi == 1:
+        bias = rng.standard_normal((E, N)).astype(np.float32) * 0.1
+        C, _ = _run(1 | 1024, A, B, bias=bias)
+        want = np.maximum(acc + bias[:, None, :], 0)
+        assert np.all(np.abs(C - want) <= 4e-6 * (scale + np.abs(bias[:, None, :])) + 1e-30)
+    else:
+        mask = np.maximum(rng.standard_normal((E, M, N)), 0).astype(np.float32)
+        C, _ = _run(2 | 1024 | (256 if m16 else 0), A, B, mask=mask, m16=m16)
+        want = np.where(mask > 0, acc, 0.0)
+        assert np.all(np.abs(C - want) <= 4e-6 * scale + 1e-30)
 
 
 @pytest.mark.parametrize("E,M,N,K,epi,m16", [(2, 896, 2048, 2048, 1, False), (2, 768, 2048, 2048, 2, True),
