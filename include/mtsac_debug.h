@@ -66,6 +66,12 @@ int mtsac_debug_x3s_ti(int M, int N, int batch);
 // choice); returns the previous fwd | bwd << 8.  Experiments only.
 int mtsac_debug_drq_groups(int fwd, int bwd);
 
+/* Eager update_many overlaps consecutive steps (the next gather and critic(s, a) forward beside
+ * the previous actor backward / all-reduce / Adam); on = 0 issues whole steps instead.  Returns
+ * the previous setting.  Tests and experiments. */
+struct mtsac_engine;
+int mtsac_debug_set_pipeline(struct mtsac_engine* engine, int32_t on);
+
 /* Per-launch record of the last timed step (mtsac_set_timing): i < 0 returns the number of
  * records; else dims = {family = GEMM kind, M, N, K, batch} and *ms its duration. */
 struct mtsac_engine;

@@ -147,6 +147,21 @@ struct mtsac_engine {
   // xa holds [s | s'] for the actor's single forward: xan = xa + krows * ld_a
   float *xa = nullptr, *xan = nullptr, *xc = nullptr, *xcn = nullptr, *xcp = nullptr;
   int Ma = 0;  // rows of the actor forward over [s | s'] (krows + B; pad rows are zero inputs)
+  // Cross-step pipelining (eager update_many): step k+1's gather and critic(s, a) forward run beside
+  // step k's actor backward, trunk all-reduce and Adam.  What the gather writes and step k's tail
+  // still reads -- the actor input rows (its layer-0 weight grad) and the task row lists (actor
+  // heads, temperature) -- alternates between two sets; everything else the early segments write
+  // is dead by the time step k's actor-loss pass (s_ap) has run, which they wait for.
+  struct InSet {
+    float* xa;
+    int *task, *counts, *rows;
+  };
+  InSet inset[2] = {};
+  int inset_cur = 0;
+  hipEvent_t ev_ap[2] = {}, ev_tail[2] = {};  // step k's s_ap / last segment, by step parity
+  bool have_prev = false;                      // a pipelined step k is in flight (its events valid)
+  bool no_pipeline = getenv("MTSAC_NO_PIPELINE") != nullptr;  // experiments: whole steps only
+  int step_par = 0;
   float *rew = nullptr, *done = nullptr, *tw = nullptr;
   int* task = nullptr;
   int *counts = nullptr, *rows = nullptr;
@@ -237,6 +252,8 @@ struct mtsac_engine {
     for (hipEvent_t x : stage_ev)
       if (x) (void)hipEventDestroy(x);
     if (add_ev) (void)hipEventDestroy(add_ev);
+    for (hipEvent_t x : {ev_ap[0], ev_ap[1], ev_tail[0], ev_tail[1]})
+      if (x) (void)hipEventDestroy(x);
     for (hipEvent_t e : evpool) (void)hipEventDestroy(e);
     for (hipStream_t x : {st, s1, s2, s3, s4})
       if (x) (void)hipStreamDestroy(x);
@@ -640,7 +657,7 @@ struct mtsac_engine {
           q.dbp = net.dbp[i - 1];
           const bool fused = gemm_x3f_ok(q, EPI_RELU_MASK, net.E);
           if (fused) g = q;
-          net.dbp_chunks[i - 1] = fused ? gemm_x3f_row_tiles(M) : 0;
+          net.dbp_chunks[i - 1] = fused ? (M + gemm_x3f_bm(q, net.E) - 1) / gemm_x3f_bm(q, net.E) : 0;
         }
       }
       gemmp(g, EPI_RELU_MASK, net.E, MTSAC_FAM_DATA_GRAD);
@@ -877,8 +894,23 @@ struct mtsac_engine {
   //   -> all-reduce, clip/Adam, temperature, logs.
   // Independent GEMM chains fill each other's tail waves.  With timing on, everything runs
   // serialised on the main stream so per-launch events measure solo kernels.
-  void step(bool device_batch, bool device_noise) {
+  void use_inset(int k) {
+    inset_cur = k;
+    xa = inset[k].xa;
+    xan = xa + actor.krows * ld_a;
+    task = inset[k].task;
+    counts = inset[k].counts;
+    rows = inset[k].rows;
+    inp[0].x = xa;  // the actor input's planes (written in s_af, after the previous step's tail)
+  }
+
+  // pipelined: eager issue that overlaps the previous step's tail (see InSet); join: the main
+  // stream waits for every lane at the end (the last step of a call, and every non-pipelined one)
+  void step(bool device_batch, bool device_noise, bool pipelined = false, bool join = true) {
     const int Bl = B;
+    pipelined = pipelined && !build && !timing_serial;
+    const bool overlap = pipelined && have_prev;
+    if (overlap) use_inset(inset_cur ^ 1);
     ev_next = 0;
     segs.clear();
     const float* twp = cfg.use_task_weights ? tw : nullptr;
@@ -905,6 +937,10 @@ struct mtsac_engine {
     ch.clip = cfg.clip;
     ch.T_glob = T_g;
 
+    if (overlap) {  // the gather and critic(s, a) reuse buffers step k's actor-loss pass reads
+      (void)hipStreamWaitEvent(st, ev_ap[step_par ^ 1], 0);
+      if (cfg.use_task_weights) (void)hipStreamWaitEvent(st, ev_tail[step_par ^ 1], 0);  // reads log_alpha
+    }
     const int s_in = seg({}, 0, [&] {
       GatherParams gp = gather_params();
       if (device_batch) {
@@ -916,12 +952,14 @@ struct mtsac_engine {
       task_rows(task, Bl, T_l, counts, rows, Bl, cur);
       if (cfg.use_task_weights) row_alpha(task, cfg.task_begin, log_alpha, T_g, Bl, 1, row_c, tw, cur);
     });
-    // critic forward on (s, a) with the current critic (mtsac.py:555)
-    const int s_cf = seg({s_in}, 1, [&] { trunk_forward(critic, critic.p, 0, xc, ld_c, hc, hcp, Bl); });
+    // critic forward on (s, a) with the current critic (mtsac.py:555); pipelined on lane 2, which
+    // the previous step's tail (lanes 1, 3, 4) does not use, so it runs beside that tail
+    const int s_cf = seg({s_in}, overlap ? 2 : 1, [&] { trunk_forward(critic, critic.p, 0, xc, ld_c, hc, hcp, Bl); });
+    if (overlap) (void)hipStreamWaitEvent(st, ev_tail[step_par ^ 1], 0);  // s_af: the updated actor
     // ONE actor forward over [s | s'] with the pre-update actor: update_critic samples a' ~ pi(.|s')
     // (mtsac.py:525-528) and update_actor a ~ pi(.|s) (:640-642) from the same parameters, so the
     // two row blocks share every trunk GEMM (rows krows.. are s'; the pad rows between are zeros)
-    const int s_af = seg({s_in}, 2, [&] {
+    const int s_af = seg({s_in}, overlap ? 0 : 2, [&] {
       trunk_forward(actor, actor.p, 0, xa, ld_a, ha, hap, Ma);
       PolicyParams q = pp;
       q.head = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
@@ -1009,6 +1047,7 @@ struct mtsac_engine {
       const float* ins[1] = {row_c};
       reduce_rows(ins, 1, Bl, actor.g + actor.n_flat + 1, cur);
     });
+    if (pipelined) (void)hipEventRecord(ev_ap[step_par], segs[s_ap].lane);
     const HeadParams ahp = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
     const int s_ahw = seg({s_ap}, 3, [&] {
       head_backward_weight(ahp, dout_a, 0, counts, rows, Bl, actor.g + actor.off_hW, actor.g + actor.off_hb, cur);
@@ -1017,7 +1056,7 @@ struct mtsac_engine {
       head_bwd(actor, ahp, dout_a, 0, dza, dzap, true);
     });
     const int s_ab = backward_segs(actor, actor.p, xa, ld_a, ha, hap, dza, dzap, s_ad, s_ahw, Bl);
-    seg({s_ab}, 1, [&] {
+    const int s_tail = seg({s_ab}, 1, [&] {
       // temperature gradient rides in the actor's scalar tail: [2] loss part, [3..] grad
       AlphaParams al = alpha_params();
       alpha_grad(al, cur);
@@ -1045,10 +1084,13 @@ struct mtsac_engine {
       write_logs(lp, cur);
       bump_counter(counter, cur);
     });
-    if (!build) {  // eager: the main stream waits for every lane
+    if (pipelined) (void)hipEventRecord(ev_tail[step_par], segs[s_tail].lane);
+    if (!build && (join || !pipelined)) {  // eager: the main stream waits for every lane
       for (const Seg& s : segs)
         if (s.lane != st && s.ev) (void)hipStreamWaitEvent(st, s.ev, 0);
     }
+    have_prev = pipelined && !join;
+    step_par ^= 1;
     cur = st;
   }
 
@@ -1519,17 +1561,23 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   if ((rc = e->alloc(&e->rmin, e->T_l))) return bad(rc);
   if ((rc = e->alloc(&e->rmax, e->T_l))) return bad(rc);
   e->Ma = (int)(e->actor.krows + B);
-  if ((rc = e->alloc(&e->xa, (size_t)e->Ma * e->ld_a))) return bad(rc);  // [s | pad | s'], pad rows stay 0
+  for (auto& q : e->inset) {
+    if ((rc = e->alloc(&q.xa, (size_t)e->Ma * e->ld_a))) return bad(rc);  // [s | pad | s'], pad rows stay 0
+    if ((rc = e->alloc(&q.task, B)) || (rc = e->alloc(&q.counts, e->T_l)) || (rc = e->alloc(&q.rows, (size_t)e->T_l * B)))
+      return bad(rc);
+  }
+  e->xa = e->inset[0].xa;
   e->xan = e->xa + e->actor.krows * e->ld_a;
+  e->task = e->inset[0].task;
+  e->counts = e->inset[0].counts;
+  e->rows = e->inset[0].rows;
   if ((rc = e->alloc(&e->xc, (size_t)B * e->ld_c))) return bad(rc);
   if ((rc = e->alloc(&e->xcn, (size_t)B * e->ld_c))) return bad(rc);
   if ((rc = e->alloc(&e->xcp, (size_t)B * e->ld_c))) return bad(rc);
   for (float** p : {&e->rew, &e->done, &e->tw, &e->logpi_n, &e->logpi, &e->y, &e->row_a, &e->row_b, &e->row_c,
                     &e->alpha_w, &e->u_done, &e->u_rew})
     if ((rc = e->alloc(p, B))) return bad(rc);
-  if ((rc = e->alloc(&e->task, B))) return bad(rc);
-  if ((rc = e->alloc(&e->counts, e->T_l))) return bad(rc);
-  if ((rc = e->alloc(&e->rows, (size_t)e->T_l * B))) return bad(rc);
+
   if ((rc = e->alloc(&e->u_obs, (size_t)B * e->D))) return bad(rc);
   if ((rc = e->alloc(&e->u_nobs, (size_t)B * e->D))) return bad(rc);
   if ((rc = e->alloc(&e->u_act, (size_t)B * e->A))) return bad(rc);
@@ -1555,7 +1603,8 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
       // kernel, cheaper than writing the planes in the data-grad epilogue (tools/step_gemms.py)
       for (int i = 1; i < net->depth; ++i)
         if ((rc = e->alloc(cr ? &e->dzcp[i] : &e->dzap[i], np))) return bad(rc);
-      const long long chunks = std::max<long long>({(long long)COLSUM_CHUNKS, gemm_x3f_row_tiles(e->B), head_backward_chunks(e->T_l)});
+      const long long chunks = std::max<long long>({(long long)COLSUM_CHUNKS, gemm_x3f_max_row_tiles(e->B),
+                                                    head_backward_chunks(e->T_l)});
       for (int i = 1; i < net->depth; ++i)
         if ((rc = e->alloc(&net->dbp[i], (size_t)(net->E * chunks * net->width)))) return bad(rc);
     }
@@ -1617,6 +1666,10 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   for (hipEvent_t& x : e->stage_ev)
     if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) return bad(fail(-5, "event"));
   if (hipEventCreateWithFlags(&e->add_ev, hipEventDisableTiming) != hipSuccess) return bad(fail(-5, "event"));
+  for (int k = 0; k < 2; ++k)
+    if (hipEventCreateWithFlags(&e->ev_ap[k], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_tail[k], hipEventDisableTiming) != hipSuccess)
+      return bad(fail(-5, "event"));
   *out = e;
   return 0;
 }
@@ -2089,7 +2142,10 @@ int mtsac_update_many(mtsac_engine* h, int32_t steps) {
   if (steps <= 0) return 0;
   if (!h->use_graph || h->timing || h->hook) {  // events / host hooks need eager issue
     h->tl_next = 0;  // timing records every launch of this call
-    for (int s = 0; s < steps; ++s) h->step(true, true);
+    // consecutive steps overlap (the last one joins every lane into the main stream); host hooks
+    // (the bring-your-own all-reduce, which blocks the issuing thread) keep whole steps
+    const bool pipe = !h->hook && !h->no_pipeline;
+    for (int s = 0; s < steps; ++s) h->step(true, true, pipe, s + 1 == steps);
     HIP_TRY(hipGetLastError());
     return 0;
   }
@@ -2342,6 +2398,13 @@ int mtsac_get_timing_kernel(mtsac_engine* h, int32_t family, char* buf, int32_t 
 }
 
 // ---------------------------------------------------------------- debug (include/mtsac_debug.h)
+int mtsac_debug_set_pipeline(mtsac_engine* h, int32_t on) {
+  if (!h) return fail(-22, "null engine");
+  const int was = h->no_pipeline ? 0 : 1;
+  h->no_pipeline = on == 0;
+  return was;
+}
+
 int mtsac_debug_timed_launch(mtsac_engine* h, int32_t i, int32_t* dims, double* ms) {
   if (!h) return fail(-22, "null engine");
   if (i < 0) return (int)std::min(h->tl_next, h->tl.size());

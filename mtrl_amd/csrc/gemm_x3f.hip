@@ -78,9 +78,13 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
   // each has at least a half step to land before the drain at the next step's barrier
   constexpr int P0 = (ABL & 512) ? (PMAX + 1) / 2 : PMAX;  // 512: the old even split (experiments)
   constexpr int PW = (ABL & 512) ? P0 : PMAX - 1;  // pieces every wave has issued after B(kt, 1)
-  static_assert(BM % 16 == 0 && 2 * STAGE <= 160 * 1024, "tile");
+  // the epilogue reuses the ring as scratch: two 16 x (BN + 4) fp32 row-block images + 8 x BN
+  // column-sum partials -- more than the ring of the short one-plane tiles holds
+  constexpr int EPI_LDS = (2 * 16 * (BN + 4) + 8 * BN) * 4;
+  constexpr int SMEM = 2 * STAGE > EPI_LDS ? 2 * STAGE : EPI_LDS;
+  static_assert(BM % 16 == 0 && SMEM <= 160 * 1024, "tile");
   static_assert(PMAX - 1 >= PW || NJ % 8 == 0, "every wave issues >= PW pieces in the first half step");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const unsigned lds_base = (unsigned)(unsigned long long)(x3pk::lds_void*)smem;
 
   const int t = threadIdx.x, lane = t & 63;
@@ -315,30 +319,50 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
 }
 
 constexpr int BM0 = 208;
-// precision bf16 (one plane, one MFMA per product): the operand ingest per CU is (BM + 256) rows
-// of 128 B per 64-deep step against BM x 256 x 64 multiply-adds, so a taller row tile feeds the
-// MFMAs with fewer bytes per flop (BM = 400: 26 B/clk/CU at the MFMA peak, against 36 at 208)
-// and its A planes fit LDS twice (2 x 50 KB).  Used where it does not cost a round of workgroups.
-constexpr int BM_BF16 = 400;
 
-template <int EPI, bool C_OUT, bool P_OUT, bool MASK16, int TAG = 0>
-void launch(const SplitGemmParams& p, dim3 grid, hipStream_t st, bool tall = false) {
-  if (p.np == 1 && tall)
-    hipLaunchKernelGGL((gemm_x3f_kernel<BM_BF16, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, dim3(512), 0, st, p);
-  else if (p.np == 1)
-    hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, dim3(512), 0, st, p);
-  else hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 3>), grid, dim3(512), 0, st, p);
+// Precision bf16 (one plane, one MFMA per product): a workgroup's 64-deep step takes BM x 256 x 64
+// multiply-adds (8 BM clocks of the CU's MFMAs) against (BM + 256) x 128 B of operands (A through
+// LDS, B to registers), and one CU ingests ~28 B/clk from L2 (MI355X_MICROARCH.md gather table), so
+// a step costs max(8 BM, 4.57 (BM + 256)) clocks: tall tiles run at the MFMA rate (400 rows: 26 B
+// per MFMA clock), short ones at the ingest rate.  The row tile is the one whose rounds of 256
+// workgroups x step cost is least -- no split-K: its fp32 partial slabs cost more HBM traffic than
+// a bf16 GEMM's whole operand set.  400 rows: the S3 critic (6400 x E 2) and the merged actor
+// forward (2 x 6400) in one round; 208: 6400-row single-member data grads; 80 / 48: MT10's 1280
+// rows (C2) without split-K.
+constexpr int BF16_BM[] = {48, 80, 208, 400};
+
+static int bf16_bm(int M, int N, int batch) {
+  const long long ny = (N + 255) / 256;
+  int best = BM0;
+  double best_t = 1e30;
+  for (int bm : BF16_BM) {
+    const long long rounds = ((M + bm - 1) / bm * ny * batch + 255) / 256;
+    const double t = (double)rounds * std::max(8.0 * bm, 4.57 * (bm + 256));
+    if (t < best_t - 1e-9) {
+      best_t = t;
+      best = bm;
+    }
+  }
+  return best;
 }
 
-// the tall bf16 tile when it needs no more rounds of 256 workgroups than 208-row tiles, weighing a
-// tile's work by its rows over its relative MFMA feed (1.2 at 400 rows); not for launches that
-// write per-row-tile column sums (dbp: their chunk count is fixed at 208-row tiles)
-static bool use_tall(const SplitGemmParams& p, int batch) {
-  if (p.np != 1 || p.dbp != nullptr) return false;
-  const long long ny = (p.N + 255) / 256;
-  const long long r0 = ((p.M + BM0 - 1) / BM0 * ny * batch + 255) / 256;
-  const long long r1 = ((p.M + BM_BF16 - 1) / BM_BF16 * ny * batch + 255) / 256;
-  return (double)r1 * BM_BF16 / 1.2 < (double)r0 * BM0;
+static long long bf16_workgroups(int M, int N, int batch) {
+  const int bm = bf16_bm(M, N, batch);
+  return (long long)((M + bm - 1) / bm) * ((N + 255) / 256) * batch;
+}
+
+template <int EPI, bool C_OUT, bool P_OUT, bool MASK16, int TAG = 0>
+void launch(const SplitGemmParams& p, dim3 grid, hipStream_t st, int bm) {
+  if (p.np != 1) {
+    hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 3>), grid, dim3(512), 0, st, p);
+    return;
+  }
+  switch (bm) {
+    case 48: hipLaunchKernelGGL((gemm_x3f_kernel<48, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, dim3(512), 0, st, p); break;
+    case 80: hipLaunchKernelGGL((gemm_x3f_kernel<80, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, dim3(512), 0, st, p); break;
+    case 400: hipLaunchKernelGGL((gemm_x3f_kernel<400, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, dim3(512), 0, st, p); break;
+    default: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, dim3(512), 0, st, p); break;
+  }
 }
 
 }  // namespace x3fk
@@ -361,8 +385,9 @@ void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t s
 }
 
 int gemm_x3f_row_tiles(int M) { return (M + x3fk::BM0 - 1) / x3fk::BM0; }
+int gemm_x3f_max_row_tiles(int M) { return (M + x3fk::BF16_BM[0] - 1) / x3fk::BF16_BM[0]; }
 
-int gemm_x3f_bm(const SplitGemmParams& p, int batch) { return x3fk::use_tall(p, batch) ? x3fk::BM_BF16 : x3fk::BM0; }
+int gemm_x3f_bm(const SplitGemmParams& p, int batch) { return p.np == 1 ? x3fk::bf16_bm(p.M, p.N, batch) : x3fk::BM0; }
 
 namespace x3fk {
 constexpr int BMS = 128;  // the split-K row tile alternative for task shards (96 KB of LDS)
@@ -418,6 +443,7 @@ int gemm_x3f_tiles(int M, int N, int batch) {
 // (splits < 0, a workspace given) and the finishing pass can apply the epilogue
 static int x3f_slices(const SplitGemmParams& p, int epi, int batch) {
   if (p.splits >= 0 || p.ws == nullptr || p.dbp != nullptr) return 1;
+  if (p.np == 1 && x3fk::bf16_workgroups(p.M, p.N, batch) >= 128) return 1;
   if (epi == EPI_RELU_MASK && !p.mask16 && !p.mask) return 1;
   if (p.N % 4 != 0 || (p.C && p.ldc % 4 != 0) || (p.Cp && p.ldcp % 4 != 0)) return 1;
   return gemm_x3f_splits(p.M, p.N, p.K, batch);
@@ -426,7 +452,7 @@ static int x3f_slices(const SplitGemmParams& p, int epi, int batch) {
 // workgroups of the launch (all slices)
 static long long x3f_workgroups(const SplitGemmParams& p, int epi, int batch) {
   const int S = x3f_slices(p, epi, batch);
-  if (S == 1) return gemm_x3f_tiles(p.M, p.N, batch);
+  if (S == 1) return p.np == 1 ? x3fk::bf16_workgroups(p.M, p.N, batch) : gemm_x3f_tiles(p.M, p.N, batch);
   const int bm = x3fk::split_plan(p.M, p.N, p.K, batch).bm;
   return (long long)((p.M + bm - 1) / bm) * ((p.N + x3fk::BN - 1) / x3fk::BN) * batch * S;
 }
@@ -470,25 +496,24 @@ int gemm_x3f(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
     return S_eff;
   }
   const SplitGemmParams& p = p0;
-  const bool tall = use_tall(p, batch);
-  const int bm = tall ? BM_BF16 : BM0;
+  const int bm = gemm_x3f_bm(p, batch);
   const dim3 grid((unsigned)(((p.M + bm - 1) / bm) * ((p.N + BN - 1) / BN) * batch));
   const bool c = p.C != nullptr, pl = p.Cp != nullptr, m16 = p.mask16 != nullptr;
   if (epi == EPI_BIAS_RELU && p.tag == 1 && pl && !c) {
-    launch<EPI_BIAS_RELU, false, true, false, TAG_INPUT>(p, grid, st, tall);  // input layer (planes out)
+    launch<EPI_BIAS_RELU, false, true, false, TAG_INPUT>(p, grid, st, bm);  // input layer (planes out)
   } else if (epi == EPI_BIAS_RELU) {
-    if (c && pl) launch<EPI_BIAS_RELU, true, true, false>(p, grid, st, tall);
-    else if (c) launch<EPI_BIAS_RELU, true, false, false>(p, grid, st, tall);
-    else launch<EPI_BIAS_RELU, false, true, false>(p, grid, st, tall);
+    if (c && pl) launch<EPI_BIAS_RELU, true, true, false>(p, grid, st, bm);
+    else if (c) launch<EPI_BIAS_RELU, true, false, false>(p, grid, st, bm);
+    else launch<EPI_BIAS_RELU, false, true, false>(p, grid, st, bm);
   } else {
     if (m16) {
-      if (c && pl) launch<EPI_RELU_MASK, true, true, true>(p, grid, st, tall);
-      else if (c) launch<EPI_RELU_MASK, true, false, true>(p, grid, st, tall);
-      else launch<EPI_RELU_MASK, false, true, true>(p, grid, st, tall);
+      if (c && pl) launch<EPI_RELU_MASK, true, true, true>(p, grid, st, bm);
+      else if (c) launch<EPI_RELU_MASK, true, false, true>(p, grid, st, bm);
+      else launch<EPI_RELU_MASK, false, true, true>(p, grid, st, bm);
     } else {
-      if (c && pl) launch<EPI_RELU_MASK, true, true, false>(p, grid, st, tall);
-      else if (c) launch<EPI_RELU_MASK, true, false, false>(p, grid, st, tall);
-      else launch<EPI_RELU_MASK, false, true, false>(p, grid, st, tall);
+      if (c && pl) launch<EPI_RELU_MASK, true, true, false>(p, grid, st, bm);
+      else if (c) launch<EPI_RELU_MASK, true, false, false>(p, grid, st, bm);
+      else launch<EPI_RELU_MASK, false, true, false>(p, grid, st, bm);
     }
   }
   return 1;

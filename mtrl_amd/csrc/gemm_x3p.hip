@@ -228,7 +228,12 @@ static void x3p_dispatch(int geo, const SplitGemmParams& p, int epi, int batch, 
 // fills the chip there); else 256x128.  g_x3p_geo forces one (experiments).
 static int pick_geo(int M, int N, int batch, bool kmajor, bool a_kmajor) {
   if (g_x3p_geo >= 0) return (g_x3p_geo == 5 && a_kmajor) ? 3 : g_x3p_geo;
-  if (kmajor) return 3;
+  if (kmajor) {  // weight grads: 256 x 256 tiles, or 128 x 128 (two workgroups per CU) for narrow
+                 // trunks whose few big tiles leave most CUs idle even at full split-K (W = 400:
+                 // 2 x 2 x E tiles of 256 -> 80 workgroups; of 128: 32 x S)
+    const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256) * batch;
+    return big < 32 ? 4 : 3;
+  }
   const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256) * batch;
   if (big < 192) return 1;
   if (a_kmajor) return 3;

@@ -92,7 +92,8 @@ bool gemm_x3f_ok(const SplitGemmParams& p, int epi, int batch);
 int gemm_x3f(const SplitGemmParams& p, int epi, int batch, hipStream_t st);  // returns the K slices used
 int gemm_x3f_tiles(int M, int N, int batch);
 int gemm_x3f_row_tiles(int M);  // row tiles of M (the dbp partials' chunk count)
-int gemm_x3f_bm(const SplitGemmParams& p, int batch);  // row tile of an unsplit launch (208, or 400 for bf16)
+int gemm_x3f_bm(const SplitGemmParams& p, int batch);  // row tile of an unsplit launch (208; bf16: 48..400)
+int gemm_x3f_max_row_tiles(int M);  // row tiles of M at the shortest tile (dbp partial buffers)
 // split-K for few rows: slices (1 = none) and workspace floats; gemm_x3f splits when the params
 // allow it (splits < 0, ws given, no dbp)
 int gemm_x3f_splits(int M, int N, int K, int batch);

@@ -225,3 +225,38 @@ def test_full_batch_bf16_drift_bound(name):
     d = np.abs(e.get_params(L.CRITIC).astype(np.float64) - st1.critic)
     assert np.median(d) < 1e-5, np.median(d)
     e.close()
+
+
+@pytest.mark.parametrize("T,tc,W,prec", [(50, 50, 2048, 1), (50, 7, 2048, 1), (10, 10, 400, 1), (10, 10, 2048, 2)],
+                         ids=["s3", "mt50_shard7", "mt10_w400", "mt10_w2048_bf16"])
+def test_pipelined_steps_equal_whole_steps(T, tc, W, prec):
+    """Eager update_many overlaps step k+1's gather and critic(s, a) forward with step k's actor
+    backward, all-reduce and Adam (engine.cpp step(), InSet): 4 device-sampled steps issued that
+    way give bitwise the logs, parameters, optimizer moments and index-stream state of 4 whole
+    steps issued one after another."""
+    from mtrl_amd import _lib as L
+    from mtrl_amd.engine import MTSACEngine, make_config
+    from mtrl_amd.init import init_mtsac
+
+    outs = []
+    for pipe in (0, 1):
+        e = MTSACEngine(make_config(num_tasks=T, task_begin=0, task_count=tc, obs_dim=39 + T, actor_width=W,
+                                    critic_width=W, batch_per_task=128, capacity=512, precision=prec))
+        a, c = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=4, task_begin=0, task_count=tc)
+        e.set_params(L.ACTOR, a)
+        e.set_params(L.CRITIC, c)
+        e.set_params(L.CRITIC_TARGET, c)
+        e.buffer_fill_synthetic(77)
+        e.seed_rng(5)
+        e.enable_graph(False)
+        e.lib.mtsac_debug_set_pipeline(e._h, pipe)
+        e.update_many(4)
+        outs.append((e.logs(), [e.get_params(w) for w in (L.ACTOR, L.CRITIC, L.CRITIC_TARGET, L.LOG_ALPHA,
+                                                           L.ACTOR_ADAM_NU, L.CRITIC_ADAM_MU)],
+                     e.get_rng_state(), e.noise_state()))
+        e.close()
+    a, b = outs
+    assert a[0] == b[0]
+    for x, y in zip(a[1], b[1]):
+        np.testing.assert_array_equal(x, y)
+    assert a[2] == b[2] and a[3] == b[3]

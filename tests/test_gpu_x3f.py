@@ -88,12 +88,15 @@ def test_rejects_small_grids():
 
 
 @pytest.mark.parametrize("E,M,N,K,epi,m16", [(2, 6400, 2048, 256, 1, False), (2, 6300, 2040, 192, 2, True),
-                                             (1, 12800, 2048, 128, 1, False), (1, 6400, 2048, 128, 2, False)],
-                         ids=["s3_critic_fwd", "ragged_mask16", "merged_actor_fwd", "e1_208rows"])
+                                             (1, 12800, 2048, 128, 1, False), (1, 6400, 2048, 128, 2, False),
+                                             (2, 1280, 2048, 512, 2, True), (1, 1270, 2040, 256, 1, False)],
+                         ids=["s3_critic_fwd", "ragged_mask16", "merged_actor_fwd", "e1_208rows", "c2_critic_80rows",
+                              "c2_e1_48rows_ragged"])
 def test_bf16_products(E, M, N, K, epi, m16):
     """Precision bf16 on gemm_x3f: exactly the products of the bf16-rounded operands, fp32 sums.
-    The first three shapes run the 400-row bf16 tile (one round of 256 workgroups), ragged rows
-    and columns included; the last keeps 208 rows (400 would leave half the chip idle)."""
+    Each shape runs the row tile the bf16 cost model picks (gemm_x3f.hip bf16_bm): 400 rows for
+    the S3 critic / merged actor forward, 208 for single-member 6400-row grads, 80 / 48 for MT10's
+    1280 rows -- ragged rows and columns included, every tile height's epilogue image in LDS."""
     import torch
 
     rng = np.random.default_rng(31 + M + K)
@@ -114,10 +117,15 @@ def test_bf16_products(E, M, N, K, epi, m16):
         assert np.all(np.abs(C - want) <= 4e-6 * scale + 1e-30)
 
 
-@pytest.mark.parametrize("E,M,N,K,epi,m16", [(2, 896, 2048, 2048, 1, False), (2, 768, 2048, 2048, 2, True),
-                                             (2, 1280, 2040, 512, 2, False), (1, 1800, 2048, 1024, 1, False)],
-                         ids=["shard7_fwd", "shard6_dgrad_m16", "mt10_ragged_dgrad", "e1_ragged_fwd"])
-def test_split_k_task_shards(E, M, N, K, epi, m16):
+@pytest.mark.parametrize("E,M,N,K,epi,m16,bf16", [(2, 896, 2048, 2048, 1, False, False),
+                                                  (2, 768, 2048, 2048, 2, True, False),
+                                                  (2, 1280, 2040, 512, 2, False, False),
+                                                  (1, 1800, 2048, 1024, 1, False, False),
+                                                  (2, 300, 2048, 2048, 1, False, True),
+                                                  (2, 320, 2048, 2048, 2, True, True)],
+                         ids=["shard7_fwd", "shard6_dgrad_m16", "mt10_ragged_dgrad", "e1_ragged_fwd", "bf16_split_fwd",
+                              "bf16_split_dgrad_m16"])
+def test_split_k_task_shards(E, M, N, K, epi, m16, bf16):
     """Few rows (task shards): K split over workgroups, raw partial slabs, then the finishing
     pass applies bias+ReLU or the ReLU mask (fp32 or the bf16 high plane) and writes the planes."""
     from mtrl_amd import _lib as L
@@ -131,8 +139,13 @@ def test_split_k_task_shards(E, M, N, K, epi, m16):
     C = np.zeros((E, M, N), np.float32)
     Cs = np.zeros((E, M, N), np.float32)
     p = lambda a: np.ascontiguousarray(a, np.float32).ctypes.data
-    L.check(lib.mtsac_debug_gemm_x3f(epi | (256 if m16 else 0) | 2048, E, M, N, K, p(A), p(B), C.ctypes.data,
-                                     p(bias), p(mask), Cs.ctypes.data))
+    L.check(lib.mtsac_debug_gemm_x3f(epi | (256 if m16 else 0) | 2048 | (1024 if bf16 else 0), E, M, N, K, p(A),
+                                     p(B), C.ctypes.data, p(bias), p(mask), Cs.ctypes.data))
+    if bf16:  # the products of the bf16-rounded operands
+        import torch
+
+        A = torch.from_numpy(A).to(torch.bfloat16).to(torch.float64).numpy()
+        B = torch.from_numpy(B).to(torch.bfloat16).to(torch.float64).numpy()
     acc, scale = _ref(A, B)
     if epi == 1:
         want = np.maximum(acc + bias[:, None, :], 0)
@@ -142,4 +155,9 @@ def test_split_k_task_shards(E, M, N, K, epi, m16):
         tol = 4e-6 * scale + 1e-30
     err = np.abs(C - want)
     assert np.all(err <= tol), float((err / (scale + 1e-30)).max())
-    np.testing.assert_array_equal(Cs, C)
+    if bf16:  # precision bf16 keeps (and its GEMMs read) the high plane only
+        import torch
+
+        np.testing.assert_array_equal(Cs, torch.from_numpy(C).to(torch.bfloat16).float().numpy())
+    else:
+        np.testing.assert_array_equal(Cs, C)
