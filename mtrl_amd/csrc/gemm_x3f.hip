@@ -48,15 +48,23 @@ __device__ inline bf16x8 gload_frag(const __bf16* base, unsigned voff) {
 }
 
 // s_waitcnt vmcnt(N) that also pins the B fragments it covers (the compiler cannot see the asm loads)
-template <int N, int NP>
-__device__ inline void wait_vm(bf16x8 (&b)[2][NP]) {
-  if constexpr (NP == 3)
+template <int N, int NP, int JB>
+__device__ inline void wait_vm(bf16x8 (&b)[JB][NP]) {
+  if constexpr (JB == 2 && NP == 3)
     asm volatile("s_waitcnt vmcnt(%6)"
                  : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[0][2]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[1][2])
                  : "n"(N)
                  : "memory");
-  else
+  else if constexpr (JB == 2)
     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(b[0][0]), "+v"(b[1][0]) : "n"(N) : "memory");
+  else if constexpr (NP == 3)
+    asm volatile("s_waitcnt vmcnt(%12)"
+                 : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[0][2]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[1][2]),
+                   "+v"(b[2][0]), "+v"(b[2][1]), "+v"(b[2][2]), "+v"(b[3][0]), "+v"(b[3][1]), "+v"(b[3][2])
+                 : "n"(N)
+                 : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(b[0][0]), "+v"(b[1][0]), "+v"(b[2][0]), "+v"(b[3][0]) : "n"(N) : "memory");
 }
 
 // ABL: ablation bits for experiments only (tools/x3f_ablate.py; results are wrong): 1 = no A
@@ -67,30 +75,36 @@ __device__ inline void wait_vm(bf16x8 (&b)[2][NP]) {
 // ABL == TAG_INPUT changes nothing: it only gives input-layer launches their own kernel symbol, so
 // rocprof stats and PMC passes separate them from the hidden layers.
 // NP: operand planes read (3: 6 products, fp32-accurate; 1: the high plane only, precision bf16)
-template <int BM, int EPI, bool C_OUT, bool P_OUT, bool MASK16, int ABL = 0, int NP = 3>
-__global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
+// WV: waves per workgroup.  8 (two per SIMD): wave w owns the BM x 32 column slab [32w, 32w + 32);
+// 4 (one per SIMD, up to 512 registers): BM x 64 slabs, so each A fragment read from LDS feeds twice
+// the MFMAs (4 column fragments) -- half the LDS traffic per product, the bound of the one-plane
+// (bf16) kernel, whose 8-wave skeleton saturates the LDS (256 B/clk/CU at the MFMA rate).
+template <int BM, int EPI, bool C_OUT, bool P_OUT, bool MASK16, int ABL = 0, int NP = 3, int WV = 8>
+__global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p) {
+  constexpr int JB = BN / 16 / WV;       // 16-column fragments per wave (2 or 4)
   constexpr int TI = BM / 16;            // 16-row accumulator tiles per wave
   constexpr int PLANE = BM * 128;        // bytes of one plane of one stage
   constexpr int STAGE = NP * PLANE;
   constexpr int NJ = NP * BM / 8;        // DMA wave-instructions per stage
-  constexpr int PMAX = (NJ + 7) / 8;     // per wave (the first NJ % 8 waves), others PMAX - 1
+  constexpr int PMAX = (NJ + WV - 1) / WV;  // per wave (the first NJ % WV waves), others PMAX - 1
   // every piece of the next stage is issued in the FIRST half step (spread over its row tiles), so
   // each has at least a half step to land before the drain at the next step's barrier
   constexpr int P0 = (ABL & 512) ? (PMAX + 1) / 2 : PMAX;  // 512: the old even split (experiments)
   constexpr int PW = (ABL & 512) ? P0 : PMAX - 1;  // pieces every wave has issued after B(kt, 1)
   // the epilogue reuses the ring as scratch: two 16 x (BN + 4) fp32 row-block images + 8 x BN
   // column-sum partials -- more than the ring of the short one-plane tiles holds
-  constexpr int EPI_LDS = (2 * 16 * (BN + 4) + 8 * BN) * 4;
+  constexpr int EPI_LDS = (2 * 16 * (BN + 4) + WV * BN) * 4;
   constexpr int SMEM = 2 * STAGE > EPI_LDS ? 2 * STAGE : EPI_LDS;
   static_assert(BM % 16 == 0 && SMEM <= 160 * 1024, "tile");
-  static_assert(PMAX - 1 >= PW || NJ % 8 == 0, "every wave issues >= PW pieces in the first half step");
+  static_assert(PMAX - 1 >= PW || NJ % WV == 0, "every wave issues >= PW pieces in the first half step");
+  static_assert(JB * 16 * WV == BN && (JB == 2 || JB == 4), "column slabs");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const unsigned lds_base = (unsigned)(unsigned long long)(x3pk::lds_void*)smem;
 
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  __builtin_assume(wave >= 0 && wave < 8);
-  const int mine = (wave < NJ % 8 || NJ % 8 == 0) ? PMAX : PMAX - 1;  // DMA pieces of this wave
+  __builtin_assume(wave >= 0 && wave < WV);
+  const int mine = (wave < NJ % WV || NJ % WV == 0) ? PMAX : PMAX - 1;  // DMA pieces of this wave
 
   // XCD-contiguous tile order (as gemm_x3p): N tile fastest inside an XCD's run
   const int ny = (p.N + BN - 1) / BN, nx = (p.M + BM - 1) / BM;
@@ -121,7 +135,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
     glds16(A + q * p.pA + (long long)row * p.lda + k0 + 8 * c, st + q * PLANE + rg * 1024);
   };
   auto wave_piece = [&](int qi, int k0, unsigned st) {  // this wave's qi-th piece of a stage
-    const int j = wave + 8 * qi;
+    const int j = wave + WV * qi;
     if (j < NJ) piece(j, k0, st);
   };
   // A fragment (row tile i, 32-k half s, plane q) from stage buffer `cur`
@@ -131,29 +145,31 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
     return *reinterpret_cast<const bf16x8*>(cur + q * PLANE + r * 128 + 16 * (c ^ (r & 7)));
   };
 
-  // ---- B: per lane, rows n0 + 32 wave + 16 j + (lane & 15), k chunk (lane >> 4)
-  unsigned boff[2];
+  // ---- B: per lane, rows n0 + 16 JB wave + 16 j + (lane & 15), k chunk (lane >> 4)
+  unsigned boff[JB];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    int n = n0 + 32 * wave + 16 * j + (lane & 15);
+  for (int j = 0; j < JB; ++j) {
+    int n = n0 + 16 * JB * wave + 16 * j + (lane & 15);
     n = n < p.N ? n : p.N - 1;
     boff[j] = (unsigned)(((long long)n * p.ldb + 8 * (lane >> 4)) * 2);
-    if (ABL & 64) boff[j] = (unsigned)((long long)(n0 + 32 * wave + 16 * j) * p.ldb * 2 + 16 * lane);
+    if (ABL & 64) boff[j] = (unsigned)((long long)(n0 + 16 * JB * wave + 16 * j) * p.ldb * 2 + 16 * lane);
   }
-  auto bload = [&](bf16x8 (&b)[2][NP], int k) {  // the 32-deep half step at k
+  auto bload = [&](bf16x8 (&b)[JB][NP], int k) {  // the 32-deep half step at k
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       const __bf16* base = B + q * p.pB + k;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j][q] = gload_frag(base, boff[j]);
+      for (int j = 0; j < JB; ++j) b[j][q] = gload_frag(base, boff[j]);
     }
   };
 
-  f32x4 acc[TI][2];
+  f32x4 acc[TI][JB];
 #pragma unroll
-  for (int i = 0; i < TI; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < JB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 b0[2][NP], b1[2][NP];
+  bf16x8 b0[JB][NP], b1[JB][NP];
   if ((ABL & 4) && wave >= 4) __builtin_amdgcn_s_setprio(1);
   // prologue: stage 0 + B of the first half step
 #pragma unroll
@@ -172,12 +188,12 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
     const char* cur = smem + (kt & 1) * STAGE;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8(&b)[2][NP] = s == 0 ? b0 : b1;
+      bf16x8(&b)[JB][NP] = s == 0 ? b0 : b1;
       if (s == 0) {
         if (!(ABL & 2) || kt == 0) bload(b1, kt * KS + 32);  // second half of this step
       } else {
-        if (ABL & 1) wait_vm<0, NP>(b1);
-        else wait_vm<MORE ? PW : 0, NP>(b1);  // B(kt, 1) landed; the DMA pieces issued after it may not have
+        if (ABL & 1) wait_vm<0, NP, JB>(b1);
+        else wait_vm<MORE ? PW : 0, NP, JB>(b1);  // B(kt, 1) landed; the DMA pieces issued after it may not have
         if (MORE && !(ABL & 2)) bload(b0, kn);  // first half of the next step
       }
       bf16x8 a[2][NP];
@@ -198,7 +214,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
         }
         const bf16x8(&x)[NP] = a[i & 1];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < JB; ++j) {
           f32x4 c = acc[i][j];
           if constexpr (NP == 3) {
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], b[j][1], c, 0, 0, 0);  // m*m
@@ -218,15 +234,17 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
   step(nk - 1, std::integral_constant<bool, false>{});
 
   // ---------------------------------------------------------------- epilogue
-  // Per 16-row block, the 8 waves' 16 x 32 pieces meet in an LDS image of the block's 16 x 256
-  // outputs (two buffers: one barrier per block); wave w then finishes rows 2w, 2w + 1, lane l
-  // taking 8 columns 8 (l & 31): every fp32 row leaves as 1 KB and every plane row as 512 B of
-  // contiguous 16-B lane stores (whole lines), instead of 16 rows x 64 B per instruction.
+  // Per 16-row block, the waves' 16 x 16 JB pieces meet in an LDS image of the block's 16 x 256
+  // outputs (two buffers: one barrier per block); the row pairs (2r, 2r + 1), r = wave, wave + WV,
+  // ..., are finished with lane l taking 8 columns 8 (l & 31): every fp32 row leaves as 1 KB and
+  // every plane row as 512 B of contiguous 16-B lane stores (whole lines), instead of 16 rows x 64 B
+  // per instruction.
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // the ring is free: scratch
   __builtin_amdgcn_sched_barrier(0);
   constexpr int TS = BN + 4;  // image row stride (floats): the 4 row groups of a write land 16 banks apart
+  constexpr int RP = 8 / WV;  // row pairs per wave and block
   float* img = reinterpret_cast<float*>(smem);
-  const int orow = 2 * wave + (lane >> 5), oc = 8 * (lane & 31);
+  const int oc = 8 * (lane & 31);
   const int col = n0 + oc;
   const bool colok = col < p.N;  // N % 8 == 0: a lane's 8 columns are all in or all out
   float bias[8];
@@ -243,10 +261,13 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
   for (int i = 0; i < TI; ++i) {
     float* tb = img + (i & 1) * 16 * TS;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < JB; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) tb[(4 * (lane >> 4) + r) * TS + 32 * wave + 16 * j + (lane & 15)] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) tb[(4 * (lane >> 4) + r) * TS + 16 * JB * wave + 16 * j + (lane & 15)] = acc[i][j][r];
     __syncthreads();
+#pragma unroll
+    for (int rp = 0; rp < RP; ++rp) {
+    const int orow = 2 * (wave + WV * rp) + (lane >> 5);
     const float4 u = *reinterpret_cast<const float4*>(tb + orow * TS + oc);
     const float4 v = *reinterpret_cast<const float4*>(tb + orow * TS + oc + 4);
     const int row = m0 + 16 * i + orow;
@@ -292,9 +313,10 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
         *reinterpret_cast<bf16x8*>(pp + 2 * p.pC) = l;
       }
     }
+    }  // row pairs
   }
   if (p.dbp) {  // the tile's column sums: lanes l, l + 32 of every wave hold the same 8 columns
-    float* red = img + 2 * 16 * TS;  // [8 waves][256]
+    float* red = img + 2 * 16 * TS;  // [WV waves][256]
 #pragma unroll
     for (int c = 0; c < 8; ++c) csum[c] += __shfl_xor(csum[c], 32);
     if (lane < 32) {
@@ -308,7 +330,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3f_kernel(SplitGemmParams p) {
       for (int c = 0; c < 8; ++c) {
         float a = red[oc + c];
 #pragma unroll
-        for (int w = 1; w < 8; ++w) a += red[w * BN + oc + c];
+        for (int w = 1; w < WV; ++w) a += red[w * BN + oc + c];
         t[c] = a;
       }
       float* d = p.dbp + ((long long)z * nx + bx) * p.N + col;
@@ -351,36 +373,63 @@ static long long bf16_workgroups(int M, int N, int batch) {
   return (long long)((M + bm - 1) / bm) * ((N + 255) / 256) * batch;
 }
 
+// The 4-wave form (WV = 4, 64-column slabs: half the LDS fragment reads per MFMA) is kept for the
+// ablations only: at the S3 shape its MFMA + LDS skeleton is 3-4 % faster, but with one wave per
+// SIMD the operand loads hide worse and the full kernel is 2 % (split3, 208 rows) to 20 % (bf16,
+// 208 rows vs 400) slower (profiles/r3_x3f_ablate.txt).
 template <int EPI, bool C_OUT, bool P_OUT, bool MASK16, int TAG = 0>
 void launch(const SplitGemmParams& p, dim3 grid, hipStream_t st, int bm) {
+  const dim3 blk(512);
   if (p.np != 1) {
-    hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 3>), grid, dim3(512), 0, st, p);
+    hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 3>), grid, blk, 0, st, p);
     return;
   }
   switch (bm) {
-    case 48: hipLaunchKernelGGL((gemm_x3f_kernel<48, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, dim3(512), 0, st, p); break;
-    case 80: hipLaunchKernelGGL((gemm_x3f_kernel<80, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, dim3(512), 0, st, p); break;
-    case 400: hipLaunchKernelGGL((gemm_x3f_kernel<400, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, dim3(512), 0, st, p); break;
-    default: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, dim3(512), 0, st, p); break;
+    case 48: hipLaunchKernelGGL((gemm_x3f_kernel<48, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, blk, 0, st, p); break;
+    case 80: hipLaunchKernelGGL((gemm_x3f_kernel<80, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, blk, 0, st, p); break;
+    case 400: hipLaunchKernelGGL((gemm_x3f_kernel<400, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, blk, 0, st, p); break;
+    default: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), grid, blk, 0, st, p); break;
   }
 }
 
 }  // namespace x3fk
 
-// experiments: the bench-shape forward (bias+ReLU, planes out) with ablation bits abl
+namespace x3fk {
+template <int BM, int NP, int WV>
+void ablate_at(const SplitGemmParams& p, int abl, dim3 grid, hipStream_t st) {
+  const dim3 blk(64 * WV);
+  switch (abl) {
+    case 1: hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_BIAS_RELU, false, true, false, 1, NP, WV>), grid, blk, 0, st, p); break;
+    case 2: hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_BIAS_RELU, false, true, false, 2, NP, WV>), grid, blk, 0, st, p); break;
+    case 3: hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_BIAS_RELU, false, true, false, 3, NP, WV>), grid, blk, 0, st, p); break;
+    case 64: hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_BIAS_RELU, false, true, false, 64, NP, WV>), grid, blk, 0, st, p); break;
+    case 131: hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_BIAS_RELU, false, true, false, 131, NP, WV>), grid, blk, 0, st, p); break;
+    default: hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_BIAS_RELU, false, true, false, 0, NP, WV>), grid, blk, 0, st, p); break;
+  }
+}
+}  // namespace x3fk
+
+// experiments: the bench-shape forward (bias+ReLU, planes out) with ablation bits abl (+ 1000: the
+// 4-wave, 64-column-slab workgroup); precision bf16 runs the 400-row tile
 void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t st) {
   using namespace x3fk;
-  const dim3 grid((unsigned)gemm_x3f_tiles(p.M, p.N, batch)), blk(512);
-  switch (abl) {
-    case 1: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 1>), grid, blk, 0, st, p); break;
-    case 2: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 2>), grid, blk, 0, st, p); break;
-    case 3: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 3>), grid, blk, 0, st, p); break;
-    case 4: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 4>), grid, blk, 0, st, p); break;
-    case 64: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 64>), grid, blk, 0, st, p); break;
-    case 128: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 128>), grid, blk, 0, st, p); break;
-    case 131: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 131>), grid, blk, 0, st, p); break;
-    case 512: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 512>), grid, blk, 0, st, p); break;
-    default: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 0>), grid, blk, 0, st, p); break;
+  const bool wv4 = abl >= 1000 && abl < 2000, short8 = abl >= 2000;
+  abl %= 1000;
+  const int bm = p.np == 1 && !wv4 && !short8 ? 400 : BM0;  // bf16: + 1000 / + 2000 = 208 rows, 4 / 8 waves
+  const dim3 grid((unsigned)(((p.M + bm - 1) / bm) * ((p.N + BN - 1) / BN) * batch));
+  if (p.np == 1) {
+    if (wv4) ablate_at<BM0, 1, 4>(p, abl, grid, st);
+    else if (short8) ablate_at<BM0, 1, 8>(p, abl, grid, st);
+    else ablate_at<400, 1, 8>(p, abl, grid, st);
+  } else if (wv4) {
+    ablate_at<BM0, 3, 4>(p, abl, grid, st);
+  } else if (abl == 4 || abl == 128 || abl == 512) {
+    const dim3 blk(512);
+    if (abl == 4) hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 4>), grid, blk, 0, st, p);
+    if (abl == 128) hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 128>), grid, blk, 0, st, p);
+    if (abl == 512) hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_BIAS_RELU, false, true, false, 512>), grid, blk, 0, st, p);
+  } else {
+    ablate_at<BM0, 3, 8>(p, abl, grid, st);
   }
 }
 
