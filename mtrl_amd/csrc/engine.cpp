@@ -92,6 +92,10 @@ struct Net {
   long long w0ps() const { return xld * wld; }   // plane stride of the layer-0 kernel planes
   long long kps(int i) const { return i == 0 ? w0ps() : wps(); }
   OptScalars* sc = nullptr;
+  // fused optimizer (optimize()): |g|^2 partials of the trunk / heads, |p_new|^2 partials of the
+  // heads / trunk and their counts from the last launch (the parameter norms are summed in the tail)
+  float *gparts = nullptr, *hparts = nullptr, *pph = nullptr, *ppt = nullptr;
+  int n_pph = 0, n_ppt = 0;
 
   void layout(int in, int in_ld_, int W, int D, int T, int hd_, int E_) {
     in_dim = in; in_ld = in_ld_; width = W; depth = D; T_l = T; hd = hd_; E = E_;
@@ -158,6 +162,9 @@ struct mtsac_engine {
   };
   InSet inset[2] = {};
   int inset_cur = 0;
+  // Device-sampled batches are interleaved (row i*T_l + t, buffers.py:548), so their per-task row
+  // lists are fixed: counts = n, rows[t][i] = i*T_l + t, uploaded once (no task_rows launch per step)
+  int *s_counts = nullptr, *s_rows = nullptr;
   hipEvent_t ev_ap[2] = {}, ev_tail[2] = {};  // step k's s_ap / last segment, by step parity
   bool have_prev = false;                      // a pipelined step k is in flight (its events valid)
   bool no_pipeline = getenv("MTSAC_NO_PIPELINE") != nullptr;  // experiments: whole steps only
@@ -405,20 +412,10 @@ struct mtsac_engine {
   void trunk_forward(Net& net, const float* params, int which, const float* X, int ldx, float** acts, __bf16** actp,
                      int M) {
     const bool pl = planes && which >= 0 && actp != nullptr;
+    // the input's planes were written with its fp32 rows: the gather (observations, logged
+    // actions) and the policy head (the a' / a columns of xc_next / xc_pi); rows >= M and columns
+    // >= in_dim stay zero
     __bf16* xp = pl ? in_planes(X) : nullptr;
-    if (xp) {  // the input's planes (rows >= M and columns >= in_dim stay zero)
-      SplitParams sp{};
-      sp.x = X;
-      sp.ldx = ldx;
-      sp.rows = M;
-      sp.cols = net.in_dim;
-      sp.out = xp;
-      sp.ldo = net.xld;
-      sp.po = net.arows * net.xld;
-      sp.out_rows = M;
-      sp.out_cols = (int)net.xld;
-      split_planes(sp, false, 1, cur);
-    }
     for (int i = 0; i < net.depth; ++i) {
       const bool last = i == net.depth - 1;
       if (pl && net.x3f && (i > 0 || xp)) {  // on planes, both row-major: in_i . (W_i^T)^T (gemm_x3f)
@@ -717,12 +714,19 @@ struct mtsac_engine {
     }
   }
 
-  // clip + Adam (+ Polyak) over one network; gradient already complete (and reduced).
-  // |p|^2 lands in pn[slot] (trunk, replicated) and pn[2 + slot] (local heads, summed later).
+  bool sharded() const { return comm != nullptr || hook != nullptr; }
+
+  // clip + Adam (+ Polyak) over one network; gradient already complete (and reduced).  Two launches
+  // (optim.hip sumsq2 + adam_fused): the |g|^2 partials (and the Adam count), then one update pass
+  // over heads, trunk leaves and trunk kernel tiles in which every block recomputes the global norm.
+  // The trunk's partials never mix with the heads' (bitwise-identical replicated trunks and norms
+  // on every rank); sharded, the heads' |g|^2 is the all-reduced scalar head_sq() left in the tail.
+  // |p_new|^2 partials stay per network and are summed in the last segment (norms_and_logs).
   void optimize(Net& net, float lr, float max_norm, bool polyak, int slot) {
     float* extra = net.g + net.n_flat;
-    int np = sumsq_partials(net.g + net.trunk_off, net.n_flat - net.trunk_off, partials, PART, cur);
-    grad_norm_finalize(partials, np, extra + 0, max_norm, net.sc, cur);
+    int gh = 0;
+    const int gt = sumsq2(sharded() ? nullptr : net.g, net.trunk_off, net.g + net.trunk_off, net.n_flat - net.trunk_off,
+                          net.hparts, net.gparts, net.sc, &gh, cur);
     AdamParams a{};
     a.p = net.p;
     a.m = net.m;
@@ -736,20 +740,16 @@ struct mtsac_engine {
     a.tau = cfg.tau;
     a.sc = net.sc;
     a.np = np;
-    a.p_partials = partials;
-    // heads and trunk as two launches so the trunk's reduction tree does not depend on the
-    // shard's head count (bitwise-identical replicated trunks and norms on every rank)
-    a.n = net.trunk_off;
-    int nh = adam_update(a, max_norm, 0, PART, cur);
-    sum_partials(partials, nh, pn + 2 + slot, cur);
-    a.p += net.trunk_off;
-    a.m += net.trunk_off;
-    a.v += net.trunk_off;
-    a.g += net.trunk_off;
-    if (a.target) a.target += net.trunk_off;
-    a.n = net.n_flat - net.trunk_off;
+    a.n = net.trunk_off;  // heads
+    AdamParams at = a;    // trunk
+    at.p += net.trunk_off;
+    at.m += net.trunk_off;
+    at.v += net.trunk_off;
+    at.g += net.trunk_off;
+    if (at.target) at.target += net.trunk_off;
+    at.n = net.n_flat - net.trunk_off;
+    TileParams tp{};
     if (tiles_fusable(net)) {  // kernel leaves in tiles: natural + transposed planes from the update
-      TileParams tp{};
       for (int i = 0; i < net.depth; ++i) {
         TileLeaf& lf = tp.leaf[tp.n++];
         lf.off = net.off_W[i] - net.trunk_off;
@@ -768,23 +768,29 @@ struct mtsac_engine {
         lf.tr[1] = polyak ? net.wtp[1][i] : nullptr;
         lf.tr_ld = net.wtk(i);
         lf.tr_ps = net.wtps(i);
-        a.skip_b[a.nskip] = lf.off / 4;
-        a.skip_e[a.nskip++] = (lf.off + lf.ms * net.E) / 4;
+        at.skip_b[at.nskip] = lf.off / 4;
+        at.skip_e[at.nskip++] = (lf.off + lf.ms * net.E) / 4;
       }
-      int na = adam_update(a, max_norm, 0, PART, cur);
-      a.p_partials = partials + na;
-      int nt = adam_update_tiles(a, tp, max_norm, PART, cur);
-      sum_partials(partials, na + nt, pn + slot, cur);
-      return;
-    }
-    if (planes_fusable(net))  // hidden kernels' planes (params and Polyak target) from the update
-      for (int i = 0; i < net.depth && a.nseg + 2 <= MAX_PLANE_SEGS; ++i) {
-        a.seg[a.nseg++] = PlaneSeg{net.off_W[i] - net.trunk_off, net.ms_W[i], net.E, net.wp[0][i], net.kps(i), 0};
+    } else if (planes_fusable(net)) {  // hidden kernels' planes (params and Polyak target) from the update
+      for (int i = 0; i < net.depth && at.nseg + 2 <= MAX_PLANE_SEGS; ++i) {
+        at.seg[at.nseg++] = PlaneSeg{net.off_W[i] - net.trunk_off, net.ms_W[i], net.E, net.wp[0][i], net.kps(i), 0};
         if (polyak)
-          a.seg[a.nseg++] = PlaneSeg{net.off_W[i] - net.trunk_off, net.ms_W[i], net.E, net.wp[1][i], net.kps(i), 1};
+          at.seg[at.nseg++] = PlaneSeg{net.off_W[i] - net.trunk_off, net.ms_W[i], net.E, net.wp[1][i], net.kps(i), 1};
       }
-    int na = adam_update(a, max_norm, 0, PART, cur);
-    sum_partials(partials, na, pn + slot, cur);
+    }
+    FusedOpt f{};
+    f.gparts = net.gparts;
+    f.ng = gt;
+    f.hparts = net.hparts;
+    f.nh = gh;
+    f.head_sq = sharded() ? extra + 0 : nullptr;
+    f.max_norm = max_norm;
+    f.ph = net.pph;
+    f.pt = net.ppt;
+    adam_fused(a, at, tp, f, cur);
+    net.n_pph = f.bh;
+    net.n_ppt = f.bt + f.btile;
+    if (sharded()) sum_partials(net.pph, f.bh, pn + 2 + slot, cur);  // the heads' |p|^2, all-reduced later
   }
 
   // gemm_x3f / gemm_x3s nets: every plane the GEMMs read comes out of the tiled update
@@ -911,6 +917,8 @@ struct mtsac_engine {
     pipelined = pipelined && !build && !timing_serial;
     const bool overlap = pipelined && have_prev;
     if (overlap) use_inset(inset_cur ^ 1);
+    counts = device_batch ? s_counts : inset[inset_cur].counts;
+    rows = device_batch ? s_rows : inset[inset_cur].rows;
     ev_next = 0;
     segs.clear();
     const float* twp = cfg.use_task_weights ? tw : nullptr;
@@ -921,6 +929,8 @@ struct mtsac_engine {
     pp.ls_min = cfg.log_std_min;
     pp.ls_max = cfg.log_std_max;
     pp.ld_a_out = ld_c;
+    pp.ap_ps = critic.arows * critic.xld;
+    pp.ap_ld = (int)critic.xld;
     pp.counts = counts;
     pp.rows = rows;
     pp.max_rows = Bl;
@@ -948,8 +958,8 @@ struct mtsac_engine {
         replay_gather(gp, cur);
       } else {
         batch_scatter(gp, u_obs, u_act, u_nobs, u_done, u_rew, Bl, cur);
+        task_rows(task, Bl, T_l, counts, rows, Bl, cur);  // a user batch: lists from its task ids
       }
-      task_rows(task, Bl, T_l, counts, rows, Bl, cur);
       if (cfg.use_task_weights) row_alpha(task, cfg.task_begin, log_alpha, T_g, Bl, 1, row_c, tw, cur);
     });
     // critic forward on (s, a) with the current critic (mtsac.py:555); pipelined on lane 2, which
@@ -966,6 +976,7 @@ struct mtsac_engine {
       q.eps = device_noise ? nullptr : eps_c;
       q.stream_id = 2;
       q.a_out = xcp;
+      q.a_planes = in_planes(xcp);
       q.logpi = logpi;
       q.cache = cache;
       policy_head(q, cur);
@@ -974,6 +985,7 @@ struct mtsac_engine {
       q.eps = device_noise ? nullptr : eps_n;
       q.stream_id = 1;
       q.a_out = xcn;
+      q.a_planes = in_planes(xcn);
       q.logpi = logpi_n;
       policy_head(q, cur);
     });
@@ -1009,7 +1021,7 @@ struct mtsac_engine {
     const int s_cb = backward_segs(critic, critic.p, xc, ld_c, hc, hcp, dzc, dzcp, s_cl, s_chw, Bl);
     // reduce over shards, clip + Adam + Polyak (mtsac.py:599-613)
     const int s_co = seg({s_cb}, 1, [&] {
-      head_sq(critic);
+      if (sharded()) head_sq(critic);  // the heads' |g|^2 into the all-reduced scalar tail
       reduce_rest(critic);
       optimize(critic, cfg.critic_lr, cfg.critic_max_grad_norm, true, 0);
       refresh_wt(critic, critic.p, 0, cur, true);
@@ -1060,7 +1072,7 @@ struct mtsac_engine {
       // temperature gradient rides in the actor's scalar tail: [2] loss part, [3..] grad
       AlphaParams al = alpha_params();
       alpha_grad(al, cur);
-      head_sq(actor);
+      if (sharded()) head_sq(actor);
       reduce_rest(actor);
       optimize(actor, cfg.actor_lr, cfg.actor_max_grad_norm, false, 1);
       refresh_wt(actor, actor.p, 0, cur, true);
@@ -1068,7 +1080,16 @@ struct mtsac_engine {
       alpha_adam(al, cfg.alpha_lr, cfg.adam_b1, cfg.adam_b2, cfg.adam_eps, cfg.alpha_max_grad_norm, cur);
       // post-update parameter norms: trunk |p|^2 replicated, head |p|^2 summed over shards
       allreduce(pn + 2, 2);
-      pnorm_finalize(pn, pn + 2, critic.sc, actor.sc, cur);
+      PnormParts q{};
+      Net* nets[2] = {&critic, &actor};
+      for (int w = 0; w < 2; ++w) {
+        q.pt[w] = nets[w]->ppt;
+        q.nt[w] = nets[w]->n_ppt;
+        q.ph[w] = nets[w]->pph;
+        q.nh[w] = nets[w]->n_pph;
+        q.sc[w] = nets[w]->sc;
+      }
+      pnorm_from_parts(q, sharded() ? pn + 2 : nullptr, cur);
       LogParams lp{};
       lp.critic_sums = critic.g + critic.n_flat + 1;
       lp.actor_sums = actor.g + actor.n_flat + 1;
@@ -1182,6 +1203,8 @@ struct mtsac_engine {
     const int Bl = B, n_rows = B / T_l;
     cur = st;
     cur_lane = 0;
+    counts = inset[inset_cur].counts;  // task_rows below (check_interleaved holds the layout)
+    rows = inset[inset_cur].rows;
     GatherParams gp = gather_params();
     if (device_batch) {
       replay_indices(rng, jump, buf_size, n, idx, cur);
@@ -1360,6 +1383,17 @@ struct mtsac_engine {
     // set by the host, so (r - 0) / (den - 0 + 0) = r / den in float64
     gp.norm_eps = cfg.normalize_rewards == 2 ? 0.0 : 1e-8;
     gp.err = err;
+    if (planes) {
+      gp.pa = inp[0].p;
+      gp.pa_ps = actor.arows * actor.xld;
+      gp.pa_ld = (int)actor.xld;
+      gp.pa_next = actor.krows;
+      gp.pc = in_planes(xc);
+      gp.pcn = in_planes(xcn);
+      gp.pcp = in_planes(xcp);
+      gp.pc_ps = critic.arows * critic.xld;
+      gp.pc_ld = (int)critic.xld;
+    }
     return gp;
   }
 
@@ -1494,6 +1528,9 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     if ((rc = e->alloc(&net->m, net->n_flat))) return bad(rc);
     if ((rc = e->alloc(&net->v, net->n_flat))) return bad(rc);
     if ((rc = e->alloc(&net->sc, 1))) return bad(rc);
+    if ((rc = e->alloc(&net->gparts, 1024)) || (rc = e->alloc(&net->hparts, FUSED_HEAD_PARTS)) ||
+        (rc = e->alloc(&net->pph, FUSED_HEAD_PARTS)) || (rc = e->alloc(&net->ppt, 2048)))
+      return bad(rc);
   }
   if ((rc = e->alloc(&e->critic.tgt, e->critic.n_flat))) return bad(rc);
   e->planes = c.precision == MTSAC_FP32_SPLIT3 || c.precision == MTSAC_BF16;
@@ -1571,6 +1608,15 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   e->task = e->inset[0].task;
   e->counts = e->inset[0].counts;
   e->rows = e->inset[0].rows;
+  {
+    std::vector<int> sc(e->T_l, e->n), sr((size_t)e->T_l * B, 0);
+    for (int t = 0; t < e->T_l; ++t)
+      for (int i = 0; i < e->n; ++i) sr[(size_t)t * B + i] = i * e->T_l + t;
+    if ((rc = e->alloc(&e->s_counts, e->T_l)) || (rc = e->alloc(&e->s_rows, (size_t)e->T_l * B))) return bad(rc);
+    if (hipMemcpy(e->s_counts, sc.data(), sizeof(int) * sc.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(e->s_rows, sr.data(), sizeof(int) * sr.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return bad(fail(-5, "row lists"));
+  }
   if ((rc = e->alloc(&e->xc, (size_t)B * e->ld_c))) return bad(rc);
   if ((rc = e->alloc(&e->xcn, (size_t)B * e->ld_c))) return bad(rc);
   if ((rc = e->alloc(&e->xcp, (size_t)B * e->ld_c))) return bad(rc);

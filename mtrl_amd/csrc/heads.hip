@@ -10,6 +10,7 @@
 #include "devrng.h"
 #include <algorithm>
 
+#include "gemm_common.h"
 #include "kernels.h"
 
 namespace mtsac {
@@ -131,6 +132,14 @@ __device__ inline void policy_finish(const PolicyParams& p, int b, int t, const 
     term = -0.5f * eps * eps - HALF_LOG_2PI - logf(sigma) - 2.0f * (LOG2F - x - softplusf(-2.0f * x));
     p.a_out[(long long)b * p.ld_a_out + lane] = a;
     if (p.a_out2) p.a_out2[(long long)b * p.ld_a_out2 + lane] = a;
+    if (p.a_planes) {  // the critic input's planes of the action columns (the obs columns: the gather)
+      __bf16 h, m, l;
+      split3_dev(a, h, m, l);
+      const long long o = (long long)b * p.ap_ld + lane;
+      p.a_planes[o] = h;
+      p.a_planes[o + p.ap_ps] = m;
+      p.a_planes[o + 2 * p.ap_ps] = l;
+    }
     if (p.cache) {
       float* c = p.cache + (long long)b * 5 * A;
       c[lane] = mu;

@@ -159,6 +159,15 @@ struct GatherParams {
   const double* rmax;
   double norm_eps;
   int* err;             // error flag (one-hot violation)
+  // bf16 planes of the GEMM inputs (split3 / bf16 engines; null otherwise), written beside the fp32
+  // rows so no split pass runs before the trunk forward: xa's [3][.][pa_ld] (s rows at b, s' rows at
+  // pa_next + b), xc / xc_next / xc_pi's [3][.][pc_ld] (the a' / a columns come from the policy head)
+  __bf16* pa;
+  long long pa_ps, pa_next;
+  int pa_ld;
+  __bf16 *pc, *pcn, *pcp;
+  long long pc_ps;
+  int pc_ld;
 };
 void replay_gather(const GatherParams& p, hipStream_t st);
 // a user batch (ReplayBufferSamples layout) into the same input buffers
@@ -198,6 +207,9 @@ struct PolicyParams {
   int ld_a_out;
   float* a_out2;        // optional second copy
   int ld_a_out2;
+  __bf16* a_planes;     // optional bf16 planes of a_out's action columns ([3][.][ap_ld], plane stride ap_ps)
+  long long ap_ps;
+  int ap_ld;
   float* logpi;         // [B]
   float* cache;         // optional [B][5A]: mu, ls, x, a, eps
   // optional per-task row lists (task_rows): rows grouped by task share head-kernel reads
@@ -332,6 +344,30 @@ void pnorm_finalize(const float* trunk_sq, const float* head_sq, OptScalars* s0,
 // *out = sum(partials)  (one block, double accumulation)
 void sum_partials(const float* partials, int nparts, float* out, hipStream_t st);
 void adam_count_incr(OptScalars* sc, hipStream_t st);
+// Fused optimizer step of one network (two launches): sumsq2 writes the |g|^2 partials of the heads'
+// range [hparts, gh of them; h null: none] and the trunk's [tparts, returned count] and bumps the
+// Adam count; adam_fused recomputes the global norm in every block (trunk partials + head partials,
+// or the all-reduced head |g|^2 when head_sq is set), then updates the heads (ah) elementwise and
+// the trunk (at) elementwise + in 64 x 64 tiles (tp; total 0: none), |p_new|^2 partials to ph / pt.
+constexpr int FUSED_HEAD_PARTS = 256;
+struct FusedOpt {
+  const float* gparts; int ng;      // trunk |g|^2 partials
+  const float* hparts; int nh;      // head |g|^2 partials (unsharded) ...
+  const float* head_sq;             // ... or the all-reduced head |g|^2 (sharded), else null
+  float max_norm;
+  float *ph, *pt;                   // |p_new|^2 partials out: heads [bh], trunk [bt + btile]
+  int bh, bt, btile;                // set by adam_fused
+};
+int sumsq2(const float* h, long long nh, const float* t, long long nt, float* hparts, float* tparts, OptScalars* sc,
+           int* gh_out, hipStream_t st);
+void adam_fused(const AdamParams& ah, const AdamParams& at, const TileParams& tp, FusedOpt& f, hipStream_t st);
+struct PnormParts {  // [0] critic, [1] actor
+  const float* pt[2]; int nt[2];
+  const float* ph[2]; int nh[2];
+  OptScalars* sc[2];
+};
+// sc[w]->pnorm = sqrt(sum pt[w] + (head_sq ? head_sq[w] : sum ph[w]))
+void pnorm_from_parts(const PnormParts& q, const float* head_sq, hipStream_t st);
 
 struct AlphaParams {
   const float* logpi;   // [B] (actor pass)

@@ -85,15 +85,30 @@ __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restri
 // clip (t / ||g||) * max when !(||g|| < max); Adam: mu = (1-b1) g + b1 mu,
 // nu = (1-b2) g^2 + b2 nu, mu_hat = mu / (1 - b1^k), nu_hat = nu / (1 - b2^k),
 // p += -lr * mu_hat / (sqrt(nu_hat) + eps); then target = tau p + (1 - tau) target.
+struct AdamConsts {
+  bool clip;
+  float gn, max_norm, bc1, bc2, omb1, omb2, neg_lr, omtau;
+};
+
+__device__ inline AdamConsts adam_consts(const AdamParams& a, float gnorm, int count, float max_norm) {
+  AdamConsts k;
+  k.clip = (max_norm >= 0.f) && !(gnorm < max_norm);
+  k.gn = gnorm;
+  k.max_norm = max_norm;
+  k.bc1 = 1.0f - powf(a.b1, (float)count);
+  k.bc2 = 1.0f - powf(a.b2, (float)count);
+  k.omb1 = 1.0f - a.b1;
+  k.omb2 = 1.0f - a.b2;
+  k.neg_lr = -a.lr;
+  k.omtau = 1.0f - a.tau;
+  return k;
+}
+
+// the elementwise pass over float4 i = blk, blk + nblk, ... < n4 (tiled leaves skipped); returns
+// this thread's |p_new|^2 over i >= norm_from4
 template <bool POLYAK>
-__global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm, long long norm_from4) {
-  const OptScalars sc = *a.sc;
-  const bool clip = (max_norm >= 0.f) && !(sc.gnorm < max_norm);
-  const float gn = sc.gnorm;
-  const float bc1 = 1.0f - powf(a.b1, (float)sc.count);
-  const float bc2 = 1.0f - powf(a.b2, (float)sc.count);
-  const float omb1 = 1.0f - a.b1, omb2 = 1.0f - a.b2, neg_lr = -a.lr;
-  const float omtau = 1.0f - a.tau;
+__device__ inline float adam_elems(const AdamParams& a, const AdamConsts& k, long long norm_from4, long long blk,
+                                   long long nblk) {
   const long long n4 = a.n >> 2;
   float acc = 0.f;
   float4* p4 = reinterpret_cast<float4*>(a.p);
@@ -101,10 +116,10 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm,
   float4* v4 = reinterpret_cast<float4*>(a.v);
   const float4* g4 = reinterpret_cast<const float4*>(a.g);
   float4* t4 = reinterpret_cast<float4*>(a.target);
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+  for (long long i = blk * 256 + threadIdx.x; i < n4; i += nblk * 256) {
     bool skip = false;
-    for (int k = 0; k < a.nskip; ++k) skip |= i >= a.skip_b[k] && i < a.skip_e[k];
-    if (skip) continue;  // a tiled leaf (adam_tiles_kernel)
+    for (int q = 0; q < a.nskip; ++q) skip |= i >= a.skip_b[q] && i < a.skip_e[q];
+    if (skip) continue;  // a tiled leaf (adam_tiles)
     float4 g = g4[i], p = p4[i], m = m4[i], v = v4[i];
     float* gp = &g.x;
     float* pp = &p.x;
@@ -112,16 +127,16 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm,
     float* vp = &v.x;
     float sq = 0.f;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float gk = gp[k];
-      if (clip) gk = (gk / gn) * max_norm;
-      mp[k] = omb1 * gk + a.b1 * mp[k];
-      vp[k] = omb2 * (gk * gk) + a.b2 * vp[k];
-      const float mh = mp[k] / bc1;
-      const float vh = vp[k] / bc2;
+    for (int c = 0; c < 4; ++c) {
+      float gk = gp[c];
+      if (k.clip) gk = (gk / k.gn) * k.max_norm;
+      mp[c] = k.omb1 * gk + a.b1 * mp[c];
+      vp[c] = k.omb2 * (gk * gk) + a.b2 * vp[c];
+      const float mh = mp[c] / k.bc1;
+      const float vh = vp[c] / k.bc2;
       const float u = mh / (sqrtf(vh) + a.eps);
-      pp[k] = pp[k] + u * neg_lr;
-      sq += pp[k] * pp[k];
+      pp[c] = pp[c] + u * k.neg_lr;
+      sq += pp[c] * pp[c];
     }
     if (i >= norm_from4) acc += sq;  // |p|^2 of the replicated (trunk) range only
     p4[i] = p;
@@ -130,17 +145,17 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm,
     float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
     if (POLYAK) {
       t = t4[i];
-      t.x = a.tau * p.x + omtau * t.x;
-      t.y = a.tau * p.y + omtau * t.y;
-      t.z = a.tau * p.z + omtau * t.z;
-      t.w = a.tau * p.w + omtau * t.w;
+      t.x = a.tau * p.x + k.omtau * t.x;
+      t.y = a.tau * p.y + k.omtau * t.y;
+      t.z = a.tau * p.z + k.omtau * t.z;
+      t.w = a.tau * p.w + k.omtau * t.w;
       t4[i] = t;
     }
     for (int sg = 0; sg < a.nseg; ++sg) {  // split planes of the new values (next GEMMs' operands)
       const PlaneSeg& ps = a.seg[sg];
       const long long f = 4 * i - ps.begin;
       if (f < 0 || f >= ps.member_n * ps.members) continue;
-      const long long e = f / ps.member_n, k = f - e * ps.member_n;
+      const long long e = f / ps.member_n, kk = f - e * ps.member_n;
       const float* src = ps.of_target ? &t.x : pp;
       typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
       bf16x4 h, mm, l;
@@ -153,7 +168,7 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm,
         mm[c] = m1;
         l[c] = (__bf16)(r1 - (float)m1);
       }
-      __bf16* dst = ps.planes + e * 3 * ps.ps + k;
+      __bf16* dst = ps.planes + e * 3 * ps.ps + kk;
       *reinterpret_cast<bf16x4*>(dst) = h;
       if (a.np != 1) {
         *reinterpret_cast<bf16x4*>(dst + ps.ps) = mm;
@@ -161,6 +176,14 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm,
       }
     }
   }
+  return acc;
+}
+
+template <bool POLYAK>
+__global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm, long long norm_from4) {
+  const OptScalars sc = *a.sc;
+  const AdamConsts k = adam_consts(a, sc.gnorm, sc.count, max_norm);
+  float acc = adam_elems<POLYAK>(a, k, norm_from4, blockIdx.x, gridDim.x);
   acc = block_sum256(acc);
   if (threadIdx.x == 0) a.p_partials[blockIdx.x] = acc;
 }
@@ -170,20 +193,13 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm,
 // LDS so the transposed planes leave as 2 x 16 B per lane (16 k of one output row).
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+// 64 x 64 tile pass over tiles blk, blk + nblk, ... of tp; returns this thread's |p_new|^2
 template <bool POLYAK>
-__global__ __launch_bounds__(256) void adam_tiles_kernel(AdamParams a, TileParams tp, float max_norm) {
-  __shared__ float sp[64][65];
-  __shared__ float stg[POLYAK ? 64 : 1][65];
-  const OptScalars sc = *a.sc;
-  const bool clip = (max_norm >= 0.f) && !(sc.gnorm < max_norm);
-  const float gn = sc.gnorm;
-  const float bc1 = 1.0f - powf(a.b1, (float)sc.count);
-  const float bc2 = 1.0f - powf(a.b2, (float)sc.count);
-  const float omb1 = 1.0f - a.b1, omb2 = 1.0f - a.b2, neg_lr = -a.lr;
-  const float omtau = 1.0f - a.tau;
-  const int t = threadIdx.x, rr = t >> 4, c4 = 4 * (t & 15);
+__device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, const AdamConsts& k, int blk, int nblk,
+                                   float (*sp)[65], float (*stg)[65]) {
   float acc = 0.f;
-  for (int tile = blockIdx.x; tile < tp.total; tile += gridDim.x) {
+  const int t = threadIdx.x, rr = t >> 4, c4 = 4 * (t & 15);
+  for (int tile = blk; tile < tp.total; tile += nblk) {
     int L = 0;
     while (L + 1 < tp.n && tile >= tp.leaf[L + 1].tile_begin) ++L;
     const TileLeaf& lf = tp.leaf[L];
@@ -207,26 +223,26 @@ __global__ __launch_bounds__(256) void adam_tiles_kernel(AdamParams a, TileParam
         float* mp = &m.x;
         float* vp = &v.x;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          float gk = gp[k];
-          if (clip) gk = (gk / gn) * max_norm;
-          mp[k] = omb1 * gk + a.b1 * mp[k];
-          vp[k] = omb2 * (gk * gk) + a.b2 * vp[k];
-          const float mh = mp[k] / bc1;
-          const float vh = vp[k] / bc2;
+        for (int q = 0; q < 4; ++q) {
+          float gk = gp[q];
+          if (k.clip) gk = (gk / k.gn) * k.max_norm;
+          mp[q] = k.omb1 * gk + a.b1 * mp[q];
+          vp[q] = k.omb2 * (gk * gk) + a.b2 * vp[q];
+          const float mh = mp[q] / k.bc1;
+          const float vh = vp[q] / k.bc2;
           const float u = mh / (sqrtf(vh) + a.eps);
-          pp[k] = pp[k] + u * neg_lr;
-          acc += pp[k] * pp[k];
+          pp[q] = pp[q] + u * k.neg_lr;
+          acc += pp[q] * pp[q];
         }
         reinterpret_cast<float4*>(a.p)[i4] = p;
         reinterpret_cast<float4*>(a.m)[i4] = m;
         reinterpret_cast<float4*>(a.v)[i4] = v;
         if (POLYAK) {
           tv = reinterpret_cast<float4*>(a.target)[i4];
-          tv.x = a.tau * p.x + omtau * tv.x;
-          tv.y = a.tau * p.y + omtau * tv.y;
-          tv.z = a.tau * p.z + omtau * tv.z;
-          tv.w = a.tau * p.w + omtau * tv.w;
+          tv.x = a.tau * p.x + k.omtau * tv.x;
+          tv.y = a.tau * p.y + k.omtau * tv.y;
+          tv.z = a.tau * p.z + k.omtau * tv.z;
+          tv.w = a.tau * p.w + k.omtau * tv.w;
           reinterpret_cast<float4*>(a.target)[i4] = tv;
         }
 #pragma unroll
@@ -236,10 +252,10 @@ __global__ __launch_bounds__(256) void adam_tiles_kernel(AdamParams a, TileParam
           const float* src = w ? &tv.x : &p.x;
           bf16x4_t h, mm, l;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
+          for (int q = 0; q < 4; ++q) {
             __bf16 x0, x1, x2;
-            split3_dev(src[k], x0, x1, x2);
-            h[k] = x0; mm[k] = x1; l[k] = x2;
+            split3_dev(src[q], x0, x1, x2);
+            h[q] = x0; mm[q] = x1; l[q] = x2;
           }
           __bf16* dst = np_ + e * 3 * lf.nat_ps + (long long)r * lf.nat_ld + c;
           *reinterpret_cast<bf16x4_t*>(dst) = h;
@@ -258,8 +274,8 @@ __global__ __launch_bounds__(256) void adam_tiles_kernel(AdamParams a, TileParam
     __syncthreads();
     {  // transposed planes: output row o (a column of the leaf), k = r0 + 16 (t & 3) .. + 15
       const int oc = t >> 2, kq = 16 * (t & 3);
-      const int o = c0 + oc, k = r0 + kq;
-      if (o < lf.cols && k < lf.tr_ld) {
+      const int o = c0 + oc, kk = r0 + kq;
+      if (o < lf.cols && kk < lf.tr_ld) {
 #pragma unroll
         for (int w = 0; w < 2; ++w) {
           __bf16* tp_ = lf.tr[w];
@@ -272,10 +288,10 @@ __global__ __launch_bounds__(256) void adam_tiles_kernel(AdamParams a, TileParam
             split3_dev(x, x0, x1, x2);
             h[q >> 3][q & 7] = x0; mm[q >> 3][q & 7] = x1; l[q >> 3][q & 7] = x2;
           }
-          __bf16* dst = tp_ + e * 3 * lf.tr_ps + (long long)o * lf.tr_ld + k;
+          __bf16* dst = tp_ + e * 3 * lf.tr_ps + (long long)o * lf.tr_ld + kk;
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
-            if (k + 8 * hh >= lf.tr_ld) break;
+            if (kk + 8 * hh >= lf.tr_ld) break;
             *reinterpret_cast<bf16x8*>(dst + 8 * hh) = h[hh];
             if (a.np != 1) {
               *reinterpret_cast<bf16x8*>(dst + lf.tr_ps + 8 * hh) = mm[hh];
@@ -287,8 +303,88 @@ __global__ __launch_bounds__(256) void adam_tiles_kernel(AdamParams a, TileParam
     }
     __syncthreads();
   }
+  return acc;
+}
+
+template <bool POLYAK>
+__global__ __launch_bounds__(256) void adam_tiles_kernel(AdamParams a, TileParams tp, float max_norm) {
+  __shared__ float sp[64][65];
+  __shared__ float stg[POLYAK ? 64 : 1][65];
+  const OptScalars sc = *a.sc;
+  const AdamConsts k = adam_consts(a, sc.gnorm, sc.count, max_norm);
+  float acc = adam_tiles<POLYAK>(a, tp, k, blockIdx.x, gridDim.x, sp, stg);
   acc = block_sum256(acc);
   if (threadIdx.x == 0) a.p_partials[blockIdx.x] = acc;
+}
+
+// One launch for a whole network's optimizer step (engine.cpp optimize): every block recomputes the
+// global gradient norm from the sum-of-squares partials in the same fixed order (so every block, and
+// every rank's replicated trunk, sees the same clip factor), then blocks [0, bh) run the heads'
+// elementwise update, [bh, bh + bt) the trunk's elementwise leaves, the rest its 64 x 64 kernel
+// tiles.  |p_new|^2 partials: heads to f.ph[blk], trunk to f.pt[blk - bh].
+template <bool POLYAK>
+__global__ __launch_bounds__(256) void adam_fused_kernel(AdamParams ah, AdamParams at, TileParams tp, FusedOpt f) {
+  __shared__ float sp[64][65];
+  __shared__ float stg[POLYAK ? 64 : 1][65];
+  __shared__ double red[4];
+  __shared__ float gsh;
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < f.ng; i += 256) acc += (double)f.gparts[i];
+  acc = wsumd(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot = (red[0] + red[1]) + (red[2] + red[3]);
+    float head = 0.f;
+    if (f.head_sq) {
+      head = *f.head_sq;
+    } else {
+      double h = 0.0;
+      for (int i = 0; i < f.nh; ++i) h += (double)f.hparts[i];
+      head = (float)h;
+    }
+    gsh = (float)sqrt(tot + (double)head);
+  }
+  __syncthreads();
+  const float gn = gsh;
+  const int count = ah.sc->count;  // incremented by the sum-of-squares launch
+  float pa = 0.f;
+  const int b = blockIdx.x;
+  if (b < f.bh) {
+    pa = adam_elems<POLYAK>(ah, adam_consts(ah, gn, count, f.max_norm), 0, b, f.bh);
+  } else if (b < f.bh + f.bt) {
+    pa = adam_elems<POLYAK>(at, adam_consts(at, gn, count, f.max_norm), 0, b - f.bh, f.bt);
+  } else {
+    pa = adam_tiles<POLYAK>(at, tp, adam_consts(at, gn, count, f.max_norm), b - f.bh - f.bt, f.btile, sp, stg);
+  }
+  pa = block_sum256(pa);
+  if (threadIdx.x == 0) {
+    if (b < f.bh) f.ph[b] = pa;
+    else f.pt[b - f.bh] = pa;
+    if (b == 0) ah.sc->gnorm = gn;
+  }
+}
+
+// |g|^2 partials of a network: blocks [0, gh) over the heads' range, [gh, gh + gt) over the trunk's;
+// block 0 bumps the Adam step count (optax's count, read by adam_fused_kernel)
+__global__ __launch_bounds__(256) void sumsq2_kernel(const float* __restrict__ h, long long nh4, int gh,
+                                                     const float* __restrict__ t, long long nt4, float* __restrict__ hp,
+                                                     float* __restrict__ tp, OptScalars* sc) {
+  const bool head = (int)blockIdx.x < gh;
+  const float4* x4 = reinterpret_cast<const float4*>(head ? h : t);
+  const long long n4 = head ? nh4 : nt4;
+  const long long b = head ? blockIdx.x : blockIdx.x - gh, nb = head ? gh : gridDim.x - gh;
+  float acc = 0.f;
+  for (long long i = b * 256 + threadIdx.x; i < n4; i += nb * 256) {
+    const float4 v = x4[i];
+    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  acc = block_sum256(acc);
+  if (threadIdx.x == 0) {
+    if (head) hp[b] = acc;
+    else tp[b] = acc;
+    if (blockIdx.x == 0) sc->count += 1;
+  }
 }
 
 struct RowPtrs {
@@ -437,8 +533,48 @@ __global__ void pnorm_finalize_kernel(const float* __restrict__ trunk_sq, const 
   s1->pnorm = sqrtf(trunk_sq[1] + head_sq[1]);
 }
 
+// both networks' post-update |p| from their fused-Adam partials: trunk sums (and, unsharded, the
+// head sums; sharded: the all-reduced head sums in head_sq) in fixed order, one wave per network
+__global__ __launch_bounds__(128) void pnorm_parts_kernel(PnormParts q, const float* __restrict__ head_sq) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double t = 0.0, h = 0.0;
+  for (int i = lane; i < q.nt[w]; i += 64) t += (double)q.pt[w][i];
+  for (int i = lane; i < q.nh[w]; i += 64) h += (double)q.ph[w][i];
+  t = wsumd(t);
+  h = wsumd(h);
+  if (lane == 0) {
+    const float hs = head_sq ? head_sq[w] : (float)h;
+    q.sc[w]->pnorm = sqrtf((float)t + hs);
+  }
+}
+
 void pnorm_finalize(const float* trunk_sq, const float* head_sq, OptScalars* s0, OptScalars* s1, hipStream_t st) {
   hipLaunchKernelGGL(pnorm_finalize_kernel, dim3(1), dim3(1), 0, st, trunk_sq, head_sq, s0, s1);
+}
+
+void pnorm_from_parts(const PnormParts& q, const float* head_sq, hipStream_t st) {
+  hipLaunchKernelGGL(pnorm_parts_kernel, dim3(1), dim3(128), 0, st, q, head_sq);
+}
+
+int sumsq2(const float* h, long long nh, const float* t, long long nt, float* hparts, float* tparts, OptScalars* sc,
+           int* gh_out, hipStream_t st) {
+  const long long nh4 = nh >> 2, nt4 = nt >> 2;
+  const int gh = h ? (int)std::max<long long>(1, std::min<long long>(FUSED_HEAD_PARTS, (nh4 + 255) / 256)) : 0;
+  const int gt = (int)std::max<long long>(1, std::min<long long>(1024, (nt4 + 255) / 256));
+  hipLaunchKernelGGL(sumsq2_kernel, dim3((unsigned)(gh + gt)), dim3(256), 0, st, h, nh4, gh, t, nt4, hparts, tparts, sc);
+  *gh_out = gh;
+  return gt;
+}
+
+void adam_fused(const AdamParams& ah, const AdamParams& at, const TileParams& tp, FusedOpt& f, hipStream_t st) {
+  f.bh = (int)std::max<long long>(1, std::min<long long>(FUSED_HEAD_PARTS, ((ah.n >> 2) + 255) / 256));
+  f.bt = (int)std::max<long long>(1, std::min<long long>(1024, ((at.n >> 2) + 255) / 256));
+  f.btile = std::min(tp.total, 1024);
+  const dim3 grid((unsigned)(f.bh + f.bt + f.btile));
+  if (at.target)
+    hipLaunchKernelGGL(adam_fused_kernel<true>, grid, dim3(256), 0, st, ah, at, tp, f);
+  else
+    hipLaunchKernelGGL(adam_fused_kernel<false>, grid, dim3(256), 0, st, ah, at, tp, f);
 }
 
 void sum_partials(const float* partials, int nparts, float* out, hipStream_t st) {

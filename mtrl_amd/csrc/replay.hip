@@ -9,6 +9,7 @@
 // (36.8 KB at MT50), which the gather kernel streams with coalesced 4-byte lanes
 // straight into the GEMM-ready input matrices (padded, zero-filled widths).
 #include "devrng.h"
+#include "gemm_common.h"
 #include "kernels.h"
 
 namespace mtsac {
@@ -146,6 +147,15 @@ __global__ __launch_bounds__(256) void gather_kernel(GatherParams p, const float
   float* xcn = p.xc_next + (long long)b * p.ld_c;
   float* xcp = p.xc_pi + (long long)b * p.ld_c;
   const int oh0 = D - p.T_glob;  // first one-hot column
+  // the planes of the same entries: x = h + m + l (split3_dev)
+  auto put = [](__bf16* q, long long ps, long long o, float x) {
+    __bf16 h, m, l;
+    split3_dev(x, h, m, l);
+    q[o] = h;
+    q[o + ps] = m;
+    q[o + 2 * ps] = l;
+  };
+  const long long oa = (long long)b * p.pa_ld, oan = (p.pa_next + b) * p.pa_ld, oc = (long long)b * p.pc_ld;
   int ones = 0, first = 0x7fffffff, bad = 0, n_ones = 0, n_first = 0x7fffffff, n_bad = 0;
   for (int c = lane; c < D; c += 64) {
     const float v = SRC_STORE ? rec[c] : u_obs[(long long)b * D + c];
@@ -155,6 +165,13 @@ __global__ __launch_bounds__(256) void gather_kernel(GatherParams p, const float
     xcp[A + c] = v;
     xan[c] = w;
     xcn[A + c] = w;
+    if (p.pa) {
+      put(p.pa, p.pa_ps, oa + c, v);
+      put(p.pa, p.pa_ps, oan + c, w);
+      put(p.pc, p.pc_ps, oc + A + c, v);
+      put(p.pcp, p.pc_ps, oc + A + c, v);
+      put(p.pcn, p.pc_ps, oc + A + c, w);
+    }
     if (c >= oh0) {
       if (v == 1.0f) { ++ones; first = min(first, c - oh0); }
       else if (v != 0.0f) bad = 1;
@@ -162,7 +179,11 @@ __global__ __launch_bounds__(256) void gather_kernel(GatherParams p, const float
       else if (w != 0.0f) n_bad = 1;
     }
   }
-  if (lane < A) xc[lane] = SRC_STORE ? rec[D + lane] : u_act[(long long)b * A + lane];
+  if (lane < A) {
+    const float a = SRC_STORE ? rec[D + lane] : u_act[(long long)b * A + lane];
+    xc[lane] = a;
+    if (p.pa) put(p.pc, p.pc_ps, oc + lane, a);
+  }
   ones = wave_sum_i(ones);
   n_ones = wave_sum_i(n_ones);
   bad = wave_sum_i(bad + n_bad);

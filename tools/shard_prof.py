@@ -6,10 +6,11 @@ from mtrl_amd import _lib as L  # noqa: E402
 from mtrl_amd.engine import MTSACEngine, make_config  # noqa: E402
 from mtrl_amd.init import init_mtsac  # noqa: E402
 
-T, W = 50, 2048
 tl = int(sys.argv[1]) if len(sys.argv) > 1 else 7
+T = int(sys.argv[2]) if len(sys.argv) > 2 else 50  # usage: shard_prof.py T_local [T W]
+W = int(sys.argv[3]) if len(sys.argv) > 3 else 2048
 cfg = make_config(num_tasks=T, task_begin=0, task_count=tl, obs_dim=39 + T, actor_width=W, critic_width=W,
-                  batch_per_task=128, capacity=100_000, clip=1, precision=1)
+                  batch_per_task=128, capacity=20_000, clip=1, precision=1)
 eng = MTSACEngine(cfg, device=0)
 actor, critic = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=1, task_begin=0, task_count=tl)
 eng.set_params(L.ACTOR, actor)
