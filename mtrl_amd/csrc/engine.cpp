@@ -652,9 +652,12 @@ struct mtsac_engine {
           SplitGemmParams q = g;
           q.C = nullptr;
           q.dbp = net.dbp[i - 1];
-          const bool fused = gemm_x3f_ok(q, EPI_RELU_MASK, net.E);
-          if (fused) g = q;
-          net.dbp_chunks[i - 1] = fused ? (M + gemm_x3f_bm(q, net.E) - 1) / gemm_x3f_bm(q, net.E) : 0;
+          // (or gemm_x3s, the same partials over its 16 TI-row tiles)
+          const bool fx = gemm_x3f_ok(q, EPI_RELU_MASK, net.E);
+          const bool fs = !fx && !gemm_x3f_ok(g, EPI_RELU_MASK, net.E) && gemm_x3s_ok(q, EPI_RELU_MASK, net.E);
+          if (fx || fs) g = q;
+          const int bm = fx ? gemm_x3f_bm(q, net.E) : 16 * gemm_x3s_ti(M, net.width, net.E);
+          net.dbp_chunks[i - 1] = (fx || fs) ? (M + bm - 1) / bm : 0;
         }
       }
       gemmp(g, EPI_RELU_MASK, net.E, MTSAC_FAM_DATA_GRAD);
@@ -1012,8 +1015,10 @@ struct mtsac_engine {
       c.inv_norm = 1.0f / ((float)critic.E * (float)B_glob);
       critic_head(c, cur);
       head_bwd(critic, chp, dq, Bl, dzc, dzcp, true);
-      const float* ins[2] = {row_a, row_b};
-      reduce_rows(ins, 2, Bl, critic.g + critic.n_flat + 1, cur);
+      if (sharded()) {  // the loss sums ride in the all-reduced scalar tail (else: step_finish)
+        const float* ins[2] = {row_a, row_b};
+        reduce_rows(ins, 2, Bl, critic.g + critic.n_flat + 1, cur);
+      }
     });
     const int s_chw = seg({s_cl}, 3, [&] {
       head_backward_weight(chp, dq, Bl, counts, rows, Bl, critic.g + critic.off_hW, critic.g + critic.off_hb, cur);
@@ -1056,8 +1061,10 @@ struct mtsac_engine {
       ag.ls_max = cfg.log_std_max;
       ag.dout = dout_a;
       action_grad(ag, cur);
-      const float* ins[1] = {row_c};
-      reduce_rows(ins, 1, Bl, actor.g + actor.n_flat + 1, cur);
+      if (sharded()) {
+        const float* ins[1] = {row_c};
+        reduce_rows(ins, 1, Bl, actor.g + actor.n_flat + 1, cur);
+      }
     });
     if (pipelined) (void)hipEventRecord(ev_ap[step_par], segs[s_ap].lane);
     const HeadParams ahp = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
@@ -1076,21 +1083,35 @@ struct mtsac_engine {
       reduce_rest(actor);
       optimize(actor, cfg.actor_lr, cfg.actor_max_grad_norm, false, 1);
       refresh_wt(actor, actor.p, 0, cur, true);
-      // temperature (mtsac.py:713-731)
-      alpha_adam(al, cfg.alpha_lr, cfg.adam_b1, cfg.adam_b2, cfg.adam_eps, cfg.alpha_max_grad_norm, cur);
-      // post-update parameter norms: trunk |p|^2 replicated, head |p|^2 summed over shards
+      // temperature (mtsac.py:713-731), post-update parameter norms (trunk |p|^2 replicated, head
+      // |p|^2 summed over shards), logs: one launch
       allreduce(pn + 2, 2);
-      PnormParts q{};
+      StepFinish f{};
+      if (!sharded()) {
+        f.rows[0] = row_a;
+        f.row_out[0] = critic.g + critic.n_flat + 1;
+        f.rows[1] = row_b;
+        f.row_out[1] = critic.g + critic.n_flat + 2;
+        f.rows[2] = row_c;
+        f.row_out[2] = actor.g + actor.n_flat + 1;
+      }
+      f.B = Bl;
+      f.alpha = al;
+      f.lr = cfg.alpha_lr;
+      f.b1 = cfg.adam_b1;
+      f.b2 = cfg.adam_b2;
+      f.eps = cfg.adam_eps;
+      f.max_norm = cfg.alpha_max_grad_norm;
       Net* nets[2] = {&critic, &actor};
       for (int w = 0; w < 2; ++w) {
-        q.pt[w] = nets[w]->ppt;
-        q.nt[w] = nets[w]->n_ppt;
-        q.ph[w] = nets[w]->pph;
-        q.nh[w] = nets[w]->n_pph;
-        q.sc[w] = nets[w]->sc;
+        f.pn.pt[w] = nets[w]->ppt;
+        f.pn.nt[w] = nets[w]->n_ppt;
+        f.pn.ph[w] = nets[w]->pph;
+        f.pn.nh[w] = nets[w]->n_pph;
+        f.pn.sc[w] = nets[w]->sc;
       }
-      pnorm_from_parts(q, sharded() ? pn + 2 : nullptr, cur);
-      LogParams lp{};
+      f.head_sq = sharded() ? pn + 2 : nullptr;
+      LogParams& lp = f.logs;
       lp.critic_sums = critic.g + critic.n_flat + 1;
       lp.actor_sums = actor.g + actor.n_flat + 1;
       lp.critic = critic.sc;
@@ -1102,8 +1123,8 @@ struct mtsac_engine {
       lp.inv_actor = 1.0f / (float)B_glob;
       lp.inv_b = 1.0f / (float)B_glob;
       lp.logs = logs;
-      write_logs(lp, cur);
-      bump_counter(counter, cur);
+      f.counter = counter;
+      step_finish(f, cur);
     });
     if (pipelined) (void)hipEventRecord(ev_tail[step_par], segs[s_tail].lane);
     if (!build && (join || !pipelined)) {  // eager: the main stream waits for every lane

@@ -439,7 +439,8 @@ int gemm_x3f_max_row_tiles(int M) { return (M + x3fk::BF16_BM[0] - 1) / x3fk::BF
 int gemm_x3f_bm(const SplitGemmParams& p, int batch) { return p.np == 1 ? x3fk::bf16_bm(p.M, p.N, batch) : x3fk::BM0; }
 
 namespace x3fk {
-constexpr int BMS = 128;  // the split-K row tile alternative for task shards (96 KB of LDS)
+constexpr int BMS = 128;  // the split-K row tile alternatives for task shards (96 / 84 KB of LDS)
+constexpr int BMT = 112;
 
 struct SplitPlan {
   int bm, s;
@@ -449,8 +450,10 @@ struct SplitPlan {
 // least (rounds of tiles x S workgroups) x (row-tile work relative to 208 rows / its MFMA
 // efficiency) / S, plus ~4 % of a round per extra slice (its partial slab traffic and the finishing
 // pass); >= 4 64-deep steps per slice.  A 128-row tile wins where 208 rows leave a mostly empty last
-// tile (896 rows: 4 x 208 + 64 -> 7 x 128, 2 slices instead of 3).  MTSAC_X3F_SPLIT_BM=208|128 forces
-// the row tile (experiments).
+// tile (896 rows: 4 x 208 + 64 -> 7 x 128, 2 slices instead of 3).  MTSAC_X3F_SPLIT_BM=208|128|112
+// forces the row tile (experiments; 112 rows -- 8 x 8 x 2 = 256 workgroups in 2 slices at 896 rows,
+// one full round -- measured no faster than 128: 2.17 vs 2.15 ms per 7-task shard step,
+// profiles/r3c_shard_steps*.txt).
 static SplitPlan split_plan(int M, int N, int K, int batch) {
   if ((long long)gemm_x3f_tiles(M, N, batch) >= 192) return {BM0, 1};
   static const int forced = [] {
@@ -460,10 +463,11 @@ static SplitPlan split_plan(int M, int N, int K, int batch) {
   const int smax = std::min(8, std::max(1, K / KS / 4));
   SplitPlan best{BM0, 1};
   double best_cost = 1e30;
-  for (int bm : {BM0, BMS}) {
-    if (forced && bm != forced) continue;
+  for (int bm : {BM0, BMS, BMT}) {
+    if (forced ? bm != forced : bm == BMT) continue;  // 112 rows: experiments only (no faster than 128)
     const long long tiles = (long long)((M + bm - 1) / bm) * ((N + BN - 1) / BN) * batch;
-    const double work = bm == BM0 ? 1.0 : (double)bm / BM0 / 0.9;  // 128-row tiles: ~0.9 of the MFMA rate
+    // shorter tiles ingest more operand bytes per MFMA: ~0.9 (128 rows), ~0.85 (112) of the rate
+    const double work = bm == BM0 ? 1.0 : (double)bm / BM0 / (bm == BMS ? 0.9 : 0.85);
     for (int sp = 1; sp <= smax; ++sp) {
       const double cost = (double)((tiles * sp + 255) / 256) * work / sp + 0.04 * (sp - 1);
       if (cost < best_cost - 1e-9) {
@@ -529,15 +533,14 @@ int gemm_x3f(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
     q.splits = S_eff;
     const int bm = split_plan(p0.M, p0.N, p0.K, batch).bm;
     const dim3 grid((unsigned)(((p0.M + bm - 1) / bm) * ((p0.N + BN - 1) / BN) * batch * S_eff));
-    if (bm == BMS) {
-      if (p0.np == 1)
-        hipLaunchKernelGGL((gemm_x3f_kernel<BMS, EPI_STORE, true, false, false, 0, 1>), grid, dim3(512), 0, st, q);
-      else
-        hipLaunchKernelGGL((gemm_x3f_kernel<BMS, EPI_STORE, true, false, false, 0, 3>), grid, dim3(512), 0, st, q);
-    } else if (p0.np == 1) {
-      hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_STORE, true, false, false, 0, 1>), grid, dim3(512), 0, st, q);
-    } else {
-      hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_STORE, true, false, false, 0, 3>), grid, dim3(512), 0, st, q);
+    const dim3 blk(512);
+    switch (bm * 4 + (p0.np == 1 ? 1 : 3)) {
+      case BMS * 4 + 1: hipLaunchKernelGGL((gemm_x3f_kernel<BMS, EPI_STORE, true, false, false, 0, 1>), grid, blk, 0, st, q); break;
+      case BMS * 4 + 3: hipLaunchKernelGGL((gemm_x3f_kernel<BMS, EPI_STORE, true, false, false, 0, 3>), grid, blk, 0, st, q); break;
+      case BMT * 4 + 1: hipLaunchKernelGGL((gemm_x3f_kernel<BMT, EPI_STORE, true, false, false, 0, 1>), grid, blk, 0, st, q); break;
+      case BMT * 4 + 3: hipLaunchKernelGGL((gemm_x3f_kernel<BMT, EPI_STORE, true, false, false, 0, 3>), grid, blk, 0, st, q); break;
+      case BM0 * 4 + 1: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_STORE, true, false, false, 0, 1>), grid, blk, 0, st, q); break;
+      default: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_STORE, true, false, false, 0, 3>), grid, blk, 0, st, q); break;
     }
     SplitGemmParams f = p0;
     f.sC = p0.sC;

@@ -23,7 +23,8 @@
 //   * epilogue: the 4 partial tiles meet in LDS (fixed order w = 0..3: deterministic), then each
 //     thread finishes 4 consecutive columns of a row: bias+ReLU or ReLU mask (from the bf16
 //     high plane of the activation: h > 0 <=> h_hi > 0), fp32 C (16 B per lane) and / or the
-//     three bf16 planes of C (8 B per lane per plane).
+//     three bf16 planes of C (8 B per lane per plane); with p.dbp, the tile's column sums
+//     (dbp[z][row tile][N], the data grad's bias-grad partials, as gemm_x3f writes them).
 #include <algorithm>
 #include <type_traits>
 
@@ -205,16 +206,17 @@ __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
   // each thread finishes 4 consecutive columns of a row: 16 threads per 64-column row
   const int c4 = 4 * (t & 15);
   const int col = n0 + c4;
-  if (col >= p.N) return;  // N % 4 == 0: a thread's 4 columns are all in or all out
+  const bool colok = col < p.N;  // N % 4 == 0: a thread's 4 columns are all in or all out
   const float* part = red + c4;
   float bias[4] = {0.f, 0.f, 0.f, 0.f};
-  if (EPI == EPI_BIAS_RELU) {
+  if (EPI == EPI_BIAS_RELU && colok) {
     const float4 u = *reinterpret_cast<const float4*>(p.bias + z * p.sBias + col);
     bias[0] = u.x; bias[1] = u.y; bias[2] = u.z; bias[3] = u.w;
   }
+  float csum[4] = {0.f, 0.f, 0.f, 0.f};  // column sums over this thread's rows (dbp)
   for (int rr = t >> 4; rr < BM; rr += NW * 4) {  // row in the tile
     const int row = m0 + rr;
-    if (row >= p.M) break;
+    if (row >= p.M || !colok) break;
     float e[4];
     {  // the four partials in a fixed order: deterministic
       const float4 v0 = *reinterpret_cast<const float4*>(part + 0 * BM * RLD + rr * RLD);
@@ -236,6 +238,8 @@ __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) e[c] = (float)mk[c] > 0.f ? e[c] : 0.f;
     }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) csum[c] += e[c];
     if (C_OUT)
       *reinterpret_cast<float4*>(p.C + z * p.sC + (long long)row * p.ldc + col) = make_float4(e[0], e[1], e[2], e[3]);
     if (P_OUT) {
@@ -250,6 +254,20 @@ __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
       *reinterpret_cast<bf16x4*>(pp) = h;
       *reinterpret_cast<bf16x4*>(pp + p.pC) = m;
       *reinterpret_cast<bf16x4*>(pp + 2 * p.pC) = l;
+    }
+  }
+  if (p.dbp) {  // the tile's column sums (the next weight grad's bias grad, finished by colsum_finish):
+    // the 16 row groups (t >> 4) added in order
+    __syncthreads();  // every partial-tile read is done: red is scratch
+    *reinterpret_cast<float4*>(red + (t >> 4) * BN + c4) = make_float4(csum[0], csum[1], csum[2], csum[3]);
+    __syncthreads();
+    if (t < 16 && colok) {
+      float4 a = *reinterpret_cast<const float4*>(red + c4);
+      for (int g = 1; g < 16; ++g) {
+        const float4 b = *reinterpret_cast<const float4*>(red + g * BN + c4);
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      *reinterpret_cast<float4*>(p.dbp + ((long long)z * nx + bx) * p.N + col) = a;
     }
   }
 }
@@ -292,6 +310,7 @@ void gemm_x3s_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t s
 // rows per tile / 16: the fewest (rounds of 256 workgroups) x (rows per tile), ties to the smaller
 // tile (more workgroups to balance the last round)
 int gemm_x3s_ti(int M, int N, int batch) {
+  if (M <= 0) return 4;
   int best = 4;
   long long bc = -1;
   for (int ti = 4; ti <= 8; ++ti) {

@@ -366,8 +366,6 @@ struct PnormParts {  // [0] critic, [1] actor
   const float* ph[2]; int nh[2];
   OptScalars* sc[2];
 };
-// sc[w]->pnorm = sqrt(sum pt[w] + (head_sq ? head_sq[w] : sum ph[w]))
-void pnorm_from_parts(const PnormParts& q, const float* head_sq, hipStream_t st);
 
 struct AlphaParams {
   const float* logpi;   // [B] (actor pass)
@@ -383,9 +381,8 @@ struct AlphaParams {
   float* task_loss;     // [T_glob] scratch: that sum per task
   OptScalars* sc;
 };
+// grad[t], task_loss[t] and *loss_part (one launch)
 void alpha_grad(const AlphaParams& a, hipStream_t st);
-void alpha_adam(const AlphaParams& a, float lr, float b1, float b2, float eps, float max_norm,
-                hipStream_t st);
 
 struct LogParams {
   const float* critic_sums;  // [0] sum w (q - y)^2 over members, [1] sum q
@@ -396,8 +393,18 @@ struct LogParams {
   float inv_critic; float inv_actor; float inv_b;
   float* logs;
 };
-void write_logs(const LogParams& p, hipStream_t st);
-void bump_counter(unsigned long long* c, hipStream_t st);
+
+// The step's scalar tail, one launch: *row_out[k] = sum rows[k][0..B) for the non-null rows[k]
+// (reduce_rows' order); the temperature Adam; sc[w]->pnorm = sqrt(sum pt[w] + (head_sq ?
+// head_sq[w] : sum ph[w])); the logs; *counter += 1
+struct StepFinish {
+  const float* rows[3]; float* row_out[3]; int B;
+  AlphaParams alpha; float lr, b1, b2, eps, max_norm;
+  PnormParts pn; const float* head_sq;
+  LogParams logs;
+  unsigned long long* counter;
+};
+void step_finish(const StepFinish& f, hipStream_t st);
 
 // ------------------------------------------------------------------ gradient-conflict statistics
 // (conflict.hip; MTSAC.compute_weights, mtsac.py:733-1170 and algorithms/utils.py:49-174)

@@ -410,34 +410,37 @@ __global__ __launch_bounds__(1024) void reduce_rows_kernel(RowPtrs in, int n_in,
 
 // temperature gradient: d/dlogalpha_t mean_b(-(x_b . logalpha)(logpi_b + H))
 //   = -(1/B) sum_{b in t}(logpi_b + H)    (x one-hot, validated by the gather)
-// one wave per global task (zero outside this shard's tasks); the loss term of each task goes to
-// task_loss[t], summed in task order by alpha_loss_kernel
-__global__ __launch_bounds__(64) void alpha_grad_kernel(AlphaParams a) {
-  const int tg = blockIdx.x, lane = threadIdx.x;
-  const int t = tg - a.task_begin;
-  float s = 0.f;
-  if (t >= 0 && t < a.T_l) {
-    const int n = a.counts[t];
-    const int* rl = a.rows + (long long)t * a.max_rows;
-    for (int j = lane; j < n; j += 64) s += a.logpi[rl[j]] + a.target_entropy;
+// zero outside this shard's tasks; the loss term of each task goes to task_loss[t]
+// one block of 16 waves, wave w over the global tasks w, w + 16, ...; after the barrier wave 0
+// sums the per-task loss terms in task order
+__global__ __launch_bounds__(1024) void alpha_grad_kernel(AlphaParams a) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int tg = wave; tg < a.T_glob; tg += 16) {
+    const int t = tg - a.task_begin;
+    float s = 0.f;
+    if (t >= 0 && t < a.T_l) {
+      const int n = a.counts[t];
+      const int* rl = a.rows + (long long)t * a.max_rows;
+      for (int j = lane; j < n; j += 64) s += a.logpi[rl[j]] + a.target_entropy;
+      s = wsumf(s);
+    }
+    if (lane == 0) {
+      a.grad[tg] = (t >= 0 && t < a.T_l) ? -s / (float)a.B_glob : 0.f;
+      a.task_loss[tg] = (t >= 0 && t < a.T_l) ? -a.log_alpha[tg] * s : 0.f;
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float s = 0.f;
+    for (int t = lane; t < a.T_glob; t += 64) s += a.task_loss[t];
     s = wsumf(s);
-  }
-  if (lane == 0) {
-    a.grad[tg] = (t >= 0 && t < a.T_l) ? -s / (float)a.B_glob : 0.f;
-    a.task_loss[tg] = (t >= 0 && t < a.T_l) ? -a.log_alpha[tg] * s : 0.f;
+    if (lane == 0) *a.loss_part = s;
   }
 }
 
-__global__ __launch_bounds__(64) void alpha_loss_kernel(AlphaParams a) {
-  float s = 0.f;
-  for (int t = threadIdx.x; t < a.T_glob; t += 64) s += a.task_loss[t];
-  s = wsumf(s);
-  if (threadIdx.x == 0) *a.loss_part = s;
-}
-
-__global__ __launch_bounds__(64) void alpha_adam_kernel(AlphaParams a, float lr, float b1, float b2, float eps,
-                                                        float max_norm) {
-  const int lane = threadIdx.x;
+// temperature Adam (optax clip_by_global_norm + adam over log_alpha); one wave
+__device__ void alpha_adam_wave(const AlphaParams& a, float lr, float b1, float b2, float eps, float max_norm) {
+  const int lane = threadIdx.x & 63;
   float sq = 0.f;
   for (int i = lane; i < a.T_glob; i += 64) sq += a.grad[i] * a.grad[i];
   const float gn = sqrtf(wsumf(sq));
@@ -465,7 +468,7 @@ __global__ __launch_bounds__(64) void alpha_adam_kernel(AlphaParams a, float lr,
   }
 }
 
-__global__ void write_logs_kernel(LogParams p) {
+__device__ void write_logs_thread(const LogParams& p) {
   p.logs[0] = p.critic_sums[1] * p.inv_critic;  // losses/qf_values
   p.logs[1] = p.critic_sums[0] * p.inv_critic;  // losses/qf_loss
   p.logs[2] = p.critic->gnorm;              // metrics/critic_grad_magnitude
@@ -480,7 +483,51 @@ __global__ void write_logs_kernel(LogParams p) {
   p.logs[9] = s;                            // alpha
 }
 
-__global__ void bump_kernel(unsigned long long* c) { *c += 1ull; }
+// fixed-order sum of one [B] row vector by a 1024-thread block (reduce_rows' order)
+__device__ float block_rows_sum(const float* __restrict__ x, int B, double* s) {
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < B; i += 1024) acc += (double)x[i];
+  acc = wsumd(acc);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  double t = 0.0;
+  for (int w = 0; w < 16; ++w) t += s[w];
+  __syncthreads();
+  return (float)t;
+}
+
+__device__ void pnorm_wave(const PnormParts& q, const float* __restrict__ head_sq, int w) {
+  const int lane = threadIdx.x & 63;
+  double t = 0.0, h = 0.0;
+  for (int i = lane; i < q.nt[w]; i += 64) t += (double)q.pt[w][i];
+  for (int i = lane; i < q.nh[w]; i += 64) h += (double)q.ph[w][i];
+  t = wsumd(t);
+  h = wsumd(h);
+  if (lane == 0) {
+    const float hs = head_sq ? head_sq[w] : (float)h;
+    q.sc[w]->pnorm = sqrtf((float)t + hs);
+  }
+}
+
+// the step's scalar tail in one block: the loss row sums (unsharded: they need no all-reduce),
+// the temperature Adam (wave 0) beside both networks' post-update |p| (waves 1, 2), then the
+// logs and the step counter
+__global__ __launch_bounds__(1024) void step_finish_kernel(StepFinish f) {
+  __shared__ double s[16];
+  for (int k = 0; k < 3; ++k) {
+    if (!f.rows[k]) continue;
+    const float v = block_rows_sum(f.rows[k], f.B, s);
+    if (threadIdx.x == 0) *f.row_out[k] = v;
+  }
+  const int wave = threadIdx.x >> 6;
+  if (wave == 0) alpha_adam_wave(f.alpha, f.lr, f.b1, f.b2, f.eps, f.max_norm);
+  else if (wave <= 2) pnorm_wave(f.pn, f.head_sq, wave - 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    write_logs_thread(f.logs);
+    *f.counter += 1ull;
+  }
+}
 
 }  // namespace
 
@@ -533,28 +580,10 @@ __global__ void pnorm_finalize_kernel(const float* __restrict__ trunk_sq, const 
   s1->pnorm = sqrtf(trunk_sq[1] + head_sq[1]);
 }
 
-// both networks' post-update |p| from their fused-Adam partials: trunk sums (and, unsharded, the
-// head sums; sharded: the all-reduced head sums in head_sq) in fixed order, one wave per network
-__global__ __launch_bounds__(128) void pnorm_parts_kernel(PnormParts q, const float* __restrict__ head_sq) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  double t = 0.0, h = 0.0;
-  for (int i = lane; i < q.nt[w]; i += 64) t += (double)q.pt[w][i];
-  for (int i = lane; i < q.nh[w]; i += 64) h += (double)q.ph[w][i];
-  t = wsumd(t);
-  h = wsumd(h);
-  if (lane == 0) {
-    const float hs = head_sq ? head_sq[w] : (float)h;
-    q.sc[w]->pnorm = sqrtf((float)t + hs);
-  }
-}
-
 void pnorm_finalize(const float* trunk_sq, const float* head_sq, OptScalars* s0, OptScalars* s1, hipStream_t st) {
   hipLaunchKernelGGL(pnorm_finalize_kernel, dim3(1), dim3(1), 0, st, trunk_sq, head_sq, s0, s1);
 }
 
-void pnorm_from_parts(const PnormParts& q, const float* head_sq, hipStream_t st) {
-  hipLaunchKernelGGL(pnorm_parts_kernel, dim3(1), dim3(128), 0, st, q, head_sq);
-}
 
 int sumsq2(const float* h, long long nh, const float* t, long long nt, float* hparts, float* tparts, OptScalars* sc,
            int* gh_out, hipStream_t st) {
@@ -582,16 +611,11 @@ void sum_partials(const float* partials, int nparts, float* out, hipStream_t st)
 }
 
 void alpha_grad(const AlphaParams& a, hipStream_t st) {
-  hipLaunchKernelGGL(alpha_grad_kernel, dim3((unsigned)a.T_glob), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(alpha_loss_kernel, dim3(1), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(alpha_grad_kernel, dim3(1), dim3(1024), 0, st, a);
 }
 
-void alpha_adam(const AlphaParams& a, float lr, float b1, float b2, float eps, float max_norm, hipStream_t st) {
-  hipLaunchKernelGGL(alpha_adam_kernel, dim3(1), dim3(64), 0, st, a, lr, b1, b2, eps, max_norm);
+void step_finish(const StepFinish& f, hipStream_t st) {
+  hipLaunchKernelGGL(step_finish_kernel, dim3(1), dim3(1024), 0, st, f);
 }
-
-void write_logs(const LogParams& p, hipStream_t st) { hipLaunchKernelGGL(write_logs_kernel, dim3(1), dim3(1), 0, st, p); }
-
-void bump_counter(unsigned long long* c, hipStream_t st) { hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(1), 0, st, c); }
 
 }  // namespace mtsac
