@@ -52,6 +52,39 @@ __global__ void augment_kernel(const unsigned char* __restrict__ obs, const int*
   out[i] = ((v / 255.0f - 0.5f) * 2.0f) * noise[b];
 }
 
+// the update's 3B-image input [s | s' | s'] in one launch: element i < n of the obs half and its
+// next-obs twin, the augmented next obs written twice (online and target rows of the encoder pass)
+__global__ void augment3_kernel(const unsigned char* __restrict__ obs, const int* __restrict__ crop_o,
+                                const float* __restrict__ noise_o, const unsigned char* __restrict__ nobs,
+                                const int* __restrict__ crop_n, const float* __restrict__ noise_n,
+                                float* __restrict__ out, int B, int C, int H, int W, int pad) {
+  const int n = B * H * W * C;  // < 2^31 (checked at drq_create)
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * n) return;
+  const bool next = i >= n;
+  if (next) i -= n;
+  const unsigned char* src = next ? nobs : obs;
+  const int* crop = next ? crop_n : crop_o;
+  const float* noise = next ? noise_n : noise_o;
+  int r = i / C;
+  const int c = i - r * C;
+  int r2 = r / W;
+  const int x = r - r2 * W;
+  r = r2 / H;
+  const int y = r2 - r * H;
+  const int b = r;
+  const int sy = min(max(y + crop[2 * b] - pad, 0), H - 1);
+  const int sx = min(max(x + crop[2 * b + 1] - pad, 0), W - 1);
+  const float v = (float)src[(((long long)b * C + c) * H + sy) * W + sx];
+  const float o = ((v / 255.0f - 0.5f) * 2.0f) * noise[b];
+  if (next) {
+    out[(long long)n + i] = o;
+    out[2LL * n + i] = o;
+  } else {
+    out[i] = o;
+  }
+}
+
 // ------------------------------------------------------------------ Atari replay sample
 // MemoryEfficientAtariMultiTaskReplayBuffer.sample (buffers.py:1188-1227) from the device store:
 // row b = (sample i = b / T, task t = b % T); draw k = idx[i] -> slot via the guard window
@@ -494,12 +527,12 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ dout, const unsigne
 // ------------------------------------------------------------------ encoder output + embedding
 // feat[b] = [relu(enc[b]) (NHWC flatten) | emb[task_b] / (|emb| + 1e-8)], row stride ldf
 __global__ void concat_kernel(const float* __restrict__ enc, int nenc, const float* __restrict__ emb, int D,
-                              const int* __restrict__ task, float* __restrict__ feat, int ldf, int B) {
+                              const int* __restrict__ task, int r0, int tmod, float* __restrict__ feat, int ldf, int B) {
   const int b = blockIdx.x;
   if (b >= B) return;
   for (int i = threadIdx.x; i < nenc; i += blockDim.x) feat[(long long)b * ldf + i] = fmaxf(enc[(long long)b * nenc + i], 0.f);
   if (threadIdx.x < 64) {
-    const int t = task[b];
+    const int t = task[(r0 + b) % tmod];
     float s = 0.f;
     for (int d = threadIdx.x; d < D; d += 64) s += emb[t * D + d] * emb[t * D + d];
     s = wsum(s);
@@ -994,6 +1027,13 @@ void augment(const unsigned char* obs, const int* crop, const float* noise, floa
   hipLaunchKernelGGL(augment_kernel, dim3(blocks(n)), dim3(256), 0, st, obs, crop, noise, out, B, C, H, W, pad);
 }
 
+void augment3(const unsigned char* obs, const int* crop_o, const float* noise_o, const unsigned char* nobs,
+              const int* crop_n, const float* noise_n, float* out, int B, int C, int H, int W, int pad, hipStream_t st) {
+  const long long n = 2LL * B * C * H * W;
+  hipLaunchKernelGGL(augment3_kernel, dim3(blocks(n)), dim3(256), 0, st, obs, crop_o, noise_o, nobs, crop_n, noise_n,
+                     out, B, C, H, W, pad);
+}
+
 #define CONV_CASES(M)                   \
   M(4, 8) M(8, 8) M(8, 16) M(16, 16)
 
@@ -1108,9 +1148,9 @@ void maxpool_bwd(const float* dout, const unsigned char* arg, float* din, int B,
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(blocks(n)), dim3(256), 0, st, dout, arg, din, B, H, W, C, Ho, Wo, lo);
 }
 
-void concat_feat(const float* enc, int nenc, const float* emb, int D, const int* task, float* feat, int ldf, int B,
-                 hipStream_t st) {
-  hipLaunchKernelGGL(concat_kernel, dim3(B), dim3(256), 0, st, enc, nenc, emb, D, task, feat, ldf, B);
+void concat_feat(const float* enc, int nenc, const float* emb, int D, const int* task, int r0, int tmod, float* feat,
+                 int ldf, int B, hipStream_t st) {
+  hipLaunchKernelGGL(concat_kernel, dim3(B), dim3(256), 0, st, enc, nenc, emb, D, task, r0, tmod, feat, ldf, B);
 }
 
 void ln_fwd(const float* x, const float* xb, int ldx, int F, const float* scale, const float* bias, float eps,

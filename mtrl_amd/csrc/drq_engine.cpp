@@ -66,6 +66,7 @@ struct drq_engine {
   float *p = nullptr, *g = nullptr, *mu = nullptr, *nu = nullptr, *tgt = nullptr;
   // inputs
   unsigned char *obs_u8 = nullptr, *nobs_u8 = nullptr;
+  int task_mod = 1 << 30;  // head rows r read task[r % task_mod] (the update's 3B rows: B)
   int *act = nullptr, *task = nullptr, *crop_o = nullptr, *crop_n = nullptr, *a_next = nullptr;
   float *rew = nullptr, *done = nullptr, *noise_o = nullptr, *noise_n = nullptr;
   float* nobs = nullptr;  // augmented next_obs
@@ -165,7 +166,8 @@ struct drq_engine {
   // the dense head of rows [r0, r0 + n) at params P
   void head_rows(const float* P, int r0, int n, float* out) {
     const long long r = r0;
-    drq::concat_feat(stk[2].c[2] + r * NENC, NENC, P + off_emb, D, task + r0, feat + r * F, F, n, st);
+    // the update's 3B rows [s | s' | s'] share the batch's B task ids
+    drq::concat_feat(stk[2].c[2] + r * NENC, NENC, P + off_emb, D, task, r0, task_mod, feat + r * F, F, n, st);
     drq::ln_fwd(feat + r * F, nullptr, F, F, P + off_ln1s, P + off_ln1b, cfg.ln_eps, ln1 + r * F, F, xhat1 + r * F,
                 rstd1 + r, n, false, st);
     gemm_store(ln1 + r * F, F, P + off_w0, H, z1 + r * H, H, n, H, F, GEMM_NN);
@@ -356,17 +358,14 @@ struct drq_engine {
   // the loss gradient of the staged batch into g (drqeps.py:268-308 up to the optimizer)
   void grad_pass() {
     const int C0 = cfg.in_ch;
-    drq::augment(nobs_u8, crop_n, noise_n, nobs, B, C0, cfg.hw, cfg.hw, 4, st);
-    drq::augment(obs_u8, crop_o, noise_o, stk[0].xin_own, B, C0, cfg.hw, cfg.hw, 4, st);
-    // ONE pass over the 3B images [s | s' | s'] (nobs = xin_own + B images): online params for
-    // the first 2B, target params for the last B (per-image arithmetic does not depend on the
-    // batch).  Its first B rows are the activations the backward reads; head rows [B, 2B) are the
-    // online head at s', [2B, 3B) the target's.
-    const size_t img_bytes = sizeof(float) * (size_t)B * C0 * cfg.hw * cfg.hw;
-    (void)hipMemcpyAsync(nobs + (size_t)B * C0 * cfg.hw * cfg.hw, nobs, img_bytes, hipMemcpyDeviceToDevice, st);
-    (void)hipMemcpyAsync(task + B, task, sizeof(int) * B, hipMemcpyDeviceToDevice, st);
-    (void)hipMemcpyAsync(task + 2 * B, task, sizeof(int) * B, hipMemcpyDeviceToDevice, st);
+    // ONE pass over the 3B images [s | s' | s'] (nobs = xin_own + B images, written with its copy
+    // by one augmentation launch): online params for the first 2B, target params for the last B
+    // (per-image arithmetic does not depend on the batch).  Its first B rows are the activations
+    // the backward reads; head rows [B, 2B) are the online head at s', [2B, 3B) the target's.
+    drq::augment3(obs_u8, crop_o, noise_o, nobs_u8, crop_n, noise_n, stk[0].xin_own, B, C0, cfg.hw, cfg.hw, 4, st);
+    task_mod = B;
     forward_rows(p, stk[0].xin_own, hc, 3 * B, tgt, 2 * B);
+    task_mod = 1 << 30;
     drq::c51_target(hc + (long long)B * NC, hc + 2LL * B * NC, NC, p + off_bc, tgt + off_bc, A, Z, rew, done, gamma_n,
                     cfg.v_min, cfg.v_max, m, a_next, B, st);
     drq::c51_loss(hc, NC, p + off_bc, A, Z, act, m, dhc, loss_b, logit_b, B, st);

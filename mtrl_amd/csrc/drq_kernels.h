@@ -9,6 +9,9 @@ namespace drq {
 // edge pad `pad`, crop offsets crop[b] = (along H, along W) in [0, 2 pad]
 void augment(const unsigned char* obs, const int* crop, const float* noise, float* out, int B, int C, int H, int W,
              int pad, hipStream_t st);
+// the update's encoder input [s | s' | s'] (3B images) from obs and next obs in one launch
+void augment3(const unsigned char* obs, const int* crop_o, const float* noise_o, const unsigned char* nobs,
+              const int* crop_n, const float* noise_n, float* out, int B, int C, int H, int W, int pad, hipStream_t st);
 // MemoryEfficientAtariMultiTaskReplayBuffer.sample rows from the device store (img_bytes % 16 == 0);
 // nstore != null: AtariMultiTaskReplayBuffer's separate next_obs array (no guard: pass full = 0)
 void atari_sample(const unsigned char* store, const unsigned char* nstore, const int* act, const float* rew,
@@ -54,9 +57,9 @@ void sum_parts_multi(const SumSeg* segs, int nseg, int blocks, hipStream_t st);
 // max pool 3x3 / stride 2 / SAME (out (H + 1) / 2), argmax tap per output
 void maxpool_fwd(const float* in, float* out, unsigned char* arg, int B, int H, int W, int C, hipStream_t st);
 void maxpool_bwd(const float* dout, const unsigned char* arg, float* din, int B, int H, int W, int C, hipStream_t st);
-// feat[b] = [relu(enc[b]) | normalised emb[task[b]]]
-void concat_feat(const float* enc, int nenc, const float* emb, int D, const int* task, float* feat, int ldf, int B,
-                 hipStream_t st);
+// feat[b] = [relu(enc[b]) | normalised emb[task[(r0 + b) % tmod]]]
+void concat_feat(const float* enc, int nenc, const float* emb, int D, const int* task, int r0, int tmod, float* feat,
+                 int ldf, int B, hipStream_t st);
 // LayerNorm over F columns of (x + xb) (xb nullable), y = ln * scale + bias (ReLU when relu)
 void ln_fwd(const float* x, const float* xb, int ldx, int F, const float* scale, const float* bias, float eps,
             float* y, int ldy, float* xhat, float* rstd, int B, bool relu, hipStream_t st);

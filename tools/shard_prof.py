@@ -9,8 +9,9 @@ from mtrl_amd.init import init_mtsac  # noqa: E402
 tl = int(sys.argv[1]) if len(sys.argv) > 1 else 7
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 50  # usage: shard_prof.py T_local [T W]
 W = int(sys.argv[3]) if len(sys.argv) > 3 else 2048
+prec = int(sys.argv[4]) if len(sys.argv) > 4 else 1  # usage: ... [precision: 1 split3, 2 bf16]
 cfg = make_config(num_tasks=T, task_begin=0, task_count=tl, obs_dim=39 + T, actor_width=W, critic_width=W,
-                  batch_per_task=128, capacity=20_000, clip=1, precision=1)
+                  batch_per_task=128, capacity=20_000, clip=1, precision=prec)
 eng = MTSACEngine(cfg, device=0)
 actor, critic = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=1, task_begin=0, task_count=tl)
 eng.set_params(L.ACTOR, actor)
