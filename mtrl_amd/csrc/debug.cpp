@@ -125,6 +125,7 @@ int mtsac_debug_gemm_x3p(int epi, int M, int N, int K, const float* A, int a_kma
 
 int mtsac_debug_gemm_x3p_bench(int epi, int batch, int M, int N, int K, int iters, double* ms_per_launch) {
   const int layout = (epi >> 8) & 3;  // bit 0: A k-major, bit 1: B k-major
+  const int splits = (epi >> 16) & 255;  // split-K slices (0/1: none; EPI_STORE: + splitk_reduce)
   epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || iters < 1 || !ms_per_launch) return -22;
   DevBuf d;
@@ -155,6 +156,11 @@ int mtsac_debug_gemm_x3p_bench(int epi, int batch, int M, int N, int K, int iter
   g.bias = bias; g.sBias = N;
   g.mask = C; g.ldm = N; g.sMask = (long long)M * N;
   g.M = M; g.N = N; g.K = (int)up32(K);
+  if (splits > 1) {
+    g.splits = splits;
+    g.ws = d.get<float>((size_t)M * N * batch * splits);
+    if (!g.ws) return -12;
+  }
   gemm_x3p(g, epi, batch, nullptr);
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return -5;

@@ -496,7 +496,11 @@ int gemm_x3f_tiles(int M, int N, int batch) {
 // (splits < 0, a workspace given) and the finishing pass can apply the epilogue
 static int x3f_slices(const SplitGemmParams& p, int epi, int batch) {
   if (p.splits >= 0 || p.ws == nullptr || p.dbp != nullptr) return 1;
-  if (p.np == 1 && x3fk::bf16_workgroups(p.M, p.N, batch) >= 128) return 1;
+  static const bool bf16_split = [] {  // experiments: split-K for the one-plane kernel too
+    const char* e = getenv("MTSAC_BF16_SPLIT");
+    return e && atoi(e) != 0;
+  }();
+  if (p.np == 1 && !bf16_split && x3fk::bf16_workgroups(p.M, p.N, batch) >= 128) return 1;
   if (epi == EPI_RELU_MASK && !p.mask16 && !p.mask) return 1;
   if (p.N % 4 != 0 || (p.C && p.ldc % 4 != 0) || (p.Cp && p.ldcp % 4 != 0)) return 1;
   return gemm_x3f_splits(p.M, p.N, p.K, batch);

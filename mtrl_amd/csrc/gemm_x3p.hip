@@ -248,14 +248,17 @@ int gemm_x3p_splits(int M, int N, int K, int batch, bool kmajor) {
   geo_tile(pick_geo(M, N, batch, kmajor, kmajor), bm, bn);
   const long long tiles = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch;
   if (tiles >= 192) return 1;
-  // slices: least (rounds of tiles x S workgroups on the CUs) / S, plus ~3 % of a round per extra
-  // slice for its partial slab traffic; >= 8 K-granules per slice
+  // slices: least (rounds of tiles x S workgroups on the CUs) / S, plus a share of a round per
+  // extra slice for its partial slab traffic (3 %; 1.5 % for the k-major weight grads, whose
+  // 128 x 128 tiles of a W = 400 trunk measured 27 vs 31.5 us at 8 vs 5 slices,
+  // profiles/r3f_x3p_w400.txt); >= 8 K-granules per slice (k-major: >= 4)
   const long long ncu = cu_count();
-  const int smax = std::min(kmajor ? 16 : 8, std::max(1, K / BK / 8));
+  const int smax = std::min(kmajor ? 16 : 8, std::max(1, K / BK / (kmajor ? 4 : 8)));
+  const double per_slice = kmajor ? 0.015 : 0.03;
   int best = 1;
   double best_cost = 1e30;
   for (int sp = 1; sp <= smax; ++sp) {
-    const double cost = (double)((tiles * sp + ncu - 1) / ncu) / sp + 0.03 * (sp - 1);
+    const double cost = (double)((tiles * sp + ncu - 1) / ncu) / sp + per_slice * (sp - 1);
     if (cost < best_cost - 1e-9) {
       best_cost = cost;
       best = sp;

@@ -468,7 +468,12 @@ __device__ void alpha_adam_wave(const AlphaParams& a, float lr, float b1, float 
   }
 }
 
-__device__ void write_logs_thread(const LogParams& p) {
+// wave 0: the alpha log summed lane-strided (the loads in flight together), then lane 0 writes
+__device__ void write_logs_wave(const LogParams& p) {
+  float s = 0.f;
+  for (int i = threadIdx.x; i < p.T_glob; i += 64) s += expf(p.log_alpha[i]);
+  s = wsumf(s);
+  if (threadIdx.x != 0) return;
   p.logs[0] = p.critic_sums[1] * p.inv_critic;  // losses/qf_values
   p.logs[1] = p.critic_sums[0] * p.inv_critic;  // losses/qf_loss
   p.logs[2] = p.critic->gnorm;              // metrics/critic_grad_magnitude
@@ -478,8 +483,6 @@ __device__ void write_logs_thread(const LogParams& p) {
   p.logs[6] = p.actor->pnorm;               // metrics/actor_params_norm
   p.logs[7] = 0.0f;                         // metrics/explore_loss (explore=False, mtsac.py:277)
   p.logs[8] = *p.alpha_loss_sum * p.inv_b;  // losses/alpha_loss
-  float s = 0.f;
-  for (int i = 0; i < p.T_glob; ++i) s += expf(p.log_alpha[i]);
   p.logs[9] = s;                            // alpha
 }
 
@@ -496,16 +499,29 @@ __device__ float block_rows_sum(const float* __restrict__ x, int B, double* s) {
   return (float)t;
 }
 
-__device__ void pnorm_wave(const PnormParts& q, const float* __restrict__ head_sq, int w) {
-  const int lane = threadIdx.x & 63;
+// both networks' post-update |p| from their fused-Adam partials: threads [512 w, 512 w + 512) sum
+// network w's trunk and head partials (<= 4 strided loads per thread, all in flight), the 8 waves'
+// sums added in order
+__device__ void pnorm_half(const PnormParts& q, const float* __restrict__ head_sq, double* s) {
+  const int w = threadIdx.x >> 9, u = threadIdx.x & 511;
   double t = 0.0, h = 0.0;
-  for (int i = lane; i < q.nt[w]; i += 64) t += (double)q.pt[w][i];
-  for (int i = lane; i < q.nh[w]; i += 64) h += (double)q.ph[w][i];
+  for (int i = u; i < q.nt[w]; i += 512) t += (double)q.pt[w][i];
+  for (int i = u; i < q.nh[w]; i += 512) h += (double)q.ph[w][i];
   t = wsumd(t);
   h = wsumd(h);
-  if (lane == 0) {
-    const float hs = head_sq ? head_sq[w] : (float)h;
-    q.sc[w]->pnorm = sqrtf((float)t + hs);
+  if ((threadIdx.x & 63) == 0) {
+    s[2 * (threadIdx.x >> 6)] = t;
+    s[2 * (threadIdx.x >> 6) + 1] = h;
+  }
+  __syncthreads();
+  if ((threadIdx.x & 511) == 0) {
+    double tt = 0.0, hh = 0.0;
+    for (int k = 0; k < 8; ++k) {
+      tt += s[2 * (8 * w + k)];
+      hh += s[2 * (8 * w + k) + 1];
+    }
+    const float hs = head_sq ? head_sq[w] : (float)hh;
+    q.sc[w]->pnorm = sqrtf((float)tt + hs);
   }
 }
 
@@ -513,19 +529,18 @@ __device__ void pnorm_wave(const PnormParts& q, const float* __restrict__ head_s
 // the temperature Adam (wave 0) beside both networks' post-update |p| (waves 1, 2), then the
 // logs and the step counter
 __global__ __launch_bounds__(1024) void step_finish_kernel(StepFinish f) {
-  __shared__ double s[16];
+  __shared__ double s[32];
   for (int k = 0; k < 3; ++k) {
     if (!f.rows[k]) continue;
     const float v = block_rows_sum(f.rows[k], f.B, s);
     if (threadIdx.x == 0) *f.row_out[k] = v;
   }
-  const int wave = threadIdx.x >> 6;
-  if (wave == 0) alpha_adam_wave(f.alpha, f.lr, f.b1, f.b2, f.eps, f.max_norm);
-  else if (wave <= 2) pnorm_wave(f.pn, f.head_sq, wave - 1);
+  pnorm_half(f.pn, f.head_sq, s);
+  if (threadIdx.x < 64) alpha_adam_wave(f.alpha, f.lr, f.b1, f.b2, f.eps, f.max_norm);
   __syncthreads();
-  if (threadIdx.x == 0) {
-    write_logs_thread(f.logs);
-    *f.counter += 1ull;
+  if (threadIdx.x < 64) {
+    write_logs_wave(f.logs);
+    if (threadIdx.x == 0) *f.counter += 1ull;
   }
 }
 

@@ -1,0 +1,12 @@
+# gpu_r3n.sh -- full GPU suite, shard steps, C1/S3 benches after the finish-kernel and x3p split changes
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r3n
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; echo "pytest exit $rc" >> $O/tests.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python tools/shard_step.py 50 25 13 7 > $O/shard_steps.txt 2>&1 || exit 1
+timeout -k 10 300 python bench.py --workload mt10_w400 --no-cpu-baseline > $O/bench_c1.json 2> $O/bench_c1.err || exit 1
+timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_s3.json 2> $O/bench_s3.err || exit 1
+echo done
