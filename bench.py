@@ -67,15 +67,18 @@ DRQ_METRIC = "DrQ-eps gradient-steps/sec, experiments/atari.py (26 games, IMPALA
 FP32_VALU_PEAK_TF = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector)
 
 
-def pmc_traffic(precision, family):
-    """HBM bytes per launch of a GEMM family from the committed rocprofv3 PMC summary
-    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py), or None."""
+def pmc_traffic(precision, family, workload):
+    """HBM bytes per launch of a GEMM family from the committed rocprofv3 PMC summary of THIS
+    workload (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py; a file without a
+    "workload" key is the default mt50_w2048 run), or None."""
     import glob
 
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
+            if d.get("workload", "mt50_w2048") != workload:
+                continue
             v = d.get(precision, {}).get(str(family))
             if v is not None:
                 return v["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
@@ -471,7 +474,7 @@ def main():
     gemm_ms = sum(v[0] for v in fam.values()) / timed_steps
     gemm_fl = sum(v[2] for v in fam.values()) / timed_steps
     achieved = (fl / nl) / (ms / nl * 1e-3) / 1e12 if nl else 0.0
-    traffic, traffic_src = pmc_traffic(args.precision, dom)
+    traffic, traffic_src = pmc_traffic(args.precision, dom, args.workload)
     if args.precision == "split3":  # 6 bf16 MFMA products per fp32 multiply-add
         peak, basis = BF16_MFMA_PEAK_TF / 6.0, "bf16 dense MFMA peak / 6 products (fp32-accurate split)"
     elif args.precision == "bf16":

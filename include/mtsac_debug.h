@@ -72,6 +72,11 @@ int mtsac_debug_drq_groups(int fwd, int bwd);
 struct mtsac_engine;
 int mtsac_debug_set_pipeline(struct mtsac_engine* engine, int32_t on);
 
+/* 1 when the engine issues every compute segment on its main stream (the default; the 5-lane
+ * form needs MTSAC_LANES=1 and enough hardware queues: GPU_MAX_HW_QUEUES as the process started
+ * >= 5 per live engine + 3), else 0. */
+int mtsac_debug_lane_mode(struct mtsac_engine* engine);
+
 /* Per-launch record of the last timed step (mtsac_set_timing): i < 0 returns the number of
  * records; else dims = {family = GEMM kind, M, N, K, batch} and *ms its duration. */
 struct mtsac_engine;

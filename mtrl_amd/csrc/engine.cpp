@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -130,6 +131,8 @@ struct mtsac_engine {
   hipStream_t cur = nullptr;
   std::vector<hipEvent_t> evpool;
   size_t ev_next = 0;
+  bool ev_rotate = getenv("MTSAC_EV_ROTATE") != nullptr;   // experiments (race hunt)
+  bool lanes_alt = getenv("MTSAC_LANES_ALT") != nullptr;   // experiments: every step on the overlap lanes
   int T_l = 0, T_g = 0, A = 0, D = 0, B = 0, n = 0, R = 0, ld_a = 0, ld_c = 0, B_glob = 0;
   Net actor, critic;
   // replay
@@ -236,6 +239,16 @@ struct mtsac_engine {
   // timing
   bool timing = false;
   bool timing_serial = false;  // timing with every segment on the main stream (solo kernels)
+  // Default: every compute segment on the main stream, the RCCL buckets on their own (lane 4), no
+  // cross-step overlap.  The 5-lane form (MTSAC_LANES=1, experiments) ran the independent chains of
+  // a step on separate streams with event edges, but its results were not bitwise reproducible run
+  // to run (last-bit to 7e-5 differences in the logged losses / norms of MT10/W400 in 3 of 8 fresh
+  // processes, profiles/r3g_hw_queue_flake.txt; root cause not found in the DAG; fewer hardware
+  // queues than streams made it worse) and it was not faster where it could be (MT10/W400: 1194
+  // steps/s with lanes, 1265 on one stream, profiles/r3h_bench_c1_*.json).  Lanes are also refused when the
+  // process's hardware queues (as started) cannot give every live engine's 5 streams + 3 their own.
+  bool one_stream = false;
+  bool counted_lanes = false;
   struct TimedLaunch {
     int family;
     double flops;
@@ -264,6 +277,64 @@ struct mtsac_engine {
     for (hipEvent_t e : evpool) (void)hipEventDestroy(e);
     for (hipStream_t x : {st, s1, s2, s3, s4})
       if (x) (void)hipStreamDestroy(x);
+    if (counted_lanes) {
+      Registry& r = registry();
+      std::lock_guard<std::mutex> g(r.mu);
+      r.live.erase(std::remove(r.live.begin(), r.live.end(), this), r.live.end());
+      relane(r);
+    }
+  }
+
+  static constexpr int LANES = 5;  // st, s1 .. s4
+  struct Registry {
+    std::mutex mu;
+    std::vector<mtsac_engine*> live;
+  };
+  static Registry& registry() {
+    static Registry r;
+    return r;
+  }
+  // Lanes (only when MTSAC_LANES=1) while every live engine's streams, plus a reserve of 3 for the
+  // null stream, torch's and RCCL's, fit GPU_MAX_HW_QUEUES (HIP's default 4 when unset; the value
+  // the process started with).  Re-decided for ALL live engines whenever one is created or
+  // destroyed -- between calls, when every lane has joined the main stream (the last step of
+  // update_many joins) -- so in-process multi-engine runs use one stream each.
+  // GPU_MAX_HW_QUEUES as the process STARTED (/proc/self/environ): the HIP runtime reads it once,
+  // and a value set later from inside the process may or may not have reached it
+  static int start_hw_queues() {
+    static const int v = [] {
+      int q = 4;  // HIP's default
+      if (FILE* f = fopen("/proc/self/environ", "rb")) {
+        std::string env;
+        char buf[4096];
+        size_t n;
+        while ((n = fread(buf, 1, sizeof(buf), f)) > 0) env.append(buf, n);
+        fclose(f);
+        const std::string key = "GPU_MAX_HW_QUEUES=";
+        for (size_t i = 0; i < env.size();) {
+          const size_t e = env.find('\0', i);
+          const std::string kv = env.substr(i, (e == std::string::npos ? env.size() : e) - i);
+          if (kv.compare(0, key.size(), key) == 0 && atoi(kv.c_str() + key.size()) > 0) q = atoi(kv.c_str() + key.size());
+          if (e == std::string::npos) break;
+          i = e + 1;
+        }
+      }
+      return q;
+    }();
+    return v;
+  }
+  static void relane(Registry& r) {
+    const char* want = getenv("MTSAC_LANES");
+    const int hwq = start_hw_queues();
+    const bool one = !(want && atoi(want) != 0) || (int)r.live.size() * LANES + 3 > hwq;
+    for (mtsac_engine* e : r.live) e->one_stream = one;
+  }
+  void lane_mode_for() {
+    Registry& r = registry();
+    std::lock_guard<std::mutex> g(r.mu);
+    r.live.push_back(this);
+    counted_lanes = true;
+    relane(r);
   }
 
   template <typename T>
@@ -285,11 +356,11 @@ struct mtsac_engine {
   // timing-free events (captured into the graph as dependencies).
   void dep(hipStream_t from, hipStream_t to) {
     if (from == to) return;
-    if (ev_next >= evpool.size()) {  // pool is pre-created (no event creation inside a capture)
+    if (evpool.empty()) {  // pool is pre-created (no event creation inside a capture)
       comm_error = "event pool exhausted";
       return;
     }
-    hipEvent_t e = evpool[ev_next++];
+    hipEvent_t e = evpool[ev_next++ % evpool.size()];
     static const bool trace = getenv("MTSAC_TRACE") != nullptr;
     if (trace) fprintf(stderr, "[mtsac] dep %zu %p -> %p\n", ev_next, (void*)from, (void*)to), fflush(stderr);
     hipError_t r = hipEventRecord(e, from);
@@ -844,14 +915,16 @@ struct mtsac_engine {
       if (g) (void)hipGraphDestroy(g);
       if (r != hipSuccess) comm_error = std::string("step graph build: ") + hipGetErrorString(r);
     } else {
-      hipStream_t L = timing_serial ? st : (lane == 0 ? st : lane == 1 ? s1 : lane == 2 ? s2 : lane == 3 ? s3 : s4);
+      hipStream_t L = timing_serial ? st
+                      : one_stream  ? (lane == 4 && comm != nullptr ? s4 : st)  // collectives keep their stream
+                                    : (lane == 0 ? st : lane == 1 ? s1 : lane == 2 ? s2 : lane == 3 ? s3 : s4);
       for (int d : deps)
         if (segs[d].lane != L) (void)hipStreamWaitEvent(L, segs[d].ev, 0);
       cur = L;
       body();
       s.lane = L;
-      if (ev_next < evpool.size()) {
-        s.ev = evpool[ev_next++];
+      if (!evpool.empty()) {  // rotating: an event is re-recorded only pool-size segments later
+        s.ev = evpool[ev_next++ % evpool.size()];
         (void)hipEventRecord(s.ev, L);
       } else {
         comm_error = "event pool exhausted";
@@ -910,19 +983,20 @@ struct mtsac_engine {
     task = inset[k].task;
     counts = inset[k].counts;
     rows = inset[k].rows;
-    inp[0].x = xa;  // the actor input's planes (written in s_af, after the previous step's tail)
+    inp[0].x = xa;  // one plane buffer: the gather writes it after step k's actor pass (ev_ap), and
+                    // nothing after that pass reads it (the input-layer weight grad reads fp32 xa)
   }
 
   // pipelined: eager issue that overlaps the previous step's tail (see InSet); join: the main
   // stream waits for every lane at the end (the last step of a call, and every non-pipelined one)
   void step(bool device_batch, bool device_noise, bool pipelined = false, bool join = true) {
     const int Bl = B;
-    pipelined = pipelined && !build && !timing_serial;
+    pipelined = pipelined && !build && !timing_serial && !one_stream;
     const bool overlap = pipelined && have_prev;
     if (overlap) use_inset(inset_cur ^ 1);
     counts = device_batch ? s_counts : inset[inset_cur].counts;
     rows = device_batch ? s_rows : inset[inset_cur].rows;
-    ev_next = 0;
+    if (!ev_rotate) ev_next = 0;
     segs.clear();
     const float* twp = cfg.use_task_weights ? tw : nullptr;
     PolicyParams pp{};
@@ -967,12 +1041,13 @@ struct mtsac_engine {
     });
     // critic forward on (s, a) with the current critic (mtsac.py:555); pipelined on lane 2, which
     // the previous step's tail (lanes 1, 3, 4) does not use, so it runs beside that tail
-    const int s_cf = seg({s_in}, overlap ? 2 : 1, [&] { trunk_forward(critic, critic.p, 0, xc, ld_c, hc, hcp, Bl); });
+    const bool ol = overlap || lanes_alt;
+    const int s_cf = seg({s_in}, ol ? 2 : 1, [&] { trunk_forward(critic, critic.p, 0, xc, ld_c, hc, hcp, Bl); });
     if (overlap) (void)hipStreamWaitEvent(st, ev_tail[step_par ^ 1], 0);  // s_af: the updated actor
     // ONE actor forward over [s | s'] with the pre-update actor: update_critic samples a' ~ pi(.|s')
     // (mtsac.py:525-528) and update_actor a ~ pi(.|s) (:640-642) from the same parameters, so the
     // two row blocks share every trunk GEMM (rows krows.. are s'; the pad rows between are zeros)
-    const int s_af = seg({s_in}, overlap ? 0 : 2, [&] {
+    const int s_af = seg({s_in}, ol ? 0 : 2, [&] {
       trunk_forward(actor, actor.p, 0, xa, ld_a, ha, hap, Ma);
       PolicyParams q = pp;
       q.head = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
@@ -982,15 +1057,14 @@ struct mtsac_engine {
       q.a_planes = in_planes(xcp);
       q.logpi = logpi;
       q.cache = cache;
-      policy_head(q, cur);
-      q = pp;
-      q.head = head(actor, actor.p, han[actor.depth - 1], Bl, task);
-      q.eps = device_noise ? nullptr : eps_n;
-      q.stream_id = 1;
-      q.a_out = xcn;
-      q.a_planes = in_planes(xcn);
-      q.logpi = logpi_n;
-      policy_head(q, cur);
+      PolicyParams qn = pp;
+      qn.head = head(actor, actor.p, han[actor.depth - 1], Bl, task);
+      qn.eps = device_noise ? nullptr : eps_n;
+      qn.stream_id = 1;
+      qn.a_out = xcn;
+      qn.a_planes = in_planes(xcn);
+      qn.logpi = logpi_n;
+      policy_head_pair(q, qn, cur);
     });
     // target critic at (s', a'), TD target (mtsac.py:529-553)
     const int s_tg = seg({s_af}, 0, [&] {
@@ -1078,7 +1152,7 @@ struct mtsac_engine {
     const int s_tail = seg({s_ab}, 1, [&] {
       // temperature gradient rides in the actor's scalar tail: [2] loss part, [3..] grad
       AlphaParams al = alpha_params();
-      alpha_grad(al, cur);
+      if (sharded()) alpha_grad(al, cur);  // unsharded: inside step_finish
       if (sharded()) head_sq(actor);
       reduce_rest(actor);
       optimize(actor, cfg.actor_lr, cfg.actor_max_grad_norm, false, 1);
@@ -1097,6 +1171,7 @@ struct mtsac_engine {
       }
       f.B = Bl;
       f.alpha = al;
+      f.alpha_grad = sharded() ? 0 : 1;
       f.lr = cfg.alpha_lr;
       f.b1 = cfg.adam_b1;
       f.b2 = cfg.adam_b2;
@@ -1182,7 +1257,8 @@ struct mtsac_engine {
           (rc = alloc(&ps_nz, 64)) || (rc = alloc(&ps_thr, 64)))
         return rc;
     }
-    return 0;
+    // alloc()'s null-stream zero fills before the engine streams use the buffers
+    return hipDeviceSynchronize() == hipSuccess ? 0 : fail(-5, "device synchronize");
   }
 
   // dW_t, db_t of trunk layer i for every task t (one batched TN GEMM per ensemble member)
@@ -1534,6 +1610,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   };
   for (hipStream_t* x : {&e->st, &e->s1, &e->s2, &e->s3, &e->s4})
     if (hipStreamCreateWithFlags(x, hipStreamNonBlocking) != hipSuccess) return bad(fail(-5, "stream"));
+  e->lane_mode_for();
   e->cur = e->st;
   for (int i = 0; i < 128; ++i) {
     hipEvent_t ev;
@@ -1737,6 +1814,9 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     if (hipEventCreateWithFlags(&e->ev_ap[k], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_tail[k], hipEventDisableTiming) != hipSuccess)
       return bad(fail(-5, "event"));
+  // the zero fills of alloc() run on the null stream, which the engine's non-blocking streams do not
+  // wait for: finish them before any engine work can touch the buffers
+  if (hipDeviceSynchronize() != hipSuccess) return bad(fail(-5, "device synchronize"));
   *out = e;
   return 0;
 }
@@ -2470,6 +2550,11 @@ int mtsac_debug_set_pipeline(mtsac_engine* h, int32_t on) {
   const int was = h->no_pipeline ? 0 : 1;
   h->no_pipeline = on == 0;
   return was;
+}
+
+int mtsac_debug_lane_mode(mtsac_engine* h) {
+  if (!h) return fail(-22, "null engine");
+  return h->one_stream ? 1 : 0;
 }
 
 int mtsac_debug_timed_launch(mtsac_engine* h, int32_t i, int32_t* dims, double* ms) {

@@ -253,7 +253,11 @@ int gemm_x3p_splits(int M, int N, int K, int batch, bool kmajor) {
   // 128 x 128 tiles of a W = 400 trunk measured 27 vs 31.5 us at 8 vs 5 slices,
   // profiles/r3f_x3p_w400.txt); >= 8 K-granules per slice (k-major: >= 4)
   const long long ncu = cu_count();
-  const int smax = std::min(kmajor ? 16 : 8, std::max(1, K / BK / (kmajor ? 4 : 8)));
+  static const int kdiv = [] {  // experiments: K-granules per slice floor of the k-major form
+    const char* e = getenv("MTSAC_X3P_KMAJOR_GRANULES");
+    return e && atoi(e) > 0 ? atoi(e) : 4;
+  }();
+  const int smax = std::min(kmajor ? 16 : 8, std::max(1, K / BK / (kmajor ? kdiv : 8)));
   const double per_slice = kmajor ? 0.015 : 0.03;
   int best = 1;
   double best_cost = 1e30;

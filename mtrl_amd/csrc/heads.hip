@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyParams p) {
 // with the trunk GEMMs running on other streams.  RW = 4 when that still gives a workgroup per CU;
 // small task shards take fewer rows per wave (more waves in flight; each row's sums are the same).
 template <int HD, int RW>
-__global__ __launch_bounds__(256) void policy_head_grouped_kernel(PolicyParams p) {
+__device__ inline void policy_head_grouped_body(const PolicyParams& p) {
   constexpr int ROWS = 4 * RW;  // rows per workgroup
   const HeadParams& hp = p.head;
   const int t = blockIdx.x;
@@ -193,6 +193,17 @@ __global__ __launch_bounds__(256) void policy_head_grouped_kernel(PolicyParams p
 #pragma unroll
   for (int r = 0; r < RW; ++r)
     if (j0 + wave * RW + r < n) policy_finish<HD>(p, row[r], t, acc[r], lane);
+}
+
+template <int HD, int RW>
+__global__ __launch_bounds__(256) void policy_head_grouped_kernel(PolicyParams p) {
+  policy_head_grouped_body<HD, RW>(p);
+}
+
+// the two policy heads of the merged actor forward (s and s' rows) in one launch (blockIdx.z: which)
+template <int HD, int RW>
+__global__ __launch_bounds__(256) void policy_head_pair_kernel(PolicyPair pp) {
+  policy_head_grouped_body<HD, RW>(pp.p[blockIdx.z]);
 }
 
 // rows per wave for a launch that would have wgs_at_rw1 workgroups at one row per wave: the largest
@@ -604,6 +615,28 @@ void policy_head(const PolicyParams& p, hipStream_t st) {
     hipLaunchKernelGGL(policy_head_kernel<4>, grid, dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL(policy_head_kernel<2>, grid, dim3(256), 0, st, p);
+}
+
+void policy_head_pair(const PolicyParams& a, const PolicyParams& b, hipStream_t st) {
+  if (!a.counts || !b.counts || a.head.hd != b.head.hd || a.T_l != b.T_l || a.max_count != b.max_count) {
+    policy_head(a, st);
+    policy_head(b, st);
+    return;
+  }
+  const int rw = rows_per_wave(2LL * a.T_l * ((a.max_count + 3) / 4));
+  const dim3 grid((unsigned)a.T_l, (unsigned)((a.max_count + 4 * rw - 1) / (4 * rw)), 2);
+  PolicyPair pp{};
+  pp.p[0] = a;
+  pp.p[1] = b;
+#define PHP(HDV)                                                                                       \
+  if (rw == 4) hipLaunchKernelGGL((policy_head_pair_kernel<HDV, 4>), grid, dim3(256), 0, st, pp);       \
+  else if (rw == 2) hipLaunchKernelGGL((policy_head_pair_kernel<HDV, 2>), grid, dim3(256), 0, st, pp);  \
+  else hipLaunchKernelGGL((policy_head_pair_kernel<HDV, 1>), grid, dim3(256), 0, st, pp);
+  if (a.head.hd == 8) { PHP(8) }
+  else if (a.head.hd == 6) { PHP(6) }
+  else if (a.head.hd == 4) { PHP(4) }
+  else { PHP(2) }
+#undef PHP
 }
 
 void critic_head(const CriticHeadParams& p, hipStream_t st) {

@@ -219,6 +219,11 @@ struct PolicyParams {
   int max_count;        // bound on counts[] (sizes the grid)
 };
 void policy_head(const PolicyParams& p, hipStream_t st);
+// the s and s' heads of the merged actor forward in one launch (grouped form; else two launches)
+struct PolicyPair {
+  PolicyParams p[2];
+};
+void policy_head_pair(const PolicyParams& a, const PolicyParams& b, hipStream_t st);
 
 enum CriticHeadMode { CH_TARGET = 0, CH_CRITIC = 1, CH_ACTOR = 2 };
 struct CriticHeadParams {
@@ -399,7 +404,8 @@ struct LogParams {
 // head_sq[w] : sum ph[w])); the logs; *counter += 1
 struct StepFinish {
   const float* rows[3]; float* row_out[3]; int B;
-  AlphaParams alpha; float lr, b1, b2, eps, max_norm;
+  AlphaParams alpha; int alpha_grad;  // alpha_grad: also the temperature gradient (alpha_grad's work) first
+  float lr, b1, b2, eps, max_norm;
   PnormParts pn; const float* head_sq;
   LogParams logs;
   unsigned long long* counter;

@@ -413,7 +413,7 @@ __global__ __launch_bounds__(1024) void reduce_rows_kernel(RowPtrs in, int n_in,
 // zero outside this shard's tasks; the loss term of each task goes to task_loss[t]
 // one block of 16 waves, wave w over the global tasks w, w + 16, ...; after the barrier wave 0
 // sums the per-task loss terms in task order
-__global__ __launch_bounds__(1024) void alpha_grad_kernel(AlphaParams a) {
+__device__ void alpha_grad_block(const AlphaParams& a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int tg = wave; tg < a.T_glob; tg += 16) {
     const int t = tg - a.task_begin;
@@ -437,6 +437,8 @@ __global__ __launch_bounds__(1024) void alpha_grad_kernel(AlphaParams a) {
     if (lane == 0) *a.loss_part = s;
   }
 }
+
+__global__ __launch_bounds__(1024) void alpha_grad_kernel(AlphaParams a) { alpha_grad_block(a); }
 
 // temperature Adam (optax clip_by_global_norm + adam over log_alpha); one wave
 __device__ void alpha_adam_wave(const AlphaParams& a, float lr, float b1, float b2, float eps, float max_norm) {
@@ -530,6 +532,10 @@ __device__ void pnorm_half(const PnormParts& q, const float* __restrict__ head_s
 // logs and the step counter
 __global__ __launch_bounds__(1024) void step_finish_kernel(StepFinish f) {
   __shared__ double s[32];
+  if (f.alpha_grad) {  // unsharded: the temperature gradient needs no all-reduce, so it runs here
+    alpha_grad_block(f.alpha);
+    __syncthreads();
+  }
   for (int k = 0; k < 3; ++k) {
     if (!f.rows[k]) continue;
     const float v = block_rows_sum(f.rows[k], f.B, s);

@@ -229,28 +229,29 @@ def test_full_batch_bf16_drift_bound(name):
 
 @pytest.mark.parametrize("T,tc,W,prec", [(50, 50, 2048, 1), (50, 7, 2048, 1), (10, 10, 400, 1), (10, 10, 2048, 2)],
                          ids=["s3", "mt50_shard7", "mt10_w400", "mt10_w2048_bf16"])
-def test_pipelined_steps_equal_whole_steps(T, tc, W, prec):
-    """Eager update_many overlaps step k+1's gather and critic(s, a) forward with step k's actor
-    backward, all-reduce and Adam (engine.cpp step(), InSet): 4 device-sampled steps issued that
-    way give bitwise the logs, parameters, optimizer moments and index-stream state of 4 whole
-    steps issued one after another."""
+def test_update_many_equals_single_steps(T, tc, W, prec):
+    """The default issue (every compute segment on one stream, engine.cpp one_stream): 4 device-
+    sampled steps in one update_many call give bitwise the logs, parameters, optimizer moments and
+    index-stream state of 4 calls of one step each -- run to run reproducible, which the 5-lane
+    form was not ("Lanes and hardware queues")."""
     from mtrl_amd import _lib as L
     from mtrl_amd.engine import MTSACEngine, make_config
     from mtrl_amd.init import init_mtsac
 
+    a0, c0 = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=4, task_begin=0, task_count=tc)
     outs = []
-    for pipe in (0, 1):
+    for calls in ((4,), (1, 1, 1, 1)):
         e = MTSACEngine(make_config(num_tasks=T, task_begin=0, task_count=tc, obs_dim=39 + T, actor_width=W,
                                     critic_width=W, batch_per_task=128, capacity=512, precision=prec))
-        a, c = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=4, task_begin=0, task_count=tc)
-        e.set_params(L.ACTOR, a)
-        e.set_params(L.CRITIC, c)
-        e.set_params(L.CRITIC_TARGET, c)
+        assert e.lib.mtsac_debug_lane_mode(e._h) == 1
+        e.set_params(L.ACTOR, a0)
+        e.set_params(L.CRITIC, c0)
+        e.set_params(L.CRITIC_TARGET, c0)
         e.buffer_fill_synthetic(77)
         e.seed_rng(5)
         e.enable_graph(False)
-        e.lib.mtsac_debug_set_pipeline(e._h, pipe)
-        e.update_many(4)
+        for k in calls:
+            e.update_many(k)
         outs.append((e.logs(), [e.get_params(w) for w in (L.ACTOR, L.CRITIC, L.CRITIC_TARGET, L.LOG_ALPHA,
                                                            L.ACTOR_ADAM_NU, L.CRITIC_ADAM_MU)],
                      e.get_rng_state(), e.noise_state()))
@@ -260,3 +261,50 @@ def test_pipelined_steps_equal_whole_steps(T, tc, W, prec):
     for x, y in zip(a[1], b[1]):
         np.testing.assert_array_equal(x, y)
     assert a[2] == b[2] and a[3] == b[3]
+
+
+_LANE_CHILD = """
+import sys
+sys.path.insert(0, {root!r})
+from mtrl_amd.engine import MTSACEngine, make_config
+mk = lambda: MTSACEngine(make_config(num_tasks=2, task_count=2, obs_dim=41, actor_width=64, critic_width=64,
+                                     batch_per_task=8, capacity=16))
+a = mk()
+m1 = a.lib.mtsac_debug_lane_mode(a._h)
+b, c = mk(), mk()
+m3 = [e.lib.mtsac_debug_lane_mode(e._h) for e in (a, b, c)]
+b.close(); c.close()
+m1b = a.lib.mtsac_debug_lane_mode(a._h)
+a.close()
+print("modes", m1, m3, m1b)
+"""
+
+
+def _child(code: str, env: dict, timeout: int = 200):
+    import subprocess
+    import sys
+
+    r = subprocess.run([sys.executable, "-u", "-c", code], capture_output=True, text=True, timeout=timeout, env=env)
+    print(r.stdout[-3000:], r.stderr[-3000:])
+    return r
+
+
+def test_lane_mode():
+    """One compute stream by default; the experimental 5-lane form (MTSAC_LANES=1) only while every
+    live engine's 5 streams + 3 reserved fit the hardware queues the process STARTED with
+    (GPU_MAX_HW_QUEUES, read from /proc/self/environ; re-decided for all live engines at each
+    create / destroy).  Child processes: lanes requested at 16 queues -> one engine has lanes, three
+    (15 + 3 > 16) one stream each, the survivor its lanes back; requested at 4 -> one stream; not
+    requested -> one stream."""
+    import os
+
+    from mtrl_amd.hwq import child_env
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _LANE_CHILD.format(root=root)
+    r = _child(code, child_env(16))
+    assert r.returncode == 0 and "modes 0 [1, 1, 1] 0" in r.stdout
+    r = _child(code, dict(child_env(16), GPU_MAX_HW_QUEUES="4"))
+    assert r.returncode == 0 and "modes 1 [1, 1, 1] 1" in r.stdout
+    r = _child(code, child_env(16, lanes=False))
+    assert r.returncode == 0 and "modes 1 [1, 1, 1] 1" in r.stdout

@@ -60,8 +60,8 @@ def test_x3p_matches_fp64(shape, layout, geo):
     assert np.all(err <= 4e-6 * mag + 1e-30), float((err / mag).max())
 
 
-@pytest.mark.parametrize("splits", [2, 3, 16])
-@pytest.mark.parametrize("shape", [(256, 128, 6400), (100, 300, 1000), (8, 8, 33)])
+@pytest.mark.parametrize("splits", [2, 3, 8, 16])
+@pytest.mark.parametrize("shape", [(256, 128, 6400), (100, 300, 1000), (8, 8, 33), (400, 400, 1280)])
 def test_x3p_splitk_weight_grad(shape, splits, geo):
     M, N, K = shape
     A, B, ref, mag = _operands(M, N, K, (1, 1), seed=2)
