@@ -125,7 +125,8 @@ int mtsac_debug_gemm_x3p(int epi, int M, int N, int K, const float* A, int a_kma
 
 int mtsac_debug_gemm_x3p_bench(int epi, int batch, int M, int N, int K, int iters, double* ms_per_launch) {
   const int layout = (epi >> 8) & 3;  // bit 0: A k-major, bit 1: B k-major
-  const int splits = (epi >> 16) & 255;  // split-K slices (0/1: none; EPI_STORE: + splitk_reduce)
+  const int splits = (epi >> 16) & 255;  // split-K slices (0/1: none; EPI_STORE: + splitk_reduce; 255: auto)
+  const bool fin = (epi >> 12) & 1;      // arrival counters: the weight grads' in-launch reduce
   epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || iters < 1 || !ms_per_launch) return -22;
   DevBuf d;
@@ -157,9 +158,14 @@ int mtsac_debug_gemm_x3p_bench(int epi, int batch, int M, int N, int K, int iter
   g.mask = C; g.ldm = N; g.sMask = (long long)M * N;
   g.M = M; g.N = N; g.K = (int)up32(K);
   if (splits > 1) {
-    g.splits = splits;
-    g.ws = d.get<float>((size_t)M * N * batch * splits);
+    g.splits = splits == 255 ? -1 : splits;
+    const int sw = splits == 255 ? gemm_x3p_splits(M, N, g.K, batch, layout == 3) : splits;
+    g.ws = d.get<float>((size_t)M * N * batch * std::max(sw, 1));
     if (!g.ws) return -12;
+    if (fin) {
+      g.cnt = d.get<int>((size_t)GEMM_X3F_CNT);
+      if (!g.cnt) return -12;
+    }
   }
   gemm_x3p(g, epi, batch, nullptr);
   hipEvent_t e0, e1;
@@ -186,6 +192,7 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
   const bool small = (epi >> 9) & 1;  // gemm_x3s instead
   const int np = ((epi >> 10) & 1) ? 1 : 3;  // bf16: the high plane only
   const bool autosplit = (epi >> 11) & 1;     // split-K by the launcher's own choice (workspace given)
+  const bool fin = (epi >> 12) & 1;           // ... with arrival counters: the in-launch finish
   epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || !A || !B || !C) return -22;
   DevBuf d;
@@ -239,6 +246,10 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
     g.ws = d.get<float>((size_t)std::max(gemm_x3f_ws_floats(M, N, (int)Kp, batch), 1LL));
     if (!g.ws) return -12;
     g.splits = -1;
+    if (fin) {
+      g.cnt = d.get<int>((size_t)GEMM_X3F_CNT);
+      if (!g.cnt || hipMemset(g.cnt, 0, sizeof(int) * GEMM_X3F_CNT) != hipSuccess) return -12;
+    }
   }
   if (small) {
     if (!gemm_x3s_ok(g, epi, batch)) return -95;
@@ -269,6 +280,7 @@ int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int 
   const int outs = (epi >> 8) & 3;  // 0: fp32 + planes, 1: planes only, 2: fp32 only
   const int np = ((epi >> 10) & 1) ? 1 : 3;  // bf16: the high plane only
   const bool autosplit = (epi >> 11) & 1;     // split-K by the launcher's own choice (workspace given)
+  const bool fin = (epi >> 12) & 1;           // ... with arrival counters: the in-launch finish
   epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || iters < 1 || !ms_per_launch) return -22;
   DevBuf d;
@@ -311,6 +323,10 @@ int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int 
     g.ws = d.get<float>((size_t)std::max(wsf, 1LL));
     if (!g.ws) return -12;
     g.splits = -1;
+    if (fin) {
+      g.cnt = d.get<int>((size_t)GEMM_X3F_CNT);
+      if (!g.cnt) return -12;
+    }
   }
   if (which >= 1 && !gemm_x3f_ok(g, epi, batch)) return -95;
   if (which < 0 && !gemm_x3s_ok(g, epi, batch)) return -95;

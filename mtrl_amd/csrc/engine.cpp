@@ -211,6 +211,17 @@ struct mtsac_engine {
   // split-K workspaces, one per lane: segments on different lanes may run concurrently, the
   // segments of one lane are ordered by the step DAG (see seg())
   float* ws_lane[5] = {};
+  int* cnt_lane[5] = {};  // split-K arrival counters per lane (zero between launches)
+  // the in-launch split-K finish (gemm_x3f / gemm_x3p FIN) is opt-in (MTSAC_SPLITK_FIN=1): at the
+  // task-shard shapes its 128-256 KB slabs per tile made it slower than the separate finishing pass
+  // (profiles/r3t_fin_bench.txt)
+  int* fin_cnt() {
+    static const bool on = [] {
+      const char* e = getenv("MTSAC_SPLITK_FIN");
+      return e && atoi(e) != 0;
+    }();
+    return on ? cnt_lane[cur_lane] : nullptr;
+  }
   int cur_lane = 0;
   float* pn = nullptr;  // [critic trunk |p|^2, actor trunk, critic heads, actor heads]
   float* log_alpha = nullptr;
@@ -518,6 +529,7 @@ struct mtsac_engine {
         g.tag = i == 0 ? 1 : 0;
         g.splits = -1;  // split-K when the row tiles do not fill the chip (task shards)
         g.ws = ws_lane[cur_lane];
+        g.cnt = fin_cnt();
         gemmp(g, EPI_BIAS_RELU, net.E, i == 0 ? MTSAC_FAM_INPUT_FORWARD : MTSAC_FAM_FORWARD);
         continue;
       }
@@ -550,6 +562,7 @@ struct mtsac_engine {
         g.tag = i == 0 ? 1 : 0;
         g.splits = -1;
         g.ws = ws_lane[cur_lane];
+        g.cnt = fin_cnt();
         gemmp(g, EPI_BIAS_RELU, net.E, i == 0 ? MTSAC_FAM_INPUT_FORWARD : MTSAC_FAM_FORWARD);
         continue;
       }
@@ -648,6 +661,7 @@ struct mtsac_engine {
       g.tag = i == 0 ? 1 : 0;
       g.splits = -1;  // by tile count (gemm_x3p_splits); the lane workspace is sized for it
       g.ws = ws_lane[cur_lane];
+        g.cnt = fin_cnt();
       gemmp(g, EPI_STORE, net.E, i == 0 ? MTSAC_FAM_INPUT_WEIGHT_GRAD : MTSAC_FAM_WEIGHT_GRAD);
       if (net.dbp_chunks[i] > 0)  // dz[i]'s producer left its column sums
         colsum_finish(net.dbp[i], net.width, net.dbp_chunks[i], net.E, net.g + net.off_b[i], net.ms_b, cur);
@@ -716,6 +730,7 @@ struct mtsac_engine {
       g.K = (int)net.ald;
       g.splits = -1;
       g.ws = ws_lane[cur_lane];
+        g.cnt = fin_cnt();
       if (i - 1 >= 1 && g.Cp) {  // dz[i-1]'s fp32 copy only feeds the bias grad's column sums
         if (!want_db) {
           g.C = nullptr;
@@ -727,7 +742,7 @@ struct mtsac_engine {
           const bool fx = gemm_x3f_ok(q, EPI_RELU_MASK, net.E);
           const bool fs = !fx && !gemm_x3f_ok(g, EPI_RELU_MASK, net.E) && gemm_x3s_ok(q, EPI_RELU_MASK, net.E);
           if (fx || fs) g = q;
-          const int bm = fx ? gemm_x3f_bm(q, net.E) : 16 * gemm_x3s_ti(M, net.width, net.E);
+          const int bm = fx ? gemm_x3f_out_bm(q, EPI_RELU_MASK, net.E) : 16 * gemm_x3s_ti(M, net.width, net.E);
           net.dbp_chunks[i - 1] = (fx || fs) ? (M + bm - 1) / bm : 0;
         }
       }
@@ -1685,6 +1700,8 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
       }
     for (float*& w : e->ws_lane)
       if ((rc = e->alloc(&w, (size_t)std::max(ws, 1LL)))) return bad(rc);
+    for (int*& c : e->cnt_lane)
+      if ((rc = e->alloc(&c, (size_t)GEMM_X3F_CNT))) return bad(rc);
   }
 
   const int B = e->B;

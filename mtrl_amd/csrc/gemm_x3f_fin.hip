@@ -1,0 +1,45 @@
+// gemm_x3f_fin.hip -- the split-K gemm_x3f instances with the in-launch finish (FIN, see
+// gemm_x3f_impl.h): task-shard trunk GEMMs whose row tiles do not fill the chip, one launch instead
+// of the raw-slab GEMM plus splitk_epilogue_kernel (and, for data grads, plus a column-sum pass).
+#include "gemm_x3f_impl.h"
+
+namespace mtsac {
+namespace x3fk {
+
+template <int BM>
+static bool fin_at(const SplitGemmParams& q, int epi, dim3 grid, hipStream_t st) {
+  const dim3 blk(512);
+  const bool c = q.C != nullptr, pl = q.Cp != nullptr;
+  if (epi == EPI_BIAS_RELU) {
+    if (c && pl) hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_BIAS_RELU, true, true, false, 0, 3, 8, true>), grid, blk, 0, st, q);
+    else if (c) hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_BIAS_RELU, true, false, false, 0, 3, 8, true>), grid, blk, 0, st, q);
+    else if (pl) hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_BIAS_RELU, false, true, false, 0, 3, 8, true>), grid, blk, 0, st, q);
+    else return false;
+    return true;
+  }
+  if (epi == EPI_RELU_MASK && q.mask16) {
+    if (c && pl) hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_RELU_MASK, true, true, true, 0, 3, 8, true>), grid, blk, 0, st, q);
+    else if (pl) hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_RELU_MASK, false, true, true, 0, 3, 8, true>), grid, blk, 0, st, q);
+    else hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_RELU_MASK, true, false, true, 0, 3, 8, true>), grid, blk, 0, st, q);
+    return true;
+  }
+  return false;
+}
+
+}  // namespace x3fk
+
+// Launches the FIN form when an instance exists for (bm, epilogue, outputs); false: the caller
+// runs the raw-slab launch + finishing pass instead.
+bool gemm_x3f_fin_supported(const SplitGemmParams& q, int epi, int bm) {
+  if (q.cnt == nullptr || q.np == 1 || (bm != 128 && bm != 208)) return false;
+  const bool c = q.C != nullptr, pl = q.Cp != nullptr;
+  if (epi == EPI_BIAS_RELU) return c || pl;
+  return epi == EPI_RELU_MASK && q.mask16 != nullptr && (c || pl);
+}
+
+bool gemm_x3f_fin(const SplitGemmParams& q, int epi, int bm, dim3 grid, hipStream_t st) {
+  if (!gemm_x3f_fin_supported(q, epi, bm)) return false;
+  return bm == 128 ? x3fk::fin_at<128>(q, epi, grid, st) : x3fk::fin_at<208>(q, epi, grid, st);
+}
+
+}  // namespace mtsac

@@ -226,13 +226,16 @@ static void x3p_dispatch(int geo, const SplitGemmParams& p, int epi, int batch, 
 // Auto geometry by size (measured, tools/x3p_bench.py): 256x256 tiles (least operand traffic
 // per MFMA) when they give >= 192 workgroups or the form is the k-major weight gradient (split-K
 // fills the chip there); else 256x128.  g_x3p_geo forces one (experiments).
-static int pick_geo(int M, int N, int batch, bool kmajor, bool a_kmajor) {
+static int pick_geo(int M, int N, int K, int batch, bool kmajor, bool a_kmajor) {
   if (g_x3p_geo >= 0) return (g_x3p_geo == 5 && a_kmajor) ? 3 : g_x3p_geo;
-  if (kmajor) {  // weight grads: 256 x 256 tiles, or 128 x 128 (two workgroups per CU) for narrow
-                 // trunks whose few big tiles leave most CUs idle even at full split-K (W = 400:
-                 // 2 x 2 x E tiles of 256 -> 80 workgroups; of 128: 32 x S)
+  if (kmajor) {  // weight grads over K = rows: 256 x 256 tiles (+ split-K) at the full MT50 batch;
+                 // 256 x 128 k16 tiles where K is a task shard's or MT10's rows, and for narrow
+                 // trunks (W = 400) -- measured per launch (profiles/r3u_wgrad_geo.txt): W = 2048,
+                 // E = 2, K = 896: 83.9 vs 105.8 us (no split-K, no reduce pass), K = 1664: 153.8
+                 // vs 170.0, K = 3200: 280.3 vs 282.2, K = 6400: 547.7 vs 541.5; W = 400, E = 2,
+                 // K = 1280: 26.0 vs 26.6 (128 x 128), K = 6400: 67.0 vs 73.0
     const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256) * batch;
-    return big < 32 ? 4 : 3;
+    return (big < 32 || K < 4096) ? 2 : 3;
   }
   const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256) * batch;
   if (big < 192) return 1;
@@ -245,7 +248,7 @@ static int pick_geo(int M, int N, int batch, bool kmajor, bool a_kmajor) {
 
 int gemm_x3p_splits(int M, int N, int K, int batch, bool kmajor) {
   int bm, bn;
-  geo_tile(pick_geo(M, N, batch, kmajor, kmajor), bm, bn);
+  geo_tile(pick_geo(M, N, K, batch, kmajor, kmajor), bm, bn);
   const long long tiles = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch;
   if (tiles >= 192) return 1;
   // slices: least (rounds of tiles x S workgroups on the CUs) / S, plus a share of a round per
@@ -335,7 +338,7 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
   SplitGemmParams p = p0;
   p.dbg |= g_x3p_dbg;
   const bool kmajor = p.a_kmajor && p.b_kmajor;
-  const int geo = pick_geo(p.M, p.N, batch, kmajor, p.a_kmajor != 0);
+  const int geo = pick_geo(p.M, p.N, p.K, batch, kmajor, p.a_kmajor != 0);
   if (p.splits < 0) p.splits = gemm_x3p_splits(p.M, p.N, p.K, batch, kmajor);  // auto
   // split-K: every epilogue works (the finishing pass applies it); the vector finish needs
   // N, ldc, ldm, ldcp multiples of 4
@@ -355,8 +358,15 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
     q.Cp = nullptr;
     kepi = EPI_STORE;
   }
+  // k-major weight grads with arrival counters: the last slice of each tile reduces in-launch
+  int bm, bn;
+  geo_tile(geo, bm, bn);
+  const bool fin = S > 1 && epi == EPI_STORE && !p.Cp && kmajor && p.np != 1 && p.cnt != nullptr &&
+                   p.N % 4 == 0 && p.ldc % 4 == 0 &&
+                   (long long)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * batch <= GEMM_X3F_CNT;
+  if (!fin) q.cnt = nullptr;
   x3p_dispatch(geo, q, kepi, batch, st);
-  if (S == 1) return;
+  if (S == 1 || fin) return;
   if (epi == EPI_STORE && !p.Cp) {
     GemmParams r{};
     r.M = p.M;

@@ -132,15 +132,19 @@ struct Geo {
 };
 
 // NP: operand planes read (3: 6 products per tile and slice, fp32-accurate; 1: h*h only, bf16)
-template <class G, bool AKM, bool BKM, int EPI, bool PLANES_OUT, int NP = 3>
+// FIN (split-K weight grads, EPI_STORE, p.cnt): every slice writes its raw slab and draws a ticket
+// from the tile's arrival counter (plain stores, one agent-scope release, relaxed agent fetch_add);
+// the slice drawing S - 1 acquires and adds the tile's S slabs in slice order into C (the bits of
+// splitk_reduce_kernel), then re-arms the counter -- no separate reduce launch.
+template <class G, bool AKM, bool BKM, int EPI, bool PLANES_OUT, int NP = 3, bool FIN = false>
 __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) {
   using OA = Oper<G::BM, AKM, G::KS, NP>;
   using OB = Oper<G::BN, BKM, G::KS, NP>;
   constexpr int STAGE = OA::BYTES + OB::BYTES;
   // the stage's wave-instructions are dealt round robin: waves < DMA_X issue one more
   constexpr int DMA_LO = (OA::NJ + OB::NJ) / G::NW, DMA_X = (OA::NJ + OB::NJ) % G::NW;
-  static_assert(G::STAGES * STAGE <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[G::STAGES * STAGE];
+  static_assert(G::STAGES * STAGE + (FIN ? 16 : 0) <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[G::STAGES * STAGE + (FIN ? 16 : 0)];  // FIN: + the 'last' word
   char* lds = smem;
   const unsigned lds_base = (unsigned)(unsigned long long)(lds_void*)smem;  // LDS byte address
 
@@ -291,14 +295,73 @@ __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) 
     const int n = gridDim.x, q8 = n / 8, r8 = n % 8, x = lin % 8;
     lin = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + lin / 8;
   }
-  const int by = lin % ny, bx = (lin / ny) % nx;
   const int S = p.splits > 1 ? p.splits : 1;
-  const int zz = lin / (ny * nx), z = zz / S, sp = zz - z * S;
+  // FIN: a tile's slices adjacent (one XCD: the last arriver reads same-XCD slabs)
+  const int sp0 = FIN ? lin % S : 0;
+  if (FIN) lin /= S;
+  const int by = lin % ny, bx = (lin / ny) % nx;
+  const int z = FIN ? lin / (ny * nx) : lin / (ny * nx) / S;
+  const int sp = FIN ? sp0 : lin / (ny * nx) - z * S;
+  const int zz = z * S + sp;
   const long long k0 = (long long)sp * p.kchunk;
   const int nks = (S > 1 ? min(p.kchunk, p.K - (int)k0) : p.K) / G::KS;
   const int m0 = bx * G::BM, n0 = by * G::BN;
   kloop(p.A + z * p.sA + (AKM ? k0 * p.lda : k0), p.B + z * p.sB + (BKM ? k0 * p.ldb : k0), m0, n0, nks);
   epilogue(z, zz, S > 1, m0, n0);
+  if constexpr (FIN) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
+    __syncthreads();
+    int* last = reinterpret_cast<int*>(smem + G::STAGES * STAGE);
+    const int tile = lin;  // (z, bx, by)
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int tk = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int me = tk == S - 1;
+      if (me) __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+      *last = me;
+    }
+    __syncthreads();
+    if (*last == 0) return;  // block-uniform
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // C tile = sum of the S slabs in slice order (N, ldc multiples of 4: the host checks)
+    const long long slab = (long long)p.M * p.N;
+    const float* w = p.ws + (long long)z * S * slab;
+    float* c = p.C + z * p.sC;
+    constexpr int Q = G::BN / 4;  // float4 columns per tile row
+    constexpr int U = 8;          // float4s per thread in flight
+    static_assert(G::BM * Q % (G::NTH * U) == 0, "reduce tiling");
+    for (int e0 = t; e0 < G::BM * Q; e0 += G::NTH * U) {
+      float4 a[U];
+      long long off[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + u * G::NTH, r = m0 + e / Q, cc = n0 + 4 * (e % Q);
+        ok[u] = r < p.M && cc < p.N;
+        off[u] = (long long)r * p.N + cc;
+        if (ok[u]) a[u] = *reinterpret_cast<const float4*>(w + off[u]);
+      }
+      for (int s = 1; s < S; ++s) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (ok[u]) {
+            const float4 v = *reinterpret_cast<const float4*>(w + s * slab + off[u]);
+            a[u].x += v.x; a[u].y += v.y; a[u].z += v.z; a[u].w += v.w;
+          }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (ok[u]) {
+          const int e = e0 + u * G::NTH, r = m0 + e / Q, cc = n0 + 4 * (e % Q);
+          *reinterpret_cast<float4*>(c + (long long)r * p.ldc + cc) = a[u];
+        }
+    }
+  }
 }
 
 using GeoSmall = Geo<128, 128, 2, 2, 3, 32>;   // 4 waves, 3 x 48 KiB
@@ -317,6 +380,12 @@ template <class G, bool AKM, bool BKM, int NP>
 void launch_x3p_np(const SplitGemmParams& p, int epi, dim3 grid, hipStream_t st) {
   const bool planes = p.Cp != nullptr;
   const dim3 block(G::NTH);
+  if constexpr (AKM && BKM && NP == 3 && G::STAGES * (G::BM + G::BN) * G::KS * 2 * 3 + 16 <= 160 * 1024) {
+    if (epi == EPI_STORE && !planes && p.cnt != nullptr && p.splits > 1) {  // weight grads: in-launch finish
+      hipLaunchKernelGGL((gemm_x3p_kernel<G, true, true, EPI_STORE, false, 3, true>), grid, block, 0, st, p);
+      return;
+    }
+  }
   if (epi == EPI_BIAS_RELU) {
     if (planes) hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_BIAS_RELU, true, NP>), grid, block, 0, st, p);
     else hipLaunchKernelGGL((gemm_x3p_kernel<G, AKM, BKM, EPI_BIAS_RELU, false, NP>), grid, block, 0, st, p);

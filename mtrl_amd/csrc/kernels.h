@@ -78,7 +78,10 @@ struct SplitGemmParams {
                           // (precision bf16: the high plane only, one MFMA per product)
   float* dbp;             // gemm_x3f: column sums of the epilogue's output per row tile, [z][row tiles][N]
                           // (the next weight grad's bias grad, finished by colsum_finish), or null
+  int* cnt;               // gemm_x3f split-K: per-tile arrival counters (zero, >= GEMM_X3F_CNT ints) for
+                          // the in-launch finish, or null (a separate finishing pass)
 };
+constexpr int GEMM_X3F_CNT = 4096;
 void gemm_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
 // split-K finishing pass: C / Cp = epi(sum over the S slabs of p.ws, in slice order); the ReLU mask
 // from p.mask16 when set, else p.mask
@@ -98,6 +101,7 @@ int gemm_x3f_max_row_tiles(int M);  // row tiles of M at the shortest tile (dbp 
 // allow it (splits < 0, ws given, no dbp)
 int gemm_x3f_splits(int M, int N, int K, int batch);
 int gemm_x3f_split_bm(int M, int N, int K, int batch);  // row tile of the split-K launches (208 or 128)
+int gemm_x3f_out_bm(const SplitGemmParams& p, int epi, int batch);  // row tile of the launch gemm_x3f makes
 long long gemm_x3f_ws_floats(int M, int N, int K, int batch);
 void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t st);  // experiments
 // the same contract for small row counts (task shards, MT10): 16 TI x 64 tiles, 4 waves splitting

@@ -161,3 +161,45 @@ def test_split_k_task_shards(E, M, N, K, epi, m16, bf16):
         np.testing.assert_array_equal(Cs, torch.from_numpy(C).to(torch.bfloat16).float().numpy())
     else:
         np.testing.assert_array_equal(Cs, C)
+
+
+@pytest.mark.parametrize("E,M,N,K,epi,m16,planes", [(2, 896, 2048, 2048, 1, False, True),
+                                                    (2, 896, 2048, 2048, 1, False, False),
+                                                    (2, 768, 2048, 2048, 2, True, True),
+                                                    (1, 1792, 2048, 2048, 1, False, True),
+                                                    (2, 1280, 2040, 512, 2, True, True),
+                                                    (2, 300, 2048, 2048, 2, True, False)],
+                         ids=["shard7_fwd_planes", "shard7_fwd_top_fp32", "shard6_dgrad_m16", "shard7_actor_2b",
+                              "mt10_ragged_dgrad_m16", "short_dgrad_fp32_only"])
+def test_split_k_in_launch_finish_bitwise(E, M, N, K, epi, m16, planes):
+    """The in-launch split-K finish (every slice writes its slab and draws a ticket; the last one adds
+    the slabs in slice order with its own partial in its place and applies the epilogue) gives the
+    separate finishing pass's bits exactly, and meets the fp32 bound against float64."""
+    from mtrl_amd import _lib as L
+
+    lib = L.load()
+    rng = np.random.default_rng(M + 3 * K + epi)
+    A = rng.standard_normal((E, M, K)).astype(np.float32)
+    B = (rng.standard_normal((E, N, K)) / np.sqrt(K)).astype(np.float32)
+    bias = rng.standard_normal((E, N)).astype(np.float32) * 0.1
+    mask = np.maximum(rng.standard_normal((E, M, N)), 0).astype(np.float32)
+    p = lambda a: np.ascontiguousarray(a, np.float32).ctypes.data
+    out = []
+    for fin in (0, 4096):
+        C = np.zeros((E, M, N), np.float32)
+        Cs = np.zeros((E, M, N), np.float32) if planes else None
+        L.check(lib.mtsac_debug_gemm_x3f(epi | (256 if m16 else 0) | 2048 | fin, E, M, N, K, p(A), p(B), C.ctypes.data,
+                                         p(bias), p(mask), None if Cs is None else Cs.ctypes.data))
+        out.append((C, Cs))
+    np.testing.assert_array_equal(out[1][0], out[0][0])
+    if planes:
+        np.testing.assert_array_equal(out[1][1], out[0][1])
+        np.testing.assert_array_equal(out[1][1], out[1][0])
+    acc, scale = _ref(A, B)
+    if epi == 1:
+        want = np.maximum(acc + bias[:, None, :], 0)
+        tol = 4e-6 * (scale + np.abs(bias[:, None, :])) + 1e-30
+    else:
+        want = np.where(mask > 0, acc, 0.0)
+        tol = 4e-6 * scale + 1e-30
+    assert np.all(np.abs(out[1][0] - want) <= tol)

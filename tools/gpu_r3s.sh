@@ -1,7 +1,16 @@
-# gpu_r3s.sh -- race hunt after memory churn
+# gpu_r3s.sh -- in-launch split-K finish: x3f tests, shard/full-batch parity, shard step A/B, T7 kernel sums
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r3s
 mkdir -p $O
-timeout -k 10 400 python tools/pipe_stress2.py 6 > $O/stress2.txt 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_x3f.py tests/test_gpu_shard.py tests/test_gpu_fullbatch.py tests/test_gpu_multiprocess.py -x -v -rf --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; echo "pytest exit $rc" >> $O/tests.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u tools/shard_step.py 50 25 13 7 > $O/shard_steps_fin.txt 2>&1 || exit 1
+MTSAC_X3F_FIN=0 timeout -k 10 300 python -u tools/shard_step.py 25 13 7 > $O/shard_steps_nofin.txt 2>&1 || exit 1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$O/kt_t7 -o run -- python $GRAFT_REPO_ROOT/tools/shard_prof.py 7 > $GRAFT_REPO_ROOT/$O/kt_t7.log 2>&1 || exit 1
+cd $GRAFT_REPO_ROOT
+python tools/kernel_sums.py $O/kt_t7/run_kernel_trace.csv 60 > $O/sums_t7.txt || exit 1
+rm -rf $O/kt_t7
 echo done
