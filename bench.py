@@ -427,11 +427,13 @@ def main():
         settle = settle[0]
         eng.update_many(settle)
         eng.synchronize()
-    # Eager issue: HIP events around every GEMM launch on the stream it runs on, live over the
-    # timed steps (the step keeps its concurrent streams).  A graph replay cannot carry events:
-    # then the kernel timing comes from one extra serialised step after the timed region.
+    # The timed steps run uninstrumented: an event pair around every GEMM launch costs a few us of
+    # stream time per record, 0.2 ms per step at MT10/W400 (787 vs 587 us per step).  Eager: the
+    # kernel timing comes from HIP events around every GEMM launch on the stream it runs on, over a
+    # second pass of the same number of steps right after; a graph replay cannot carry events, so
+    # then it comes from one extra serialised step.
     live = mode == "eager"
-    eng.set_timing(live)
+    eng.set_timing(False)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(local_rank)
@@ -449,6 +451,14 @@ def main():
         elapsed = float(t.item())
     logs = eng.logs()
     assert all(math.isfinite(v) for v in logs.values()), logs
+    events_ms = None
+    if live:  # the events pass: the same steps again, every GEMM launch bracketed by HIP events
+        eng.set_timing(True)
+        a = time.perf_counter()
+        eng.update_many(args.steps)
+        eng.synchronize()
+        events_ms = 1e3 * (time.perf_counter() - a) / args.steps
+        eng.set_timing(False)
 
     # dominant-kernel roofline from the per-launch HIP events
     names = dict(GEMM_FAMILIES["split3" if args.precision == "bf16" else args.precision])
@@ -495,8 +505,10 @@ def main():
                      "traffic": traffic, "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, gfx950-corrected)",
                      "traffic_source": traffic_src, "launches": nl, "avg_launch_us": 1e3 * ms / max(nl, 1),
                      "algorithmic_flops_per_launch": fl / max(nl, 1),
-                     "timing": "HIP events per launch over the timed eager steps (concurrent streams)" if live
+                     "timing": "HIP events per launch over a second pass of the timed eager steps (the "
+                               "timed pass runs without events)" if live
                      else "graph replays carry no events: HIP events per launch in one serialised step",
+                     "events_pass_ms_per_step": events_ms,
                      "solo": {"achieved": (solo[dom][2] / max(solo[dom][1], 1)) / (solo[dom][0] / max(solo[dom][1], 1) * 1e-3) / 1e12
                               if solo[dom][0] else None,
                               "avg_launch_us": 1e3 * solo[dom][0] / max(solo[dom][1], 1),
