@@ -487,6 +487,20 @@ struct mtsac_engine {
     if (want_db) net.dbp_chunks[top] = head_backward_chunks(T_l);
   }
 
+  // head_bwd plus the head's weight/bias grad (head_backward_weight) in ONE launch; false: not
+  // launched (fp32 dz without planes, or W % 4 != 0), the caller issues the two passes
+  bool head_bwd_both(Net& net, const HeadParams& hp, const float* dout, long long s_dout, __bf16** dzp, bool want_db) {
+    const int top = net.depth - 1;
+    const PlaneOut po = top_planes(net, dzp);
+    if (po.p == nullptr) return false;
+    float* dbp = want_db ? net.dbp[top] : nullptr;
+    if (!head_backward_both(hp, dout, s_dout, nullptr, counts, rows, B, T_l, po, dbp, net.g + net.off_hW,
+                            net.g + net.off_hb, cur))
+      return false;
+    if (want_db) net.dbp_chunks[top] = head_backward_chunks(T_l);
+    return true;
+  }
+
   // ------------------------------------------------------------ trunk passes
   // acts[i] = relu(in_i @ W_i + b_i) for every member (batched over the ensemble)
   // which: 0 / 1 = params is Net::p / Net::tgt (their transposed copies or planes are current),
@@ -661,11 +675,15 @@ struct mtsac_engine {
       g.tag = i == 0 ? 1 : 0;
       g.splits = -1;  // by tile count (gemm_x3p_splits); the lane workspace is sized for it
       g.ws = ws_lane[cur_lane];
-        g.cnt = fin_cnt();
+      g.cnt = fin_cnt();
+      if (net.dbp_chunks[i] > 0) {  // dz[i]'s producer left its column sums: gemm_x3p finishes the bias
+        g.cs_part = net.dbp[i];     // grad (in its split-K reduce launch when it has one)
+        g.cs_chunks = net.dbp_chunks[i];
+        g.cs_db = net.g + net.off_b[i];
+        g.cs_sdb = net.ms_b;
+      }
       gemmp(g, EPI_STORE, net.E, i == 0 ? MTSAC_FAM_INPUT_WEIGHT_GRAD : MTSAC_FAM_WEIGHT_GRAD);
-      if (net.dbp_chunks[i] > 0)  // dz[i]'s producer left its column sums
-        colsum_finish(net.dbp[i], net.width, net.dbp_chunks[i], net.E, net.g + net.off_b[i], net.ms_b, cur);
-      else
+      if (net.dbp_chunks[i] <= 0)
         colsum(dz[i], M, net.width, net.width, (long long)M * net.width, net.E, cs_part, net.g + net.off_b[i],
                net.ms_b, cur);
       return;
@@ -938,7 +956,9 @@ struct mtsac_engine {
       cur = L;
       body();
       s.lane = L;
-      if (!evpool.empty()) {  // rotating: an event is re-recorded only pool-size segments later
+      if (L == st && one_stream && comm == nullptr) {
+        s.ev = nullptr;  // one stream, no collective stream: no other stream ever waits on it
+      } else if (!evpool.empty()) {  // rotating: an event is re-recorded only pool-size segments later
         s.ev = evpool[ev_next++ % evpool.size()];
         (void)hipEventRecord(s.ev, L);
       } else {
@@ -1082,35 +1102,47 @@ struct mtsac_engine {
       policy_head_pair(q, qn, cur);
     });
     // target critic at (s', a'), TD target (mtsac.py:529-553)
+    const bool fuse_td = one_stream || timing_serial;  // lanes: s_tg and s_cf run on two lanes
     const int s_tg = seg({s_af}, 0, [&] {
       trunk_forward(critic, critic.tgt, 1, xcn, ld_c, hct, hctp, Bl);
-      CriticHeadParams c = ch;
-      c.head = head(critic, critic.tgt, hct[critic.depth - 1], Bl, task);
-      c.mode = CH_TARGET;
-      c.logpi = logpi_n;
-      c.y_out = y;
-      critic_head(c, cur);
+      if (!fuse_td) {  // one stream: the TD target rides in the critic loss launch (s_cl)
+        CriticHeadParams c = ch;
+        c.head = head(critic, critic.tgt, hct[critic.depth - 1], Bl, task);
+        c.mode = CH_TARGET;
+        c.logpi = logpi_n;
+        c.y_out = y;
+        critic_head(c, cur);
+      }
     });
     // critic loss (mtsac.py:538-566) and head backward
     const HeadParams chp = head(critic, critic.p, hc[critic.depth - 1], Bl, task);
+    bool c_both = false;  // the critic head's weight grad went with its data pass (one launch)
     const int s_cl = seg({s_cf, s_tg}, 1, [&] {
       CriticHeadParams c = ch;
       c.head = chp;
       c.mode = CH_CRITIC;
       c.y = y;
+      if (fuse_td) {
+        c.fused_target = 1;
+        c.thead = head(critic, critic.tgt, hct[critic.depth - 1], Bl, task);
+        c.logpi = logpi_n;
+        c.y_out = y;
+      }
       c.dq = dq;
       c.row_a = row_a;
       c.row_b = row_b;
       c.inv_norm = 1.0f / ((float)critic.E * (float)B_glob);
       critic_head(c, cur);
-      head_bwd(critic, chp, dq, Bl, dzc, dzcp, true);
+      c_both = head_bwd_both(critic, chp, dq, Bl, dzcp, true);
+      if (!c_both) head_bwd(critic, chp, dq, Bl, dzc, dzcp, true);
       if (sharded()) {  // the loss sums ride in the all-reduced scalar tail (else: step_finish)
         const float* ins[2] = {row_a, row_b};
         reduce_rows(ins, 2, Bl, critic.g + critic.n_flat + 1, cur);
       }
     });
     const int s_chw = seg({s_cl}, 3, [&] {
-      head_backward_weight(chp, dq, Bl, counts, rows, Bl, critic.g + critic.off_hW, critic.g + critic.off_hb, cur);
+      if (!c_both)
+        head_backward_weight(chp, dq, Bl, counts, rows, Bl, critic.g + critic.off_hW, critic.g + critic.off_hb, cur);
     });
     const int s_cb = backward_segs(critic, critic.p, xc, ld_c, hc, hcp, dzc, dzcp, s_cl, s_chw, Bl);
     // reduce over shards, clip + Adam + Polyak (mtsac.py:599-613)
@@ -1157,11 +1189,14 @@ struct mtsac_engine {
     });
     if (pipelined) (void)hipEventRecord(ev_ap[step_par], segs[s_ap].lane);
     const HeadParams ahp = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
+    // the head's data and weight passes in one launch (head_bwd_both's conditions)
+    const bool a_both = top_planes(actor, dzap).p != nullptr && actor.width % 4 == 0;
     const int s_ahw = seg({s_ap}, 3, [&] {
-      head_backward_weight(ahp, dout_a, 0, counts, rows, Bl, actor.g + actor.off_hW, actor.g + actor.off_hb, cur);
+      if (!a_both)
+        head_backward_weight(ahp, dout_a, 0, counts, rows, Bl, actor.g + actor.off_hW, actor.g + actor.off_hb, cur);
     });
     const int s_ad = seg({s_ap}, 1, [&] {
-      head_bwd(actor, ahp, dout_a, 0, dza, dzap, true);
+      if (!(a_both && head_bwd_both(actor, ahp, dout_a, 0, dzap, true))) head_bwd(actor, ahp, dout_a, 0, dza, dzap, true);
     });
     const int s_ab = backward_segs(actor, actor.p, xa, ld_a, ha, hap, dza, dzap, s_ad, s_ahw, Bl);
     const int s_tail = seg({s_ab}, 1, [&] {

@@ -366,8 +366,12 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
                    (long long)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * batch <= GEMM_X3F_CNT;
   if (!fin) q.cnt = nullptr;
   x3p_dispatch(geo, q, kepi, batch, st);
-  if (S == 1 || fin) return;
-  if (epi == EPI_STORE && !p.Cp) {
+  const bool cs = p.cs_part != nullptr && p.cs_chunks > 0;
+  if (S == 1 || fin) {
+    if (cs) colsum_finish(p.cs_part, p.N, p.cs_chunks, batch, p.cs_db, p.cs_sdb, st);
+    return;
+  }
+  if (epi == EPI_STORE && !p.Cp) {  // the slab sums and (cs) the bias grad's column sums: one launch
     GemmParams r{};
     r.M = p.M;
     r.N = p.N;
@@ -375,9 +379,10 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
     r.ldc = p.ldc;
     r.sC = p.sC;
     r.ws = p.ws;
-    splitk_reduce(r, batch, S, st);
+    splitk_reduce(r, batch, S, st, cs ? p.cs_part : nullptr, p.cs_chunks, p.cs_db, p.cs_sdb);
     return;
   }
+  if (cs) colsum_finish(p.cs_part, p.N, p.cs_chunks, batch, p.cs_db, p.cs_sdb, st);
   splitk_finish(p, epi, S, batch, st);
 }
 

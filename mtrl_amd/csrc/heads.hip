@@ -228,19 +228,32 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
     head_dot<1>(hp.h + e * hp.sh + (long long)b * hp.W, hp.Wh + e * hp.sWh + (long long)t * hp.W, hp.W, acc);
     q[e] = acc[0] + hp.bh[e * hp.sbh + t];
   }
+  float qt[4];  // fused_target: the target critic's heads of the same row (same row, same task)
+  if (p.fused_target) {
+    const HeadParams& th = p.thead;
+    for (int e = 0; e < E; ++e) {
+      float acc[1];
+      head_dot<1>(th.h + e * th.sh + (long long)b * th.W, th.Wh + e * th.sWh + (long long)t * th.W, th.W, acc);
+      qt[e] = acc[0] + th.bh[e * th.sbh + t];
+    }
+  }
   if (lane != 0) return;
   const float alpha = expf(p.log_alpha[p.task_begin + t]);  // exp(onehot . log_alpha), mtsac.py:60-63
   float w = 1.f;
   if (p.tw != nullptr) w = p.tw[b];  // T * softmax(-log_alpha)[t] (mtsac.py:103-113)
-  if (p.mode == CH_TARGET) {
-    float mn = q[0];
-    for (int e = 1; e < E; ++e) mn = fminf(mn, q[e]);
+  auto td_target = [&](const float* qq) {
+    float mn = qq[0];
+    for (int e = 1; e < E; ++e) mn = fminf(mn, qq[e]);
     const float mnext = mn - alpha * p.logpi[b];
     float y = p.rew[b] + (1.0f - p.done[b]) * p.gamma * mnext;  // mtsac.py:547-553
     if (p.clip) y = fminf(fmaxf(y, -5000.f), 5000.f);
     p.y_out[b] = y;
+    return y;
+  };
+  if (p.mode == CH_TARGET) {
+    td_target(q);
   } else if (p.mode == CH_CRITIC) {
-    const float y = p.y[b];
+    const float y = p.fused_target ? td_target(qt) : p.y[b];
     float sq = 0.f, qs = 0.f;
     for (int e = 0; e < E; ++e) {
       float qc = q[e], dcl = 1.f;
@@ -316,15 +329,15 @@ __device__ inline float4 head_bwd_row(const HeadParams& hp, const float* __restr
   return out;
 }
 
+// (bx, by, bz) of a [W / 256][T_l HB_RS][E] grid; red: 4 x 64 float4 of LDS
 template <int HD>
-__global__ __launch_bounds__(256) void head_bwd_data_kernel(HeadParams hp, const float* __restrict__ dout,
-                                                            long long s_dout, float* __restrict__ dz, PlaneOut po,
-                                                            float* __restrict__ dbp, const int* __restrict__ counts,
-                                                            const int* __restrict__ rows, int max_rows) {
-  __shared__ float4 red[4][64];
-  const int e = blockIdx.z, t = blockIdx.y / HB_RS, rs = blockIdx.y - t * HB_RS;
+__device__ inline void head_bwd_data_body(const HeadParams& hp, const float* __restrict__ dout, long long s_dout,
+                                          float* __restrict__ dz, const PlaneOut& po, float* __restrict__ dbp,
+                                          const int* __restrict__ counts, const int* __restrict__ rows, int max_rows,
+                                          int bx, int by, int bz, int gy, float4 (*red)[64]) {
+  const int e = bz, t = by / HB_RS, rs = by - t * HB_RS;
   const int lane = threadIdx.x & 63, rl = threadIdx.x >> 6;
-  const int w = blockIdx.x * 256 + 4 * lane;
+  const int w = bx * 256 + 4 * lane;
   const bool ok = w < hp.W;
   const int n = counts[t];
   const int* rw = rows + (long long)t * max_rows;
@@ -357,10 +370,20 @@ __global__ __launch_bounds__(256) void head_bwd_data_kernel(HeadParams hp, const
   __syncthreads();
   if (rl == 0 && ok) {
     const float4 a = red[0][lane], b = red[1][lane], c = red[2][lane], d = red[3][lane];
-    *reinterpret_cast<float4*>(dbp + ((long long)e * gridDim.y + blockIdx.y) * hp.W + w) =
+    *reinterpret_cast<float4*>(dbp + ((long long)e * gy + by) * hp.W + w) =
         make_float4(((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y, ((a.z + b.z) + c.z) + d.z,
                     ((a.w + b.w) + c.w) + d.w);
   }
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void head_bwd_data_kernel(HeadParams hp, const float* __restrict__ dout,
+                                                            long long s_dout, float* __restrict__ dz, PlaneOut po,
+                                                            float* __restrict__ dbp, const int* __restrict__ counts,
+                                                            const int* __restrict__ rows, int max_rows) {
+  __shared__ float4 red[4][64];
+  head_bwd_data_body<HD>(hp, dout, s_dout, dz, po, dbp, counts, rows, max_rows, blockIdx.x, blockIdx.y, blockIdx.z,
+                         gridDim.y, red);
 }
 
 // ------------------------------------------------------------------ head backward (weights)
@@ -422,16 +445,16 @@ __global__ __launch_bounds__(256) void head_bwd_weight_scalar_kernel(HeadParams 
   }
 }
 
-// W % 4 == 0: each lane owns 4 consecutive w (16-B loads), a workgroup 256 w
+// W % 4 == 0: each lane owns 4 consecutive w (16-B loads), a workgroup 256 w; (bx, by, bz) of a
+// [T_l][W / 256][E] grid; red: 4 x 64 x HD float4 of LDS
 template <int HD>
-__global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, const float* __restrict__ dout,
-                                                              long long s_dout, const int* __restrict__ counts,
-                                                              const int* __restrict__ rows, int max_rows,
-                                                              float* __restrict__ dWh, float* __restrict__ dbh) {
-  __shared__ float4 red[4][64][HD];
-  const int t = blockIdx.x, e = blockIdx.z;
+__device__ inline void head_bwd_weight_body(const HeadParams& hp, const float* __restrict__ dout, long long s_dout,
+                                            const int* __restrict__ counts, const int* __restrict__ rows, int max_rows,
+                                            float* __restrict__ dWh, float* __restrict__ dbh, int bx, int by, int bz,
+                                            float4 (*red)[64][HD]) {
+  const int t = bx, e = bz;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int w = blockIdx.y * 256 + 4 * lane;
+  const int w = by * 256 + 4 * lane;
   const int n = counts[t];
   const int* rl = rows + (long long)t * max_rows;
   const float* h = hp.h + e * hp.sh;
@@ -473,7 +496,7 @@ __global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, con
 #pragma unroll
       for (int o = 0; o < HD; ++o) out[k * HD + o] = v[k][o];
   }
-  if (blockIdx.y == 0) {  // bias grad: 256 strided partial sums, then a fixed-order tree
+  if (by == 0) {  // bias grad: 256 strided partial sums, then a fixed-order tree
     __syncthreads();
     float* part = reinterpret_cast<float*>(&red[0][0][0]);  // >= 256 * HD floats
 #pragma unroll
@@ -491,6 +514,40 @@ __global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, con
     }
     if (threadIdx.x < HD) dbh[e * hp.sbh + t * HD + threadIdx.x] = part[threadIdx.x * 256];
   }
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, const float* __restrict__ dout,
+                                                              long long s_dout, const int* __restrict__ counts,
+                                                              const int* __restrict__ rows, int max_rows,
+                                                              float* __restrict__ dWh, float* __restrict__ dbh) {
+  __shared__ float4 red[4][64][HD];
+  head_bwd_weight_body<HD>(hp, dout, s_dout, counts, rows, max_rows, dWh, dbh, blockIdx.x, blockIdx.y, blockIdx.z,
+                           red);
+}
+
+// Both halves of a head's backward in ONE launch (they read the same dout and are independent):
+// blocks [0, nd) are head_bwd_data's [W / 256][T_l HB_RS][E] grid, the rest head_bwd_weight's
+// [T_l][W / 256][E] grid -- the same arithmetic per block, one launch fewer per network.
+template <int HD>
+__global__ __launch_bounds__(256) void head_bwd_both_kernel(HeadParams hp, const float* __restrict__ dout,
+                                                            long long s_dout, float* __restrict__ dz, PlaneOut po,
+                                                            float* __restrict__ dbp, const int* __restrict__ counts,
+                                                            const int* __restrict__ rows, int max_rows, int T_l,
+                                                            float* __restrict__ dWh, float* __restrict__ dbh) {
+  __shared__ float4 red[4][64][HD];
+  const int gw = (hp.W + 255) / 256, gy = T_l * HB_RS;
+  const int nd = gw * gy * hp.E;
+  int b = blockIdx.x;
+  if (b < nd) {
+    const int bx = b % gw, by = (b / gw) % gy, bz = b / (gw * gy);
+    head_bwd_data_body<HD>(hp, dout, s_dout, dz, po, dbp, counts, rows, max_rows, bx, by, bz, gy,
+                           reinterpret_cast<float4 (*)[64]>(&red[0][0][0]));
+    return;
+  }
+  b -= nd;
+  const int bx = b % T_l, by = (b / T_l) % gw, bz = b / (T_l * gw);
+  head_bwd_weight_body<HD>(hp, dout, s_dout, counts, rows, max_rows, dWh, dbh, bx, by, bz, red);
 }
 
 // ------------------------------------------------------------------ critic -> action grad -> policy grad
@@ -660,6 +717,26 @@ void head_backward_data(const HeadParams& hp, const float* dout, long long s_dou
 }
 
 int head_backward_chunks(int T_l) { return T_l * HB_RS; }
+
+bool head_backward_both(const HeadParams& hp, const float* dout, long long s_dout, float* dz, const int* counts,
+                        const int* rows, int max_rows, int T_l, PlaneOut po, float* dbp, float* dWh, float* dbh,
+                        hipStream_t st) {
+  if (hp.W % 4 != 0) return false;  // the scalar weight kernel: two launches
+  const int gw = (hp.W + 255) / 256;
+  const dim3 grid((unsigned)(gw * T_l * HB_RS * hp.E + T_l * gw * hp.E));
+#define HBB_LAUNCH(HDV)                                                                                       \
+  hipLaunchKernelGGL(head_bwd_both_kernel<HDV>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po, dbp, counts, rows, \
+                     max_rows, T_l, dWh, dbh)
+  switch (hp.hd) {
+    case 1: HBB_LAUNCH(1); break;
+    case 2: HBB_LAUNCH(2); break;
+    case 4: HBB_LAUNCH(4); break;
+    case 6: HBB_LAUNCH(6); break;
+    default: HBB_LAUNCH(8); break;
+  }
+#undef HBB_LAUNCH
+  return true;
+}
 
 void head_backward_weight(const HeadParams& hp, const float* dout, long long s_dout, const int* counts,
                           const int* rows, int max_rows, float* dWh, float* dbh, hipStream_t st) {

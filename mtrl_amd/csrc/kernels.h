@@ -40,7 +40,24 @@ enum GemmKind { GEMM_NN = 0, GEMM_NT = 1, GEMM_TN = 2 };
 int gemm_splits(int M, int N, int K, int batch);
 long long gemm_ws_floats(int M, int N, int batch, int splits);
 // C[z] = sum_s ws[z*S + s] (+ db likewise), fixed order: deterministic
-void splitk_reduce(const GemmParams& p, int batch, int splits, hipStream_t st);
+// everything after a split-K GEMM in one launch: the slab sums into C, the per-slice bias sums
+// (p.db), and optionally a bias grad finished from column-sum partials cs_part [batch][chunks][N]
+struct ReduceJob {
+  const float* ws;
+  int S, M, N;
+  float* C;
+  int ldc;
+  long long sC;
+  const float* dbws;
+  float* db;
+  long long sDb;
+  const float* cs_part;
+  int cs_chunks;
+  float* cs_db;
+  long long cs_sdb;
+};
+void splitk_reduce(const GemmParams& p, int batch, int splits, hipStream_t st, const float* cs_part = nullptr,
+                   int cs_chunks = 0, float* cs_db = nullptr, long long cs_sdb = 0);
 // out[z][c][r] = in[z][r][c]  (rows x cols per batch entry, dense)
 void transpose_f32(const float* in, long long s_in, float* out, long long s_out, int rows, int cols, int batch,
                    hipStream_t st);
@@ -78,6 +95,10 @@ struct SplitGemmParams {
                           // (precision bf16: the high plane only, one MFMA per product)
   float* dbp;             // gemm_x3f: column sums of the epilogue's output per row tile, [z][row tiles][N]
                           // (the next weight grad's bias grad, finished by colsum_finish), or null
+  const float* cs_part;   // gemm_x3p EPI_STORE: also finish a bias grad from column-sum partials
+  int cs_chunks;          // [batch][cs_chunks][N] (folded into the split-K reduce launch), or null
+  float* cs_db;
+  long long cs_sdb;
   int* cnt;               // gemm_x3f split-K: per-tile arrival counters (zero, >= GEMM_X3F_CNT ints) for
                           // the in-launch finish, or null (a separate finishing pass)
 };
@@ -233,6 +254,8 @@ enum CriticHeadMode { CH_TARGET = 0, CH_CRITIC = 1, CH_ACTOR = 2 };
 struct CriticHeadParams {
   HeadParams head;      // E = num_critics, hd = 1
   int mode;
+  HeadParams thead;     // CH_CRITIC with fused_target: the target critic's head at (s', a') first,
+  int fused_target;     // y = TD target (logpi = logpi(a'|s'), written to y_out), in the same launch
   const float* rew;
   const float* done;
   const float* logpi;   // target: logpi(a'|s'); actor: logpi(a|s)
@@ -267,6 +290,10 @@ void head_backward_data(const HeadParams& hp, const float* dout, long long s_dou
                         const int* rows, int max_rows, int T_l, hipStream_t st, PlaneOut po = PlaneOut{},
                         float* dbp = nullptr);
 int head_backward_chunks(int T_l);
+// head_backward_data + head_backward_weight of one head in one launch (false: W % 4 != 0, not launched)
+bool head_backward_both(const HeadParams& hp, const float* dout, long long s_dout, float* dz, const int* counts,
+                        const int* rows, int max_rows, int T_l, PlaneOut po, float* dbp, float* dWh, float* dbh,
+                        hipStream_t st);
 // dWh[e][t][w][o] = sum_{b in t} h[e][b][w] dout[e][b][o];  dbh[e][t][o] = sum dout
 void head_backward_weight(const HeadParams& hp, const float* dout, long long s_dout, const int* counts,
                           const int* rows, int max_rows, float* dWh, float* dbh, hipStream_t st);

@@ -38,6 +38,68 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int S, int M,
   }
 }
 
+// One launch for everything that follows a split-K weight gradient: blocks [0, nred) reduce the
+// slabs into C (as splitk_reduce_kernel), [nred, nred + ndb) add the per-slice bias sums (as
+// splitk_db_kernel), the rest finish the bias grad from column-sum partials (as colsum_final_kernel,
+// 64 columns per block): the same sums in the same order, two or three launches fewer per layer.
+__global__ __launch_bounds__(256) void splitk_finish_all_kernel(ReduceJob j, int nred, int ndb) {
+  const int z = blockIdx.y;
+  const int bx = blockIdx.x;
+  if (bx < nred) {
+    const long long slab = (long long)j.M * j.N;
+    const float* w = j.ws + (long long)z * j.S * slab;
+    float* c = j.C + z * j.sC;
+    const long long n4 = slab / 4;
+    const bool vec = (j.N % 4 == 0) && (j.ldc % 4 == 0);
+    for (long long i = (long long)bx * 256 + threadIdx.x; i < (vec ? n4 : slab); i += (long long)nred * 256) {
+      if (vec) {
+        float4 acc = reinterpret_cast<const float4*>(w)[i];
+        for (int s = 1; s < j.S; ++s) {
+          const float4 v = reinterpret_cast<const float4*>(w + s * slab)[i];
+          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+        const long long e = 4 * i, m = e / j.N, n = e - m * j.N;
+        *reinterpret_cast<float4*>(c + m * j.ldc + n) = acc;
+      } else {
+        float acc = w[i];
+        for (int s = 1; s < j.S; ++s) acc += w[s * slab + i];
+        const long long m = i / j.N, n = i - m * j.N;
+        c[m * j.ldc + n] = acc;
+      }
+    }
+    return;
+  }
+  if (bx < nred + ndb) {
+    const int n = (bx - nred) * 256 + threadIdx.x;
+    if (n >= j.N) return;
+    const float* w = j.dbws + (long long)z * j.S * j.N;
+    float acc = w[n];
+    for (int s = 1; s < j.S; ++s) acc += w[(long long)s * j.N + n];
+    j.db[z * j.sDb + n] = acc;
+    return;
+  }
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = (bx - nred - ndb) * 64 + cl;
+  const int cols = j.N, chunks = j.cs_chunks;
+  float s = 0.f;
+  if (c < cols) {
+    const float* pz = j.cs_part + (long long)z * chunks * cols + c;
+    int ch = g;
+    for (; ch + 28 < chunks; ch += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = pz[(long long)(ch + 4 * u) * cols];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; ch < chunks; ch += 4) s += pz[(long long)ch * cols];
+  }
+  red[g][cl] = s;
+  __syncthreads();
+  if (g == 0 && c < cols) j.cs_db[z * j.cs_sdb + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+}
+
 __global__ void splitk_db_kernel(const float* __restrict__ dbws, int S, int N, float* __restrict__ db, long long sDb) {
   const int z = blockIdx.y;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -85,15 +147,25 @@ long long gemm_ws_floats(int M, int N, int batch, int splits) {
   return (long long)batch * splits * ((long long)M * N + N);
 }
 
-void splitk_reduce(const GemmParams& p, int batch, int splits, hipStream_t st) {
+void splitk_reduce(const GemmParams& p, int batch, int splits, hipStream_t st, const float* cs_part, int cs_chunks,
+                   float* cs_db, long long cs_sdb) {
   const long long slab = (long long)p.M * p.N;
   const long long work = (p.N % 4 == 0 && p.ldc % 4 == 0) ? slab / 4 : slab;
-  const int blocks = (int)std::min<long long>((work + 255) / 256, 1024);
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(std::max(blocks, 1), batch), dim3(256), 0, st, p.ws, splits, p.M,
-                     p.N, p.C, p.ldc, p.sC);
-  if (p.db)
-    hipLaunchKernelGGL(splitk_db_kernel, dim3((p.N + 255) / 256, batch), dim3(256), 0, st,
-                       p.ws + (long long)batch * splits * slab, splits, p.N, p.db, p.sDb);
+  const int nred = std::max(1, (int)std::min<long long>((work + 255) / 256, 1024));
+  ReduceJob j{};
+  j.ws = p.ws; j.S = splits; j.M = p.M; j.N = p.N; j.C = p.C; j.ldc = p.ldc; j.sC = p.sC;
+  int ndb = 0, ncs = 0;
+  if (p.db) {
+    j.dbws = p.ws + (long long)batch * splits * slab;
+    j.db = p.db;
+    j.sDb = p.sDb;
+    ndb = (p.N + 255) / 256;
+  }
+  if (cs_part && cs_chunks > 0) {
+    j.cs_part = cs_part; j.cs_chunks = cs_chunks; j.cs_db = cs_db; j.cs_sdb = cs_sdb;
+    ncs = (p.N + 63) / 64;
+  }
+  hipLaunchKernelGGL(splitk_finish_all_kernel, dim3(nred + ndb + ncs, batch), dim3(256), 0, st, j, nred, ndb);
 }
 
 void transpose_f32(const float* in, long long s_in, float* out, long long s_out, int rows, int cols, int batch,

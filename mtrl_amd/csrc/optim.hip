@@ -413,9 +413,10 @@ __global__ __launch_bounds__(1024) void reduce_rows_kernel(RowPtrs in, int n_in,
 // zero outside this shard's tasks; the loss term of each task goes to task_loss[t]
 // one block of 16 waves, wave w over the global tasks w, w + 16, ...; after the barrier wave 0
 // sums the per-task loss terms in task order
-__device__ void alpha_grad_block(const AlphaParams& a) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int tg = wave; tg < a.T_glob; tg += 16) {
+// the per-task sums of waves [0, nw): wave w takes global tasks w, w + nw, ...
+__device__ void alpha_tasks(const AlphaParams& a, int wave, int nw) {
+  const int lane = threadIdx.x & 63;
+  for (int tg = wave; tg < a.T_glob; tg += nw) {
     const int t = tg - a.task_begin;
     float s = 0.f;
     if (t >= 0 && t < a.T_l) {
@@ -429,6 +430,11 @@ __device__ void alpha_grad_block(const AlphaParams& a) {
       a.task_loss[tg] = (t >= 0 && t < a.T_l) ? -a.log_alpha[tg] * s : 0.f;
     }
   }
+}
+
+__device__ void alpha_grad_block(const AlphaParams& a) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  alpha_tasks(a, wave, 16);
   __syncthreads();
   if (wave == 0) {
     float s = 0.f;
@@ -488,66 +494,69 @@ __device__ void write_logs_wave(const LogParams& p) {
   p.logs[9] = s;                            // alpha
 }
 
-// fixed-order sum of one [B] row vector by a 1024-thread block (reduce_rows' order)
-__device__ float block_rows_sum(const float* __restrict__ x, int B, double* s) {
-  double acc = 0.0;
-  for (int i = threadIdx.x; i < B; i += 1024) acc += (double)x[i];
-  acc = wsumd(acc);
-  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  double t = 0.0;
-  for (int w = 0; w < 16; ++w) t += s[w];
-  __syncthreads();
-  return (float)t;
-}
-
-// both networks' post-update |p| from their fused-Adam partials: threads [512 w, 512 w + 512) sum
-// network w's trunk and head partials (<= 4 strided loads per thread, all in flight), the 8 waves'
-// sums added in order
-__device__ void pnorm_half(const PnormParts& q, const float* __restrict__ head_sq, double* s) {
-  const int w = threadIdx.x >> 9, u = threadIdx.x & 511;
-  double t = 0.0, h = 0.0;
-  for (int i = u; i < q.nt[w]; i += 512) t += (double)q.pt[w][i];
-  for (int i = u; i < q.nh[w]; i += 512) h += (double)q.ph[w][i];
-  t = wsumd(t);
-  h = wsumd(h);
-  if ((threadIdx.x & 63) == 0) {
-    s[2 * (threadIdx.x >> 6)] = t;
-    s[2 * (threadIdx.x >> 6) + 1] = h;
-  }
-  __syncthreads();
-  if ((threadIdx.x & 511) == 0) {
-    double tt = 0.0, hh = 0.0;
-    for (int k = 0; k < 8; ++k) {
-      tt += s[2 * (8 * w + k)];
-      hh += s[2 * (8 * w + k) + 1];
-    }
-    const float hs = head_sq ? head_sq[w] : (float)hh;
-    q.sc[w]->pnorm = sqrtf((float)tt + hs);
-  }
-}
-
-// the step's scalar tail in one block: the loss row sums (unsharded: they need no all-reduce),
-// the temperature Adam (wave 0) beside both networks' post-update |p| (waves 1, 2), then the
-// logs and the step counter
+// the step's scalar tail in one block, its independent reductions side by side before ONE barrier:
+// waves 0-7 the temperature gradient's per-task sums (unsharded), waves 8-15 the loss row sums (three
+// [B] vectors, unsharded) and both networks' post-update |p| partials (waves 8-11 critic, 12-15
+// actor); then wave 0 finishes everything in fixed orders (alpha loss, row sums, norms), the
+// temperature Adam, the logs and the step counter.
 __global__ __launch_bounds__(1024) void step_finish_kernel(StepFinish f) {
-  __shared__ double s[32];
-  if (f.alpha_grad) {  // unsharded: the temperature gradient needs no all-reduce, so it runs here
-    alpha_grad_block(f.alpha);
-    __syncthreads();
+  __shared__ double s[48];  // [8 k + w] row sum k of wave 8 + w; [24 + 2 w + {0,1}] trunk / head |p|^2 of wave 8 + w
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (wave < 8) {
+    if (f.alpha_grad) alpha_tasks(f.alpha, wave, 8);
+  } else {
+    const int u = threadIdx.x - 512, wl = wave - 8;
+    double r[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      if (f.rows[k])
+        for (int i = u; i < f.B; i += 512) r[k] += (double)f.rows[k][i];
+    const int w = u >> 8, v = u & 255;  // network: waves 8-11 critic, 12-15 actor
+    double t = 0.0, h = 0.0;
+    for (int i = v; i < f.pn.nt[w]; i += 256) t += (double)f.pn.pt[w][i];
+    for (int i = v; i < f.pn.nh[w]; i += 256) h += (double)f.pn.ph[w][i];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r[k] = wsumd(r[k]);
+    t = wsumd(t);
+    h = wsumd(h);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) s[8 * k + wl] = r[k];
+      s[24 + 2 * wl] = t;
+      s[24 + 2 * wl + 1] = h;
+    }
   }
-  for (int k = 0; k < 3; ++k) {
-    if (!f.rows[k]) continue;
-    const float v = block_rows_sum(f.rows[k], f.B, s);
-    if (threadIdx.x == 0) *f.row_out[k] = v;
-  }
-  pnorm_half(f.pn, f.head_sq, s);
-  if (threadIdx.x < 64) alpha_adam_wave(f.alpha, f.lr, f.b1, f.b2, f.eps, f.max_norm);
   __syncthreads();
-  if (threadIdx.x < 64) {
-    write_logs_wave(f.logs);
-    if (threadIdx.x == 0) *f.counter += 1ull;
+  if (wave != 0) return;
+  const AlphaParams& a = f.alpha;
+  if (f.alpha_grad) {  // the alpha loss: the per-task terms in task order
+    float sl = 0.f;
+    for (int t = lane; t < a.T_glob; t += 64) sl += a.task_loss[t];
+    sl = wsumf(sl);
+    if (lane == 0) *a.loss_part = sl;
   }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (!f.rows[k]) continue;
+      double t = 0.0;
+      for (int w = 0; w < 8; ++w) t += s[8 * k + w];
+      *f.row_out[k] = (float)t;
+    }
+    for (int n = 0; n < 2; ++n) {
+      double tt = 0.0, hh = 0.0;
+      for (int w = 4 * n; w < 4 * n + 4; ++w) {
+        tt += s[24 + 2 * w];
+        hh += s[24 + 2 * w + 1];
+      }
+      const float hs = f.head_sq ? f.head_sq[n] : (float)hh;
+      f.pn.sc[n]->pnorm = sqrtf((float)tt + hs);
+    }
+  }
+  alpha_adam_wave(f.alpha, f.lr, f.b1, f.b2, f.eps, f.max_norm);
+  __threadfence_block();  // lane 0's scalars above, before the log reads
+  write_logs_wave(f.logs);
+  if (lane == 0) *f.counter += 1ull;
 }
 
 }  // namespace
