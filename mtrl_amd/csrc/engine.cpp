@@ -952,12 +952,21 @@ struct mtsac_engine {
                       : one_stream  ? (lane == 4 && comm != nullptr ? s4 : st)  // collectives keep their stream
                                     : (lane == 0 ? st : lane == 1 ? s1 : lane == 2 ? s2 : lane == 3 ? s3 : s4);
       for (int d : deps)
-        if (segs[d].lane != L) (void)hipStreamWaitEvent(L, segs[d].ev, 0);
+        if (segs[d].lane != L) {
+          if (segs[d].ev == nullptr && !evpool.empty()) {  // recorded lazily (below): record it now --
+            segs[d].ev = evpool[ev_next++ % evpool.size()];  // the main stream's work so far covers d
+            (void)hipEventRecord(segs[d].ev, segs[d].lane);
+          }
+          (void)hipStreamWaitEvent(L, segs[d].ev, 0);
+        }
       cur = L;
       body();
       s.lane = L;
-      if (L == st && one_stream && comm == nullptr) {
-        s.ev = nullptr;  // one stream, no collective stream: no other stream ever waits on it
+      if (L == st && one_stream) {
+        // one stream: only the collective stream (lane 4, sharded) ever waits on a main-stream
+        // segment; its event is recorded when such a wait is issued (an event record per segment
+        // left ~1.3 us between consecutive kernels)
+        s.ev = nullptr;
       } else if (!evpool.empty()) {  // rotating: an event is re-recorded only pool-size segments later
         s.ev = evpool[ev_next++ % evpool.size()];
         (void)hipEventRecord(s.ev, L);

@@ -126,7 +126,8 @@ void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t s
 }
 
 int gemm_x3f_row_tiles(int M) { return (M + x3fk::BM0 - 1) / x3fk::BM0; }
-int gemm_x3f_max_row_tiles(int M) { return (M + x3fk::BF16_BM[0] - 1) / x3fk::BF16_BM[0]; }
+int splitk_dbp_rows();
+int gemm_x3f_max_row_tiles(int M) { return (M + splitk_dbp_rows() - 1) / splitk_dbp_rows(); }  // finest dbp chunking
 
 int gemm_x3f_bm(const SplitGemmParams& p, int batch) { return p.np == 1 ? x3fk::bf16_bm(p.M, p.N, batch) : x3fk::BM0; }
 
@@ -175,8 +176,12 @@ static SplitPlan split_plan(int M, int N, int K, int batch) {
 int gemm_x3f_splits(int M, int N, int K, int batch) { return x3fk::split_plan(M, N, K, batch).s; }
 
 static int x3f_slices(const SplitGemmParams& p, int epi, int batch);
+int splitk_dbp_rows();
+static bool x3f_fin_ok(const SplitGemmParams& p, int epi, int batch);
 int gemm_x3f_out_bm(const SplitGemmParams& p, int epi, int batch) {
-  return x3f_slices(p, epi, batch) > 1 ? x3fk::split_plan(p.M, p.N, p.K, batch).bm : gemm_x3f_bm(p, batch);
+  if (x3f_slices(p, epi, batch) <= 1) return gemm_x3f_bm(p, batch);
+  // split: the in-launch finish keeps the row tile; the finishing pass sums FR-row chunks
+  return x3f_fin_ok(p, epi, batch) ? x3fk::split_plan(p.M, p.N, p.K, batch).bm : splitk_dbp_rows();
 }
 int gemm_x3f_split_bm(int M, int N, int K, int batch) { return x3fk::split_plan(M, N, K, batch).bm; }
 
@@ -205,7 +210,9 @@ static bool x3f_fin_ok(const SplitGemmParams& p, int epi, int batch) {
 
 static int x3f_slices(const SplitGemmParams& p, int epi, int batch) {
   if (p.splits >= 0 || p.ws == nullptr) return 1;
-  if (p.dbp != nullptr && !x3f_fin_ok(p, epi, batch)) return 1;  // column sums: only the in-launch finish
+  // column sums (dbp): the in-launch finish, or the finishing pass by FR-row chunks (mask16 / bias)
+  if (p.dbp != nullptr && !x3f_fin_ok(p, epi, batch) && !(epi == EPI_BIAS_RELU || (epi == EPI_RELU_MASK && p.mask16)))
+    return 1;
   static const bool bf16_split = [] {  // experiments: split-K for the one-plane kernel too
     const char* e = getenv("MTSAC_BF16_SPLIT");
     return e && atoi(e) != 0;

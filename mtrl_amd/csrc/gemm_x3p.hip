@@ -330,7 +330,83 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(SplitGemmParams p,
   }
 }
 
+// the same finish with the bias grad's column-sum partials (p.dbp): block (256 columns, FR rows, z),
+// wave w its 4 rows FR chunk + 4 w .. + 3 (loads of all four rows in flight), lane l 4 columns; the
+// four waves' column sums meet in LDS and are added in wave order -> dbp[z][row chunk][N]
+constexpr int FR = 16;  // rows per finishing block = gemm_x3f's dbp row granularity for split launches
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_epilogue_dbp_kernel(SplitGemmParams p, int S) {
+  __shared__ float4 red[4][64];
+  const int z = blockIdx.z, chunk = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = blockIdx.x * 256 + 4 * lane;
+  const bool cok = col < p.N;
+  const long long slab = (long long)p.M * p.N;
+  float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 v[4];
+  bool ok[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int row = FR * chunk + 4 * wave + k;
+    ok[k] = cok && row < p.M;
+    if (ok[k]) v[k] = *reinterpret_cast<const float4*>(p.ws + (long long)z * S * slab + (long long)row * p.N + col);
+  }
+  for (int s = 1; s < S; ++s) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int row = FR * chunk + 4 * wave + k;
+      if (ok[k]) {
+        const float4 u =
+            *reinterpret_cast<const float4*>(p.ws + ((long long)z * S + s) * slab + (long long)row * p.N + col);
+        v[k].x += u.x; v[k].y += u.y; v[k].z += u.z; v[k].w += u.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (!ok[k]) continue;
+    const int row = FR * chunk + 4 * wave + k;
+    float e[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+    if (EPI == EPI_BIAS_RELU) {
+      const float4 b = *reinterpret_cast<const float4*>(p.bias + z * p.sBias + col);
+      e[0] = fmaxf(e[0] + b.x, 0.f); e[1] = fmaxf(e[1] + b.y, 0.f);
+      e[2] = fmaxf(e[2] + b.z, 0.f); e[3] = fmaxf(e[3] + b.w, 0.f);
+    }
+    if (EPI == EPI_RELU_MASK) {
+      const bf16x4_t mk = *reinterpret_cast<const bf16x4_t*>(p.mask16 + z * p.sMask + (long long)row * p.ldm + col);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) e[j] = (float)mk[j] > 0.f ? e[j] : 0.f;
+    }
+    cs.x += e[0]; cs.y += e[1]; cs.z += e[2]; cs.w += e[3];
+    if (p.C) *reinterpret_cast<float4*>(p.C + z * p.sC + (long long)row * p.ldc + col) = make_float4(e[0], e[1], e[2], e[3]);
+    if (p.Cp) {
+      bf16x4_t h, m, l;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        __bf16 a, b, c;
+        split3_dev(e[j], a, b, c);
+        h[j] = a; m[j] = b; l[j] = c;
+      }
+      __bf16* cp = p.Cp + z * p.sCp + (long long)row * p.ldcp + col;
+      *reinterpret_cast<bf16x4_t*>(cp) = h;
+      if (p.np != 1) {
+        *reinterpret_cast<bf16x4_t*>(cp + p.pC) = m;
+        *reinterpret_cast<bf16x4_t*>(cp + 2 * p.pC) = l;
+      }
+    }
+  }
+  red[wave][lane] = cs;
+  __syncthreads();
+  if (wave == 0 && cok) {
+    const float4 a = red[0][lane], b = red[1][lane], c = red[2][lane], d = red[3][lane];
+    *reinterpret_cast<float4*>(p.dbp + ((long long)z * gridDim.y + chunk) * p.N + col) =
+        make_float4(((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y, ((a.z + b.z) + c.z) + d.z,
+                    ((a.w + b.w) + c.w) + d.w);
+  }
+}
+
 }  // namespace
+
+int splitk_dbp_rows() { return FR; }
 
 
 void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
@@ -387,6 +463,12 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
 }
 
 void splitk_finish(const SplitGemmParams& p, int epi, int S, int batch, hipStream_t st) {
+  if (p.dbp != nullptr && (epi == EPI_BIAS_RELU || (epi == EPI_RELU_MASK && p.mask16))) {
+    const dim3 grid((unsigned)((p.N + 255) / 256), (unsigned)((p.M + FR - 1) / FR), (unsigned)batch);
+    if (epi == EPI_BIAS_RELU) hipLaunchKernelGGL(splitk_epilogue_dbp_kernel<EPI_BIAS_RELU>, grid, dim3(256), 0, st, p, S);
+    else hipLaunchKernelGGL(splitk_epilogue_dbp_kernel<EPI_RELU_MASK>, grid, dim3(256), 0, st, p, S);
+    return;
+  }
   const long long n = (long long)batch * p.M * (p.N / 4);
   const dim3 grid((unsigned)((n + 255) / 256));
   if (epi == EPI_BIAS_RELU)
