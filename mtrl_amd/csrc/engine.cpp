@@ -187,6 +187,12 @@ struct mtsac_engine {
   float* dzc[MAXD] = {};
   // split3 planes of the GEMM operands among them (layers 0..D-2 of activations, 1..D-1 of grads)
   bool planes = false;
+  // the input layer's weight grad on k-major planes (gemm_x3p; dz[0] planes + bias partials from the
+  // data-grad epilogue) instead of the on-the-fly split kernel; MTSAC_INPUT_WGRAD=0: the latter
+  bool in_wgrad_planes = [] {
+    const char* v = getenv("MTSAC_INPUT_WGRAD");
+    return !(v && atoi(v) == 0);
+  }();
   int np = 3;  // operand planes the plane GEMMs read: 3 (split3) or 1 (bf16)
   __bf16* hap[MAXD] = {};
   __bf16* hcp[MAXD] = {};
@@ -737,7 +743,7 @@ struct mtsac_engine {
         g.ldm = net.width;
         g.sMask = (long long)M * net.width;
       }
-      if (dzp[i - 1]) {
+      if (dzp[i - 1] && (i - 1 >= 1 || want_db)) {  // dz[0]'s planes feed only its weight grad
         g.Cp = dzp[i - 1];
         g.ldcp = net.ald;
         g.pC = net.aps();
@@ -749,7 +755,7 @@ struct mtsac_engine {
       g.splits = -1;
       g.ws = ws_lane[cur_lane];
         g.cnt = fin_cnt();
-      if (i - 1 >= 1 && g.Cp) {  // dz[i-1]'s fp32 copy only feeds the bias grad's column sums
+      if (g.Cp) {  // dz[i-1]'s fp32 copy only feeds the bias grad's column sums
         if (!want_db) {
           g.C = nullptr;
         } else {  // one gemm_x3f pass (no split-K) writes the planes and the column sums
@@ -1804,13 +1810,14 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
         if ((rc = e->alloc(cr ? &e->hcp[i] : &e->hap[i], np))) return bad(rc);
         if (cr && (rc = e->alloc(&e->hctp[i], np))) return bad(rc);
       }
-      // dz[0] keeps no planes: its weight grad (K = B, M = in_dim) runs on the on-the-fly split
-      // kernel, cheaper than writing the planes in the data-grad epilogue (tools/step_gemms.py)
-      for (int i = 1; i < net->depth; ++i)
+      // dz[0] planes (in_wgrad_planes): the input layer's weight grad (K = B, M = in_dim) on k-major
+      // planes; else it runs on the on-the-fly split kernel from the fp32 dz[0]
+      const int d0 = e->in_wgrad_planes ? 0 : 1;
+      for (int i = d0; i < net->depth; ++i)
         if ((rc = e->alloc(cr ? &e->dzcp[i] : &e->dzap[i], np))) return bad(rc);
       const long long chunks = std::max<long long>({(long long)COLSUM_CHUNKS, gemm_x3f_max_row_tiles(e->B),
                                                     head_backward_chunks(e->T_l)});
-      for (int i = 1; i < net->depth; ++i)
+      for (int i = d0; i < net->depth; ++i)
         if ((rc = e->alloc(&net->dbp[i], (size_t)(net->E * chunks * net->width)))) return bad(rc);
     }
     {
