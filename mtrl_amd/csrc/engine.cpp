@@ -188,11 +188,10 @@ struct mtsac_engine {
   // split3 planes of the GEMM operands among them (layers 0..D-2 of activations, 1..D-1 of grads)
   bool planes = false;
   // the input layer's weight grad on k-major planes (gemm_x3p; dz[0] planes + bias partials from the
-  // data-grad epilogue) instead of the on-the-fly split kernel; MTSAC_INPUT_WGRAD=0: the latter
-  bool in_wgrad_planes = [] {
-    const char* v = getenv("MTSAC_INPUT_WGRAD");
-    return !(v && atoi(v) == 0);
-  }();
+  // data-grad epilogue) instead of the on-the-fly split kernel, for batches below 4096 rows (measured,
+  // profiles/r3ff_input_wgrad_ab.txt: MT10/W400 +1.5 %, MT50/W2048 at 6400 rows -0.5 %);
+  // MTSAC_INPUT_WGRAD=0 / 1 forces either form (set at create)
+  bool in_wgrad_planes = false;
   int np = 3;  // operand planes the plane GEMMs read: 3 (split3) or 1 (bf16)
   __bf16* hap[MAXD] = {};
   __bf16* hcp[MAXD] = {};
@@ -1663,6 +1662,10 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   e->D = c.obs_dim;
   e->n = c.batch_per_task;
   e->B = c.batch_per_task * c.task_count;
+  {
+    const char* v = getenv("MTSAC_INPUT_WGRAD");
+    e->in_wgrad_planes = v ? atoi(v) != 0 : e->B < 4096;
+  }
   e->B_glob = c.batch_per_task * c.num_tasks;
   e->R = (int)align_up(2LL * e->D + e->A + 2, 4);
   e->ld_a = (int)align_up(e->D, 4);
