@@ -67,8 +67,9 @@ int mtsac_debug_x3s_ti(int M, int N, int batch);
 int mtsac_debug_drq_groups(int fwd, int bwd);
 
 /* Eager update_many overlaps consecutive steps (the next gather and critic(s, a) forward beside
- * the previous actor backward / all-reduce / Adam); on = 0 issues whole steps instead.  Returns
- * the previous setting.  Tests and experiments. */
+ * the previous actor backward / all-reduce / Adam): on = 1 always, 0 never (whole steps), -1 the
+ * default (when the trunk gradients go through a device collective: RCCL or the modelled one).
+ * Returns the previous setting.  Tests and experiments. */
 struct mtsac_engine;
 int mtsac_debug_set_pipeline(struct mtsac_engine* engine, int32_t on);
 
@@ -76,6 +77,16 @@ int mtsac_debug_set_pipeline(struct mtsac_engine* engine, int32_t on);
  * form needs MTSAC_LANES=1 and enough hardware queues: GPU_MAX_HW_QUEUES as the process started
  * >= 5 per live engine + 3), else 0. */
 int mtsac_debug_lane_mode(struct mtsac_engine* engine);
+/* on != 0: this engine issues on one stream whatever MTSAC_LANES asks, and is not counted by the
+ * lane grant of the other live engines (experiments comparing the two issue forms in one process). */
+int mtsac_debug_force_one_stream(struct mtsac_engine* engine, int32_t on);
+/* Modelled trunk-gradient collective for one-GPU runs of a task shard: with nranks > 1 the engine
+ * takes its sharded path and, at every point where it would call RCCL, issues on the collective
+ * stream a delay of 2 (nranks - 1) / nranks * bucket bytes / bus_gbps (GB/s) held by
+ * (flags >> 8) & 255 workgroups (0: 8); the data stay as they are (a one-rank sum).  flags bit 0:
+ * the bucket reads NaN until the delay is over (a consumer without a stream edge to the
+ * collective turns the step into NaN).  nranks = 1 switches it off.  Not with a communicator or hook. */
+int mtsac_debug_set_collective_model(struct mtsac_engine* engine, int32_t nranks, double bus_gbps, int32_t flags);
 
 /* Per-launch record of the last timed step (mtsac_set_timing): i < 0 returns the number of
  * records; else dims = {family = GEMM kind, M, N, K, batch} and *ms its duration. */

@@ -1,6 +1,7 @@
 // debug.cpp -- test-only entry points (include/mtsac_debug.h) for the plane GEMM.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <string>
 #include <vector>
 
@@ -50,7 +51,7 @@ void plane_geom(int rows, int K, bool kmajor, long long& ld, long long& ps) {
   ps = (kmajor ? up32(K) : (long long)rows) * ld;
 }
 
-void split_into(const float* dsrc, int rows, int K, bool kmajor, __bf16* out) {
+void split_into(const float* dsrc, int rows, int K, bool kmajor, __bf16* out, const int* e2h = nullptr) {
   long long ld, ps;
   plane_geom(rows, K, kmajor, ld, ps);
   SplitParams s{};
@@ -63,6 +64,7 @@ void split_into(const float* dsrc, int rows, int K, bool kmajor, __bf16* out) {
   s.ldo = ld;
   s.po = ps;
   s.out_cols = (int)ld;
+  s.e2h = e2h;
   split_planes(s, false, 1, nullptr);
 }
 
@@ -193,10 +195,36 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
   const int np = ((epi >> 10) & 1) ? 1 : 3;  // bf16: the high plane only
   const bool autosplit = (epi >> 11) & 1;     // split-K by the launcher's own choice (workspace given)
   const bool fin = (epi >> 12) & 1;           // ... with arrival counters: the in-launch finish
+  const bool h2 = (epi >> 13) & 1;            // precision split2h: fp16 planes scaled per tensor
   epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || !A || !B || !C) return -22;
   DevBuf d;
   const size_t nA = (size_t)M * K * batch, nB = (size_t)N * K * batch, nC = (size_t)M * N * batch;
+  // split2h: exponents and maxima of the operands (host-side, exact), the output record
+  int* dexp = d.get<int>(8);          // [0] A, [1] B, [2] mask, [3] C (written by the kernel)
+  float* dmax = d.get<float>(4);      // [0] |A|, [1] |B|, [2] |bias|
+  float* domax = d.get<float>(65536);  // per-workgroup max |C|
+  if (!dexp || !dmax || !domax) return -12;
+  if (h2) {
+    auto amax = [](const float* x, size_t n) {
+      float m = 0.f;
+      for (size_t i = 0; i < n; ++i) m = std::max(m, std::fabs(x[i]));
+      return m;
+    };
+    auto pexp = [](float b) {
+      b *= 1.00390625f;
+      if (!(b > 0.f)) return 0;
+      int ex;
+      (void)std::frexp(b, &ex);
+      return 15 - ex;
+    };
+    const float ma = amax(A, nA), mb = amax(B, nB), mbias = bias ? amax(bias, (size_t)N * batch) : 0.f;
+    const float mm = mask ? amax(mask, nC) : 1.f;
+    const int he[4] = {pexp(ma), pexp(mb), pexp(mm), 0};
+    const float hm[3] = {ma, mb, mbias};
+    (void)hipMemcpy(dexp, he, sizeof(he), hipMemcpyHostToDevice);
+    (void)hipMemcpy(dmax, hm, sizeof(hm), hipMemcpyHostToDevice);
+  }
   float* dA = d.get<float>(nA);
   float* dB = d.get<float>(nB);
   float* dC = d.get<float>(nC);
@@ -217,13 +245,16 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
     SplitParams s{};
     s.x = dA + (size_t)z * M * K; s.ldx = K; s.rows = M; s.cols = K;
     s.out = Ap + (size_t)z * 3 * M * Kp; s.ldo = Kp; s.po = (long long)M * Kp; s.out_rows = M; s.out_cols = (int)Kp;
+    s.e2h = h2 ? dexp + 0 : nullptr;
     split_planes(s, false, 1, nullptr);
     s.x = dB + (size_t)z * N * K; s.rows = N;
     s.out = Bp + (size_t)z * 3 * N * Kp; s.po = (long long)N * Kp; s.out_rows = N;
+    s.e2h = h2 ? dexp + 1 : nullptr;
     split_planes(s, false, 1, nullptr);
     if (m16) {  // planes of the mask, row stride N
       s.x = dmask + (size_t)z * M * N; s.ldx = N; s.rows = M; s.cols = N;
       s.out = dM16 + (size_t)z * 3 * M * N; s.ldo = N; s.po = (long long)M * N; s.out_rows = M; s.out_cols = N;
+      s.e2h = h2 ? dexp + 2 : nullptr;
       split_planes(s, false, 1, nullptr);
     }
   }
@@ -241,7 +272,16 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
     g.Cp = dCp; g.ldcp = N; g.pC = (long long)M * N; g.sCp = 3 * g.pC;
   }
   g.M = M; g.N = N; g.K = (int)Kp;
-  g.np = np;
+  g.np = h2 ? 2 : np;
+  if (h2) {
+    g.ea = dexp + 0; g.eb = dexp + 1; g.em = dexp + 2; g.ec = dexp + 3;
+    g.pMask = (long long)M * N;
+    g.omax = domax;
+    g.amaxA = dmax + 0; g.namaxA = 1;
+    g.amaxB = dmax + 1; g.namaxB = 1;
+    g.amaxBias = (epi == 1 && bias) ? dmax + 2 : nullptr;
+    g.kmul = (float)K;
+  }
   if (autosplit) {
     g.ws = d.get<float>((size_t)std::max(gemm_x3f_ws_floats(M, N, (int)Kp, batch), 1LL));
     if (!g.ws) return -12;
@@ -260,7 +300,19 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
   }
   if (hipDeviceSynchronize() != hipSuccess) return -5;
   if (hipMemcpy(C, dC, sizeof(float) * nC, hipMemcpyDeviceToHost) != hipSuccess) return -5;
-  if (Csum) {
+  if (Csum && h2) {  // (h + l) 2^-ec
+    std::vector<_Float16> h(3 * nC);
+    int ec = 0;
+    if (hipMemcpy(h.data(), dCp, sizeof(_Float16) * h.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&ec, dexp + 3, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+      return -5;
+    const size_t n = (size_t)M * N;
+    for (int z = 0; z < batch; ++z)
+      for (size_t i = 0; i < n; ++i) {
+        const _Float16* q = &h[(size_t)z * 3 * n];
+        Csum[(size_t)z * n + i] = std::ldexp((float)q[i] + (float)q[n + i], -ec);
+      }
+  } else if (Csum) {
     std::vector<__bf16> h(3 * nC);
     if (hipMemcpy(h.data(), dCp, sizeof(__bf16) * h.size(), hipMemcpyDeviceToHost) != hipSuccess) return -5;
     const size_t n = (size_t)M * N;
@@ -281,10 +333,14 @@ int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int 
   const int np = ((epi >> 10) & 1) ? 1 : 3;  // bf16: the high plane only
   const bool autosplit = (epi >> 11) & 1;     // split-K by the launcher's own choice (workspace given)
   const bool fin = (epi >> 12) & 1;           // ... with arrival counters: the in-launch finish
+  const bool h2 = (epi >> 13) & 1;            // precision split2h (exponents 0: operands in [-1, 1])
   epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || iters < 1 || !ms_per_launch) return -22;
   DevBuf d;
   const long long Kp = (K + 63) / 64 * 64;
+  int* dexp = d.get<int>(8);
+  float* dmax = d.get<float>(65536);
+  if (!dexp || !dmax) return -12;
   float* fa = d.get<float>((size_t)M * Kp);
   float* fb = d.get<float>((size_t)N * Kp);
   float* C = d.get<float>((size_t)M * N * batch);
@@ -303,10 +359,17 @@ int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int 
   __bf16* Bp = d.get<__bf16>((size_t)3 * pb * batch);
   if (!Ap || !Bp) return -12;
   for (int z = 0; z < batch; ++z) {
-    split_into(fa, M, (int)Kp, false, Ap + 3 * pa * z);
-    split_into(fb, N, (int)Kp, bk, Bp + 3 * pb * z);
+    split_into(fa, M, (int)Kp, false, Ap + 3 * pa * z, h2 ? dexp : nullptr);
+    split_into(fb, N, (int)Kp, bk, Bp + 3 * pb * z, h2 ? dexp : nullptr);
   }
   SplitGemmParams g{};
+  if (h2) {
+    g.ea = dexp; g.eb = dexp; g.em = dexp; g.ec = dexp + 4;
+    g.omax = dmax + 16;
+    g.amaxA = dmax; g.namaxA = 1; g.amaxB = dmax; g.namaxB = 1;
+    g.kmul = (float)K;
+    g.pMask = (long long)M * N;
+  }
   g.A = Ap; g.lda = lda; g.pA = pa; g.sA = 3 * pa;
   g.B = Bp; g.ldb = ldb; g.pB = pb; g.sB = 3 * pb; g.b_kmajor = bk;
   g.C = C; g.ldc = N; g.sC = (long long)M * N;
@@ -317,7 +380,7 @@ int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int 
   if (outs == 2) g.Cp = nullptr;
   g.M = M; g.N = N; g.K = (int)Kp;
   g.splits = 1;
-  g.np = np;
+  g.np = h2 ? 2 : np;
   if (autosplit) {
     const long long wsf = std::max(gemm_x3f_ws_floats(M, N, (int)Kp, batch), gemm_x3p_ws_floats(M, N, (int)Kp, batch, false));
     g.ws = d.get<float>((size_t)std::max(wsf, 1LL));

@@ -150,6 +150,13 @@ struct mtsac_engine {
   hipEvent_t stage_ev[NSTAGE] = {};
   int stage_next = 0;
   hipEvent_t add_ev = nullptr;  // orders device-pointer adds after the legacy default stream
+  // device-pointer adds: the caller's arrays are packed into an engine-owned staging record on a side
+  // stream (sa) that waits only on the producer; the producer waits only on that pack, and the engine
+  // stream copies the record into the store in update order (no collection behind queued updates)
+  hipStream_t sa = nullptr;
+  float* dstage = nullptr;
+  hipEvent_t dstage_ev[NSTAGE] = {}, dpack_ev[NSTAGE] = {};
+  int dstage_next = 0;
   // inputs
   // xa holds [s | s'] for the actor's single forward: xan = xa + krows * ld_a
   float *xa = nullptr, *xan = nullptr, *xc = nullptr, *xcn = nullptr, *xcp = nullptr;
@@ -161,6 +168,7 @@ struct mtsac_engine {
   // is dead by the time step k's actor-loss pass (s_ap) has run, which they wait for.
   struct InSet {
     float* xa;
+    __bf16* xap;  // planes of xa (the input-layer GEMMs' operand; the weight grad reads them after s_ap)
     int *task, *counts, *rows;
   };
   InSet inset[2] = {};
@@ -170,7 +178,29 @@ struct mtsac_engine {
   int *s_counts = nullptr, *s_rows = nullptr;
   hipEvent_t ev_ap[2] = {}, ev_tail[2] = {};  // step k's s_ap / last segment, by step parity
   bool have_prev = false;                      // a pipelined step k is in flight (its events valid)
-  bool no_pipeline = getenv("MTSAC_NO_PIPELINE") != nullptr;  // experiments: whole steps only
+  // Cross-step pipelining of eager update_many: -1 auto (on when the trunk gradients go through a
+  // device collective -- RCCL or the modelled one -- where it hides the actor's all-reduce and Adam),
+  // 0 off, 1 on.  MTSAC_PIPELINE / mtsac_debug_set_pipeline override.
+  int pipeline_req = [] {
+    if (getenv("MTSAC_NO_PIPELINE")) return 0;
+    const char* v = getenv("MTSAC_PIPELINE");
+    return v ? atoi(v) : -1;
+  }();
+  // one-stream pipelined issue: the next step's gather + critic(s, a) forward go to the prefetch
+  // stream (s2) while the previous step's tail runs on the main stream
+  bool pf_issue = false;
+  // modelled collective (mtsac_debug_set_collective_model): a one-GPU run issues, at the RCCL points
+  // and on the collective stream, a delay of what the all-reduce of each bucket costs on nranks GPUs
+  struct CollModel {
+    int nranks = 1;
+    double gbps = 0.0;
+    int blocks = 8;
+    bool poison = false;
+  } cmodel;
+  float* cm_shadow = nullptr;
+  long long cm_cap = 0;
+  bool dev_collective() const { return comm != nullptr || cmodel.nranks > 1; }
+  bool pipeline_on() const { return pipeline_req > 0 || (pipeline_req < 0 && dev_collective()); }
   int step_par = 0;
   float *rew = nullptr, *done = nullptr, *tw = nullptr;
   int* task = nullptr;
@@ -282,16 +312,26 @@ struct mtsac_engine {
       (void)hipEventDestroy(t.a);
       (void)hipEventDestroy(t.b);
     }
-    if (comm) ncclCommDestroy(comm);
+    if (comm) {  // finalize first (flushes outstanding work), polling a non-blocking communicator
+      ncclResult_t r = ncclCommFinalize(comm);
+      for (int i = 0; r == ncclInProgress && i < 200000; ++i) {
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) break;
+      }
+      ncclCommDestroy(comm);
+    }
     for (void* p : allocs) (void)hipFree(p);
     if (stage_h) (void)hipHostFree(stage_h);
     for (hipEvent_t x : stage_ev)
       if (x) (void)hipEventDestroy(x);
     if (add_ev) (void)hipEventDestroy(add_ev);
+    for (int k = 0; k < NSTAGE; ++k)
+      for (hipEvent_t x : {dstage_ev[k], dpack_ev[k]})
+        if (x) (void)hipEventDestroy(x);
     for (hipEvent_t x : {ev_ap[0], ev_ap[1], ev_tail[0], ev_tail[1]})
       if (x) (void)hipEventDestroy(x);
     for (hipEvent_t e : evpool) (void)hipEventDestroy(e);
-    for (hipStream_t x : {st, s1, s2, s3, s4})
+    for (hipStream_t x : {st, s1, s2, s3, s4, sa})
       if (x) (void)hipStreamDestroy(x);
     if (counted_lanes) {
       Registry& r = registry();
@@ -339,11 +379,14 @@ struct mtsac_engine {
     }();
     return v;
   }
+  bool force_one = false;  // mtsac_debug_force_one_stream: this engine stays on one stream (not counted)
   static void relane(Registry& r) {
     const char* want = getenv("MTSAC_LANES");
     const int hwq = start_hw_queues();
-    const bool one = !(want && atoi(want) != 0) || (int)r.live.size() * LANES + 3 > hwq;
-    for (mtsac_engine* e : r.live) e->one_stream = one;
+    int laned = 0;
+    for (mtsac_engine* e : r.live) laned += e->force_one ? 0 : 1;
+    const bool one = !(want && atoi(want) != 0) || laned * LANES + 3 > hwq;
+    for (mtsac_engine* e : r.live) e->one_stream = one || e->force_one;
   }
   void lane_mode_for() {
     Registry& r = registry();
@@ -808,6 +851,11 @@ struct mtsac_engine {
   }
 
   void allreduce(float* buf, size_t count) {
+    if (comm == nullptr && cmodel.nranks > 1) {
+      coll_model_allreduce(buf, (long long)count, cmodel.nranks, cmodel.gbps, cmodel.blocks,
+                           cmodel.poison ? cm_shadow : nullptr, cur);
+      return;
+    }
     if (comm != nullptr) {
       ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm, cur);
       while (r == ncclInProgress) {  // non-blocking communicator: the enqueue completes asynchronously
@@ -826,7 +874,7 @@ struct mtsac_engine {
     }
   }
 
-  bool sharded() const { return comm != nullptr || hook != nullptr; }
+  bool sharded() const { return comm != nullptr || hook != nullptr || cmodel.nranks > 1; }
 
   // clip + Adam (+ Polyak) over one network; gradient already complete (and reduced).  Two launches
   // (optim.hip sumsq2 + adam_fused): the |g|^2 partials (and the Adam count), then one update pass
@@ -954,7 +1002,7 @@ struct mtsac_engine {
       if (r != hipSuccess) comm_error = std::string("step graph build: ") + hipGetErrorString(r);
     } else {
       hipStream_t L = timing_serial ? st
-                      : one_stream  ? (lane == 4 && comm != nullptr ? s4 : st)  // collectives keep their stream
+                      : one_stream  ? (pf_issue ? s2 : lane == 4 && dev_collective() ? s4 : st)  // collectives keep their stream
                                     : (lane == 0 ? st : lane == 1 ? s1 : lane == 2 ? s2 : lane == 3 ? s3 : s4);
       for (int d : deps)
         if (segs[d].lane != L) {
@@ -968,11 +1016,13 @@ struct mtsac_engine {
       body();
       s.lane = L;
       if (L == st && one_stream) {
-        // one stream: only the collective stream (lane 4, sharded) ever waits on a main-stream
-        // segment; its event is recorded when such a wait is issued (an event record per segment
-        // left ~1.3 us between consecutive kernels)
+        // one stream: only the collective stream (lane 4, sharded) and the prefetch stream ever wait
+        // on a main-stream segment; its event is recorded when such a wait is issued (an event
+        // record per segment left ~1.3 us between consecutive kernels)
         s.ev = nullptr;
       } else if (!evpool.empty()) {  // rotating: an event is re-recorded only pool-size segments later
+        // lanes: a wrapped pool could re-record an event another lane has yet to wait on
+        if (!one_stream && !ev_rotate && ev_next >= evpool.size()) comm_error = "event pool exhausted";
         s.ev = evpool[ev_next++ % evpool.size()];
         (void)hipEventRecord(s.ev, L);
       } else {
@@ -992,7 +1042,7 @@ struct mtsac_engine {
   int backward_segs(Net& net, const float* params, const float* X, int ldx, float** acts, __bf16** actp, float** dz,
                     __bf16** dzp, int d_top, int w_prev, int M) {
     int dprev = d_top, wprev = w_prev, rprev = -1;
-    const bool bucket = (comm != nullptr || hook != nullptr) && net.depth > 1;
+    const bool bucket = sharded() && net.depth > 1;
     for (int i = net.depth - 1; i >= 0; --i) {
       wprev = seg({dprev, wprev}, 3, [&, i] { wgrad_layer(net, X, ldx, acts, actp, dz, dzp, i, M); });
       if (bucket && i > 0) {
@@ -1009,7 +1059,7 @@ struct mtsac_engine {
   // the trunk-gradient all-reduce left after backward_segs: everything, or (buckets) layer 0 and
   // the scalar tail
   void reduce_rest(Net& net) {
-    if ((comm != nullptr || hook != nullptr) && net.depth > 1) {
+    if (sharded() && net.depth > 1) {
       allreduce(net.g + net.trunk_off, (size_t)(net.off_b[1] - net.trunk_off));
       allreduce(net.g + net.n_flat, (size_t)EXTRA);
     } else {
@@ -1032,16 +1082,21 @@ struct mtsac_engine {
     task = inset[k].task;
     counts = inset[k].counts;
     rows = inset[k].rows;
-    inp[0].x = xa;  // one plane buffer: the gather writes it after step k's actor pass (ev_ap), and
-                    // nothing after that pass reads it (the input-layer weight grad reads fp32 xa)
+    // the planes alternate with xa: the input-layer weight grad of step k's actor backward reads
+    // them (on k-major planes below 4096 rows) after s_ap, while step k + 1's gather writes the other set
+    inp[0].x = xa;
+    inp[0].p = inset[k].xap;
   }
 
   // pipelined: eager issue that overlaps the previous step's tail (see InSet); join: the main
   // stream waits for every lane at the end (the last step of a call, and every non-pipelined one)
   void step(bool device_batch, bool device_noise, bool pipelined = false, bool join = true) {
     const int Bl = B;
-    pipelined = pipelined && !build && !timing_serial && !one_stream;
+    pipelined = pipelined && !build && !timing_serial;
     const bool overlap = pipelined && have_prev;
+    // one stream (p2): step k's tail keeps the main stream; the overlapped segments go to s2.
+    // lanes: step k's tail is on lanes 1, 3, 4 and the overlapped segments start on lane 0.
+    const bool p2 = one_stream;
     if (overlap) use_inset(inset_cur ^ 1);
     counts = device_batch ? s_counts : inset[inset_cur].counts;
     rows = device_batch ? s_rows : inset[inset_cur].rows;
@@ -1074,9 +1129,12 @@ struct mtsac_engine {
     ch.T_glob = T_g;
 
     if (overlap) {  // the gather and critic(s, a) reuse buffers step k's actor-loss pass reads
-      (void)hipStreamWaitEvent(st, ev_ap[step_par ^ 1], 0);
-      if (cfg.use_task_weights) (void)hipStreamWaitEvent(st, ev_tail[step_par ^ 1], 0);  // reads log_alpha
+      hipStream_t w = p2 ? s2 : st;
+      (void)hipStreamWaitEvent(w, ev_ap[step_par ^ 1], 0);
+      // log_alpha (row_alpha) and row_c, which step k's tail reads
+      if (cfg.use_task_weights) (void)hipStreamWaitEvent(w, ev_tail[step_par ^ 1], 0);
     }
+    pf_issue = overlap && p2;
     const int s_in = seg({}, 0, [&] {
       GatherParams gp = gather_params();
       if (device_batch) {
@@ -1092,7 +1150,8 @@ struct mtsac_engine {
     // the previous step's tail (lanes 1, 3, 4) does not use, so it runs beside that tail
     const bool ol = overlap || lanes_alt;
     const int s_cf = seg({s_in}, ol ? 2 : 1, [&] { trunk_forward(critic, critic.p, 0, xc, ld_c, hc, hcp, Bl); });
-    if (overlap) (void)hipStreamWaitEvent(st, ev_tail[step_par ^ 1], 0);  // s_af: the updated actor
+    pf_issue = false;
+    if (overlap && !p2) (void)hipStreamWaitEvent(st, ev_tail[step_par ^ 1], 0);  // s_af: the updated actor
     // ONE actor forward over [s | s'] with the pre-update actor: update_critic samples a' ~ pi(.|s')
     // (mtsac.py:525-528) and update_actor a ~ pi(.|s) (:640-642) from the same parameters, so the
     // two row blocks share every trunk GEMM (rows krows.. are s'; the pad rows between are zeros)
@@ -1676,7 +1735,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     delete e;
     return r;
   };
-  for (hipStream_t* x : {&e->st, &e->s1, &e->s2, &e->s3, &e->s4})
+  for (hipStream_t* x : {&e->st, &e->s1, &e->s2, &e->s3, &e->s4, &e->sa})
     if (hipStreamCreateWithFlags(x, hipStreamNonBlocking) != hipSuccess) return bad(fail(-5, "stream"));
   e->lane_mode_for();
   e->cur = e->st;
@@ -1831,6 +1890,8 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
         e->inp[k].x = xs[k];
         if ((rc = e->alloc(&e->inp[k].p, (size_t)3 * net.arows * net.xld))) return bad(rc);
       }
+      e->inset[0].xap = e->inp[0].p;  // the second input set's planes (cross-step pipelining)
+      if ((rc = e->alloc(&e->inset[1].xap, (size_t)3 * e->actor.arows * e->actor.xld))) return bad(rc);
     }
     const int wmax = std::max(c.actor_width, c.critic_width);
     if ((rc = e->alloc(&e->cs_part, (size_t)std::max(1, c.num_critics) * COLSUM_CHUNKS * wmax))) return bad(rc);
@@ -1881,6 +1942,11 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   for (hipEvent_t& x : e->stage_ev)
     if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) return bad(fail(-5, "event"));
   if (hipEventCreateWithFlags(&e->add_ev, hipEventDisableTiming) != hipSuccess) return bad(fail(-5, "event"));
+  for (int k = 0; k < mtsac_engine::NSTAGE; ++k)
+    if (hipEventCreateWithFlags(&e->dstage_ev[k], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->dpack_ev[k], hipEventDisableTiming) != hipSuccess)
+      return bad(fail(-5, "event"));
+  if ((rc = e->alloc(&e->dstage, (size_t)mtsac_engine::NSTAGE * e->T_l * e->R))) return bad(rc);
   for (int k = 0; k < 2; ++k)
     if (hipEventCreateWithFlags(&e->ev_ap[k], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&e->ev_tail[k], hipEventDisableTiming) != hipSuccess)
@@ -2048,17 +2114,26 @@ int mtsac_buffer_add_stream(mtsac_engine* h, const float* obs, const float* next
   if (ndev != 0 && ndev != 5) return fail(-22, "buffer_add: pass all five arrays in host memory or all in device memory");
   float* slot = h->store + (size_t)h->h_pos * T * R;
   if (ndev == 5) {
-    // Device arrays: the pack reads them after the producer's queued work, and the producer
-    // stream waits for the pack before anything it issues next (a caching allocator hands a
-    // freed block to the next allocation on that stream), so the caller may drop or overwrite
-    // the arrays as soon as this returns.
+    // Device arrays: the pack into a staging record runs on the side stream after the producer's
+    // queued work (and after the engine stream has copied that record's previous contents out);
+    // the producer stream waits for the pack only -- not for the updates queued on the engine
+    // stream -- before anything it issues next (a caching allocator hands a freed block to the next
+    // allocation on that stream), so the caller may drop or overwrite the arrays as soon as this
+    // returns.  The engine stream then copies the record into the store slot in update order.
     hipStream_t prod = static_cast<hipStream_t>(producer_stream);
+    const int k = h->dstage_next;
+    h->dstage_next = (k + 1) % mtsac_engine::NSTAGE;
+    float* rec = h->dstage + (size_t)k * T * R;
     HIP_TRY(hipEventRecord(h->add_ev, prod));
-    HIP_TRY(hipStreamWaitEvent(h->st, h->add_ev, 0));
-    buffer_pack_slot(slot, T, R, D, A, obs, next_obs, actions, rewards, dones, h->st);
+    HIP_TRY(hipStreamWaitEvent(h->sa, h->add_ev, 0));
+    HIP_TRY(hipStreamWaitEvent(h->sa, h->dstage_ev[k], 0));  // the record's previous copy-out
+    buffer_pack_slot(rec, T, R, D, A, obs, next_obs, actions, rewards, dones, h->sa);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(h->add_ev, h->st));
-    HIP_TRY(hipStreamWaitEvent(prod, h->add_ev, 0));
+    HIP_TRY(hipEventRecord(h->dpack_ev[k], h->sa));
+    HIP_TRY(hipStreamWaitEvent(prod, h->dpack_ev[k], 0));
+    HIP_TRY(hipStreamWaitEvent(h->st, h->dpack_ev[k], 0));
+    HIP_TRY(hipMemcpyAsync(slot, rec, sizeof(float) * T * R, hipMemcpyDeviceToDevice, h->st));
+    HIP_TRY(hipEventRecord(h->dstage_ev[k], h->st));
   } else {
     const int k = h->stage_next;
     h->stage_next = (k + 1) % mtsac_engine::NSTAGE;
@@ -2362,7 +2437,7 @@ int mtsac_update_many(mtsac_engine* h, int32_t steps) {
     h->tl_next = 0;  // timing records every launch of this call
     // consecutive steps overlap (the last one joins every lane into the main stream); host hooks
     // (the bring-your-own all-reduce, which blocks the issuing thread) keep whole steps
-    const bool pipe = !h->hook && !h->no_pipeline;
+    const bool pipe = !h->hook && h->pipeline_on();
     for (int s = 0; s < steps; ++s) h->step(true, true, pipe, s + 1 == steps);
     HIP_TRY(hipGetLastError());
     return 0;
@@ -2479,11 +2554,13 @@ int mtsac_comm_init(mtsac_engine* h, const void* unique_id, int32_t nranks, int3
   return mtsac_comm_init_timeout(h, unique_id, nranks, rank, v ? atof(v) : 0.0);
 }
 
-// The communicator is created non-blocking (ncclConfig_t.blocking = 0) so that a peer that never
-// joins (a dead rank, a wrong unique id) ends in an error after timeout_s instead of a hang:
-// ncclCommInitRankConfig returns at once and the init is polled through ncclCommGetAsyncError;
-// on timeout the half-built communicator is aborted.  Collectives on it may then return
-// ncclInProgress while their connections are set up; allreduce() waits those out.
+// With timeout_s > 0 the communicator is created non-blocking (ncclConfig_t.blocking = 0) so that a
+// peer that never joins (a dead rank, a wrong unique id) ends in an error after timeout_s instead of
+// a hang: ncclCommInitRankConfig returns at once and the init is polled through
+// ncclCommGetAsyncError; on timeout the half-built communicator is aborted.  Collectives on it may
+// then return ncclInProgress while their connections are set up; allreduce() waits those out.
+// timeout_s <= 0 keeps RCCL's blocking communicator.  Neither form is issued inside a graph capture:
+// sharded runs step eagerly (bench.py), and non-blocking RCCL under capture is untested on >1 device.
 int mtsac_comm_init_timeout(mtsac_engine* h, const void* unique_id, int32_t nranks, int32_t rank, double timeout_s) {
   if (!h || !unique_id) return fail(-22, "null argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(-22, "bad rank / nranks");
@@ -2492,7 +2569,9 @@ int mtsac_comm_init_timeout(mtsac_engine* h, const void* unique_id, int32_t nran
   std::memcpy(&id, unique_id, sizeof(id));
   HIP_TRY(hipSetDevice(h->device));
   ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
-  config.blocking = 0;
+  // non-blocking only when a timeout is asked for: then the init is polled and a peer that never
+  // joins ends in -110; without one the communicator (and every collective on it) stays blocking
+  config.blocking = timeout_s > 0 ? 0 : 1;
   ncclComm_t comm = nullptr;
   ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, id, rank, &config);
   if (r != ncclSuccess && r != ncclInProgress)
@@ -2618,9 +2697,46 @@ int mtsac_get_timing_kernel(mtsac_engine* h, int32_t family, char* buf, int32_t 
 // ---------------------------------------------------------------- debug (include/mtsac_debug.h)
 int mtsac_debug_set_pipeline(mtsac_engine* h, int32_t on) {
   if (!h) return fail(-22, "null engine");
-  const int was = h->no_pipeline ? 0 : 1;
-  h->no_pipeline = on == 0;
+  const int was = h->pipeline_req;
+  h->pipeline_req = on < 0 ? -1 : on != 0 ? 1 : 0;
   return was;
+}
+
+int mtsac_debug_set_collective_model(mtsac_engine* h, int32_t nranks, double bus_gbps, int32_t flags) {
+  if (!h) return fail(-22, "null engine");
+  if (h->comm || h->hook) return fail(-16, "a communicator or all-reduce hook is installed");
+  if (nranks < 1 || (nranks > 1 && !(bus_gbps > 0.0))) return fail(-22, "nranks >= 1 and bus_gbps > 0");
+  HIP_TRY(hipStreamSynchronize(h->st));
+  h->cmodel.nranks = nranks;
+  h->cmodel.gbps = bus_gbps;
+  h->cmodel.poison = (flags & 1) != 0;
+  h->cmodel.blocks = ((flags >> 8) & 255) ? (flags >> 8) & 255 : 8;
+  if (h->cmodel.poison) {  // the shadow holds the largest bucket: a whole trunk + the scalar tail
+    long long need = 0;
+    for (const Net* net : {&h->actor, &h->critic}) need = std::max(need, net->n_flat - net->trunk_off + EXTRA);
+    if (need > h->cm_cap) {
+      int rc = h->alloc(&h->cm_shadow, (size_t)need);
+      if (rc) return rc;
+      h->cm_cap = need;
+    }
+  }
+  if (h->gexec) {  // the step's structure changed (buckets, sharded reductions)
+    (void)hipGraphExecDestroy(h->gexec);
+    (void)hipGraphDestroy(h->graph);
+    h->gexec = nullptr;
+    h->graph = nullptr;
+  }
+  return 0;
+}
+
+int mtsac_debug_force_one_stream(mtsac_engine* h, int32_t on) {
+  if (!h) return fail(-22, "null engine");
+  HIP_TRY(hipStreamSynchronize(h->st));
+  mtsac_engine::Registry& r = mtsac_engine::registry();
+  std::lock_guard<std::mutex> g(r.mu);
+  h->force_one = on != 0;
+  mtsac_engine::relane(r);
+  return 0;
 }
 
 int mtsac_debug_lane_mode(mtsac_engine* h) {

@@ -53,6 +53,70 @@ struct TileOut {
   bool vec;             // every row start 16-B aligned (N, ldc, ldm, ldcp multiples of 4)
 };
 
+// ---- precision split2h: x * 2^e = h + l as two fp16 values (h = fp16(x 2^e), l = fp16(x 2^e - h);
+// the subtraction is exact), with e per tensor chosen from an upper bound of |x| so that |x 2^e| <
+// 2^15 (no overflow).  Elements above 2^-3 of the scaled range carry 22 significant bits; below,
+// the absolute error is <= 2^-25 of the scaled unit.  A positive x whose planes would both round to
+// zero keeps the smallest fp16 subnormal in l, so 'x > 0 <=> h > 0 or l > 0' holds exactly (the
+// ReLU mask of the data grad reads the planes).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+__device__ inline void split2h_dev(float x, float s, _Float16& h, _Float16& l) {
+  const float y = x * s;
+  h = (_Float16)y;
+  l = (_Float16)(y - (float)h);
+  if (x > 0.f && h == (_Float16)0.f && l == (_Float16)0.f) l = __builtin_bit_cast(_Float16, (unsigned short)1);
+}
+
+// the planes' exponent for an upper bound of |x|: |x| 2^e < 2^15 (a margin of 2^-8 covers the fp32
+// rounding of the bounded sums)
+__device__ inline int plane_exp(float bound) {
+  bound *= 1.00390625f;
+  if (!(bound > 0.f) || !(bound < 3.0e38f)) return 0;
+  int ex;
+  (void)frexpf(bound, &ex);  // bound < 2^ex
+  return min(100, max(-100, 15 - ex));
+}
+
+// block-wide max of one value per thread (every thread gets the result); scratch: 16 floats
+__device__ inline float block_max_val(float m, float* scratch) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = m;
+  __syncthreads();
+  float r = 0.f;
+  for (int w = 0; w < (int)(blockDim.x + 63) / 64; ++w) r = fmaxf(r, scratch[w]);
+  __syncthreads();
+  return r;
+}
+
+// max over n recorded partial maxima, by the whole block (every thread gets the result); scratch: 16 floats
+__device__ inline float block_max_of(const float* __restrict__ v, int n, float* scratch) {
+  float m = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, v[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = m;
+  __syncthreads();
+  float r = 0.f;
+  for (int w = 0; w < (int)(blockDim.x + 63) / 64; ++w) r = fmaxf(r, scratch[w]);
+  __syncthreads();
+  return r;
+}
+
+// the output planes' exponent of a split2h GEMM launch (SplitGemmParams bound inputs)
+__device__ inline int gemm_out_exp(const SplitGemmParams& p, float* scratch) {
+  const float ma = p.amaxA ? block_max_of(p.amaxA, p.namaxA, scratch) : 0.f;
+  const float mb = p.amaxB ? block_max_of(p.amaxB, p.namaxB, scratch) : 0.f;
+  const float mbias = p.amaxBias ? *p.amaxBias : 0.f;
+  return plane_exp(p.kmul * ma * mb + mbias);
+}
+
+__device__ inline float exp2i(int e) { return __builtin_bit_cast(float, (unsigned)(127 + e) << 23); }  // |e| <= 126
+
 __device__ inline void split3_dev(float x, __bf16& h, __bf16& m, __bf16& l) {
   h = (__bf16)x;
   const float r1 = x - (float)h;

@@ -72,6 +72,10 @@ static long long bf16_workgroups(int M, int N, int batch) {
 template <int EPI, bool C_OUT, bool P_OUT, bool MASK16, int TAG = 0>
 void launch(const SplitGemmParams& p, dim3 grid, hipStream_t st, int bm) {
   const dim3 blk(512);
+  if (p.np == 2) {  // split2h: two fp16 planes, 3 products
+    hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 2>), grid, blk, 0, st, p);
+    return;
+  }
   if (p.np != 1) {
     hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 3>), grid, blk, 0, st, p);
     return;
@@ -202,7 +206,7 @@ bool gemm_x3f_fin(const SplitGemmParams& q, int epi, int bm, dim3 grid, hipStrea
 // the in-launch finish applies to this split launch (counters given, an instance for its outputs,
 // the tiles within the counter array)
 static bool x3f_fin_ok(const SplitGemmParams& p, int epi, int batch) {
-  if (p.cnt == nullptr) return false;
+  if (p.cnt == nullptr || p.np == 2) return false;
   const x3fk::SplitPlan sp = x3fk::split_plan(p.M, p.N, p.K, batch);
   const long long tiles = (long long)((p.M + sp.bm - 1) / sp.bm) * ((p.N + x3fk::BN - 1) / x3fk::BN) * batch;
   return tiles <= GEMM_X3F_CNT && gemm_x3f_fin_supported(p, epi, sp.bm);
@@ -263,7 +267,10 @@ int gemm_x3f(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
     const int bm = split_plan(p0.M, p0.N, p0.K, batch).bm;
     const dim3 grid((unsigned)(((p0.M + bm - 1) / bm) * ((p0.N + BN - 1) / BN) * batch * S_eff));
     const dim3 blk(512);
-    switch (bm * 4 + (p0.np == 1 ? 1 : 3)) {
+    switch (bm * 4 + (p0.np == 1 ? 1 : p0.np == 2 ? 2 : 3)) {
+      case BMS * 4 + 2: hipLaunchKernelGGL((gemm_x3f_kernel<BMS, EPI_STORE, true, false, false, 0, 2>), grid, blk, 0, st, q); break;
+      case BM0 * 4 + 2: hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI_STORE, true, false, false, 0, 2>), grid, blk, 0, st, q); break;
+      case BMT * 4 + 2: hipLaunchKernelGGL((gemm_x3f_kernel<BMT, EPI_STORE, true, false, false, 0, 2>), grid, blk, 0, st, q); break;
       case BMS * 4 + 1: hipLaunchKernelGGL((gemm_x3f_kernel<BMS, EPI_STORE, true, false, false, 0, 1>), grid, blk, 0, st, q); break;
       case BMS * 4 + 3: hipLaunchKernelGGL((gemm_x3f_kernel<BMS, EPI_STORE, true, false, false, 0, 3>), grid, blk, 0, st, q); break;
       case BMT * 4 + 1: hipLaunchKernelGGL((gemm_x3f_kernel<BMT, EPI_STORE, true, false, false, 0, 1>), grid, blk, 0, st, q); break;

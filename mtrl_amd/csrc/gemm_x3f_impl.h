@@ -32,6 +32,17 @@ __device__ inline void wait_vm(bf16x8 (&b)[JB][NP]) {
                  : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[0][2]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[1][2])
                  : "n"(N)
                  : "memory");
+  else if constexpr (JB == 2 && NP == 2)
+    asm volatile("s_waitcnt vmcnt(%4)"
+                 : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1])
+                 : "n"(N)
+                 : "memory");
+  else if constexpr (NP == 2)
+    asm volatile("s_waitcnt vmcnt(%8)"
+                 : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[2][0]), "+v"(b[2][1]),
+                   "+v"(b[3][0]), "+v"(b[3][1])
+                 : "n"(N)
+                 : "memory");
   else if constexpr (JB == 2)
     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(b[0][0]), "+v"(b[1][0]) : "n"(N) : "memory");
   else if constexpr (NP == 3)
@@ -51,7 +62,9 @@ __device__ inline void wait_vm(bf16x8 (&b)[JB][NP]) {
 // two row tiles' MFMA chains changed nothing there).
 // ABL == TAG_INPUT changes nothing: it only gives input-layer launches their own kernel symbol, so
 // rocprof stats and PMC passes separate them from the hidden layers.
-// NP: operand planes read (3: 6 products, fp32-accurate; 1: the high plane only, precision bf16)
+// NP: operand planes read (3: 6 products, fp32-accurate; 1: the high plane only, precision bf16;
+// 2: precision split2h -- two fp16 planes of x 2^e per operand, 3 products h*l, l*h, h*h, the
+// accumulator unscaled by 2^-(eA + eB) in the epilogue, output planes at the exponent of the bound)
 // WV: waves per workgroup.  8 (two per SIMD): wave w owns the BM x 32 column slab [32w, 32w + 32);
 // 4 (one per SIMD, up to 512 registers): BM x 64 slabs, so each A fragment read from LDS feeds twice
 // the MFMAs (4 column fragments) -- half the LDS traffic per product, the bound of the one-plane
@@ -76,7 +89,7 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   constexpr int PW = (ABL & 512) ? P0 : PMAX - 1;  // pieces every wave has issued after B(kt, 1)
   // the epilogue reuses the ring as scratch: two 16 x (BN + 4) fp32 row-block images + 8 x BN
   // column-sum partials -- more than the ring of the short one-plane tiles holds
-  constexpr int EPI_LDS = (2 * 16 * (BN + 4) + WV * BN) * 4;
+  constexpr int EPI_LDS = (2 * 16 * (BN + 4) + WV * BN + 16) * 4;  // + the split2h max scratch
   constexpr int SMEM0 = 2 * STAGE > EPI_LDS ? 2 * STAGE : EPI_LDS;
   constexpr int SMEM = SMEM0 + (FIN ? 16 : 0);  // FIN: the 'last slice' word after the scratch
   static_assert(BM % 16 == 0 && SMEM <= 160 * 1024, "tile");
@@ -202,14 +215,20 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
 #pragma unroll
         for (int j = 0; j < JB; ++j) {
           f32x4 c = acc[i][j];
-          if constexpr (NP == 3) {
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], b[j][1], c, 0, 0, 0);  // m*m
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][2], c, 0, 0, 0);  // h*l
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[2], b[j][0], c, 0, 0, 0);  // l*h
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][1], c, 0, 0, 0);  // h*m
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], b[j][0], c, 0, 0, 0);  // m*h
+          if constexpr (NP == 2) {  // fp16 planes: h*l, l*h, h*h
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[0]), __builtin_bit_cast(f16x8, b[j][1]), c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[1]), __builtin_bit_cast(f16x8, b[j][0]), c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[0]), __builtin_bit_cast(f16x8, b[j][0]), c, 0, 0, 0);
+          } else {
+            if constexpr (NP == 3) {
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], b[j][1], c, 0, 0, 0);  // m*m
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][2], c, 0, 0, 0);  // h*l
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[2], b[j][0], c, 0, 0, 0);  // l*h
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][1], c, 0, 0, 0);  // h*m
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[1], b[j][0], c, 0, 0, 0);  // m*h
+            }
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][0], c, 0, 0, 0);  // h*h
           }
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][0], c, 0, 0, 0);  // h*h
           acc[i][j] = c;
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -230,6 +249,19 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   constexpr int TS = BN + 4;  // image row stride (floats): the 4 row groups of a write land 16 banks apart
   constexpr int RP = 8 / WV;  // row pairs per wave and block
   float* img = reinterpret_cast<float*>(smem);
+  // split2h: unscale the products, and the output planes' exponent from the bound (every workgroup
+  // alike); the scratch for the maxima sits past the epilogue's images and column-sum partials
+  float unscale = 1.f, oscale = 1.f;
+  float* mscr = img + 2 * 16 * TS + WV * BN;
+  if constexpr (NP == 2) {
+    unscale = exp2i(-*p.ea) * exp2i(-*p.eb);
+    if (P_OUT && !FIN) {
+      const int ec = gemm_out_exp(p, mscr);
+      oscale = exp2i(ec);
+      if (blockIdx.x == 0 && t == 0) *p.ec = ec;
+    }
+  }
+  float omx = 0.f;  // this lane's max |out| (split2h planes)
   const int oc = 8 * (lane & 31);
   const int col = n0 + oc;
   const bool colok = col < p.N;  // N % 8 == 0: a lane's 8 columns are all in or all out
@@ -324,6 +356,10 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
     if (row >= p.M || !colok) continue;
     if ((ABL & 128) && p.M > 0) continue;  // ablation: no epilogue stores (p.M > 0 keeps the MFMAs live)
     float e[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+    if constexpr (NP == 2 && !FIN) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) e[c] *= unscale;
+    }
     if (two) {  // s0 + s1 (fp32 addition commutes: the same bits whichever slice finishes)
 #pragma unroll
       for (int c = 0; c < 8; ++c) e[c] = e[c] + pre[i % PB][c];
@@ -352,7 +388,13 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
       for (int c = 0; c < 8; ++c) e[c] = fmaxf(e[c] + bias[c], 0.f);
     }
     if (EPI == EPI_RELU_MASK) {
-      if (MASK16) {
+      if (MASK16 && NP == 2) {  // fp16 planes: x > 0 <=> h > 0 or l > 0 (split2h_dev)
+        const __bf16* mp = p.mask16 + z * p.sMask + (long long)row * p.ldm + col;
+        const i16x8 mh = __builtin_bit_cast(i16x8, *reinterpret_cast<const bf16x8*>(mp));
+        const i16x8 ml = __builtin_bit_cast(i16x8, *reinterpret_cast<const bf16x8*>(mp + p.pMask));
+#pragma unroll
+        for (int c = 0; c < 8; ++c) e[c] = (mh[c] > 0 || ml[c] > 0) ? e[c] : 0.f;
+      } else if (MASK16) {
         const bf16x8 mk = *reinterpret_cast<const bf16x8*>(p.mask16 + z * p.sMask + (long long)row * p.ldm + col);
 #pragma unroll
         for (int c = 0; c < 8; ++c) e[c] = (float)mk[c] > 0.f ? e[c] : 0.f;
@@ -371,7 +413,19 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
       *reinterpret_cast<float4*>(cp) = make_float4(e[0], e[1], e[2], e[3]);
       *reinterpret_cast<float4*>(cp + 4) = make_float4(e[4], e[5], e[6], e[7]);
     }
-    if (P_OUT) {
+    if (P_OUT && NP == 2) {
+      f16x8 h, l;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        _Float16 a_, b_;
+        split2h_dev(e[c], oscale, a_, b_);
+        h[c] = a_; l[c] = b_;
+        omx = fmaxf(omx, fabsf(e[c]));
+      }
+      __bf16* pp = Cp + (long long)row * p.ldcp + col;
+      *reinterpret_cast<f16x8*>(pp) = h;
+      *reinterpret_cast<f16x8*>(pp + p.pC) = l;
+    } else if (P_OUT) {
       bf16x8 h, m, l;
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
@@ -387,6 +441,10 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
       }
     }
     }  // row pairs
+  }
+  if constexpr (NP == 2 && P_OUT && !FIN) {  // this workgroup's max |out|: the next producer's bound input
+    const float m = block_max_val(omx, mscr);
+    if (t == 0 && p.omax) p.omax[blockIdx.x] = m;
   }
   if (p.dbp) {  // the tile's column sums: lanes l, l + 32 of every wave hold the same 8 columns
     float* red = img + 2 * 16 * TS;  // [WV waves][256]

@@ -59,6 +59,13 @@ __global__ __launch_bounds__(256) void split_kernel(SplitParams s) {
       if (orow >= s.out_rows || ocol >= s.out_cols) continue;
       o = (long long)orow * s.ldo + ocol;
     }
+    if (s.e2h) {
+      _Float16 h, l;
+      split2h_dev(v, exp2i(*s.e2h), h, l);
+      reinterpret_cast<_Float16*>(out)[o] = h;
+      reinterpret_cast<_Float16*>(out)[o + s.po] = l;
+      continue;
+    }
     const __bf16 h = (__bf16)v;
     const float r1 = v - (float)h;
     const __bf16 m = (__bf16)r1;
@@ -85,6 +92,20 @@ __global__ __launch_bounds__(256) void split_rows_kernel(SplitParams s, long lon
   } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = (r < s.rows && c + j < s.cols) ? x[c + j] : 0.f;
+  }
+  if (s.e2h) {
+    const float sc = exp2i(*s.e2h);
+    f16x4 h, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      _Float16 a, b;
+      split2h_dev(v[j], sc, a, b);
+      h[j] = a; l[j] = b;
+    }
+    __bf16* o = s.out + z * s.so + (long long)r * s.ldo + c;
+    *reinterpret_cast<f16x4*>(o) = h;
+    *reinterpret_cast<f16x4*>(o + s.po) = l;
+    return;
   }
   bf16x4_t h, m, l;
 #pragma unroll

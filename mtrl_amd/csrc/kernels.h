@@ -101,6 +101,23 @@ struct SplitGemmParams {
   long long cs_sdb;
   int* cnt;               // gemm_x3f split-K: per-tile arrival counters (zero, >= GEMM_X3F_CNT ints) for
                           // the in-launch finish, or null (a separate finishing pass)
+  // ---- precision split2h (np == 2): every operand is two fp16 planes of x * 2^e, e per tensor
+  // (PlaneRec); the products are unscaled by 2^-(eA + eB).  Output planes: written with the exponent
+  // of the a-priori bound  kmul * max|A| * max|B| + max|bias|  (PlaneRec::exp_for), which every
+  // workgroup derives alike from the inputs' recorded maxima; workgroup 0 stores it in *ec and every
+  // workgroup its max |out| in omax[blockIdx.x] (the next producer's bound input).
+  const int* ea;
+  const int* eb;
+  const int* em;          // the mask planes' exponent (unused: the mask reads signs only)
+  long long pMask;        // plane stride of the mask16 planes (np == 2: x > 0 <=> hi > 0 or lo > 0)
+  int* ec;
+  float* omax;
+  const float* amaxA;     // A's producer maxima [namaxA]
+  int namaxA;
+  const float* amaxB;     // B's maxima [namaxB] (the weights' record)
+  int namaxB;
+  const float* amaxBias;  // max |bias| (one float) or null
+  float kmul;             // the number of terms in each output sum (unpadded K)
 };
 constexpr int GEMM_X3F_CNT = 4096;
 void gemm_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
@@ -144,6 +161,7 @@ struct SplitParams {
   __bf16* out;
   long long ldo, po, so;
   int out_rows, out_cols;
+  const int* e2h;  // non-null: precision split2h, two fp16 planes of x * 2^(*e2h) (gemm_common.h split2h_dev)
 };
 void split_planes(const SplitParams& s, bool transpose, int batch, hipStream_t st);
 // db[z][c] = sum_r x[z][r][c] (deterministic two-pass; part holds batch*COLSUM_CHUNKS*cols floats)
@@ -318,6 +336,12 @@ void row_alpha(const int* task, int task_begin, const float* log_alpha, int T_gl
 // ------------------------------------------------------------------ reductions / optimizer
 // out[i] = sum over rows of in_i (deterministic single-block tree)
 void reduce_rows(const float* const* ins, int n_in, int B, float* out, hipStream_t st);
+
+// modelled collective (coll_model.hip): 2 (N - 1) / N * bytes over bus_gbps, held by `blocks`
+// workgroups on the stream; shadow non-null: the bucket is NaN until the delay is over
+double coll_model_us(long long bytes, int nranks, double bus_gbps);
+void coll_model_allreduce(float* buf, long long count, int nranks, double bus_gbps, int blocks, float* shadow,
+                          hipStream_t st);
 // partial sums of squares of x[0..n) into partials[grid]; returns grid size used
 int sumsq_partials(const float* x, long long n, float* partials, int max_blocks, hipStream_t st);
 // optimizer scalars: sums partials, computes norm and clip scale

@@ -35,6 +35,8 @@ CASES = {
     "s3_mt50_w2048": dict(T=50, W=2048, n=128, clip=False),
     "s2_mt10_w2048_clip": dict(T=10, W=2048, n=128, clip=True),
 }
+# S4: the literal experiments/mt50_mtmhsac_v2.py (MT50 at the default width 400), sharded only
+SHARD_CASES = dict(CASES, s4_mt50_w400=dict(T=50, W=400, n=128, clip=False))
 
 
 def _cfg(spec):
@@ -46,7 +48,7 @@ def _cfg(spec):
 def _problem(name):
     """fp32-representable start state, one batch + noise, and the float64 oracle step (cached:
     the same oracle result serves both precisions and the sharded run)."""
-    spec = CASES[name]
+    spec = SHARD_CASES[name]
     cfg = _cfg(spec)
     T, n = spec["T"], spec["n"]
     B = n * T
@@ -130,16 +132,19 @@ def test_full_batch_step_matches_oracle(name, precision):
 
 
 @pytest.mark.parametrize("precision", [0, 1], ids=["fp32", "split3"])
-def test_full_batch_8way_shard_matches_oracle(precision):
+@pytest.mark.parametrize("name", ["s3_mt50_w2048", "s4_mt50_w400"])
+def test_full_batch_8way_shard_matches_oracle(precision, name):
     """The MT50 8-GPU task split (7,7,6,6,6,6,6,6 tasks, 128 rows each) as 8 engines on one
     device reducing through the in-process hook (same reduction points as RCCL), against
-    the float64 oracle of the unsharded step."""
+    the float64 oracle of the unsharded step.  S3 (W=2048) and S4, the literal
+    experiments/mt50_mtmhsac_v2.py width 400 (a shard's trunk GEMMs then run gemm_x3s and the
+    256x128 weight-grad tiles)."""
     import threading
 
     from mtrl_amd.shard import InProcessAllReduce, local_rows, shard_tasks
 
-    name, world = "s3_mt50_w2048", 8
-    spec = CASES[name]
+    world = 8
+    spec = SHARD_CASES[name]
     cfg, st, batch, en, ec, st1, want = _problem(name)
     T, n = spec["T"], spec["n"]
     shards = []
@@ -172,6 +177,94 @@ def test_full_batch_8way_shard_matches_oracle(precision):
         b0, c0 = shard_tasks(T, world, r)
         _check_params(e, st1, f"shard8/p{precision}/r{r}", b0, c0)
         e.close()
+
+
+def test_full_batch_modelled_collective_matches_oracle():
+    """S3 at full batch through the SHARDED step with the device collective on its own stream (the
+    modelled collective, a one-rank sum, with every bucket NaN until its collective is done, so a
+    consumer that does not wait for the collective stream poisons the step): the bucketed trunk
+    gradients, scalar tail, clip norm and logs of the RCCL path, against the float64 oracle."""
+    name = "s3_mt50_w2048"
+    cfg, st, batch, en, ec, st1, want = _problem(name)
+    e = _engine(CASES[name], 1)
+    _load(e, st)
+    assert e.lib.mtsac_debug_set_collective_model(e._h, 8, 150.0, 1) == 0
+    e.update(batch, en, ec)
+    _check_logs(e.logs(), want, f"{name}/modelled")
+    _check_params(e, st1, f"{name}/modelled")
+    e.close()
+
+
+def _device_steps(T, tc, W, prec, steps, pipe, model=0, calls=None):
+    """Logs, parameters, moments, index-stream and noise state after device-sampled eager steps."""
+    from mtrl_amd import _lib as L
+    from mtrl_amd.engine import MTSACEngine, make_config
+    from mtrl_amd.init import init_mtsac
+
+    a0, c0 = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=4, task_begin=0, task_count=tc)
+    e = MTSACEngine(make_config(num_tasks=T, task_begin=0, task_count=tc, obs_dim=39 + T, actor_width=W,
+                                critic_width=W, batch_per_task=128, capacity=512, precision=prec))
+    e.set_params(L.ACTOR, a0)
+    e.set_params(L.CRITIC, c0)
+    e.set_params(L.CRITIC_TARGET, c0)
+    e.buffer_fill_synthetic(77)
+    e.seed_rng(5)
+    e.enable_graph(False)
+    if model:
+        assert e.lib.mtsac_debug_set_collective_model(e._h, 8, 300.0, 1) == 0
+    e.lib.mtsac_debug_set_pipeline(e._h, pipe)
+    for k in calls or (steps,):
+        e.update_many(k)
+    out = (e.logs(), [e.get_params(w) for w in (L.ACTOR, L.CRITIC, L.CRITIC_TARGET, L.LOG_ALPHA, L.ACTOR_ADAM_MU,
+                                               L.ACTOR_ADAM_NU, L.CRITIC_ADAM_MU, L.CRITIC_ADAM_NU)],
+           e.get_rng_state(), e.noise_state())
+    e.close()
+    return out
+
+
+def _assert_same(a, b):
+    assert a[0] == b[0], {k: (a[0][k], b[0][k]) for k in a[0] if a[0][k] != b[0][k]}
+    for x, y in zip(a[1], b[1]):
+        np.testing.assert_array_equal(x, y)
+    assert a[2] == b[2] and a[3] == b[3]
+
+
+@pytest.mark.parametrize("T,tc,W,prec,model", [(50, 50, 2048, 1, 0), (50, 7, 2048, 1, 1), (50, 7, 2048, 1, 0),
+                                               (10, 10, 400, 1, 0), (50, 6, 400, 1, 1), (10, 10, 2048, 2, 0)],
+                         ids=["s3", "mt50_shard7_modelled", "mt50_shard7", "mt10_w400", "s4_shard6_modelled",
+                              "mt10_w2048_bf16"])
+def test_pipelined_steps_equal_whole_steps(T, tc, W, prec, model):
+    """Cross-step pipelining on one compute stream (engine.cpp step(), p2): step k+1's gather and
+    critic(s, a) forward run on the prefetch stream beside step k's actor backward, all-reduce and
+    Adam; 4 device-sampled steps issued that way give bitwise the logs, parameters, optimizer moments
+    and index-stream / noise state of 4 whole steps.  The modelled cases take the sharded path with
+    the device collective (NaN-poisoned buckets) on its own stream, as an 8-GPU rank does."""
+    _assert_same(_device_steps(T, tc, W, prec, 4, 0, model), _device_steps(T, tc, W, prec, 4, 1, model))
+
+
+_PIPE_LANES_CHILD = """
+import sys
+sys.path.insert(0, {root!r})
+sys.path.insert(0, {tests!r})
+import test_gpu_fullbatch as t
+a = t._device_steps(10, 10, 400, 1, 4, 0)
+b = t._device_steps(10, 10, 400, 1, 4, 1)
+t._assert_same(a, b)
+print("lanes pipelined == whole: ok")
+"""
+
+
+def test_pipelined_steps_equal_whole_steps_lanes():
+    """The same bar for the 5-lane form (MTSAC_LANES=1, a child process started with 16 hardware
+    queues): MT10/W400, 4 steps, whole vs pipelined, bitwise."""
+    import os
+
+    from mtrl_amd.hwq import child_env
+
+    tests = os.path.dirname(os.path.abspath(__file__))
+    code = _PIPE_LANES_CHILD.format(root=os.path.dirname(tests), tests=tests)
+    r = _child(code, child_env(16))
+    assert r.returncode == 0 and "ok" in r.stdout
 
 
 def test_full_batch_graph_replay_equals_eager():

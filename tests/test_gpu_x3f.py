@@ -203,3 +203,38 @@ def test_split_k_in_launch_finish_bitwise(E, M, N, K, epi, m16, planes):
         want = np.where(mask > 0, acc, 0.0)
         tol = 4e-6 * scale + 1e-30
     assert np.all(np.abs(out[1][0] - want) <= tol)
+
+
+@pytest.mark.parametrize("E,M,N,K,epi,m16,scale_a", [(1, 6400, 2048, 2048, 1, False, 1.0),
+                                                     (2, 6300, 2040, 192, 1, False, 37.0),
+                                                     (2, 6400, 2048, 256, 2, True, 1e-6),
+                                                     (2, 6400, 2048, 512, 2, False, 3e3)],
+                         ids=["s3_fwd", "ragged_e2_large", "dgrad_m16_tiny_grads", "dgrad_f32mask_large"])
+def test_split2h_products(E, M, N, K, epi, m16, scale_a):
+    """Precision split2h on gemm_x3f: operands as two fp16 planes of x 2^e (e per tensor from its
+    max), 3 products (h*l, l*h, h*h) unscaled by 2^-(eA + eB); the output planes at the exponent of
+    the bound K max|A| max|B| + max|bias|.  The fp32-GEMM bound |err| <= 4e-6 sum|a b| holds at
+    operand magnitudes from gradients (1e-6) to large activations; the planes carry the output to
+    22 bits (|planes - C| <= 2^-21 |C| + 2^-40 bound), and the ReLU mask read from the planes is
+    exactly 'x > 0' down to the tiniest positive activation."""
+    rng = np.random.default_rng(M + K + epi)
+    A = (rng.standard_normal((E, M, K)) * scale_a).astype(np.float32)
+    B = (rng.standard_normal((E, N, K)) / np.sqrt(K)).astype(np.float32)
+    acc, scale = _ref(A, B)
+    if epi == 1:
+        bias = (rng.standard_normal((E, N)) * 0.1 * scale_a).astype(np.float32)
+        C, Cs = _run(1 | 8192, A, B, bias=bias)
+        want = np.maximum(acc + bias[:, None, :], 0)
+        tol = 4e-6 * (scale + np.abs(bias[:, None, :])) + 1e-30
+        bound = K * np.abs(A).max() * np.abs(B).max() + np.abs(bias).max()
+    else:
+        mask = np.maximum(rng.standard_normal((E, M, N)), 0).astype(np.float32)
+        mask[:, :, :7] = 1e-30  # tiny positive activations: the planes' sticky subnormal keeps them active
+        C, Cs = _run(2 | 8192 | (256 if m16 else 0), A, B, mask=mask, m16=m16)
+        want = np.where(mask > 0, acc, 0.0)
+        tol = 4e-6 * scale + 1e-30
+        bound = K * np.abs(A).max() * np.abs(B).max()
+    err = np.abs(C - want)
+    print("max err / sum|ab|", float((err / (scale + 1e-30)).max()))
+    assert np.all(err <= tol), float((err / (scale + 1e-30)).max())
+    assert np.all(np.abs(Cs.astype(np.float64) - C) <= 2.0 ** -21 * np.abs(C) + 2.0 ** -40 * bound)
