@@ -40,7 +40,7 @@ WORKLOADS = {
 }
 FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
-PRECISIONS = {"fp32": 0, "split3": 1, "bf16": 2}
+PRECISIONS = {"fp32": 0, "split3": 1, "bf16": 2, "split2h": 3}
 HBM_PEAK_GBS = 8000.0
 # enum mtsac_gemm_family (include/mtsac.h) -> the rocprof kernel(s) of that family, per precision
 GEMM_FAMILIES = {
@@ -49,6 +49,13 @@ GEMM_FAMILIES = {
         1: "gemm_x3f_kernel<208, 2, *, *, true, 0, 3> (hidden-layer data grad, planes, ReLU mask from the bf16 high plane)",
         2: "gemm_x3p_kernel<Geo<256, 256, 2, 4, 3, 16, 0>, true, true, 0, false, 3> (hidden-layer weight grad, k-major planes, split-K)",
         3: "gemm_x3f_kernel<208, 1, false, true, false, 8, 3> (input-layer forward, planes, K = in_dim padded to 64)",
+        4: "gemm_x3_kernel<true, false, 0> (input-layer weight grad, on-the-fly split, split-K)",
+    },
+    "split2h": {
+        0: "gemm_x3f_kernel<208, 1, *, *, false, 0, 2> (hidden-layer forward, fp16 planes, bias+ReLU)",
+        1: "gemm_x3f_kernel<208, 2, *, *, true, 0, 2> (hidden-layer data grad, fp16 planes, ReLU mask from the planes)",
+        2: "gemm_x3p_kernel<Geo<256, 256, 2, 4, 3, 16, 0>, true, true, 0, false, 2> (hidden-layer weight grad, k-major fp16 planes, split-K)",
+        3: "gemm_x3f_kernel<208, 1, false, true, false, 8, 2> (input-layer forward, fp16 planes, K = in_dim padded to 64)",
         4: "gemm_x3_kernel<true, false, 0> (input-layer weight grad, on-the-fly split, split-K)",
     },
     "fp32": {
@@ -302,6 +309,7 @@ def main():
                     help="hipGraph replay or eager multi-stream DAG; auto = faster of the two")
     ap.add_argument("--precision", default="split3", choices=sorted(PRECISIONS),
                     help="fp32: f32-input MFMA; split3: fp32-accurate 3-way bf16 split on bf16 MFMA; "
+                         "split2h: fp32-accurate 2-way fp16 split (per-tensor power-of-two scale) on fp16 MFMA; "
                          "bf16: perf-only, trunk GEMM operands rounded to bf16 (one MFMA per product)")
     ap.add_argument("--settle-s", type=float, default=2.0,
                     help="untimed steady-state seconds after the warm-up (DVFS settles under load)")
@@ -349,6 +357,7 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": {"fp32": "fp32", "split3": "fp32 (3xbf16 split MFMA, fp32-accurate)",
+                  "split2h": "fp32 (2xfp16 split, per-tensor power-of-two scaled, 3 fp16 MFMA products, fp32-accurate)",
                   "bf16": "bf16 trunk GEMMs (fp32 accumulate, fp32 master weights / Adam / heads)"}[args.precision],
         "data": "synthetic (SURVEY.md §8d recipe, device-filled full buffer, cap=100000/task; random-init weights)",
         "config": {"workload": desc, "num_tasks": T, "width": W, "batch_per_task": 128, "global_batch": 128 * T,
@@ -491,6 +500,8 @@ def main():
     traffic, traffic_src = pmc_traffic(args.precision, dom, args.workload)
     if args.precision == "split3":  # 6 bf16 MFMA products per fp32 multiply-add
         peak, basis = BF16_MFMA_PEAK_TF / 6.0, "bf16 dense MFMA peak / 6 products (fp32-accurate split)"
+    elif args.precision == "split2h":  # 3 fp16 MFMA products (fp16 runs at the bf16 rate)
+        peak, basis = BF16_MFMA_PEAK_TF / 3.0, "fp16 dense MFMA peak / 3 products (fp32-accurate 2xfp16 split)"
     elif args.precision == "bf16":
         peak, basis = BF16_MFMA_PEAK_TF, "bf16 dense MFMA peak"
     else:

@@ -82,10 +82,15 @@ enum mtsac_precision {
   MTSAC_FP32_SPLIT3 = 1, /* fp32-accurate trunk GEMMs on bf16 MFMA: each fp32 operand split
                            exactly into 3 bf16 terms, 6 cross products accumulated in fp32
                            (dropped terms <= 2^-23 relative); everything else fp32           */
-  MTSAC_BF16 = 2         /* perf-only: the trunk GEMMs' operands rounded to bf16 (the high
+  MTSAC_BF16 = 2,        /* perf-only: the trunk GEMMs' operands rounded to bf16 (the high
                            term of the same split), one bf16 MFMA per product, fp32
                            accumulation; master weights, Adam, heads, losses stay fp32.
                            NOT the reference's arithmetic (fp32): losses drift ~1e-3 rel  */
+  MTSAC_FP32_SPLIT2H = 3 /* fp32-accurate trunk GEMMs on fp16 MFMA: each operand tensor scaled
+                           by a power of two 2^e (per tensor, from an a-priori bound of its
+                           values) and split into 2 fp16 terms (22 significant bits),
+                           3 cross products (h*l, l*h, h*h) accumulated in fp32, unscaled
+                           exactly; same GEMM error bound as split3 (<= 4e-6 sum|a b|)      */
 };
 
 /* Hyper-parameters: MTSACConfig (mtsac.py:116-127) + AlgorithmConfig

@@ -16,8 +16,8 @@ LIB_PATH = pathlib.Path(os.environ.get("MTSAC_LIB", _HERE / "libmtsac.so"))
 
 NUM_LOGS = 10
 # enum mtsac_precision (include/mtsac.h)
-FP32, FP32_SPLIT3, BF16 = 0, 1, 2
-PRECISIONS = {"fp32": FP32, "split3": FP32_SPLIT3, "bf16": BF16}
+FP32, FP32_SPLIT3, BF16, FP32_SPLIT2H = 0, 1, 2, 3
+PRECISIONS = {"fp32": FP32, "split3": FP32_SPLIT3, "bf16": BF16, "split2h": FP32_SPLIT2H}
 LOG_KEYS = (
     "losses/qf_values",
     "losses/qf_loss",

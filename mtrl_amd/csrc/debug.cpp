@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -200,11 +201,9 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
   if (M < 1 || N < 1 || K < 1 || batch < 1 || !A || !B || !C) return -22;
   DevBuf d;
   const size_t nA = (size_t)M * K * batch, nB = (size_t)N * K * batch, nC = (size_t)M * N * batch;
-  // split2h: exponents and maxima of the operands (host-side, exact), the output record
-  int* dexp = d.get<int>(8);          // [0] A, [1] B, [2] mask, [3] C (written by the kernel)
-  float* dmax = d.get<float>(4);      // [0] |A|, [1] |B|, [2] |bias|
-  float* domax = d.get<float>(65536);  // per-workgroup max |C|
-  if (!dexp || !dmax || !domax) return -12;
+  // split2h: records of A, B (its max covering the bias, as a trunk record does), the mask and C
+  PlaneRec* rec = d.get<PlaneRec>(4);
+  if (!rec) return -12;
   if (h2) {
     auto amax = [](const float* x, size_t n) {
       float m = 0.f;
@@ -218,12 +217,15 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
       (void)std::frexp(b, &ex);
       return 15 - ex;
     };
-    const float ma = amax(A, nA), mb = amax(B, nB), mbias = bias ? amax(bias, (size_t)N * batch) : 0.f;
+    const float ma = amax(A, nA), mbias = (epi == 1 && bias) ? amax(bias, (size_t)N * batch) : 0.f;
+    const float mb = std::max(amax(B, nB), mbias);
     const float mm = mask ? amax(mask, nC) : 1.f;
-    const int he[4] = {pexp(ma), pexp(mb), pexp(mm), 0};
-    const float hm[3] = {ma, mb, mbias};
-    (void)hipMemcpy(dexp, he, sizeof(he), hipMemcpyHostToDevice);
-    (void)hipMemcpy(dmax, hm, sizeof(hm), hipMemcpyHostToDevice);
+    std::vector<PlaneRec> h(4);
+    std::memset(h.data(), 0, sizeof(PlaneRec) * 4);
+    h[0].e = pexp(ma); h[0].amax[0] = ma;
+    h[1].e = pexp(mb); h[1].amax[0] = mb;
+    h[2].e = pexp(mm); h[2].amax[0] = mm;
+    (void)hipMemcpy(rec, h.data(), sizeof(PlaneRec) * 4, hipMemcpyHostToDevice);
   }
   float* dA = d.get<float>(nA);
   float* dB = d.get<float>(nB);
@@ -245,16 +247,16 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
     SplitParams s{};
     s.x = dA + (size_t)z * M * K; s.ldx = K; s.rows = M; s.cols = K;
     s.out = Ap + (size_t)z * 3 * M * Kp; s.ldo = Kp; s.po = (long long)M * Kp; s.out_rows = M; s.out_cols = (int)Kp;
-    s.e2h = h2 ? dexp + 0 : nullptr;
+    s.e2h = h2 ? &rec[0].e : nullptr;
     split_planes(s, false, 1, nullptr);
     s.x = dB + (size_t)z * N * K; s.rows = N;
     s.out = Bp + (size_t)z * 3 * N * Kp; s.po = (long long)N * Kp; s.out_rows = N;
-    s.e2h = h2 ? dexp + 1 : nullptr;
+    s.e2h = h2 ? &rec[1].e : nullptr;
     split_planes(s, false, 1, nullptr);
     if (m16) {  // planes of the mask, row stride N
       s.x = dmask + (size_t)z * M * N; s.ldx = N; s.rows = M; s.cols = N;
       s.out = dM16 + (size_t)z * 3 * M * N; s.ldo = N; s.po = (long long)M * N; s.out_rows = M; s.out_cols = N;
-      s.e2h = h2 ? dexp + 2 : nullptr;
+      s.e2h = h2 ? &rec[2].e : nullptr;
       split_planes(s, false, 1, nullptr);
     }
   }
@@ -274,12 +276,11 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
   g.M = M; g.N = N; g.K = (int)Kp;
   g.np = h2 ? 2 : np;
   if (h2) {
-    g.ea = dexp + 0; g.eb = dexp + 1; g.em = dexp + 2; g.ec = dexp + 3;
+    g.ra = rec + 0; g.na = 1;
+    g.rb = rec + 1; g.nb = 1;
+    g.rc = rec + 3;
+    g.bias_in_b = epi == 1 && bias ? 1 : 0;
     g.pMask = (long long)M * N;
-    g.omax = domax;
-    g.amaxA = dmax + 0; g.namaxA = 1;
-    g.amaxB = dmax + 1; g.namaxB = 1;
-    g.amaxBias = (epi == 1 && bias) ? dmax + 2 : nullptr;
     g.kmul = (float)K;
   }
   if (autosplit) {
@@ -304,7 +305,7 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
     std::vector<_Float16> h(3 * nC);
     int ec = 0;
     if (hipMemcpy(h.data(), dCp, sizeof(_Float16) * h.size(), hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(&ec, dexp + 3, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(&ec, &rec[3].e, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
       return -5;
     const size_t n = (size_t)M * N;
     for (int z = 0; z < batch; ++z)
@@ -338,9 +339,8 @@ int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int 
   if (M < 1 || N < 1 || K < 1 || batch < 1 || iters < 1 || !ms_per_launch) return -22;
   DevBuf d;
   const long long Kp = (K + 63) / 64 * 64;
-  int* dexp = d.get<int>(8);
-  float* dmax = d.get<float>(65536);
-  if (!dexp || !dmax) return -12;
+  PlaneRec* rec = d.get<PlaneRec>(3);  // zero exponents: the random operands lie in [-1, 1]
+  if (!rec) return -12;
   float* fa = d.get<float>((size_t)M * Kp);
   float* fb = d.get<float>((size_t)N * Kp);
   float* C = d.get<float>((size_t)M * N * batch);
@@ -359,14 +359,12 @@ int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int 
   __bf16* Bp = d.get<__bf16>((size_t)3 * pb * batch);
   if (!Ap || !Bp) return -12;
   for (int z = 0; z < batch; ++z) {
-    split_into(fa, M, (int)Kp, false, Ap + 3 * pa * z, h2 ? dexp : nullptr);
-    split_into(fb, N, (int)Kp, bk, Bp + 3 * pb * z, h2 ? dexp : nullptr);
+    split_into(fa, M, (int)Kp, false, Ap + 3 * pa * z, h2 ? &rec[0].e : nullptr);
+    split_into(fb, N, (int)Kp, bk, Bp + 3 * pb * z, h2 ? &rec[1].e : nullptr);
   }
   SplitGemmParams g{};
   if (h2) {
-    g.ea = dexp; g.eb = dexp; g.em = dexp; g.ec = dexp + 4;
-    g.omax = dmax + 16;
-    g.amaxA = dmax; g.namaxA = 1; g.amaxB = dmax; g.namaxB = 1;
+    g.ra = rec; g.rb = rec + 1; g.rc = rec + 2;
     g.kmul = (float)K;
     g.pMask = (long long)M * N;
   }

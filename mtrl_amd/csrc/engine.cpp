@@ -222,7 +222,43 @@ struct mtsac_engine {
   // profiles/r3ff_input_wgrad_ab.txt: MT10/W400 +1.5 %, MT50/W2048 at 6400 rows -0.5 %);
   // MTSAC_INPUT_WGRAD=0 / 1 forces either form (set at create)
   bool in_wgrad_planes = false;
-  int np = 3;  // operand planes the plane GEMMs read: 3 (split3) or 1 (bf16)
+  int np = 3;  // operand planes the plane GEMMs read: 3 (split3), 1 (bf16) or 2 (split2h: fp16)
+  // ---- precision split2h: a device record (kernels.h PlaneRec: exponent + partial maxima) per fp16
+  // plane tensor; n = the partial maxima its last producer wrote (0: consumers bound it by 2^(15 - e))
+  bool h2 = false;
+  struct RecRef {
+    PlaneRec* d = nullptr;
+    int n = 0;
+  };
+  PlaneRec* recs = nullptr;
+  RecRef r_in[2];         // the step's input planes (xa / xc / xc_next / xc_pi), per input set
+  RecRef r_w[2][2];       // weights [0 actor, 1 critic][0 params, 1 Polyak target]
+  RecRef r_ac[3][MAXD];   // activation planes: actor (hap), critic (hcp), target critic (hctp)
+  RecRef r_dz[2][MAXD];   // data-grad planes: actor (dzap), critic (dzcp)
+  RecRef r_dq, r_dout;    // the head backwards' inputs: critic dq, actor dout (partial maxima only)
+  float* bufmax = nullptr;  // max |stored obs / action / next_obs| (the input planes' bound)
+  float* ubmax = nullptr;   // the same over a user batch
+  float* wparts[2] = {};    // the optimizer's per-block max |p_new| [actor, critic] and the target's
+  float* tparts = nullptr;
+  int wgrid[2] = {}, wbh[2] = {};  // the last optimizer launch's grid and head blocks per network
+  RecRef* act_rec(__bf16** actp) {
+    return actp == hap ? r_ac[0] : actp == hcp ? r_ac[1] : actp == hctp ? r_ac[2] : nullptr;
+  }
+  RecRef* dz_rec(__bf16** dzp) { return dzp == dzap ? r_dz[0] : dzp == dzcp ? r_dz[1] : nullptr; }
+  RecRef& w_rec(const Net& net, int which) { return r_w[&net == &critic ? 1 : 0][which]; }
+  // the bound inputs of a split2h plane GEMM: A, B (weights: their planes' range), output C
+  void h2_gemm(SplitGemmParams& g, RecRef* a, RecRef* b, RecRef* c, float kmul, bool bias_in_b) {
+    if (!h2) return;
+    g.ra = a->d;
+    g.na = a->n;
+    g.rb = b->d;
+    g.nb = b->n;
+    g.rc = c ? c->d : nullptr;
+    g.nparts = c ? &c->n : nullptr;
+    if (c) c->n = 0;  // set by the launcher
+    g.kmul = kmul;
+    g.bias_in_b = bias_in_b ? 1 : 0;
+  }
   __bf16* hap[MAXD] = {};
   __bf16* hcp[MAXD] = {};
   __bf16* hctp[MAXD] = {};
@@ -483,19 +519,19 @@ struct mtsac_engine {
       fam_kernel[family] = split ? std::string("gemm_x3f_kernel<") +
                                        std::to_string(gemm_x3f_split_bm(p.M, p.N, p.K, batch)) +
                                        ", 0, true, false, false, 0, " +
-                                       (p.np == 1 ? "1" : "3") + "> + splitk_epilogue_kernel"
+                                       std::to_string(p.np == 0 ? 3 : p.np) + "> + splitk_epilogue_kernel"
                                  : std::string("gemm_x3f_kernel<") + std::to_string(gemm_x3f_bm(p, batch)) + ", " +
                                        std::to_string(epi) + ", " +
                                        (p.C ? "true" : "false") + ", " + (p.Cp ? "true" : "false") + ", " +
                                        (p.mask16 ? "true" : "false") + ", " + (tagged ? "8" : "0") + ", " +
-                                       (p.np == 1 ? "1" : "3") + ">";
+                                       std::to_string(p.np == 0 ? 3 : p.np) + ">";
     } else if (gemm_x3s_ok(p, epi, batch)) {
       gemm_x3s(p, epi, batch, cur);
       const bool tagged = epi == EPI_BIAS_RELU && p.tag == 1 && p.Cp && !p.C;
       fam_kernel[family] = std::string("gemm_x3s_kernel<") + std::to_string(gemm_x3s_ti(p.M, p.N, batch)) + ", " +
                            std::to_string(epi) + ", " + (p.C ? "true" : "false") + ", " + (p.Cp ? "true" : "false") +
                            ", " + (p.mask16 ? "true" : "false") + ", " + (tagged ? "8" : "0") + ", " +
-                           (p.np == 1 ? "1" : "3") + ">";
+                           std::to_string(p.np == 0 ? 3 : p.np) + ">";
     } else if ((epi == EPI_RELU_MASK && !p.mask) || (!p.C && !p.Cp)) {
       // gemm_x3p's direct epilogue reads an fp32 mask and writes through C or Cp: never launch it
       // on operands it cannot address (a null mask pointer faults the device)
@@ -516,6 +552,17 @@ struct mtsac_engine {
       po.ld = net.ald;
       po.ps = net.aps();
       po.sm = 3 * net.aps();
+      if (h2) {  // bound: hd * max|dout| * (max|head weight| + one Adam step)
+        RecRef& top = dz_rec(dzp)[net.depth - 1];
+        RecRef& d = &net == &critic ? r_dq : r_dout;
+        po.rc = top.d;
+        top.n = 0;  // no partial maxima: the planes' range bounds dz_top for the next producer
+        po.rd = d.d;
+        po.nd = d.n;
+        po.rw = w_rec(net, 0).d;
+        po.w_add = 16.0f * (&net == &critic ? cfg.critic_lr : cfg.actor_lr);
+        po.kmul = (float)net.hd;
+      }
     }
     return po;
   }
@@ -592,6 +639,11 @@ struct mtsac_engine {
         g.splits = -1;  // split-K when the row tiles do not fill the chip (task shards)
         g.ws = ws_lane[cur_lane];
         g.cnt = fin_cnt();
+        if (h2) {
+          RecRef* ar = act_rec(actp);
+          h2_gemm(g, i == 0 ? &r_in[inset_cur] : &ar[i - 1], &w_rec(net, which), last ? nullptr : &ar[i],
+                  (float)(i == 0 ? net.in_dim : net.width), true);
+        }
         gemmp(g, EPI_BIAS_RELU, net.E, i == 0 ? MTSAC_FAM_INPUT_FORWARD : MTSAC_FAM_FORWARD);
         continue;
       }
@@ -625,6 +677,11 @@ struct mtsac_engine {
         g.splits = -1;
         g.ws = ws_lane[cur_lane];
         g.cnt = fin_cnt();
+        if (h2) {
+          RecRef* ar = act_rec(actp);
+          h2_gemm(g, i == 0 ? &r_in[inset_cur] : &ar[i - 1], &w_rec(net, which), last ? nullptr : &ar[i],
+                  (float)(i == 0 ? net.in_dim : net.width), true);
+        }
         gemmp(g, EPI_BIAS_RELU, net.E, i == 0 ? MTSAC_FAM_INPUT_FORWARD : MTSAC_FAM_FORWARD);
         continue;
       }
@@ -676,6 +733,7 @@ struct mtsac_engine {
       sp.out_rows = (int)(i == 0 ? net.xld : net.wrows);
       sp.out_cols = (int)net.wld;
       sp.out = net.wp[which][i];
+      sp.e2h = h2 ? &w_rec(net, which).d->e : nullptr;  // split2h: the exponent the optimizer / set_params chose
       if (!(fused && planes_fusable(net))) split_planes(sp, false, net.E, s);
       if (net.x3f) {  // W_i^T planes for the gemm_x3f forward (zeros past the in-dim)
         SplitParams st{};
@@ -690,6 +748,7 @@ struct mtsac_engine {
         st.so = 3 * net.wtps(i);
         st.out_rows = net.width;
         st.out_cols = (int)net.wtk(i);
+        st.e2h = sp.e2h;
         split_planes(st, true, net.E, s);
       }
     }
@@ -730,6 +789,7 @@ struct mtsac_engine {
         g.cs_db = net.g + net.off_b[i];
         g.cs_sdb = net.ms_b;
       }
+      if (h2) h2_gemm(g, i == 0 ? &r_in[inset_cur] : &act_rec(actp)[i - 1], &dz_rec(dzp)[i], nullptr, (float)g.K, false);
       gemmp(g, EPI_STORE, net.E, i == 0 ? MTSAC_FAM_INPUT_WEIGHT_GRAD : MTSAC_FAM_WEIGHT_GRAD);
       if (net.dbp_chunks[i] <= 0)
         colsum(dz[i], M, net.width, net.width, (long long)M * net.width, net.E, cs_part, net.g + net.off_b[i],
@@ -796,7 +856,9 @@ struct mtsac_engine {
       g.K = (int)net.ald;
       g.splits = -1;
       g.ws = ws_lane[cur_lane];
-        g.cnt = fin_cnt();
+      g.cnt = fin_cnt();
+      g.pMask = net.aps();
+      if (h2) h2_gemm(g, &dz_rec(dzp)[i], &w_rec(net, 0), g.Cp ? &dz_rec(dzp)[i - 1] : nullptr, (float)net.width, false);
       if (g.Cp) {  // dz[i-1]'s fp32 copy only feeds the bias grad's column sums
         if (!want_db) {
           g.C = nullptr;
@@ -900,6 +962,14 @@ struct mtsac_engine {
     a.tau = cfg.tau;
     a.sc = net.sc;
     a.np = np;
+    if (h2) {
+      const int w = &net == &critic ? 1 : 0;
+      a.h2.wrec = w_rec(net, 0).d;
+      a.h2.trec = polyak ? w_rec(net, 1).d : nullptr;
+      a.h2.w_add = 16.0f * lr;  // one Adam step: |m_hat| / (sqrt(v_hat) + eps) < 7.3 for b1^2 < b2
+      a.h2.wparts = wparts[w];
+      a.h2.tparts = polyak ? tparts : nullptr;
+    }
     a.n = net.trunk_off;  // heads
     AdamParams at = a;    // trunk
     at.p += net.trunk_off;
@@ -950,6 +1020,8 @@ struct mtsac_engine {
     adam_fused(a, at, tp, f, cur);
     net.n_pph = f.bh;
     net.n_ppt = f.bt + f.btile;
+    wgrid[&net == &critic ? 1 : 0] = f.bh + f.bt + f.btile;
+    wbh[&net == &critic ? 1 : 0] = f.bh;
     if (sharded()) sum_partials(net.pph, f.bh, pn + 2 + slot, cur);  // the heads' |p|^2, all-reduced later
   }
 
@@ -1141,6 +1213,7 @@ struct mtsac_engine {
         replay_indices(rng, jump, buf_size, n, idx, cur);
         replay_gather(gp, cur);
       } else {
+        if (h2) user_batch_max(gp, Bl);
         batch_scatter(gp, u_obs, u_act, u_nobs, u_done, u_rew, Bl, cur);
         task_rows(task, Bl, T_l, counts, rows, Bl, cur);  // a user batch: lists from its task ids
       }
@@ -1163,6 +1236,7 @@ struct mtsac_engine {
       q.stream_id = 2;
       q.a_out = xcp;
       q.a_planes = in_planes(xcp);
+      q.ap_rec = h2 ? r_in[inset_cur].d : nullptr;
       q.logpi = logpi;
       q.cache = cache;
       PolicyParams qn = pp;
@@ -1171,6 +1245,7 @@ struct mtsac_engine {
       qn.stream_id = 1;
       qn.a_out = xcn;
       qn.a_planes = in_planes(xcn);
+      qn.ap_rec = q.ap_rec;
       qn.logpi = logpi_n;
       policy_head_pair(q, qn, cur);
     });
@@ -1205,6 +1280,10 @@ struct mtsac_engine {
       c.row_a = row_a;
       c.row_b = row_b;
       c.inv_norm = 1.0f / ((float)critic.E * (float)B_glob);
+      if (h2) {
+        c.dq_rec = r_dq.d;
+        c.dq_parts = &r_dq.n;
+      }
       critic_head(c, cur);
       c_both = head_bwd_both(critic, chp, dq, Bl, dzcp, true);
       if (!c_both) head_bwd(critic, chp, dq, Bl, dzc, dzcp, true);
@@ -1237,6 +1316,10 @@ struct mtsac_engine {
       c.row_a = row_c;
       c.alpha_w = alpha_w;
       c.inv_norm = 1.0f / (float)B_glob;
+      if (h2) {
+        c.dq_rec = r_dq.d;
+        c.dq_parts = &r_dq.n;
+      }
       critic_head(c, cur);
       head_bwd(critic, c.head, dq, Bl, dzc, dzcp, false);
       for (int i = critic.depth - 1; i > 0; --i) dgrad_layer(critic, critic.p, hc, hcp, dzc, dzcp, i, Bl, false);
@@ -1254,6 +1337,10 @@ struct mtsac_engine {
       ag.ls_min = cfg.log_std_min;
       ag.ls_max = cfg.log_std_max;
       ag.dout = dout_a;
+      if (h2) {
+        ag.dout_rec = r_dout.d;
+        ag.dout_parts = &r_dout.n;
+      }
       action_grad(ag, cur);
       if (sharded()) {
         const float* ins[1] = {row_c};
@@ -1322,6 +1409,12 @@ struct mtsac_engine {
       lp.inv_b = 1.0f / (float)B_glob;
       lp.logs = logs;
       f.counter = counter;
+      if (h2) {  // the optimizers' weight maxima into the records (the next updates' plane exponents)
+        f.wmax[0] = WeightMaxJob{wparts[0], wgrid[0], wbh[0], r_w[0][0].d};
+        f.wmax[1] = WeightMaxJob{wparts[1], wgrid[1], wbh[1], r_w[1][0].d};
+        f.wmax[2] = WeightMaxJob{tparts, wgrid[1], -1, r_w[1][1].d};
+        f.nwmax = 3;
+      }
       step_finish(f, cur);
     });
     if (pipelined) (void)hipEventRecord(ev_tail[step_par], segs[s_tail].lane);
@@ -1430,6 +1523,7 @@ struct mtsac_engine {
       replay_indices(rng, jump, buf_size, n, idx, cur);
       replay_gather(gp, cur);
     } else {
+      if (h2) user_batch_max(gp, Bl);
       batch_scatter(gp, u_obs, u_act, u_nobs, u_done, u_rew, Bl, cur);
     }
     check_interleaved(task, Bl, T_l, err, cur);
@@ -1576,6 +1670,15 @@ struct mtsac_engine {
     return al;
   }
 
+  // split2h, a user batch: its own max |value| bounds the input planes (the stored rows' does not)
+  void user_batch_max(GatherParams& gp, int Bl) {
+    (void)hipMemsetAsync(ubmax, 0, sizeof(float), cur);
+    absmax_into(u_obs, (long long)Bl * D, ubmax, cur);
+    absmax_into(u_nobs, (long long)Bl * D, ubmax, cur);
+    absmax_into(u_act, (long long)Bl * A, ubmax, cur);
+    gp.in_max = ubmax;
+  }
+
   GatherParams gather_params() {
     GatherParams gp{};
     gp.store = store;
@@ -1603,6 +1706,10 @@ struct mtsac_engine {
     // set by the host, so (r - 0) / (den - 0 + 0) = r / den in float64
     gp.norm_eps = cfg.normalize_rewards == 2 ? 0.0 : 1e-8;
     gp.err = err;
+    if (h2) {
+      gp.in_rec = r_in[inset_cur].d;
+      gp.in_max = bufmax;
+    }
     if (planes) {
       gp.pa = inp[0].p;
       gp.pa_ps = actor.arows * actor.xld;
@@ -1707,7 +1814,8 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   if (c.normalize_rewards < 0 || c.normalize_rewards > 2) return fail(-22, "normalize_rewards must be 0, 1 or 2");
   if (c.capacity < c.batch_per_task || c.capacity >= (1ll << 31))
     return fail(-22, "capacity must be in [batch_per_task, 2^31)");
-  if (c.precision != MTSAC_FP32 && c.precision != MTSAC_FP32_SPLIT3 && c.precision != MTSAC_BF16)
+  if (c.precision != MTSAC_FP32 && c.precision != MTSAC_FP32_SPLIT3 && c.precision != MTSAC_BF16 &&
+      c.precision != MTSAC_FP32_SPLIT2H)
     return fail(-22, "unsupported precision");
   hipError_t he = hipSetDevice(hip_device);
   if (he != hipSuccess) return fail(-19, std::string("hipSetDevice: ") + hipGetErrorString(he));
@@ -1758,8 +1866,26 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
       return bad(rc);
   }
   if ((rc = e->alloc(&e->critic.tgt, e->critic.n_flat))) return bad(rc);
-  e->planes = c.precision == MTSAC_FP32_SPLIT3 || c.precision == MTSAC_BF16;
-  e->np = c.precision == MTSAC_BF16 ? 1 : 3;
+  e->planes = c.precision == MTSAC_FP32_SPLIT3 || c.precision == MTSAC_BF16 || c.precision == MTSAC_FP32_SPLIT2H;
+  e->np = c.precision == MTSAC_BF16 ? 1 : c.precision == MTSAC_FP32_SPLIT2H ? 2 : 3;
+  e->h2 = c.precision == MTSAC_FP32_SPLIT2H;
+  if (e->h2) {  // the plane records, the stored rows' bound, the optimizer's maxima
+    const int nrec = 2 + 4 + 3 * MAXD + 2 * MAXD + 2;
+    if ((rc = e->alloc(&e->recs, (size_t)nrec))) return bad(rc);
+    PlaneRec* r = e->recs;
+    for (auto& x : e->r_in) x.d = r++;
+    for (auto& w : e->r_w)
+      for (auto& x : w) x.d = r++;
+    for (auto& a : e->r_ac)
+      for (auto& x : a) x.d = r++;
+    for (auto& a : e->r_dz)
+      for (auto& x : a) x.d = r++;
+    e->r_dq.d = r++;
+    e->r_dout.d = r++;
+    if ((rc = e->alloc(&e->bufmax, 1)) || (rc = e->alloc(&e->ubmax, 1)) || (rc = e->alloc(&e->wparts[0], 4096)) ||
+        (rc = e->alloc(&e->wparts[1], 4096)) || (rc = e->alloc(&e->tparts, 4096)))
+      return bad(rc);
+  }
   for (Net* net : {&e->actor, &e->critic}) {
     net->wld = align_up(net->width, 32);
     net->wrows = align_up(net->width, 32);
@@ -2015,6 +2141,7 @@ static int copy_params(mtsac_engine* h, int which, float* host, int64_t n, bool 
     o += lf.second;
   }
   if (to_device && (buf == net->p || buf == net->tgt)) {
+    if (h->h2) weights_record(buf, net->trunk_off, net->n_flat, h->w_rec(*net, buf == net->p ? 0 : 1).d, h->st);
     h->refresh_wt(*net, buf, buf == net->p ? 0 : 1, h->st);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(h->st));
@@ -2092,6 +2219,14 @@ static int write_slots(mtsac_engine* h, int64_t s0, int64_t ns, const float* obs
   }
   HIP_TRY(hipStreamSynchronize(h->st));
   HIP_TRY(hipMemcpy(h->store + (size_t)s0 * T * R, rec.data(), sizeof(float) * rec.size(), hipMemcpyHostToDevice));
+  if (h->bufmax) {  // split2h: the stored rows' max |obs|, |action|, |next_obs| only grows
+    float m = 0.f, cur = 0.f;
+    for (float v : o) m = std::max(m, std::fabs(v));
+    for (float v : no) m = std::max(m, std::fabs(v));
+    for (float v : a) m = std::max(m, std::fabs(v));
+    HIP_TRY(hipMemcpy(&cur, h->bufmax, sizeof(float), hipMemcpyDeviceToHost));
+    if (m > cur) HIP_TRY(hipMemcpy(h->bufmax, &m, sizeof(float), hipMemcpyHostToDevice));
+  }
   return 0;
 }
 
@@ -2155,7 +2290,7 @@ int mtsac_buffer_add_stream(mtsac_engine* h, const float* obs, const float* next
   if (np >= h->cfg.capacity) h->h_full = 1;
   h->h_pos = np % h->cfg.capacity;
   buffer_commit_slot(slot, T, R, D + A, h->cfg.normalize_rewards == 1 ? h->rmin : nullptr, h->rmax, h->buf_size,
-                     h->h_full ? h->cfg.capacity : h->h_pos, h->st);
+                     h->h_full ? h->cfg.capacity : h->h_pos, h->st, D, h->bufmax);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -2204,7 +2339,8 @@ int mtsac_buffer_read(mtsac_engine* h, int64_t s0, int64_t ns, float* obs, float
 
 int mtsac_buffer_fill_synthetic(mtsac_engine* h, uint64_t seed) {
   if (!h) return fail(-22, "null engine");
-  fill_synthetic(h->store, h->cfg.capacity, h->T_l, h->R, h->D, h->A, h->T_g, h->cfg.task_begin, seed, h->st);
+  fill_synthetic(h->store, h->cfg.capacity, h->T_l, h->R, h->D, h->A, h->T_g, h->cfg.task_begin, seed, h->st,
+                 h->bufmax);
   HIP_TRY(hipGetLastError());
   h->h_pos = 0;
   h->h_full = 1;

@@ -51,6 +51,10 @@ struct TileOut {
   long long ldcp, pC;
   int M, N;
   bool vec;             // every row start 16-B aligned (N, ldc, ldm, ldcp multiples of 4)
+  // split2h (h2): the accumulator times unscale = 2^-(eA + eB); output planes are two fp16 planes
+  // of x * oscale; the fp32 ReLU mask is read as is (x3p never takes a plane mask)
+  bool h2;
+  float unscale, oscale;
 };
 
 // ---- precision split2h: x * 2^e = h + l as two fp16 values (h = fp16(x 2^e), l = fp16(x 2^e - h);
@@ -107,15 +111,21 @@ __device__ inline float block_max_of(const float* __restrict__ v, int n, float* 
   return r;
 }
 
-// the output planes' exponent of a split2h GEMM launch (SplitGemmParams bound inputs)
-__device__ inline int gemm_out_exp(const SplitGemmParams& p, float* scratch) {
-  const float ma = p.amaxA ? block_max_of(p.amaxA, p.namaxA, scratch) : 0.f;
-  const float mb = p.amaxB ? block_max_of(p.amaxB, p.namaxB, scratch) : 0.f;
-  const float mbias = p.amaxBias ? *p.amaxBias : 0.f;
-  return plane_exp(p.kmul * ma * mb + mbias);
+__device__ inline float exp2i(int e) { return __builtin_bit_cast(float, (unsigned)(127 + e) << 23); }  // |e| <= 126
+
+// max |x| of a record's tensor: its partial maxima, or (none recorded) the planes' range 2^(15 - e)
+__device__ inline float rec_max(const PlaneRec* r, int n, float* scratch) {
+  if (r == nullptr) return 0.f;
+  if (n <= 0) return exp2i(15 - r->e);
+  return block_max_of(r->amax, n, scratch);
 }
 
-__device__ inline float exp2i(int e) { return __builtin_bit_cast(float, (unsigned)(127 + e) << 23); }  // |e| <= 126
+// the output planes' exponent of a split2h GEMM launch (SplitGemmParams bound inputs)
+__device__ inline int gemm_out_exp(const SplitGemmParams& p, float* scratch) {
+  const float ma = rec_max(p.ra, p.na, scratch);
+  const float mb = rec_max(p.rb, p.nb, scratch);
+  return plane_exp(p.kmul * ma * mb + (p.bias_in_b ? mb : 0.f));
+}
 
 __device__ inline void split3_dev(float x, __bf16& h, __bf16& m, __bf16& l) {
   h = (__bf16)x;
@@ -128,7 +138,8 @@ __device__ inline void split3_dev(float x, __bf16& h, __bf16& m, __bf16& l) {
 // at (row0, col0): restaged through a wave-private 32 x 36-float LDS scratch so every lane
 // stores 16 B of fp32 (and 8 B of each bf16 plane) -- whole 128-B row segments per 8 lanes.
 template <int EPI>
-__device__ inline void store_tile32(const f32x16_t& acc, float* scr, int lane, int row0, int col0, const TileOut& o) {
+__device__ inline void store_tile32(const f32x16_t& acc, float* scr, int lane, int row0, int col0, const TileOut& o,
+                                    float& omx) {
   const int lr = lane & 31, lh = lane >> 5;
 #pragma unroll
   for (int r = 0; r < 16; ++r) scr[((r & 3) + 8 * (r >> 2) + 4 * lh) * 36 + lr] = acc[r];
@@ -144,6 +155,10 @@ __device__ inline void store_tile32(const f32x16_t& acc, float* scr, int lane, i
     if (row >= o.M) continue;
     float4 v = *reinterpret_cast<const float4*>(scr + rr * 36 + c4);
     float e[4] = {v.x, v.y, v.z, v.w};
+    if (o.h2) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) e[j] *= o.unscale;
+    }
     if (o.vec && col + 3 < o.N) {
       if (EPI == EPI_BIAS_RELU) {
         const float4 b = *reinterpret_cast<const float4*>(o.bias + col);
@@ -156,7 +171,19 @@ __device__ inline void store_tile32(const f32x16_t& acc, float* scr, int lane, i
         e[2] = mk.z > 0.f ? e[2] : 0.f; e[3] = mk.w > 0.f ? e[3] : 0.f;
       }
       if (o.C) *reinterpret_cast<float4*>(o.C + (long long)row * o.ldc + col) = make_float4(e[0], e[1], e[2], e[3]);
-      if (o.Cp) {
+      if (o.Cp && o.h2) {
+        f16x4 h, l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          _Float16 a, b;
+          split2h_dev(e[j], o.oscale, a, b);
+          h[j] = a; l[j] = b;
+          omx = fmaxf(omx, fabsf(e[j]));
+        }
+        __bf16* cp = o.Cp + (long long)row * o.ldcp + col;
+        *reinterpret_cast<f16x4*>(cp) = h;
+        *reinterpret_cast<f16x4*>(cp + o.pC) = l;
+      } else if (o.Cp) {
         bf16x4_t h, m, l;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -178,7 +205,13 @@ __device__ inline void store_tile32(const f32x16_t& acc, float* scr, int lane, i
         if (EPI == EPI_BIAS_RELU) x = fmaxf(x + o.bias[cc], 0.f);
         if (EPI == EPI_RELU_MASK) x = o.mask[(long long)row * o.ldm + cc] > 0.f ? x : 0.f;
         if (o.C) o.C[(long long)row * o.ldc + cc] = x;
-        if (o.Cp) {
+        if (o.Cp && o.h2) {
+          _Float16 a, b;
+          split2h_dev(x, o.oscale, a, b);
+          omx = fmaxf(omx, fabsf(x));
+          reinterpret_cast<_Float16*>(o.Cp)[(long long)row * o.ldcp + cc] = a;
+          reinterpret_cast<_Float16*>(o.Cp)[(long long)row * o.ldcp + cc + o.pC] = b;
+        } else if (o.Cp) {
           __bf16 a, b, c;
           split3_dev(x, a, b, c);
           __bf16* cp = o.Cp + (long long)row * o.ldcp + cc;

@@ -216,10 +216,11 @@ __global__ __launch_bounds__(NTH, 2) void gemm_x3_kernel(GemmParams p, int dbg) 
           (!p.Cp || p.ldcp % 4 == 0);
   __syncthreads();  // operand tiles (and the db scratch) are dead: reuse LDS as store scratch
   float* scr = reinterpret_cast<float*>(smem) + wave * (32 * 36);
-  store_tile32<EPI>(acc00, scr, lane, m0 + wm, n0 + wn, o);
-  store_tile32<EPI>(acc01, scr, lane, m0 + wm, n0 + wn + 32, o);
-  store_tile32<EPI>(acc10, scr, lane, m0 + wm + 32, n0 + wn, o);
-  store_tile32<EPI>(acc11, scr, lane, m0 + wm + 32, n0 + wn + 32, o);
+  float omx = 0.f;  // (split2h maxima: the fp32-operand kernel writes split3 planes only)
+  store_tile32<EPI>(acc00, scr, lane, m0 + wm, n0 + wn, o, omx);
+  store_tile32<EPI>(acc01, scr, lane, m0 + wm, n0 + wn + 32, o, omx);
+  store_tile32<EPI>(acc10, scr, lane, m0 + wm + 32, n0 + wn, o, omx);
+  store_tile32<EPI>(acc11, scr, lane, m0 + wm + 32, n0 + wn + 32, o, omx);
 }
 
 }  // namespace

@@ -286,6 +286,7 @@ int gemm_x3f(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
   const SplitGemmParams& p = p0;
   const int bm = gemm_x3f_bm(p, batch);
   const dim3 grid((unsigned)(((p.M + bm - 1) / bm) * ((p.N + BN - 1) / BN) * batch));
+  if (p.nparts) *p.nparts = (int)grid.x;
   const bool c = p.C != nullptr, pl = p.Cp != nullptr, m16 = p.mask16 != nullptr;
   if (epi == EPI_BIAS_RELU && p.tag == 1 && pl && !c) {
     launch<EPI_BIAS_RELU, false, true, false, TAG_INPUT>(p, grid, st, bm);  // input layer (planes out)

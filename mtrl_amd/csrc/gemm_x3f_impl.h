@@ -254,11 +254,11 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   float unscale = 1.f, oscale = 1.f;
   float* mscr = img + 2 * 16 * TS + WV * BN;
   if constexpr (NP == 2) {
-    unscale = exp2i(-*p.ea) * exp2i(-*p.eb);
+    unscale = exp2i(-p.ra->e) * exp2i(-p.rb->e);
     if (P_OUT && !FIN) {
       const int ec = gemm_out_exp(p, mscr);
       oscale = exp2i(ec);
-      if (blockIdx.x == 0 && t == 0) *p.ec = ec;
+      if (blockIdx.x == 0 && t == 0) p.rc->e = ec;
     }
   }
   float omx = 0.f;  // this lane's max |out| (split2h planes)
@@ -444,7 +444,7 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   }
   if constexpr (NP == 2 && P_OUT && !FIN) {  // this workgroup's max |out|: the next producer's bound input
     const float m = block_max_val(omx, mscr);
-    if (t == 0 && p.omax) p.omax[blockIdx.x] = m;
+    if (t == 0 && blockIdx.x < PLANE_REC_PARTS) p.rc->amax[blockIdx.x] = m;
   }
   if (p.dbp) {  // the tile's column sums: lanes l, l + 32 of every wave hold the same 8 columns
     float* red = img + 2 * 16 * TS;  // [WV waves][256]

@@ -224,6 +224,7 @@ static void x3p_dispatch(int geo, const SplitGemmParams& p, int epi, int batch, 
   geo_tile(geo, bm, bn);
   const unsigned n = (unsigned)(((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * batch * (p.splits > 1 ? p.splits : 1));
   const dim3 grid(n);
+  if (p.nparts && p.Cp) *p.nparts = (int)n;  // split-K launches write no planes (the finishing pass does)
   const int form = (p.a_kmajor ? 1 : 0) | (p.b_kmajor ? 2 : 0);
   switch (geo) {
     case 0: x3p_unit_g0(p, epi, grid, st); break;
@@ -307,8 +308,18 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(SplitGemmParams p,
   const long long slab = (long long)p.M * p.N;
   const int n4 = p.N / 4;
   const long long per = (long long)p.M * n4;
-  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= per * batch) return;
+  // split2h planes: the bound's exponent (every block alike) and this block's max |out|
+  __shared__ float mscr[16];
+  const bool h2 = p.np == 2 && p.Cp;
+  float oscale = 1.f, omx = 0.f;
+  if (h2) {
+    const int ec = gemm_out_exp(p, mscr);
+    oscale = exp2i(ec);
+    if (blockIdx.x == 0 && threadIdx.x == 0) p.rc->e = ec;
+  }
+  // grid-stride (a bounded grid: one partial max per block)
+  for (long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x; gid < per * batch;
+       gid += (long long)gridDim.x * blockDim.x) {
   const int z = (int)(gid / per);
   const long long r = gid - z * per;
   const int row = (int)(r / n4), col = (int)(r - (long long)row * n4) * 4;
@@ -324,7 +335,13 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(SplitGemmParams p,
     e[0] = fmaxf(e[0] + b.x, 0.f); e[1] = fmaxf(e[1] + b.y, 0.f);
     e[2] = fmaxf(e[2] + b.z, 0.f); e[3] = fmaxf(e[3] + b.w, 0.f);
   }
-  if (EPI == EPI_RELU_MASK && p.mask16) {  // the activation's bf16 high plane (gemm_x3f nets)
+  if (EPI == EPI_RELU_MASK && p.mask16 && p.np == 2) {  // fp16 planes: x > 0 <=> h > 0 or l > 0
+    const __bf16* mp = p.mask16 + z * p.sMask + (long long)row * p.ldm + col;
+    const i16x4 mh = __builtin_bit_cast(i16x4, *reinterpret_cast<const bf16x4_t*>(mp));
+    const i16x4 ml = __builtin_bit_cast(i16x4, *reinterpret_cast<const bf16x4_t*>(mp + p.pMask));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e[j] = (mh[j] > 0 || ml[j] > 0) ? e[j] : 0.f;
+  } else if (EPI == EPI_RELU_MASK && p.mask16) {  // the activation's bf16 high plane (gemm_x3f nets)
     const bf16x4_t mk = *reinterpret_cast<const bf16x4_t*>(p.mask16 + z * p.sMask + (long long)row * p.ldm + col);
 #pragma unroll
     for (int j = 0; j < 4; ++j) e[j] = (float)mk[j] > 0.f ? e[j] : 0.f;
@@ -334,7 +351,19 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(SplitGemmParams p,
     e[2] = mk.z > 0.f ? e[2] : 0.f; e[3] = mk.w > 0.f ? e[3] : 0.f;
   }
   if (p.C) *reinterpret_cast<float4*>(p.C + z * p.sC + (long long)row * p.ldc + col) = make_float4(e[0], e[1], e[2], e[3]);
-  if (p.Cp) {
+  if (h2) {
+    f16x4 h, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      _Float16 a, b;
+      split2h_dev(e[j], oscale, a, b);
+      h[j] = a; l[j] = b;
+      omx = fmaxf(omx, fabsf(e[j]));
+    }
+    __bf16* cp = p.Cp + z * p.sCp + (long long)row * p.ldcp + col;
+    *reinterpret_cast<f16x4*>(cp) = h;
+    *reinterpret_cast<f16x4*>(cp + p.pC) = l;
+  } else if (p.Cp) {
     bf16x4_t h, m, l;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -349,6 +378,11 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(SplitGemmParams p,
       *reinterpret_cast<bf16x4_t*>(cp + 2 * p.pC) = l;
     }
   }
+  }  // grid-stride
+  if (h2) {
+    const float m = block_max_val(omx, mscr);
+    if (threadIdx.x == 0 && blockIdx.x < PLANE_REC_PARTS) p.rc->amax[blockIdx.x] = m;
+  }
 }
 
 // the same finish with the bias grad's column-sum partials (p.dbp): block (256 columns, FR rows, z),
@@ -358,10 +392,21 @@ constexpr int FR = 16;  // rows per finishing block = gemm_x3f's dbp row granula
 template <int EPI>
 __global__ __launch_bounds__(256) void splitk_epilogue_dbp_kernel(SplitGemmParams p, int S) {
   __shared__ float4 red[4][64];
-  const int z = blockIdx.z, chunk = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ float mscr[16];
+  const int z = blockIdx.z, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = blockIdx.x * 256 + 4 * lane;
   const bool cok = col < p.N;
   const long long slab = (long long)p.M * p.N;
+  const int nchunks = (p.M + FR - 1) / FR;
+  const bool h2 = p.np == 2 && p.Cp;
+  float oscale = 1.f, omx = 0.f;
+  if (h2) {
+    const int ec = gemm_out_exp(p, mscr);
+    oscale = exp2i(ec);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) p.rc->e = ec;
+  }
+  // a bounded grid (one partial max per block): blocks step over the row chunks
+  for (int chunk = blockIdx.y; chunk < nchunks; chunk += gridDim.y) {
   float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 v[4];
   bool ok[4];
@@ -392,14 +437,32 @@ __global__ __launch_bounds__(256) void splitk_epilogue_dbp_kernel(SplitGemmParam
       e[0] = fmaxf(e[0] + b.x, 0.f); e[1] = fmaxf(e[1] + b.y, 0.f);
       e[2] = fmaxf(e[2] + b.z, 0.f); e[3] = fmaxf(e[3] + b.w, 0.f);
     }
-    if (EPI == EPI_RELU_MASK) {
+    if (EPI == EPI_RELU_MASK && p.np == 2) {  // fp16 planes: x > 0 <=> h > 0 or l > 0
+      const __bf16* mp = p.mask16 + z * p.sMask + (long long)row * p.ldm + col;
+      const i16x4 mh = __builtin_bit_cast(i16x4, *reinterpret_cast<const bf16x4_t*>(mp));
+      const i16x4 ml = __builtin_bit_cast(i16x4, *reinterpret_cast<const bf16x4_t*>(mp + p.pMask));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) e[j] = (mh[j] > 0 || ml[j] > 0) ? e[j] : 0.f;
+    } else if (EPI == EPI_RELU_MASK) {
       const bf16x4_t mk = *reinterpret_cast<const bf16x4_t*>(p.mask16 + z * p.sMask + (long long)row * p.ldm + col);
 #pragma unroll
       for (int j = 0; j < 4; ++j) e[j] = (float)mk[j] > 0.f ? e[j] : 0.f;
     }
     cs.x += e[0]; cs.y += e[1]; cs.z += e[2]; cs.w += e[3];
     if (p.C) *reinterpret_cast<float4*>(p.C + z * p.sC + (long long)row * p.ldc + col) = make_float4(e[0], e[1], e[2], e[3]);
-    if (p.Cp) {
+    if (h2) {
+      f16x4 h, l;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        _Float16 a, b;
+        split2h_dev(e[j], oscale, a, b);
+        h[j] = a; l[j] = b;
+        omx = fmaxf(omx, fabsf(e[j]));
+      }
+      __bf16* cp = p.Cp + z * p.sCp + (long long)row * p.ldcp + col;
+      *reinterpret_cast<f16x4*>(cp) = h;
+      *reinterpret_cast<f16x4*>(cp + p.pC) = l;
+    } else if (p.Cp) {
       bf16x4_t h, m, l;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -419,9 +482,17 @@ __global__ __launch_bounds__(256) void splitk_epilogue_dbp_kernel(SplitGemmParam
   __syncthreads();
   if (wave == 0 && cok) {
     const float4 a = red[0][lane], b = red[1][lane], c = red[2][lane], d = red[3][lane];
-    *reinterpret_cast<float4*>(p.dbp + ((long long)z * gridDim.y + chunk) * p.N + col) =
+    *reinterpret_cast<float4*>(p.dbp + ((long long)z * nchunks + chunk) * p.N + col) =
         make_float4(((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y, ((a.z + b.z) + c.z) + d.z,
                     ((a.w + b.w) + c.w) + d.w);
+  }
+  __syncthreads();  // red is reused by the next chunk
+  cs = make_float4(0.f, 0.f, 0.f, 0.f);
+  }  // chunks
+  if (h2) {
+    const float m = block_max_val(omx, mscr);
+    const unsigned b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    if (threadIdx.x == 0 && b < PLANE_REC_PARTS) p.rc->amax[b] = m;
   }
 }
 
@@ -458,7 +529,7 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
   // k-major weight grads with arrival counters: the last slice of each tile reduces in-launch
   int bm, bn;
   geo_tile(geo, bm, bn);
-  const bool fin = S > 1 && epi == EPI_STORE && !p.Cp && kmajor && p.np != 1 && p.cnt != nullptr &&
+  const bool fin = S > 1 && epi == EPI_STORE && !p.Cp && kmajor && p.np != 1 && p.np != 2 && p.cnt != nullptr &&
                    p.N % 4 == 0 && p.ldc % 4 == 0 &&
                    (long long)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn) * batch <= GEMM_X3F_CNT;
   if (!fin) q.cnt = nullptr;
@@ -485,13 +556,18 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
 
 void splitk_finish(const SplitGemmParams& p, int epi, int S, int batch, hipStream_t st) {
   if (p.dbp != nullptr && (epi == EPI_BIAS_RELU || (epi == EPI_RELU_MASK && p.mask16))) {
-    const dim3 grid((unsigned)((p.N + 255) / 256), (unsigned)((p.M + FR - 1) / FR), (unsigned)batch);
+    // at most PLANE_REC_PARTS blocks (one partial max each, split2h): blocks step over row chunks
+    const int gx = (p.N + 255) / 256, chunks = (p.M + FR - 1) / FR;
+    const int gy = std::max(1, std::min(chunks, PLANE_REC_PARTS / std::max(1, gx * batch)));
+    const dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)batch);
+    if (p.nparts) *p.nparts = gx * gy * batch;
     if (epi == EPI_BIAS_RELU) hipLaunchKernelGGL(splitk_epilogue_dbp_kernel<EPI_BIAS_RELU>, grid, dim3(256), 0, st, p, S);
     else hipLaunchKernelGGL(splitk_epilogue_dbp_kernel<EPI_RELU_MASK>, grid, dim3(256), 0, st, p, S);
     return;
   }
   const long long n = (long long)batch * p.M * (p.N / 4);
-  const dim3 grid((unsigned)((n + 255) / 256));
+  const dim3 grid((unsigned)std::min<long long>((n + 255) / 256, PLANE_REC_PARTS));
+  if (p.nparts) *p.nparts = (int)grid.x;
   if (epi == EPI_BIAS_RELU)
     hipLaunchKernelGGL(splitk_epilogue_kernel<EPI_BIAS_RELU>, grid, dim3(256), 0, st, p, S, batch);
   else if (epi == EPI_RELU_MASK)

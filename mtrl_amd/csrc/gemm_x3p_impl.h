@@ -246,6 +246,14 @@ __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) 
               for (int q = slot * PIECES / SLOTS; q < (slot + 1) * PIECES / SLOTS; ++q) piece(rs, rk, q);
             }
             f32x16 c = acc[i][j];
+            if constexpr (NP == 2) {  // fp16 planes: h*l, l*h, h*h
+              typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+              c = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8, a[i][0]), __builtin_bit_cast(h8, b[j][1]), c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8, a[i][1]), __builtin_bit_cast(h8, b[j][0]), c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8, a[i][0]), __builtin_bit_cast(h8, b[j][0]), c, 0, 0, 0);
+              acc[i][j] = c;
+              continue;
+            }
             if constexpr (NP == 3) {
               c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], c, 0, 0, 0);  // m*m
               c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], c, 0, 0, 0);  // h*l
@@ -281,12 +289,30 @@ __global__ __launch_bounds__(G::NTH, 1) void gemm_x3p_kernel(SplitGemmParams p) 
     o.N = p.N;
     o.vec = (p.N % 4 == 0) && (o.ldc % 4 == 0) && (EPI != EPI_RELU_MASK || p.ldm % 4 == 0) &&
             (!PLANES_OUT || p.ldcp % 4 == 0);
+    o.h2 = NP == 2;
+    o.unscale = o.oscale = 1.f;
     __builtin_amdgcn_s_barrier();  // every wave is done with the ring: reuse it as scratch
+    float* mscr = reinterpret_cast<float*>(smem) + G::NW * (32 * 36);
+    if constexpr (NP == 2) {
+      o.unscale = exp2i(-p.ra->e) * exp2i(-p.rb->e);
+      if (o.Cp) {  // block-uniform (raw is)
+        const int ec = gemm_out_exp(p, mscr);
+        o.oscale = exp2i(ec);
+        if (blockIdx.x == 0 && t == 0) p.rc->e = ec;
+      }
+    }
+    float omx = 0.f;
     float* scr = reinterpret_cast<float*>(smem) + wave * (32 * 36);
 #pragma unroll
     for (int i = 0; i < G::TI; ++i)
 #pragma unroll
-      for (int j = 0; j < G::TJ; ++j) store_tile32<EPI>(acc[i][j], scr, lane, m0 + wm + 32 * i, n0 + wn + 32 * j, o);
+      for (int j = 0; j < G::TJ; ++j) store_tile32<EPI>(acc[i][j], scr, lane, m0 + wm + 32 * i, n0 + wn + 32 * j, o, omx);
+    if constexpr (NP == 2) {
+      if (o.Cp) {  // this workgroup's max |out|: the next producer's bound input
+        const float m = block_max_val(omx, mscr);
+        if (t == 0 && blockIdx.x < PLANE_REC_PARTS) p.rc->amax[blockIdx.x] = m;
+      }
+    }
   };
 
   // one tile (or one split-K slice of one) per workgroup, XCD-contiguous order
@@ -401,6 +427,7 @@ void launch_x3p_np(const SplitGemmParams& p, int epi, dim3 grid, hipStream_t st)
 template <class G, bool AKM, bool BKM>
 void launch_x3p_v(const SplitGemmParams& p, int epi, dim3 grid, hipStream_t st) {
   if (p.np == 1) launch_x3p_np<G, AKM, BKM, 1>(p, epi, grid, st);
+  else if (p.np == 2) launch_x3p_np<G, AKM, BKM, 2>(p, epi, grid, st);
   else launch_x3p_np<G, AKM, BKM, 3>(p, epi, grid, st);
 }
 

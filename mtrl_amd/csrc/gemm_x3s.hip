@@ -44,12 +44,14 @@ constexpr int TAG_INPUT = 8;
 // prologue, bit 32 = no MFMAs
 constexpr int ABL_NOLOAD = 16, ABL_NOMFMA = 32;
 
-// NP: operand planes read (3: 6 products, fp32-accurate; 1: the high plane only, precision bf16)
+// NP: operand planes read (3: 6 products, fp32-accurate; 1: the high plane only, precision bf16;
+// 2: precision split2h, two fp16 planes of x 2^e, 3 products, unscaled in the epilogue)
 template <int TI, int EPI, bool C_OUT, bool P_OUT, bool MASK16, int TAG = 0, int NP = 3>
 __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
   constexpr int BM = 16 * TI;
   constexpr int RLD = BN + 4;  // floats per row of a wave's partial tile in LDS
   __shared__ __attribute__((aligned(16))) float red[NW * BM * RLD];
+  __shared__ float mscr[16];  // split2h: block reductions of maxima
 
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -129,6 +131,14 @@ __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
     if (TAG & ABL_NOMFMA) return;
     if constexpr (NP == 1) {
       asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[i][0]), "v"(b[j][0]));  // h*h
+      return;
+    }
+    if constexpr (NP == 2) {  // fp16 planes: h*l, l*h, h*h
+      asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0\n\t"
+          "v_mfma_f32_16x16x32_f16 %0, %3, %4, %0\n\t"
+          "v_mfma_f32_16x16x32_f16 %0, %1, %4, %0"
+          : "+a"(acc[i][j])
+          : "v"(a[i][0]), "v"(b[j][1]), "v"(a[i][1]), "v"(b[j][0]));
       return;
     }
     asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"   // m*m
@@ -214,6 +224,15 @@ __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
     bias[0] = u.x; bias[1] = u.y; bias[2] = u.z; bias[3] = u.w;
   }
   float csum[4] = {0.f, 0.f, 0.f, 0.f};  // column sums over this thread's rows (dbp)
+  float unscale = 1.f, oscale = 1.f, omx = 0.f;
+  if constexpr (NP == 2) {
+    unscale = exp2i(-p.ra->e) * exp2i(-p.rb->e);
+    if (P_OUT) {
+      const int ec = gemm_out_exp(p, mscr);
+      oscale = exp2i(ec);
+      if (blockIdx.x == 0 && t == 0) p.rc->e = ec;
+    }
+  }
   for (int rr = t >> 4; rr < BM; rr += NW * 4) {  // row in the tile
     const int row = m0 + rr;
     if (row >= p.M || !colok) break;
@@ -228,21 +247,45 @@ __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
       e[2] = ((v0.z + v1.z) + v2.z) + v3.z;
       e[3] = ((v0.w + v1.w) + v2.w) + v3.w;
     }
+    if constexpr (NP == 2) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) e[c] *= unscale;
+    }
     if (EPI == EPI_BIAS_RELU) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) e[c] = fmaxf(e[c] + bias[c], 0.f);
     }
     if (EPI == EPI_RELU_MASK) {
       static_assert(MASK16 || EPI != EPI_RELU_MASK, "ReLU mask from the bf16 high plane only");
-      const bf16x4 mk = *reinterpret_cast<const bf16x4*>(p.mask16 + z * p.sMask + (long long)row * p.ldm + col);
+      const __bf16* mp = p.mask16 + z * p.sMask + (long long)row * p.ldm + col;
+      if constexpr (NP == 2) {  // fp16 planes: x > 0 <=> h > 0 or l > 0
+        const i16x4 mh = __builtin_bit_cast(i16x4, *reinterpret_cast<const bf16x4*>(mp));
+        const i16x4 ml = __builtin_bit_cast(i16x4, *reinterpret_cast<const bf16x4*>(mp + p.pMask));
 #pragma unroll
-      for (int c = 0; c < 4; ++c) e[c] = (float)mk[c] > 0.f ? e[c] : 0.f;
+        for (int c = 0; c < 4; ++c) e[c] = (mh[c] > 0 || ml[c] > 0) ? e[c] : 0.f;
+      } else {
+        const bf16x4 mk = *reinterpret_cast<const bf16x4*>(mp);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) e[c] = (float)mk[c] > 0.f ? e[c] : 0.f;
+      }
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c) csum[c] += e[c];
     if (C_OUT)
       *reinterpret_cast<float4*>(p.C + z * p.sC + (long long)row * p.ldc + col) = make_float4(e[0], e[1], e[2], e[3]);
-    if (P_OUT) {
+    if (P_OUT && NP == 2) {
+      f16x4 h, l;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        _Float16 a_, b_;
+        split2h_dev(e[c], oscale, a_, b_);
+        h[c] = a_; l[c] = b_;
+        omx = fmaxf(omx, fabsf(e[c]));
+      }
+      __bf16* pp = p.Cp + z * p.sCp + (long long)row * p.ldcp + col;
+      *reinterpret_cast<f16x4*>(pp) = h;
+      *reinterpret_cast<f16x4*>(pp + p.pC) = l;
+    } else if (P_OUT) {
       bf16x4 h, m, l;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -255,6 +298,10 @@ __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
       *reinterpret_cast<bf16x4*>(pp + p.pC) = m;
       *reinterpret_cast<bf16x4*>(pp + 2 * p.pC) = l;
     }
+  }
+  if constexpr (NP == 2 && P_OUT) {  // this workgroup's max |out|: the next producer's bound input
+    const float m = block_max_val(omx, mscr);
+    if (t == 0 && blockIdx.x < PLANE_REC_PARTS) p.rc->amax[blockIdx.x] = m;
   }
   if (p.dbp) {  // the tile's column sums (the next weight grad's bias grad, finished by colsum_finish):
     // the 16 row groups (t >> 4) added in order
@@ -275,8 +322,11 @@ __global__ __launch_bounds__(256, 1) void gemm_x3s_kernel(SplitGemmParams p) {
 template <int TI, int EPI, bool C_OUT, bool P_OUT, bool MASK16, int TAG = 0>
 void launch(const SplitGemmParams& p, int batch, hipStream_t st) {
   const unsigned grid = (unsigned)(((p.M + 16 * TI - 1) / (16 * TI)) * ((p.N + BN - 1) / BN) * batch);
+  if (p.nparts) *p.nparts = (int)grid;
   if (p.np == 1)
     hipLaunchKernelGGL((gemm_x3s_kernel<TI, EPI, C_OUT, P_OUT, MASK16, TAG, 1>), dim3(grid), dim3(64 * NW), 0, st, p);
+  else if (p.np == 2)
+    hipLaunchKernelGGL((gemm_x3s_kernel<TI, EPI, C_OUT, P_OUT, MASK16, TAG, 2>), dim3(grid), dim3(64 * NW), 0, st, p);
   else
     hipLaunchKernelGGL((gemm_x3s_kernel<TI, EPI, C_OUT, P_OUT, MASK16, TAG, 3>), dim3(grid), dim3(64 * NW), 0, st, p);
 }

@@ -132,7 +132,13 @@ __device__ inline void policy_finish(const PolicyParams& p, int b, int t, const 
     term = -0.5f * eps * eps - HALF_LOG_2PI - logf(sigma) - 2.0f * (LOG2F - x - softplusf(-2.0f * x));
     p.a_out[(long long)b * p.ld_a_out + lane] = a;
     if (p.a_out2) p.a_out2[(long long)b * p.ld_a_out2 + lane] = a;
-    if (p.a_planes) {  // the critic input's planes of the action columns (the obs columns: the gather)
+    if (p.a_planes && p.ap_rec) {  // split2h: fp16 planes at the input tensor's exponent
+      _Float16 h, l;
+      split2h_dev(a, exp2i(p.ap_rec->e), h, l);
+      const long long o = (long long)b * p.ap_ld + lane;
+      reinterpret_cast<_Float16*>(p.a_planes)[o] = h;
+      reinterpret_cast<_Float16*>(p.a_planes)[o + p.ap_ps] = l;
+    } else if (p.a_planes) {  // the critic input's planes of the action columns (the obs columns: the gather)
       __bf16 h, m, l;
       split3_dev(a, h, m, l);
       const long long o = (long long)b * p.ap_ld + lane;
@@ -215,11 +221,13 @@ static int rows_per_wave(long long wgs_at_rw1) {
 }
 
 // ------------------------------------------------------------------ critic heads + losses
+// grid-stride over rows (one wave per row at a time); split2h: each wave's max |dq| to dq_rec
 __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
   const int lane = threadIdx.x & 63;
   const HeadParams& hp = p.head;
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= hp.B) return;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  float dqmax = 0.f;
+  for (int b = wid; b < hp.B; b += gridDim.x * 4) {
   const int t = hp.task[b];
   float q[4];
   const int E = hp.E;
@@ -237,7 +245,7 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
       qt[e] = acc[0] + th.bh[e * th.sbh + t];
     }
   }
-  if (lane != 0) return;
+  if (lane != 0) continue;
   const float alpha = expf(p.log_alpha[p.task_begin + t]);  // exp(onehot . log_alpha), mtsac.py:60-63
   float w = 1.f;
   if (p.tw != nullptr) w = p.tw[b];  // T * softmax(-log_alpha)[t] (mtsac.py:103-113)
@@ -264,7 +272,9 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
       const float diff = qc - y;
       sq += w * diff * diff;
       qs += qc;
-      p.dq[e * hp.B + b] = w * 2.0f * diff * p.inv_norm * dcl;
+      const float g = w * 2.0f * diff * p.inv_norm * dcl;
+      p.dq[e * hp.B + b] = g;
+      dqmax = fmaxf(dqmax, fabsf(g));
     }
     p.row_a[b] = sq;
     p.row_b[b] = qs;
@@ -273,10 +283,16 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
     for (int e = 1; e < E; ++e) mn = fminf(mn, q[e]);
     int cnt = 0;
     for (int e = 0; e < E; ++e) cnt += (q[e] == mn) ? 1 : 0;
-    for (int e = 0; e < E; ++e) p.dq[e * hp.B + b] = (q[e] == mn) ? (-w * p.inv_norm / (float)cnt) : 0.f;
+    for (int e = 0; e < E; ++e) {
+      const float g = (q[e] == mn) ? (-w * p.inv_norm / (float)cnt) : 0.f;
+      p.dq[e * hp.B + b] = g;
+      dqmax = fmaxf(dqmax, fabsf(g));
+    }
     p.row_a[b] = w * (alpha * p.logpi[b] - mn);
     p.alpha_w[b] = w * alpha * p.inv_norm;
   }
+  }  // rows
+  if (p.dq_rec && lane == 0 && wid < PLANE_REC_PARTS) p.dq_rec->amax[wid] = dqmax;
 }
 
 // ------------------------------------------------------------------ head backward (data)
@@ -308,7 +324,20 @@ __device__ inline float4 head_bwd_row(const HeadParams& hp, const float* __restr
   out.z = h.z > 0.f ? g[2] : 0.f;
   out.w = h.w > 0.f ? g[3] : 0.f;
   if (dz) *reinterpret_cast<float4*>(dz + off) = out;
-  if (po.p) {  // the bf16 split planes the next GEMMs read
+  if (po.p && po.rc) {  // split2h: fp16 planes at the bound's exponent (oscale folded into po.kmul below)
+    const float v[4] = {out.x, out.y, out.z, out.w};
+    f16x4 ph, pl;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      _Float16 a, b2;
+      split2h_dev(v[k], po.w_add, a, b2);  // w_add carries the block's output scale here (head_bwd_data_body)
+      ph[k] = a;
+      pl[k] = b2;
+    }
+    __bf16* q = po.p + e * po.sm + (long long)b * po.ld + w;
+    *reinterpret_cast<f16x4*>(q) = ph;
+    *reinterpret_cast<f16x4*>(q + po.ps) = pl;
+  } else if (po.p) {  // the bf16 split planes the next GEMMs read
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
     const float v[4] = {out.x, out.y, out.z, out.w};
     bf16x4 ph, pm, pl;
@@ -332,9 +361,18 @@ __device__ inline float4 head_bwd_row(const HeadParams& hp, const float* __restr
 // (bx, by, bz) of a [W / 256][T_l HB_RS][E] grid; red: 4 x 64 float4 of LDS
 template <int HD>
 __device__ inline void head_bwd_data_body(const HeadParams& hp, const float* __restrict__ dout, long long s_dout,
-                                          float* __restrict__ dz, const PlaneOut& po, float* __restrict__ dbp,
+                                          float* __restrict__ dz, const PlaneOut& po_in, float* __restrict__ dbp,
                                           const int* __restrict__ counts, const int* __restrict__ rows, int max_rows,
                                           int bx, int by, int bz, int gy, float4 (*red)[64]) {
+  // split2h: the planes' exponent from the bound kmul * max|dout| * (max|head weight| + w_add), every
+  // workgroup alike (red is the scratch of the maxima); the scale rides in po.w_add from here on
+  PlaneOut po = po_in;
+  if (po.p && po.rc) {
+    const float md = rec_max(po.rd, po.nd, reinterpret_cast<float*>(red));
+    const int ec = plane_exp(po.kmul * md * (po.rw->amax[1] + po.w_add));
+    po.w_add = exp2i(ec);
+    if (bx == 0 && by == 0 && bz == 0 && threadIdx.x == 0) po.rc->e = ec;
+  }
   const int e = bz, t = by / HB_RS, rs = by - t * HB_RS;
   const int lane = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int w = bx * 256 + 4 * lane;
@@ -557,8 +595,12 @@ __global__ __launch_bounds__(256) void head_bwd_both_kernel(HeadParams hp, const
 template <int AG_RW>
 __global__ __launch_bounds__(256) void action_grad_kernel(ActionGradParams p) {
   const int lane = threadIdx.x & 63;
-  const int b0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * AG_RW;
-  if (b0 >= p.B) return;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int b0 = wid * AG_RW;
+  if (b0 >= p.B) {
+    if (p.dout_rec && lane == 0 && wid < PLANE_REC_PARTS) p.dout_rec->amax[wid] = 0.f;
+    return;
+  }
   const int A = p.A;
   int rows[AG_RW];
 #pragma unroll
@@ -606,6 +648,7 @@ __global__ __launch_bounds__(256) void action_grad_kernel(ActionGradParams p) {
       }
     }
   }
+  float omx = 0.f;
 #pragma unroll
   for (int r = 0; r < AG_RW; ++r) {
     const int b = b0 + r;
@@ -624,6 +667,12 @@ __global__ __launch_bounds__(256) void action_grad_kernel(ActionGradParams p) {
     const float g_ls = (g_x * sigma * eps - g_logpi) * clip_grad(ls, p.ls_min, p.ls_max);
     p.dout[(long long)b * 2 * A + lane] = g_x;
     p.dout[(long long)b * 2 * A + A + lane] = g_ls;
+    omx = fmaxf(omx, fmaxf(fabsf(g_x), fabsf(g_ls)));
+  }
+  if (p.dout_rec) {  // split2h: this wave's max |dout| (the actor head backward's bound input)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) omx = fmaxf(omx, __shfl_xor(omx, o));
+    if (lane == 0 && wid < PLANE_REC_PARTS) p.dout_rec->amax[wid] = omx;
   }
 }
 
@@ -697,7 +746,9 @@ void policy_head_pair(const PolicyParams& a, const PolicyParams& b, hipStream_t 
 }
 
 void critic_head(const CriticHeadParams& p, hipStream_t st) {
-  hipLaunchKernelGGL(critic_head_kernel, dim3((p.head.B + 3) / 4), dim3(256), 0, st, p);
+  const int g = std::min((p.head.B + 3) / 4, PLANE_REC_PARTS / 4);  // one max per wave (split2h)
+  if (p.dq_parts) *p.dq_parts = 4 * g;
+  hipLaunchKernelGGL(critic_head_kernel, dim3(g), dim3(256), 0, st, p);
 }
 
 void head_backward_data(const HeadParams& hp, const float* dout, long long s_dout, float* dz, const int* counts,
@@ -758,6 +809,7 @@ void head_backward_weight(const HeadParams& hp, const float* dout, long long s_d
 void action_grad(const ActionGradParams& p, hipStream_t st) {
   const int rw = rows_per_wave((p.B + 3) / 4);
   const dim3 grid((unsigned)((p.B + 4 * rw - 1) / (4 * rw)));
+  if (p.dout_parts) *p.dout_parts = std::min<int>(4 * (int)grid.x, PLANE_REC_PARTS);
   if (rw == 4) hipLaunchKernelGGL(action_grad_kernel<4>, grid, dim3(256), 0, st, p);
   else if (rw == 2) hipLaunchKernelGGL(action_grad_kernel<2>, grid, dim3(256), 0, st, p);
   else hipLaunchKernelGGL(action_grad_kernel<1>, grid, dim3(256), 0, st, p);

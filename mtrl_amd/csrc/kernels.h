@@ -65,6 +65,18 @@ void gemm_f32(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_
 // same contract, fp32-accurate via 3-way bf16 operand split on bf16 MFMA (gemm_x3.hip)
 void gemm_x3(const GemmParams& p, GemmKind kind, int epi, int batch, hipStream_t st);
 
+// ------------------------------------------------------------------ split2h plane records
+// Device record of one fp16-plane tensor (precision split2h): the planes hold x * 2^e; amax holds
+// the partial maxima |x| of the last write, one per producer workgroup (the host knows how many are
+// valid).  Weight records keep amax[0] = max |trunk parameter| (kernels and biases), amax[1] = max
+// |head parameter| (the optimizer's last workgroup reduces them).
+constexpr int PLANE_REC_PARTS = 2048;
+struct PlaneRec {
+  int e;
+  int pad[3];
+  float amax[PLANE_REC_PARTS];
+};
+
 // ------------------------------------------------------------------ pre-split plane GEMM
 // C[z][m][n] = sum_k A(m,k) B(n,k) on bf16 planes (gemm_x3p.hip).  A planes [3][M][lda]
 // (k contiguous) or, with a_kmajor, [3][K][lda] (m contiguous); B likewise with N.  K is a
@@ -101,23 +113,21 @@ struct SplitGemmParams {
   long long cs_sdb;
   int* cnt;               // gemm_x3f split-K: per-tile arrival counters (zero, >= GEMM_X3F_CNT ints) for
                           // the in-launch finish, or null (a separate finishing pass)
-  // ---- precision split2h (np == 2): every operand is two fp16 planes of x * 2^e, e per tensor
-  // (PlaneRec); the products are unscaled by 2^-(eA + eB).  Output planes: written with the exponent
-  // of the a-priori bound  kmul * max|A| * max|B| + max|bias|  (PlaneRec::exp_for), which every
-  // workgroup derives alike from the inputs' recorded maxima; workgroup 0 stores it in *ec and every
-  // workgroup its max |out| in omax[blockIdx.x] (the next producer's bound input).
-  const int* ea;
-  const int* eb;
-  const int* em;          // the mask planes' exponent (unused: the mask reads signs only)
-  long long pMask;        // plane stride of the mask16 planes (np == 2: x > 0 <=> hi > 0 or lo > 0)
-  int* ec;
-  float* omax;
-  const float* amaxA;     // A's producer maxima [namaxA]
-  int namaxA;
-  const float* amaxB;     // B's maxima [namaxB] (the weights' record)
-  int namaxB;
-  const float* amaxBias;  // max |bias| (one float) or null
+  // ---- precision split2h (np == 2): every operand is two fp16 planes of x * 2^e with e per tensor
+  // (PlaneRec); the products are unscaled by 2^-(eA + eB).  Output planes are written at the exponent
+  // of the a-priori bound  kmul * max|A| * max|B| (+ max|B| again when the bias lives in B's record:
+  // the trunk's biases are bounded by the same trunk maximum), which every workgroup derives alike
+  // from the operands' records; workgroup 0 stores it in rc->e and every workgroup its max |out| in
+  // rc->amax[blockIdx.x] (the next producer's bound input).
+  const PlaneRec* ra;
+  int na;                 // valid partial maxima in ra (0: the bound 2^(15 - e) of its planes)
+  const PlaneRec* rb;
+  int nb;
+  PlaneRec* rc;
+  int bias_in_b;
   float kmul;             // the number of terms in each output sum (unpadded K)
+  long long pMask;        // plane stride of the mask16 planes (np == 2: x > 0 <=> hi > 0 or lo > 0)
+  int* nparts;            // host: the launcher stores how many partial maxima it wrote to rc (or null)
 };
 constexpr int GEMM_X3F_CNT = 4096;
 void gemm_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
@@ -211,6 +221,10 @@ struct GatherParams {
   __bf16 *pc, *pcn, *pcp;
   long long pc_ps;
   int pc_ld;
+  // split2h: fp16 planes at the exponent of max(*in_max, 1) (the stored rows' max |value|; 1 covers the
+  // policy's actions), written to in_rec->e
+  PlaneRec* in_rec;
+  const float* in_max;
 };
 void replay_gather(const GatherParams& p, hipStream_t st);
 // a user batch (ReplayBufferSamples layout) into the same input buffers
@@ -221,9 +235,12 @@ void batch_scatter(const GatherParams& p, const float* obs, const float* act, co
 void buffer_pack_slot(float* rec, int T_l, int R, int D, int A, const float* obs, const float* nobs,
                       const float* act, const float* rew, const float* done, hipStream_t st);
 void buffer_commit_slot(const float* rec, int T_l, int R, int rcol, double* rmin, double* rmax, long long* buf_size,
-                        long long size, hipStream_t st);
+                        long long size, hipStream_t st, int D = 0, float* bufmax = nullptr);
+// bufmax (nullable): *bufmax = max(*bufmax, max |obs|, |action|, |next_obs| written) -- split2h's input bound
 void fill_synthetic(float* store, long long cap, int T_l, int R, int obs_dim, int act_dim, int T_glob,
-                    int task_begin, unsigned long long seed, hipStream_t st);
+                    int task_begin, unsigned long long seed, hipStream_t st, float* bufmax = nullptr);
+// *m = max(*m, max |x[0..n)|) (one block)
+void absmax_into(const float* x, long long n, float* m, hipStream_t st);
 // stable per-task row lists: rows_of[t*max_rows + j], counts[t]
 void task_rows(const int* task, int B, int T_l, int* counts, int* rows, int max_rows, hipStream_t st);
 
@@ -253,6 +270,7 @@ struct PolicyParams {
   __bf16* a_planes;     // optional bf16 planes of a_out's action columns ([3][.][ap_ld], plane stride ap_ps)
   long long ap_ps;
   int ap_ld;
+  const PlaneRec* ap_rec;  // split2h: the planes are fp16 at the input record's exponent (|a| <= 1 fits)
   float* logpi;         // [B]
   float* cache;         // optional [B][5A]: mu, ls, x, a, eps
   // optional per-task row lists (task_rows): rows grouped by task share head-kernel reads
@@ -292,13 +310,24 @@ struct CriticHeadParams {
   int use_task_weights;
   int T_glob;
   float inv_norm;       // 1/(E*B) critic, 1/B actor (global B)
+  PlaneRec* dq_rec;     // split2h: per-workgroup max |dq| (the head backward's bound input), or null
+  int* dq_parts;        // host: how many the launch wrote
 };
 void critic_head(const CriticHeadParams& p, hipStream_t st);
 
-// optional bf16 split planes of an output: [E][3][rows][ld], plane stride ps, member stride sm
+// optional bf16 split planes of an output: [E][3][rows][ld], plane stride ps, member stride sm.
+// split2h (rc non-null): two fp16 planes at the exponent of the bound  kmul * max|dout| * (max|head
+// weight| + w_add)  (dout's record rd with nd partial maxima; the weights' record rw keeps max|head|
+// in amax[1], w_add covers the optimizer steps since), per-workgroup maxima to rc
 struct PlaneOut {
   __bf16* p;
   long long ld, ps, sm;
+  PlaneRec* rc;
+  const PlaneRec* rd;
+  int nd;
+  const PlaneRec* rw;
+  float w_add, kmul;
+  int* nparts;          // host: how many partial maxima the launch wrote
 };
 // dz[e][b][w] = (sum_o dout[e][b][o] * Wh[e][t_b][w][o]) * (h[e][b][w] > 0)  (+ its planes), rows
 // walked per task (counts / rows of task_rows); dz may be null (planes only).  dbp (nullable):
@@ -326,6 +355,8 @@ struct ActionGradParams {
   const float* alpha_w; // [B] per-row dL/dlogpi (alpha * w / B)
   float ls_min, ls_max;
   float* dout;          // [B][2A]
+  PlaneRec* dout_rec;   // split2h: per-workgroup max |dout| (the head backward's bound input), or null
+  int* dout_parts;      // host: how many the launch wrote
 };
 void action_grad(const ActionGradParams& p, hipStream_t st);
 
@@ -362,6 +393,17 @@ struct PlaneSeg {
   long long ps;
   int of_target;        // 1: planes of the Polyak target's new value instead of the params'
 };
+// split2h (np == 2) weights: the optimizer writes fp16 planes of p * 2^e with e from the bound
+// max|p_old| + w_add (w_add = 16 lr covers one Adam step: |m_hat| / (sqrt(v_hat) + eps) < 7.3 for
+// b1^2 < b2), the target's at max(max|t_old|, that), stores both exponents in the records and
+// leaves per-block max |p_new| / |t_new| partials for step_finish to reduce into the records
+struct WeightH2 {
+  PlaneRec* wrec;       // params: e, amax[0] trunk max, amax[1] head max
+  PlaneRec* trec;       // Polyak target (null: none)
+  float w_add;
+  float* wparts;        // per-block max |p_new| [grid]
+  float* tparts;        // per-block max |t_new| [grid] (target)
+};
 constexpr int MAX_PLANE_SEGS = 8;
 struct AdamParams {
   float* p; float* m; float* v; const float* g;
@@ -375,6 +417,7 @@ struct AdamParams {
   int np;               // planes the GEMMs read: 1 (precision bf16) writes only the high plane
   int nskip;            // float4 ranges [skip_b, skip_e) of p left to adam_update_tiles
   long long skip_b[MAX_PLANE_SEGS], skip_e[MAX_PLANE_SEGS];
+  WeightH2 h2;          // np == 2
 };
 // p_partials accumulate |p_new|^2 over [norm_from, n) only (the replicated trunk range)
 int adam_update(const AdamParams& a, float max_norm, long long norm_from, int max_blocks, hipStream_t st);
@@ -457,6 +500,12 @@ struct LogParams {
 // The step's scalar tail, one launch: *row_out[k] = sum rows[k][0..B) for the non-null rows[k]
 // (reduce_rows' order); the temperature Adam; sc[w]->pnorm = sqrt(sum pt[w] + (head_sq ?
 // head_sq[w] : sum ph[w])); the logs; *counter += 1
+// split2h: the optimizer's per-block weight maxima into the weight records (blocks [0, nh) of a
+// params job cover the heads -> amax[1], the rest the trunk -> amax[0]; a target job (nh < 0) -> amax[0])
+struct WeightMaxJob {
+  const float* parts; int n, nh;
+  PlaneRec* rec;
+};
 struct StepFinish {
   const float* rows[3]; float* row_out[3]; int B;
   AlphaParams alpha; int alpha_grad;  // alpha_grad: also the temperature gradient (alpha_grad's work) first
@@ -464,8 +513,11 @@ struct StepFinish {
   PnormParts pn; const float* head_sq;
   LogParams logs;
   unsigned long long* counter;
+  WeightMaxJob wmax[3]; int nwmax;
 };
 void step_finish(const StepFinish& f, hipStream_t st);
+// split2h: a weight record from the parameters as they lie (set_params): maxima and the planes' exponent
+void weights_record(const float* p, long long trunk_off, long long n_flat, PlaneRec* rec, hipStream_t st);
 
 // ------------------------------------------------------------------ gradient-conflict statistics
 // (conflict.hip; MTSAC.compute_weights, mtsac.py:733-1170 and algorithms/utils.py:49-174)

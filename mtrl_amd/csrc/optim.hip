@@ -106,11 +106,26 @@ __device__ inline AdamConsts adam_consts(const AdamParams& a, float gnorm, int c
 
 // the elementwise pass over float4 i = blk, blk + nblk, ... < n4 (tiled leaves skipped); returns
 // this thread's |p_new|^2 over i >= norm_from4
+// split2h: the exponents of the weights' planes this update writes (params, target), from the
+// records' maxima of the values before the update (every block alike)
+struct H2Scales {
+  float sw, st;
+};
+__device__ inline H2Scales h2_scales(const AdamParams& a) {
+  H2Scales s{1.f, 1.f};
+  if (a.np != 2 || a.h2.wrec == nullptr) return s;
+  const float bw = a.h2.wrec->amax[0] + a.h2.w_add;
+  s.sw = exp2i(plane_exp(bw));
+  if (a.h2.trec) s.st = exp2i(plane_exp(fmaxf(a.h2.trec->amax[0], bw)));
+  return s;
+}
+
 template <bool POLYAK>
 __device__ inline float adam_elems(const AdamParams& a, const AdamConsts& k, long long norm_from4, long long blk,
-                                   long long nblk) {
+                                   long long nblk, float& pmx, float& tmx) {
   const long long n4 = a.n >> 2;
   float acc = 0.f;
+  const H2Scales hs = h2_scales(a);
   float4* p4 = reinterpret_cast<float4*>(a.p);
   float4* m4 = reinterpret_cast<float4*>(a.m);
   float4* v4 = reinterpret_cast<float4*>(a.v);
@@ -139,6 +154,7 @@ __device__ inline float adam_elems(const AdamParams& a, const AdamConsts& k, lon
       sq += pp[c] * pp[c];
     }
     if (i >= norm_from4) acc += sq;  // |p|^2 of the replicated (trunk) range only
+    pmx = fmaxf(pmx, fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fmaxf(fabsf(p.z), fabsf(p.w))));
     p4[i] = p;
     m4[i] = m;
     v4[i] = v;
@@ -150,6 +166,7 @@ __device__ inline float adam_elems(const AdamParams& a, const AdamConsts& k, lon
       t.z = a.tau * p.z + k.omtau * t.z;
       t.w = a.tau * p.w + k.omtau * t.w;
       t4[i] = t;
+      tmx = fmaxf(tmx, fmaxf(fmaxf(fabsf(t.x), fabsf(t.y)), fmaxf(fabsf(t.z), fabsf(t.w))));
     }
     for (int sg = 0; sg < a.nseg; ++sg) {  // split planes of the new values (next GEMMs' operands)
       const PlaneSeg& ps = a.seg[sg];
@@ -158,6 +175,20 @@ __device__ inline float adam_elems(const AdamParams& a, const AdamConsts& k, lon
       const long long e = f / ps.member_n, kk = f - e * ps.member_n;
       const float* src = ps.of_target ? &t.x : pp;
       typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      if (a.np == 2) {  // split2h planes
+        const float sc = ps.of_target ? hs.st : hs.sw;
+        f16x4 h2h, h2l;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          _Float16 x0, x1;
+          split2h_dev(src[c], sc, x0, x1);
+          h2h[c] = x0; h2l[c] = x1;
+        }
+        __bf16* dst = ps.planes + e * 3 * ps.ps + kk;
+        *reinterpret_cast<f16x4*>(dst) = h2h;
+        *reinterpret_cast<f16x4*>(dst + ps.ps) = h2l;
+        continue;
+      }
       bf16x4 h, mm, l;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -183,7 +214,8 @@ template <bool POLYAK>
 __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm, long long norm_from4) {
   const OptScalars sc = *a.sc;
   const AdamConsts k = adam_consts(a, sc.gnorm, sc.count, max_norm);
-  float acc = adam_elems<POLYAK>(a, k, norm_from4, blockIdx.x, gridDim.x);
+  float pmx = 0.f, tmx = 0.f;
+  float acc = adam_elems<POLYAK>(a, k, norm_from4, blockIdx.x, gridDim.x, pmx, tmx);
   acc = block_sum256(acc);
   if (threadIdx.x == 0) a.p_partials[blockIdx.x] = acc;
 }
@@ -196,8 +228,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // 64 x 64 tile pass over tiles blk, blk + nblk, ... of tp; returns this thread's |p_new|^2
 template <bool POLYAK>
 __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, const AdamConsts& k, int blk, int nblk,
-                                   float (*sp)[65], float (*stg)[65]) {
+                                   float (*sp)[65], float (*stg)[65], float& pmx, float& tmx) {
   float acc = 0.f;
+  const H2Scales hs = h2_scales(a);
   const int t = threadIdx.x, rr = t >> 4, c4 = 4 * (t & 15);
   for (int tile = blk; tile < tp.total; tile += nblk) {
     int L = 0;
@@ -233,6 +266,7 @@ __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, co
           const float u = mh / (sqrtf(vh) + a.eps);
           pp[q] = pp[q] + u * k.neg_lr;
           acc += pp[q] * pp[q];
+          pmx = fmaxf(pmx, fabsf(pp[q]));
         }
         reinterpret_cast<float4*>(a.p)[i4] = p;
         reinterpret_cast<float4*>(a.m)[i4] = m;
@@ -244,12 +278,26 @@ __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, co
           tv.z = a.tau * p.z + k.omtau * tv.z;
           tv.w = a.tau * p.w + k.omtau * tv.w;
           reinterpret_cast<float4*>(a.target)[i4] = tv;
+          tmx = fmaxf(tmx, fmaxf(fmaxf(fabsf(tv.x), fabsf(tv.y)), fmaxf(fabsf(tv.z), fabsf(tv.w))));
         }
 #pragma unroll
         for (int w = 0; w < 2; ++w) {
           __bf16* np_ = lf.nat[w];
           if (np_ == nullptr || (w == 1 && !POLYAK)) continue;
           const float* src = w ? &tv.x : &p.x;
+          if (a.np == 2) {  // split2h planes
+            f16x4 h2h, h2l;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              _Float16 x0, x1;
+              split2h_dev(src[q], w ? hs.st : hs.sw, x0, x1);
+              h2h[q] = x0; h2l[q] = x1;
+            }
+            __bf16* dst = np_ + e * 3 * lf.nat_ps + (long long)r * lf.nat_ld + c;
+            *reinterpret_cast<f16x4*>(dst) = h2h;
+            *reinterpret_cast<f16x4*>(dst + lf.nat_ps) = h2l;
+            continue;
+          }
           bf16x4_t h, mm, l;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -280,6 +328,24 @@ __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, co
         for (int w = 0; w < 2; ++w) {
           __bf16* tp_ = lf.tr[w];
           if (tp_ == nullptr || (w == 1 && !POLYAK)) continue;
+          __bf16* dst = tp_ + e * 3 * lf.tr_ps + (long long)o * lf.tr_ld + kk;
+          if (a.np == 2) {  // split2h planes
+            f16x8 h2h[2], h2l[2];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+              const float x = w ? stg[POLYAK ? kq + q : 0][oc] : sp[kq + q][oc];
+              _Float16 x0, x1;
+              split2h_dev(x, w ? hs.st : hs.sw, x0, x1);
+              h2h[q >> 3][q & 7] = x0; h2l[q >> 3][q & 7] = x1;
+            }
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+              if (kk + 8 * hh >= lf.tr_ld) break;
+              *reinterpret_cast<f16x8*>(dst + 8 * hh) = h2h[hh];
+              *reinterpret_cast<f16x8*>(dst + lf.tr_ps + 8 * hh) = h2l[hh];
+            }
+            continue;
+          }
           bf16x8 h[2], mm[2], l[2];
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
@@ -288,7 +354,6 @@ __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, co
             split3_dev(x, x0, x1, x2);
             h[q >> 3][q & 7] = x0; mm[q >> 3][q & 7] = x1; l[q >> 3][q & 7] = x2;
           }
-          __bf16* dst = tp_ + e * 3 * lf.tr_ps + (long long)o * lf.tr_ld + kk;
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
             if (kk + 8 * hh >= lf.tr_ld) break;
@@ -312,7 +377,8 @@ __global__ __launch_bounds__(256) void adam_tiles_kernel(AdamParams a, TileParam
   __shared__ float stg[POLYAK ? 64 : 1][65];
   const OptScalars sc = *a.sc;
   const AdamConsts k = adam_consts(a, sc.gnorm, sc.count, max_norm);
-  float acc = adam_tiles<POLYAK>(a, tp, k, blockIdx.x, gridDim.x, sp, stg);
+  float pmx = 0.f, tmx = 0.f;
+  float acc = adam_tiles<POLYAK>(a, tp, k, blockIdx.x, gridDim.x, sp, stg, pmx, tmx);
   acc = block_sum256(acc);
   if (threadIdx.x == 0) a.p_partials[blockIdx.x] = acc;
 }
@@ -348,20 +414,35 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(AdamParams ah, AdamPara
   __syncthreads();
   const float gn = gsh;
   const int count = ah.sc->count;  // incremented by the sum-of-squares launch
-  float pa = 0.f;
+  float pa = 0.f, pmx = 0.f, tmx = 0.f;
   const int b = blockIdx.x;
   if (b < f.bh) {
-    pa = adam_elems<POLYAK>(ah, adam_consts(ah, gn, count, f.max_norm), 0, b, f.bh);
+    pa = adam_elems<POLYAK>(ah, adam_consts(ah, gn, count, f.max_norm), 0, b, f.bh, pmx, tmx);
   } else if (b < f.bh + f.bt) {
-    pa = adam_elems<POLYAK>(at, adam_consts(at, gn, count, f.max_norm), 0, b - f.bh, f.bt);
+    pa = adam_elems<POLYAK>(at, adam_consts(at, gn, count, f.max_norm), 0, b - f.bh, f.bt, pmx, tmx);
   } else {
-    pa = adam_tiles<POLYAK>(at, tp, adam_consts(at, gn, count, f.max_norm), b - f.bh - f.bt, f.btile, sp, stg);
+    pa = adam_tiles<POLYAK>(at, tp, adam_consts(at, gn, count, f.max_norm), b - f.bh - f.bt, f.btile, sp, stg, pmx,
+                            tmx);
   }
   pa = block_sum256(pa);
   if (threadIdx.x == 0) {
     if (b < f.bh) f.ph[b] = pa;
     else f.pt[b - f.bh] = pa;
     if (b == 0) ah.sc->gnorm = gn;
+  }
+  if (at.np == 2 && at.h2.wrec) {  // split2h: the block's max |p_new| (|t_new|), reduced by step_finish
+    __shared__ float mscr[16];
+    pmx = block_max_val(pmx, mscr);
+    tmx = block_max_val(tmx, mscr);
+    if (threadIdx.x == 0) {
+      at.h2.wparts[b] = pmx;
+      if (at.h2.tparts) at.h2.tparts[b] = tmx;
+      if (b == 0) {  // the exponents the planes of this update carry (every block derived them alike)
+        const float bw = at.h2.wrec->amax[0] + at.h2.w_add;
+        at.h2.wrec->e = plane_exp(bw);
+        if (at.h2.trec) at.h2.trec->e = plane_exp(fmaxf(at.h2.trec->amax[0], bw));
+      }
+    }
   }
 }
 
@@ -557,9 +638,55 @@ __global__ __launch_bounds__(1024) void step_finish_kernel(StepFinish f) {
   __threadfence_block();  // lane 0's scalars above, before the log reads
   write_logs_wave(f.logs);
   if (lane == 0) *f.counter += 1ull;
+  // split2h: the optimizer's per-block weight maxima into the weight records (the next update's bound)
+  for (int j = 0; j < f.nwmax; ++j) {
+    const WeightMaxJob& w = f.wmax[j];
+    float mh = 0.f, mt = 0.f;
+    for (int i = lane; i < w.n; i += 64) {
+      if (i < w.nh) mh = fmaxf(mh, w.parts[i]);
+      else mt = fmaxf(mt, w.parts[i]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      mh = fmaxf(mh, __shfl_xor(mh, o));
+      mt = fmaxf(mt, __shfl_xor(mt, o));
+    }
+    if (lane == 0) {
+      if (w.nh < 0) {
+        w.rec->amax[0] = mt;  // a target: heads and trunk together (a looser, valid bound)
+      } else {
+        w.rec->amax[0] = mt;
+        w.rec->amax[1] = mh;
+      }
+    }
+  }
 }
 
 }  // namespace
+
+// split2h, weights set from outside (set_params): the record's maxima (trunk -> amax[0], heads ->
+// amax[1]) and the planes' exponent from the exact trunk maximum; one block (a rare call)
+__global__ __launch_bounds__(1024) void weights_record_kernel(const float* __restrict__ p, long long trunk_off,
+                                                             long long n_flat, PlaneRec* rec) {
+  __shared__ float mscr[16];
+  float mh = 0.f, mt = 0.f;
+  for (long long i = threadIdx.x; i < n_flat; i += 1024) {
+    const float v = fabsf(p[i]);
+    if (i < trunk_off) mh = fmaxf(mh, v);
+    else mt = fmaxf(mt, v);
+  }
+  mh = block_max_val(mh, mscr);
+  mt = block_max_val(mt, mscr);
+  if (threadIdx.x == 0) {
+    rec->amax[0] = mt;
+    rec->amax[1] = mh;
+    rec->e = plane_exp(mt);
+  }
+}
+
+void weights_record(const float* p, long long trunk_off, long long n_flat, PlaneRec* rec, hipStream_t st) {
+  hipLaunchKernelGGL(weights_record_kernel, dim3(1), dim3(1024), 0, st, p, trunk_off, n_flat, rec);
+}
 
 void reduce_rows(const float* const* ins, int n_in, int B, float* out, hipStream_t st) {
   RowPtrs r{};

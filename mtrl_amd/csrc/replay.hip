@@ -147,8 +147,20 @@ __global__ __launch_bounds__(256) void gather_kernel(GatherParams p, const float
   float* xcn = p.xc_next + (long long)b * p.ld_c;
   float* xcp = p.xc_pi + (long long)b * p.ld_c;
   const int oh0 = D - p.T_glob;  // first one-hot column
-  // the planes of the same entries: x = h + m + l (split3_dev)
-  auto put = [](__bf16* q, long long ps, long long o, float x) {
+  // split2h: one exponent for every input plane tensor of the step, from the stored rows' max
+  const bool h2 = p.in_rec != nullptr;
+  const int ein = h2 ? plane_exp(fmaxf(*p.in_max, 1.0f)) : 0;
+  const float sin = h2 ? exp2i(ein) : 1.f;
+  if (h2 && blockIdx.x == 0 && threadIdx.x == 0) p.in_rec->e = ein;
+  // the planes of the same entries: x = h + m + l (split3_dev), or split2h's two fp16 planes
+  auto put = [h2, sin](__bf16* q, long long ps, long long o, float x) {
+    if (h2) {
+      _Float16 h, l;
+      split2h_dev(x, sin, h, l);
+      reinterpret_cast<_Float16*>(q)[o] = h;
+      reinterpret_cast<_Float16*>(q)[o + ps] = l;
+      return;
+    }
     __bf16 h, m, l;
     split3_dev(x, h, m, l);
     q[o] = h;
@@ -222,10 +234,17 @@ void batch_scatter(const GatherParams& p, const float* obs, const float* act, co
 // ------------------------------------------------------------------ synthetic fill (bench)
 // SURVEY.md §8d recipe: obs[:D-T] ~ N(0,1), one-hot of the slot's task, actions U(-1,1),
 // rewards U(0,10), dones Bernoulli(1/500); one thread per record.
+__device__ inline void atomic_max_abs(float* m, float v) {  // v >= 0: the float order is the bits' order
+  atomicMax(reinterpret_cast<unsigned*>(m), __float_as_uint(v));
+}
+
 __global__ __launch_bounds__(256) void fill_kernel(float* __restrict__ store, long long nrec, int T_l, int R, int D,
-                                                   int A, int T_glob, int task_begin, unsigned long long seed) {
+                                                   int A, int T_glob, int task_begin, unsigned long long seed,
+                                                   float* bufmax) {
+  __shared__ float mscr[16];
   const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nrec) return;
+  float mx = 0.f;
+  if (r < nrec) {
   const int t = (int)(r % T_l);
   float* rec = store + r * R;
   const int F = D - T_glob;
@@ -248,13 +267,31 @@ __global__ __launch_bounds__(256) void fill_kernel(float* __restrict__ store, lo
   rec[D + A] = 10.0f * u[0];
   rec[D + A + 1] = (u[1] < (1.0f / 500.0f)) ? 1.0f : 0.0f;
   for (int c = 2 * D + A + 2; c < R; ++c) rec[c] = 0.0f;
+  for (int c = 0; c < D + A; ++c) mx = fmaxf(mx, fabsf(rec[c]));
+  for (int c = D + A + 2; c < 2 * D + A + 2; ++c) mx = fmaxf(mx, fabsf(rec[c]));
+  }
+  mx = block_max_val(mx, mscr);
+  if (threadIdx.x == 0 && bufmax) atomic_max_abs(bufmax, mx);
 }
 
 void fill_synthetic(float* store, long long cap, int T_l, int R, int obs_dim, int act_dim, int T_glob, int task_begin,
-                    unsigned long long seed, hipStream_t st) {
+                    unsigned long long seed, hipStream_t st, float* bufmax) {
   const long long nrec = cap * T_l;
   hipLaunchKernelGGL(fill_kernel, dim3((unsigned)((nrec + 255) / 256)), dim3(256), 0, st, store, nrec, T_l, R,
-                     obs_dim, act_dim, T_glob, task_begin, seed);
+                     obs_dim, act_dim, T_glob, task_begin, seed, bufmax);
+}
+
+// *m = max(*m, max |x[0..n)|)  (one block; the split2h input bound of a user batch)
+__global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x, long long n, float* m) {
+  __shared__ float mscr[16];
+  float v = 0.f;
+  for (long long i = threadIdx.x; i < n; i += 256) v = fmaxf(v, fabsf(x[i]));
+  v = block_max_val(v, mscr);
+  if (threadIdx.x == 0) *m = fmaxf(*m, v);
+}
+
+void absmax_into(const float* x, long long n, float* m, hipStream_t st) {
+  hipLaunchKernelGGL(absmax_kernel, dim3(1), dim3(256), 0, st, x, n, m);
 }
 
 // ------------------------------------------------------------------ per-task row lists
@@ -319,7 +356,7 @@ __global__ __launch_bounds__(256) void pack_slot_kernel(float* __restrict__ rec,
 // and the sampled range pos-or-capacity (buffers.py:523) -- device-side, so adds never block
 __global__ __launch_bounds__(64) void commit_slot_kernel(const float* __restrict__ rec, int T_l, int R, int rcol,
                                                          double* rmin, double* rmax, long long* buf_size,
-                                                         long long size) {
+                                                         long long size, int D, float* bufmax) {
   const int t = threadIdx.x;
   if (rmin != nullptr && t < T_l) {
     const double r = (double)rec[t * R + rcol];
@@ -327,6 +364,16 @@ __global__ __launch_bounds__(64) void commit_slot_kernel(const float* __restrict
     rmax[t] = fmax(rmax[t], r);
   }
   if (t == 0) *buf_size = size;
+  if (bufmax) {  // the stored rows' max |obs|, |action|, |next_obs| (split2h input planes' bound)
+    float m = 0.f;
+    for (int i = t; i < T_l * R; i += 64) {
+      const int c = i % R;
+      if (c < rcol || (c >= rcol + 2 && c < rcol + 2 + D)) m = fmaxf(m, fabsf(rec[i]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (t == 0) atomicMax(reinterpret_cast<unsigned*>(bufmax), __float_as_uint(m));
+  }
 }
 
 }  // namespace
@@ -339,8 +386,9 @@ void buffer_pack_slot(float* rec, int T_l, int R, int D, int A, const float* obs
 }
 
 void buffer_commit_slot(const float* rec, int T_l, int R, int rcol, double* rmin, double* rmax, long long* buf_size,
-                        long long size, hipStream_t st) {
-  hipLaunchKernelGGL(commit_slot_kernel, dim3(1), dim3(64), 0, st, rec, T_l, R, rcol, rmin, rmax, buf_size, size);
+                        long long size, hipStream_t st, int D, float* bufmax) {
+  hipLaunchKernelGGL(commit_slot_kernel, dim3(1), dim3(64), 0, st, rec, T_l, R, rcol, rmin, rmax, buf_size, size, D,
+                     bufmax);
 }
 
 }  // namespace mtsac

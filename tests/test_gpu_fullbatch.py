@@ -118,7 +118,7 @@ def _check_params(e, st1, tag, begin=0, count=None):
         assert d.max() < 2 * 3e-4 + 1e-6, (tag, which, d.max())
 
 
-@pytest.mark.parametrize("precision", [0, 1], ids=["fp32", "split3"])
+@pytest.mark.parametrize("precision", [0, 1, 3], ids=["fp32", "split3", "split2h"])
 @pytest.mark.parametrize("name", list(CASES))
 def test_full_batch_step_matches_oracle(name, precision):
     cfg, st, batch, en, ec, st1, want = _problem(name)
@@ -131,7 +131,7 @@ def test_full_batch_step_matches_oracle(name, precision):
     e.close()
 
 
-@pytest.mark.parametrize("precision", [0, 1], ids=["fp32", "split3"])
+@pytest.mark.parametrize("precision", [0, 1, 3], ids=["fp32", "split3", "split2h"])
 @pytest.mark.parametrize("name", ["s3_mt50_w2048", "s4_mt50_w400"])
 def test_full_batch_8way_shard_matches_oracle(precision, name):
     """The MT50 8-GPU task split (7,7,6,6,6,6,6,6 tasks, 128 rows each) as 8 engines on one
@@ -230,9 +230,10 @@ def _assert_same(a, b):
 
 
 @pytest.mark.parametrize("T,tc,W,prec,model", [(50, 50, 2048, 1, 0), (50, 7, 2048, 1, 1), (50, 7, 2048, 1, 0),
-                                               (10, 10, 400, 1, 0), (50, 6, 400, 1, 1), (10, 10, 2048, 2, 0)],
+                                               (10, 10, 400, 1, 0), (50, 6, 400, 1, 1), (10, 10, 2048, 2, 0),
+                                               (50, 50, 2048, 3, 0), (50, 7, 2048, 3, 1), (10, 10, 400, 3, 0)],
                          ids=["s3", "mt50_shard7_modelled", "mt50_shard7", "mt10_w400", "s4_shard6_modelled",
-                              "mt10_w2048_bf16"])
+                              "mt10_w2048_bf16", "s3_split2h", "mt50_shard7_modelled_split2h", "mt10_w400_split2h"])
 def test_pipelined_steps_equal_whole_steps(T, tc, W, prec, model):
     """Cross-step pipelining on one compute stream (engine.cpp step(), p2): step k+1's gather and
     critic(s, a) forward run on the prefetch stream beside step k's actor backward, all-reduce and
@@ -320,8 +321,9 @@ def test_full_batch_bf16_drift_bound(name):
     e.close()
 
 
-@pytest.mark.parametrize("T,tc,W,prec", [(50, 50, 2048, 1), (50, 7, 2048, 1), (10, 10, 400, 1), (10, 10, 2048, 2)],
-                         ids=["s3", "mt50_shard7", "mt10_w400", "mt10_w2048_bf16"])
+@pytest.mark.parametrize("T,tc,W,prec", [(50, 50, 2048, 1), (50, 7, 2048, 1), (10, 10, 400, 1), (10, 10, 2048, 2),
+                                         (50, 50, 2048, 3), (10, 10, 400, 3)],
+                         ids=["s3", "mt50_shard7", "mt10_w400", "mt10_w2048_bf16", "s3_split2h", "mt10_w400_split2h"])
 def test_update_many_equals_single_steps(T, tc, W, prec):
     """The default issue (every compute segment on one stream, engine.cpp one_stream): 4 device-
     sampled steps in one update_many call give bitwise the logs, parameters, optimizer moments and

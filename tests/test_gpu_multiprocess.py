@@ -58,7 +58,7 @@ def _spawn(args, world, timeout):
     return rcs
 
 
-@pytest.mark.parametrize("precision", [1], ids=["split3"])
+@pytest.mark.parametrize("precision", [1, 3], ids=["split3", "split2h"])
 def test_two_rank_processes_match_oracle(tmp_path, precision):
     from mtrl_amd import _lib as L
     from mtrl_amd.init import slice_heads

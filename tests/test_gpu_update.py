@@ -71,7 +71,7 @@ CONFIGS = {
 }
 
 
-@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("precision", [0, 1, 3], ids=["fp32", "split3", "split2h"])
 @pytest.mark.parametrize("name", list(CONFIGS))
 def test_update_matches_oracle(name, precision):
     from mtrl_amd import _lib as L
@@ -117,7 +117,7 @@ def test_update_matches_oracle(name, precision):
     eng.close()
 
 
-@pytest.mark.parametrize("precision", [0, 1], ids=["fp32", "split3"])
+@pytest.mark.parametrize("precision", [0, 1, 3], ids=["fp32", "split3", "split2h"])
 def test_graph_replay_is_deterministic_and_matches_eager(precision):
     from mtrl_amd import _lib as L
 
@@ -196,7 +196,7 @@ def test_rollout_actions_match_oracle():
     eng.close()
 
 
-@pytest.mark.parametrize("precision", [0, 1], ids=["fp32", "split3"])
+@pytest.mark.parametrize("precision", [0, 1, 3], ids=["fp32", "split3", "split2h"])
 @pytest.mark.parametrize("graph", [True, False], ids=["graph", "eager"])
 def test_rccl_single_rank_graph_path(graph, precision):
     """The RCCL all-reduce points (per-layer buckets on their own stream, then layer 0 and the
