@@ -305,14 +305,17 @@ def main():
     ap.add_argument("--workload", default="mt50_w2048", choices=sorted(WORKLOADS) + [DRQ_WORKLOAD])
     ap.add_argument("--drq-capacity", type=int, default=2000, help="atari_drq: device buffer slots per task")
     ap.add_argument("--no-graph", action="store_true", help="same as --exec eager")
-    ap.add_argument("--exec", default="auto", choices=["auto", "graph", "eager"],
-                    help="hipGraph replay or eager multi-stream DAG; auto = faster of the two")
+    ap.add_argument("--exec", default="auto", choices=["auto", "graph", "eager", "pipelined"],
+                    help="hipGraph replay, eager steps, or eager steps with cross-step pipelining (the next "
+                         "step's gather + critic forward beside the previous step's tail); auto = the fastest "
+                         "(task shards: pipelined)")
     ap.add_argument("--precision", default="split3", choices=sorted(PRECISIONS),
                     help="fp32: f32-input MFMA; split3: fp32-accurate 3-way bf16 split on bf16 MFMA; "
                          "split2h: fp32-accurate 2-way fp16 split (per-tensor power-of-two scale) on fp16 MFMA; "
                          "bf16: perf-only, trunk GEMM operands rounded to bf16 (one MFMA per product)")
-    ap.add_argument("--settle-s", type=float, default=2.0,
-                    help="untimed steady-state seconds after the warm-up (DVFS settles under load)")
+    ap.add_argument("--settle-s", type=float, default=6.0,
+                    help="untimed steady-state seconds after the warm-up (DVFS settles under load; long enough "
+                         "for a once-per-second utilisation sampler to see the GPU busy)")
     ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--cpu-c0-steps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -401,17 +404,23 @@ def main():
 
     mode = "eager" if args.no_graph else args.exec
     if mode == "auto" and world > 1:
-        # task shards run faster eager (profiles/r2c_shard_steps.txt: 25 / 13 / 7 tasks 4.83 / 3.21 /
-        # 2.38 ms eager vs 4.88 / 3.38 / 2.60 graph), where the per-layer all-reduce buckets on the
-        # collective stream overlap the rest of the backward; no RCCL collective is captured in a graph
-        mode = "eager"
-    eng.enable_graph(mode != "eager")
+        # task shards run eager (profiles/r2c_shard_steps.txt: 25 / 13 / 7 tasks 4.83 / 3.21 / 2.38 ms
+        # eager vs 4.88 / 3.38 / 2.60 graph), where the per-layer all-reduce buckets on the collective
+        # stream overlap the rest of the backward, and pipelined: the actor's all-reduce and Adam overlap
+        # the next step's gather and critic forward; no RCCL collective is captured in a graph
+        mode = "pipelined"
+
+    def set_mode(m):
+        eng.enable_graph(m == "graph")
+        eng.lib.mtsac_debug_set_pipeline(eng._h, 1 if m == "pipelined" else 0)
+
+    set_mode(mode if mode != "auto" else "eager")
     eng.update_many(args.warmup)
     eng.synchronize()
-    if mode == "auto":  # pick the faster execution mode on rank 0, same choice everywhere
+    if mode == "auto":  # pick the fastest execution mode on rank 0, same choice everywhere
         trial = {}
-        for m in ("graph", "eager"):
-            eng.enable_graph(m == "graph")
+        for m in ("graph", "eager", "pipelined"):
+            set_mode(m)
             eng.update_many(1)
             eng.synchronize()
             if dist:
@@ -424,7 +433,7 @@ def main():
         if dist:
             dist.broadcast_object_list(choice, src=0)
         mode = choice[0]
-        eng.enable_graph(mode == "graph")
+        set_mode(mode)
         eng.update_many(1)
         eng.synchronize()
     # steady state: run untimed for --settle-s seconds (the same count on every rank)
@@ -445,7 +454,7 @@ def main():
     # kernel timing comes from HIP events around every GEMM launch on the stream it runs on, over a
     # second pass of the same number of steps right after; a graph replay cannot carry events, so
     # then it comes from one extra serialised step.
-    live = mode == "eager"
+    live = mode != "graph"
     eng.set_timing(False)
     if dist:
         dist.barrier()

@@ -246,6 +246,19 @@ struct mtsac_engine {
   }
   RecRef* dz_rec(__bf16** dzp) { return dzp == dzap ? r_dz[0] : dzp == dzcp ? r_dz[1] : nullptr; }
   RecRef& w_rec(const Net& net, int which) { return r_w[&net == &critic ? 1 : 0][which]; }
+  // |one Adam step| / lr: by Cauchy-Schwarz |m_t| <= (1 - b1) / sqrt((1 - b2)(1 - b1^2 / b2)) sqrt(v_t) for
+  // any gradient sequence, times the bias corrections' ratio sqrt(1 - b2^t) / (1 - b1^t) at its worst
+  // step t (<= 1 at b1 = 0.9, b2 = 0.999: 7.27 in all); 25 % margin.  Computed once at create.
+  float adam_bound = 0.f;
+  float adam_step_bound() const { return adam_bound; }
+  static float adam_step_bound_of(double b1, double b2) {
+    double r = 1.0;
+    for (int t = 1; t <= 200000; t = t < 1000 ? t + 1 : t + t / 100) {
+      const double f = std::sqrt(1.0 - std::pow(b2, t)) / (1.0 - std::pow(b1, t));
+      r = std::max(r, f);
+    }
+    return (float)(1.25 * r * (1.0 - b1) / std::sqrt((1.0 - b2) * (1.0 - b1 * b1 / b2)));
+  }
   // the bound inputs of a split2h plane GEMM: A, B (weights: their planes' range), output C
   void h2_gemm(SplitGemmParams& g, RecRef* a, RecRef* b, RecRef* c, float kmul, bool bias_in_b) {
     if (!h2) return;
@@ -560,7 +573,7 @@ struct mtsac_engine {
         po.rd = d.d;
         po.nd = d.n;
         po.rw = w_rec(net, 0).d;
-        po.w_add = 16.0f * (&net == &critic ? cfg.critic_lr : cfg.actor_lr);
+        po.w_add = adam_step_bound() * (&net == &critic ? cfg.critic_lr : cfg.actor_lr);
         po.kmul = (float)net.hd;
       }
     }
@@ -966,7 +979,7 @@ struct mtsac_engine {
       const int w = &net == &critic ? 1 : 0;
       a.h2.wrec = w_rec(net, 0).d;
       a.h2.trec = polyak ? w_rec(net, 1).d : nullptr;
-      a.h2.w_add = 16.0f * lr;  // one Adam step: |m_hat| / (sqrt(v_hat) + eps) < 7.3 for b1^2 < b2
+      a.h2.w_add = adam_step_bound() * lr;
       a.h2.wparts = wparts[w];
       a.h2.tparts = polyak ? tparts : nullptr;
     }
@@ -1817,6 +1830,10 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   if (c.precision != MTSAC_FP32 && c.precision != MTSAC_FP32_SPLIT3 && c.precision != MTSAC_BF16 &&
       c.precision != MTSAC_FP32_SPLIT2H)
     return fail(-22, "unsupported precision");
+  if (c.precision == MTSAC_FP32_SPLIT2H && (long long)c.batch_per_task * c.task_count > 8192)
+    return fail(-22, "split2h: at most 8192 rows per engine (one partial maximum per wave of the action grad)");
+  if (c.precision == MTSAC_FP32_SPLIT2H && !(c.adam_b1 * c.adam_b1 < c.adam_b2))
+    return fail(-22, "split2h bounds an Adam step (|m_hat| / sqrt(v_hat)), which needs adam_b1^2 < adam_b2");
   hipError_t he = hipSetDevice(hip_device);
   if (he != hipSuccess) return fail(-19, std::string("hipSetDevice: ") + hipGetErrorString(he));
 
@@ -1869,6 +1886,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   e->planes = c.precision == MTSAC_FP32_SPLIT3 || c.precision == MTSAC_BF16 || c.precision == MTSAC_FP32_SPLIT2H;
   e->np = c.precision == MTSAC_BF16 ? 1 : c.precision == MTSAC_FP32_SPLIT2H ? 2 : 3;
   e->h2 = c.precision == MTSAC_FP32_SPLIT2H;
+  if (e->h2) e->adam_bound = mtsac_engine::adam_step_bound_of(c.adam_b1, c.adam_b2);
   if (e->h2) {  // the plane records, the stored rows' bound, the optimizer's maxima
     const int nrec = 2 + 4 + 3 * MAXD + 2 * MAXD + 2;
     if ((rc = e->alloc(&e->recs, (size_t)nrec))) return bad(rc);

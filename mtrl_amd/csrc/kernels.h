@@ -394,8 +394,8 @@ struct PlaneSeg {
   int of_target;        // 1: planes of the Polyak target's new value instead of the params'
 };
 // split2h (np == 2) weights: the optimizer writes fp16 planes of p * 2^e with e from the bound
-// max|p_old| + w_add (w_add = 16 lr covers one Adam step: |m_hat| / (sqrt(v_hat) + eps) < 7.3 for
-// b1^2 < b2), the target's at max(max|t_old|, that), stores both exponents in the records and
+// max|p_old| + w_add (w_add covers one Adam step, engine.cpp adam_step_bound: |m_hat| / sqrt(v_hat)
+// <= 7.27 at b1 = 0.9, b2 = 0.999), the target's at max(max|t_old|, that), stores both exponents in the records and
 // leaves per-block max |p_new| / |t_new| partials for step_finish to reduce into the records
 struct WeightH2 {
   PlaneRec* wrec;       // params: e, amax[0] trunk max, amax[1] head max

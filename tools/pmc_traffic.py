@@ -20,6 +20,15 @@ FAMILY_KEYS = {
         3: ("gemm_x3f_kernel<208, 1, false, true, false, 8,",),
         4: ("gemm_x3_kernel<true, false, 0>",),
     },
+    # split2h: the same kernel templates with NP = 2 (the prefixes above match both)
+    "split2h": {
+        0: ("gemm_x3f_kernel<208, 1, false, true, false, 0,", "gemm_x3f_kernel<208, 1, true, false, false, 0,",
+            "gemm_x3f_kernel<208, 1, true, true, false, 0,"),
+        1: ("gemm_x3f_kernel<208, 2,",),
+        2: ("gemm_x3p_kernel<mtsac::x3pk::Geo<256, 256, 2, 4, 3, 16, 0>, true, true, 0,",),
+        3: ("gemm_x3f_kernel<208, 1, false, true, false, 8,",),
+        4: ("gemm_x3_kernel<true, false, 0>",),
+    },
     "fp32": {
         0: ("gemm_f32_kernel<false, true, 1>",),
         1: ("gemm_f32_kernel<false, true, 2>",),
