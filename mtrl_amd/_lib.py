@@ -152,6 +152,7 @@ SIGNATURES = {
     "mtsac_debug_gemm_fwd_bench": (ctypes.c_int, [ctypes.c_int] * 7 + [PD]),
     "mtsac_debug_x3s_ti": (ctypes.c_int, [ctypes.c_int] * 3),
     "mtsac_debug_drq_groups": (ctypes.c_int, [ctypes.c_int] * 2),
+    "mtsac_debug_drq_mfma": (ctypes.c_int, [ctypes.c_int]),
     "mtsac_debug_set_pipeline": (ctypes.c_int, [P, I32]),
     "mtsac_debug_lane_mode": (ctypes.c_int, [P]),
     "mtsac_debug_force_one_stream": (ctypes.c_int, [P, ctypes.c_int32]),

@@ -437,4 +437,12 @@ int mtsac_debug_drq_groups(int fwd, int bwd) {
   return old;
 }
 
+// DrQ convs on f32 MFMA (bit 1 forward, 2 data grad, 4 weight grad) or the VALU kernels; returns the
+// previous mask (< 0: query only)
+int mtsac_debug_drq_mfma(int mask) {
+  const int old = drq::g_drq_mfma;
+  if (mask >= 0) drq::g_drq_mfma = mask & 7;
+  return old;
+}
+
 }  // extern "C"

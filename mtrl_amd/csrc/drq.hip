@@ -11,6 +11,7 @@
 // runs on gemm_f32 (exact fp32).  Weight gradients reduce over batch x pixels into per-block
 // partials summed in a fixed order (bitwise reproducible).
 #include <algorithm>
+#include <cstdlib>
 
 #include "drq_kernels.h"
 
@@ -411,6 +412,182 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
     for (int g = 1; g < BG; ++g) v += bred[g * CO + t];
     pp[NW + t] = v;
   }
+}
+
+// ------------------------------------------------------------------ convolutions on f32 MFMA
+// v_mfma_f32_16x16x4_f32 (exact fp32: bit for bit a k-ordered fmaf chain, MI355X_MICROARCH.md) at the
+// FP32 rate, which the VALU kernels above reach only with packed FMAs fed from SGPRs; here the VALU
+// only computes addresses and the operands come straight from L1/L2 one fp32 per lane.
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+// Weight gradient as 9 / TPM small GEMMs over pixels: dW[tap][ci][co] = sum_p act(in)[p + off(tap)][ci]
+// * dout[p][co].  M-tile m stacks TPM = 16 / CI taps (rows r: tap m TPM + r / CI, channel r % CI), N = CO
+// (columns >= CO zero), K = pixels, 4 per MFMA (lane slot l >> 4).  A lane's A operand is one input
+// channel of one shifted pixel (16 lanes read 16 consecutive floats), its B operand dout[p][l & 15],
+// shared by every M-tile.  Wave w of a block takes pixels c0 + 16 j + 4 w + slot of the block's chunk;
+// the four waves' tiles are added in wave order in LDS.  part[g][9 CI CO + CO] as conv_wgrad_kernel.
+template <int CI, int CO, bool RELU_IN>
+__global__ __launch_bounds__(256) void conv_wgrad_mfma_kernel(const float* __restrict__ in, const float* __restrict__ dout,
+                                                              float* __restrict__ part, int B, int H, int W, int chunk) {
+  constexpr int TPM = 16 / CI, MT = (9 + TPM - 1) / TPM;
+  constexpr int NW = 9 * CI * CO;
+  static_assert(CI == 4 || CI == 8 || CI == 16, "CI");
+  static_assert(CO == 8 || CO == 16, "CO");
+  __shared__ float red[4][MT * 256];
+  __shared__ float bred[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int row = lane & 15, slot = lane >> 4;
+  const int ci = row % CI, tsub = row / CI;
+  const int npix = B * H * W;
+  const int c0 = blockIdx.x * chunk, c1 = min(npix, c0 + chunk);
+  // this lane's tap offsets per M-tile (in pixels) and whether the tap exists
+  int dys[MT], dxs[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int tap = m * TPM + tsub;
+    dys[m] = tap < 9 ? tap / 3 - 1 : 99;
+    dxs[m] = tap < 9 ? tap % 3 - 1 : 0;
+  }
+  f32x4_t acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  int p = c0 + 4 * wv + slot;
+  int x = p % W, y = (p / W) % H;
+  for (; p - slot - 4 * wv < c1; p += 16) {
+    const bool vp = p < c1;
+    const float g = (vp && row < CO) ? dout[(long long)p * CO + row] : 0.f;
+    bsum += g;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int yy = y + dys[m], xx = x + dxs[m];
+      float a = 0.f;
+      if (vp && yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        a = in[(long long)(p + dys[m] * W + dxs[m]) * CI + ci];
+        if (RELU_IN) a = fmaxf(a, 0.f);
+      }
+      acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, g, acc[m], 0, 0, 0);
+    }
+    x += 16;  // next pixel of this lane: 16 on (W >= 4: at most 4 wraps)
+    while (x >= W) {
+      x -= W;
+      if (++y == H) y = 0;
+    }
+  }
+  // C layout: register r of lane l = row 4 (l >> 4) + r of the tile, column l & 15
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wv][m * 256 + (4 * slot + r) * 16 + row] = acc[m][r];
+  bred[wv][lane] = bsum;
+  __syncthreads();
+  float* pp = part + (long long)blockIdx.x * (NW + CO);
+  for (int e = threadIdx.x; e < MT * 256; e += 256) {
+    const int m = e >> 8, rr = (e >> 4) & 15, cc = e & 15;
+    const int tap = m * TPM + rr / CI;
+    if (tap >= 9 || cc >= CO) continue;
+    const float v = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+    pp[(tap * CI + rr % CI) * CO + cc] = v;
+  }
+  if (threadIdx.x < CO) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) v += bred[w][16 * s + threadIdx.x];
+    pp[NW + threadIdx.x] = v;
+  }
+}
+
+// Forward (FWD) and data gradient (!FWD) as pixel-tile GEMMs: out[p][n] = sum_{tap, c} X[p + off][c] *
+// Wk[tap][c][n], K = 9 KC, N = NC.  FWD: X = act(in), KC = CI, NC = CO, off = +tap, Wk = w, C starts at
+// the bias, + res.  !FWD: X = dout, KC = CO, NC = CI, off = -tap, Wk[tap][c][n] = w[tap][n][c], C starts
+// at 0, * [mask > 0] + dres.  A lane loads float4s: lane group g = l >> 4 takes tap TPG-group member
+// g / (KC / 4) and channels 4 (g % (KC / 4)) .. + 3, element j of them feeding k-step j (TPG = 16 / KC taps
+// per load round).  The B fragments (one weight per k-step) stay in VGPRs; each wave runs TW 16-pixel
+// tiles side by side (independent accumulators) over the block's 64 TW consecutive pixels.  Images
+// [0, B1) use (w_a, bias_a), [B1, B) (w_b, bias_b): separate blocks, as conv_fwd_kernel.
+template <int KC, int NC, bool FWD, bool RELU_IN, bool ADD_RES, int TW>
+__global__ __launch_bounds__(256) void conv_mfma_kernel(const float* __restrict__ X, const float* __restrict__ w_a,
+                                                        const float* __restrict__ bias_a, const float* __restrict__ w_b,
+                                                        const float* __restrict__ bias_b, const float* __restrict__ mask,
+                                                        const float* __restrict__ res, float* __restrict__ out, int B,
+                                                        int B1, int H, int W) {
+  constexpr int CG4 = KC / 4, TPG = 4 / CG4, ROUNDS = (9 + TPG - 1) / TPG, NK = ROUNDS * 4;
+  constexpr int PB = 4 * 16 * TW;  // pixels per block
+  static_assert(KC == 4 || KC == 8 || KC == 16, "KC");
+  static_assert(NC == 4 || NC == 8 || NC == 16, "NC");
+  const int n1 = B1 * H * W, nb1 = (n1 + PB - 1) / PB;
+  const bool second = (int)blockIdx.x >= nb1;
+  const int base = second ? n1 + ((int)blockIdx.x - nb1) * PB : (int)blockIdx.x * PB;
+  const int end = second ? B * H * W : n1;
+  const float* __restrict__ w = second ? w_b : w_a;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int tg = g / CG4, c4 = 4 * (g % CG4);
+  float bw[NK];
+#pragma unroll
+  for (int r = 0; r < ROUNDS; ++r) {
+    const int tap = r * TPG + tg;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = 0.f;
+      if (tap < 9 && col < NC) {
+        const int c = c4 + j;
+        v = FWD ? w[(tap * KC + c) * NC + col] : w[(tap * NC + col) * KC + c];
+      }
+      bw[r * 4 + j] = v;
+    }
+  }
+  const float b0 = (FWD && col < NC) ? (second ? bias_b : bias_a)[col] : 0.f;
+  f32x4_t acc[TW];
+  int px[TW], xs[TW], ys[TW];
+  const int p0 = base + wv * 16 * TW;
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    acc[t] = f32x4_t{b0, b0, b0, b0};
+    px[t] = p0 + 16 * t + col;
+    xs[t] = px[t] % W;
+    ys[t] = (px[t] / W) % H;
+  }
+#pragma unroll
+  for (int r = 0; r < ROUNDS; ++r) {
+    const int tap = r * TPG + tg;
+    const int dy = FWD ? tap / 3 - 1 : 1 - tap / 3, dx = FWD ? tap % 3 - 1 : 1 - tap % 3;
+    float4 a[TW];
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int yy = ys[t] + dy, xx = xs[t] + dx;
+      a[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (tap < 9 && px[t] < end && yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        a[t] = *reinterpret_cast<const float4*>(X + (long long)(px[t] + dy * W + dx) * KC + c4);
+        if (RELU_IN) {
+          a[t].x = fmaxf(a[t].x, 0.f); a[t].y = fmaxf(a[t].y, 0.f);
+          a[t].z = fmaxf(a[t].z, 0.f); a[t].w = fmaxf(a[t].w, 0.f);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t].x, bw[r * 4 + 0], acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t].y, bw[r * 4 + 1], acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t].z, bw[r * 4 + 2], acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t].w, bw[r * 4 + 3], acc[t], 0, 0, 0);
+    }
+  }
+  if (col >= NC) return;
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int p = p0 + 16 * t + 4 * g + r;
+      if (p >= end) continue;
+      const long long o = (long long)p * NC + col;
+      float v = acc[t][r];
+      if (!FWD && mask != nullptr) v = mask[o] > 0.f ? v : 0.f;
+      if (ADD_RES) v += res[o];
+      out[o] = v;
+    }
 }
 
 // dw[e] / db[e - nw] = sum_g part[g][e] (e < n): block of 16 entries x 16 lane groups over g
@@ -1059,6 +1236,13 @@ static int conv_bwd_group(int ci) {
   return ci == 16 ? 4 : ci;
 }
 
+// f32-MFMA convolutions (bit 1 forward, 2 data grad, 4 weight grad); the VALU kernels otherwise
+int g_drq_mfma = [] {
+  const char* e = getenv("MTSAC_DRQ_MFMA");  // experiments: the VALU kernels per pass
+  return e ? (atoi(e) & 7) : 7;
+}();
+constexpr int MFMA_TW = 4;  // 16-pixel tiles per wave of conv_mfma_kernel
+
 void conv_fwd(const float* in, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
               int ci, int co, bool relu_in, hipStream_t st, const float* w2, const float* bias2, int B1) {
   const long long npix = (long long)B * H * W;
@@ -1067,6 +1251,21 @@ void conv_fwd(const float* in, const float* w, const float* bias, const float* r
     w2 = w;
     bias2 = bias;
     B1 = B;
+  }
+  if (g_drq_mfma & 1) {
+    constexpr int PB = 64 * MFMA_TW;
+    const long long n1 = (long long)B1 * H * W;
+    const dim3 gm((unsigned)((n1 + PB - 1) / PB + (npix - n1 + PB - 1) / PB)), tm(256);
+#define C_FWDM(a, b)                                                                                                 \
+  if (ci == a && co == b) {                                                                                          \
+    if (relu_in && res) hipLaunchKernelGGL((conv_mfma_kernel<a, b, true, true, true, MFMA_TW>), gm, tm, 0, st, in, w, bias, w2, bias2, nullptr, res, out, B, B1, H, W); \
+    else if (relu_in) hipLaunchKernelGGL((conv_mfma_kernel<a, b, true, true, false, MFMA_TW>), gm, tm, 0, st, in, w, bias, w2, bias2, nullptr, res, out, B, B1, H, W); \
+    else if (res) hipLaunchKernelGGL((conv_mfma_kernel<a, b, true, false, true, MFMA_TW>), gm, tm, 0, st, in, w, bias, w2, bias2, nullptr, res, out, B, B1, H, W); \
+    else hipLaunchKernelGGL((conv_mfma_kernel<a, b, true, false, false, MFMA_TW>), gm, tm, 0, st, in, w, bias, w2, bias2, nullptr, res, out, B, B1, H, W); \
+    return;                                                                                                          \
+  }
+    CONV_CASES(C_FWDM)
+#undef C_FWDM
   }
   const long long n1 = (long long)B1 * H * W;
   const dim3 g(blocks(n1) + blocks(npix - n1), co / G), t(256);
@@ -1090,6 +1289,18 @@ void conv_fwd(const float* in, const float* w, const float* bias, const float* r
 void conv_bwd_data(const float* dout, const float* w, const float* mask, const float* dres, float* din, int B, int H,
                    int W, int ci, int co, hipStream_t st) {
   const long long npix = (long long)B * H * W;
+  if (g_drq_mfma & 2) {  // K channels = co, N = ci
+    constexpr int PB = 64 * MFMA_TW;
+    const dim3 gm((unsigned)((npix + PB - 1) / PB)), tm(256);
+#define C_BDM(a, b)                                                                                                  \
+  if (ci == a && co == b) {                                                                                          \
+    if (dres) hipLaunchKernelGGL((conv_mfma_kernel<b, a, false, false, true, MFMA_TW>), gm, tm, 0, st, dout, w, nullptr, w, nullptr, mask, dres, din, B, B, H, W); \
+    else hipLaunchKernelGGL((conv_mfma_kernel<b, a, false, false, false, MFMA_TW>), gm, tm, 0, st, dout, w, nullptr, w, nullptr, mask, dres, din, B, B, H, W); \
+    return;                                                                                                          \
+  }
+    CONV_CASES(C_BDM)
+#undef C_BDM
+  }
   const int G = conv_bwd_group(ci);
   const dim3 g(blocks(npix), ci / G), t(256);
 #define C_BD_G(a, b, cg)                                                                                            \
@@ -1111,14 +1322,21 @@ void conv_bwd_data(const float* dout, const float* w, const float* mask, const f
 
 // enough 64-pixel tiles in flight per CU to cover the staging loads' latency (the partials'
 // reduction is cheap next to them)
-int conv_wgrad_blocks(long long npix) { return (int)std::min<long long>(2048, std::max<long long>(1, (npix + 63) / 64)); }
+// (the MFMA kernel: chunks of >= 128 pixels, 16-pixel aligned; round 3's 2048 blocks of 64-pixel
+// tiles wrote 19 MB of partials for an 84 x 84 conv)
+int conv_wgrad_blocks(long long npix) { return (int)std::min<long long>(1024, std::max<long long>(1, npix / 128)); }
 
 void conv_wgrad(const float* in, const float* dout, float* part, float* dw, float* db, int B, int H, int W, int ci,
                 int co, bool relu_in, hipStream_t st, bool defer_sum) {
-  const int G = conv_wgrad_blocks((long long)B * H * W);
+  const long long npix = (long long)B * H * W;
+  const int G = conv_wgrad_blocks(npix);
+  const int chunk = (int)(((npix + G - 1) / G + 15) / 16 * 16);
 #define C_WG(a, b)                                                                                             \
   if (ci == a && co == b) {                                                                                    \
-    if (relu_in) hipLaunchKernelGGL((conv_wgrad_kernel<a, b, true>), dim3(G), dim3(256), 0, st, in, dout, part, B, H, W); \
+    if (g_drq_mfma & 4) {                                                                                      \
+      if (relu_in) hipLaunchKernelGGL((conv_wgrad_mfma_kernel<a, b, true>), dim3(G), dim3(256), 0, st, in, dout, part, B, H, W, chunk); \
+      else hipLaunchKernelGGL((conv_wgrad_mfma_kernel<a, b, false>), dim3(G), dim3(256), 0, st, in, dout, part, B, H, W, chunk);      \
+    } else if (relu_in) hipLaunchKernelGGL((conv_wgrad_kernel<a, b, true>), dim3(G), dim3(256), 0, st, in, dout, part, B, H, W); \
     else hipLaunchKernelGGL((conv_wgrad_kernel<a, b, false>), dim3(G), dim3(256), 0, st, in, dout, part, B, H, W);        \
   }
   CONV_CASES(C_WG)

@@ -67,18 +67,25 @@ CONV_FLOOR_TOL = 3e-4
 CONV_VS_FP32_REF = 4.0
 
 
+@pytest.mark.parametrize("mfma", [7, 0], ids=["mfma", "valu"])
 @pytest.mark.parametrize("hw,hidden,B", [(20, 64, 8), (84, 512, 16), (84, 512, 256)],
                          ids=["small", "reference_geometry", "reference_geometry_b256"])
-def test_update_matches_oracle(hw, hidden, B):
+def test_update_matches_oracle(hw, hidden, B, mfma):
     """b256 is the benched configuration (bench.py --workload atari_drq): the single 3B-image
     encoder pass, the split-K dense layers at M = 256..768 and the segment-table partial sums of
-    all 15 convs run at the bench's own sizes."""
+    all 15 convs run at the bench's own sizes.  mfma: the convolutions on f32 MFMA (the default) or
+    on the VALU kernels (mtsac_debug_drq_mfma(0))."""
     import torch
 
     from mtrl_amd import _lib as L
 
-    cfg = od.DrQConfig(hw=hw, n_hidden=hidden)
-    e, st, new, got, want, internals = _run_both(cfg, B, seed=hw + B)
+    lib = L.load()
+    old = lib.mtsac_debug_drq_mfma(mfma)
+    try:
+        cfg = od.DrQConfig(hw=hw, n_hidden=hidden)
+        e, st, new, got, want, internals = _run_both(cfg, B, seed=hw + B)
+    finally:
+        lib.mtsac_debug_drq_mfma(old)
     for k, v in want.items():
         assert abs(got[k] - v) <= 1e-5 * max(1.0, abs(v)), (k, got[k], v)
     g_gpu = e.get_params(L.DRQ_GRAD).astype(np.float64)
