@@ -65,8 +65,8 @@ int mtsac_debug_x3s_ti(int M, int N, int batch);
 // DrQ conv channel groups per lane (fwd: output channels, bwd: input channels; 0 = the engine's
 // choice); returns the previous fwd | bwd << 8.  Experiments only.
 int mtsac_debug_drq_groups(int fwd, int bwd);
-// DrQ convolutions on f32 MFMA: bit 1 forward, 2 data grad, 4 weight grad (default 7); 0 = the VALU
-// kernels.  Returns the previous mask; mask < 0 only queries.
+// DrQ convolutions on f32 MFMA (experiment, measured slower than the VALU kernels): bit 1 forward,
+// 2 data grad, 4 weight grad (default 0 = the VALU kernels).  Returns the previous mask; < 0 queries.
 int mtsac_debug_drq_mfma(int mask);
 
 /* Eager update_many overlaps consecutive steps (the next gather and critic(s, a) forward beside

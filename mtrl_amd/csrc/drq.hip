@@ -424,23 +424,26 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 // * dout[p][co].  M-tile m stacks TPM = 16 / CI taps (rows r: tap m TPM + r / CI, channel r % CI), N = CO
 // (columns >= CO zero), K = pixels, 4 per MFMA (lane slot l >> 4).  A lane's A operand is one input
 // channel of one shifted pixel (16 lanes read 16 consecutive floats), its B operand dout[p][l & 15],
-// shared by every M-tile.  Wave w of a block takes pixels c0 + 16 j + 4 w + slot of the block's chunk;
-// the four waves' tiles are added in wave order in LDS.  part[g][9 CI CO + CO] as conv_wgrad_kernel.
+// shared by every M-tile.  Every load is unconditional (a clamped in-range address, the value selected
+// afterwards): a load under a branch was waited for at the branch's end, one latency per operand.
+// Wave w of a block takes pixels c0 + 16 j + 4 w + slot of the block's chunk; each fp32 MFMA chain runs
+// FLUSH k-steps and is then added into double accumulators (the bias sum is double throughout); the four
+// waves' sums are added in wave order in LDS.  part[g][9 CI CO + CO] as conv_wgrad_kernel.
 template <int CI, int CO, bool RELU_IN>
 __global__ __launch_bounds__(256) void conv_wgrad_mfma_kernel(const float* __restrict__ in, const float* __restrict__ dout,
                                                               float* __restrict__ part, int B, int H, int W, int chunk) {
   constexpr int TPM = 16 / CI, MT = (9 + TPM - 1) / TPM;
   constexpr int NW = 9 * CI * CO;
+  constexpr int FLUSH = 32;
   static_assert(CI == 4 || CI == 8 || CI == 16, "CI");
   static_assert(CO == 8 || CO == 16, "CO");
-  __shared__ float red[4][MT * 256];
-  __shared__ float bred[4][64];
+  __shared__ double red[MT * 256];
+  __shared__ double bred[4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int row = lane & 15, slot = lane >> 4;
   const int ci = row % CI, tsub = row / CI;
   const int npix = B * H * W;
   const int c0 = blockIdx.x * chunk, c1 = min(npix, c0 + chunk);
-  // this lane's tap offsets per M-tile (in pixels) and whether the tap exists
   int dys[MT], dxs[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
@@ -448,37 +451,74 @@ __global__ __launch_bounds__(256) void conv_wgrad_mfma_kernel(const float* __res
     dys[m] = tap < 9 ? tap / 3 - 1 : 99;
     dxs[m] = tap < 9 ? tap % 3 - 1 : 0;
   }
-  f32x4_t acc[MT];
+  double accd[MT][4];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) acc[m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) accd[m][r] = 0.0;
+  double bsum = 0.0;
+  const bool gcol = row < CO;
   int p = c0 + 4 * wv + slot;
   int x = p % W, y = (p / W) % H;
-  for (; p - slot - 4 * wv < c1; p += 16) {
-    const bool vp = p < c1;
-    const float g = (vp && row < CO) ? dout[(long long)p * CO + row] : 0.f;
-    bsum += g;
+  const int nsteps = c1 > c0 ? (c1 - c0 + 15) / 16 : 0;
+  // operands of one k-step (this lane's pixel p at (x, y)), loaded one k-step ahead of its MFMAs
+  float av[MT], g = 0.f;
+  auto load = [&](int pp, int xx0, int yy0, float* a, float& gg) {
+    const bool vp = pp < c1;
+    const int pc = vp ? pp : c0;  // an in-range pixel for the unconditional loads
+    const float gl = dout[(long long)pc * CO + (gcol ? row : 0)];
+    gg = (vp && gcol) ? gl : 0.f;
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const int yy = y + dys[m], xx = x + dxs[m];
-      float a = 0.f;
-      if (vp && yy >= 0 && yy < H && xx >= 0 && xx < W) {
-        a = in[(long long)(p + dys[m] * W + dxs[m]) * CI + ci];
-        if (RELU_IN) a = fmaxf(a, 0.f);
-      }
-      acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, g, acc[m], 0, 0, 0);
+      const int yy = yy0 + dys[m], xx = xx0 + dxs[m];
+      const bool ok = vp && yy >= 0 && yy < H && xx >= 0 && xx < W;
+      const int q = ok ? pp + dys[m] * W + dxs[m] : pc;
+      const float v = in[(long long)q * CI + ci];
+      a[m] = ok ? (RELU_IN ? fmaxf(v, 0.f) : v) : 0.f;
     }
-    x += 16;  // next pixel of this lane: 16 on (W >= 4: at most 4 wraps)
+  };
+  auto advance = [&]() {  // this lane's next pixel: 16 on (W >= 4: at most 4 wraps)
+    p += 16;
+    x += 16;
     while (x >= W) {
       x -= W;
       if (++y == H) y = 0;
     }
+  };
+  if (nsteps > 0) load(p, x, y, av, g);
+  for (int s0 = 0; s0 < nsteps; s0 += FLUSH) {
+    f32x4_t acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int s1 = min(nsteps, s0 + FLUSH);
+    for (int s = s0; s < s1; ++s) {
+      advance();
+      float an[MT], gn = 0.f;
+      if (s + 1 < nsteps) load(p, x, y, an, gn);  // uniform: the whole wave takes it
+      bsum += (double)g;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], g, acc[m], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) av[m] = an[m];
+      g = gn;
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) accd[m][r] += (double)acc[m][r];
   }
-  // C layout: register r of lane l = row 4 (l >> 4) + r of the tile, column l & 15
+  // C layout: register r of lane l = row 4 (l >> 4) + r of the tile, column l & 15; waves in order
+  for (int w = 0; w < 4; ++w) {
+    if (wv == w)
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[wv][m * 256 + (4 * slot + r) * 16 + row] = acc[m][r];
+        for (int r = 0; r < 4; ++r) {
+          const int e = m * 256 + (4 * slot + r) * 16 + row;
+          red[e] = w == 0 ? accd[m][r] : red[e] + accd[m][r];
+        }
+    __syncthreads();
+  }
   bred[wv][lane] = bsum;
   __syncthreads();
   float* pp = part + (long long)blockIdx.x * (NW + CO);
@@ -486,16 +526,15 @@ __global__ __launch_bounds__(256) void conv_wgrad_mfma_kernel(const float* __res
     const int m = e >> 8, rr = (e >> 4) & 15, cc = e & 15;
     const int tap = m * TPM + rr / CI;
     if (tap >= 9 || cc >= CO) continue;
-    const float v = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
-    pp[(tap * CI + rr % CI) * CO + cc] = v;
+    pp[(tap * CI + rr % CI) * CO + cc] = (float)red[e];
   }
   if (threadIdx.x < CO) {
-    float v = 0.f;
+    double v = 0.0;
 #pragma unroll
     for (int w = 0; w < 4; ++w)
 #pragma unroll
       for (int s = 0; s < 4; ++s) v += bred[w][16 * s + threadIdx.x];
-    pp[NW + threadIdx.x] = v;
+    pp[NW + threadIdx.x] = (float)v;
   }
 }
 
@@ -556,16 +595,15 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(const float* __restrict_
     const int dy = FWD ? tap / 3 - 1 : 1 - tap / 3, dx = FWD ? tap % 3 - 1 : 1 - tap % 3;
     float4 a[TW];
 #pragma unroll
-    for (int t = 0; t < TW; ++t) {
+    for (int t = 0; t < TW; ++t) {  // unconditional loads from clamped addresses, values selected after
       const int yy = ys[t] + dy, xx = xs[t] + dx;
-      a[t] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (tap < 9 && px[t] < end && yy >= 0 && yy < H && xx >= 0 && xx < W) {
-        a[t] = *reinterpret_cast<const float4*>(X + (long long)(px[t] + dy * W + dx) * KC + c4);
-        if (RELU_IN) {
-          a[t].x = fmaxf(a[t].x, 0.f); a[t].y = fmaxf(a[t].y, 0.f);
-          a[t].z = fmaxf(a[t].z, 0.f); a[t].w = fmaxf(a[t].w, 0.f);
-        }
-      }
+      const bool ok = tap < 9 && px[t] < end && yy >= 0 && yy < H && xx >= 0 && xx < W;
+      const int q = ok ? px[t] + dy * W + dx : base;
+      const float4 v = *reinterpret_cast<const float4*>(X + (long long)q * KC + c4);
+      a[t].x = ok ? (RELU_IN ? fmaxf(v.x, 0.f) : v.x) : 0.f;
+      a[t].y = ok ? (RELU_IN ? fmaxf(v.y, 0.f) : v.y) : 0.f;
+      a[t].z = ok ? (RELU_IN ? fmaxf(v.z, 0.f) : v.z) : 0.f;
+      a[t].w = ok ? (RELU_IN ? fmaxf(v.w, 0.f) : v.w) : 0.f;
     }
 #pragma unroll
     for (int t = 0; t < TW; ++t) {
@@ -1237,9 +1275,13 @@ static int conv_bwd_group(int ci) {
 }
 
 // f32-MFMA convolutions (bit 1 forward, 2 data grad, 4 weight grad); the VALU kernels otherwise
+// Measured, not kept (profiles/r4c_*, r4d_*: batch 256, 303-395 vs 494 DrQ steps/s): the f32 MFMA has
+// the packed-FMA rate, so it can only win on operand delivery, and these kernels -- operands one fp32
+// per lane straight from L1/L2, 16-column tiles half empty at 8 channels -- lose to the VALU kernels'
+// scalar-operand FMAs (weight grads 2-3x slower, forwards 1.2-2x).  Opt-in experiments only.
 int g_drq_mfma = [] {
-  const char* e = getenv("MTSAC_DRQ_MFMA");  // experiments: the VALU kernels per pass
-  return e ? (atoi(e) & 7) : 7;
+  const char* e = getenv("MTSAC_DRQ_MFMA");
+  return e ? (atoi(e) & 7) : 0;
 }();
 constexpr int MFMA_TW = 4;  // 16-pixel tiles per wave of conv_mfma_kernel
 
@@ -1322,9 +1364,8 @@ void conv_bwd_data(const float* dout, const float* w, const float* mask, const f
 
 // enough 64-pixel tiles in flight per CU to cover the staging loads' latency (the partials'
 // reduction is cheap next to them)
-// (the MFMA kernel: chunks of >= 128 pixels, 16-pixel aligned; round 3's 2048 blocks of 64-pixel
-// tiles wrote 19 MB of partials for an 84 x 84 conv)
-int conv_wgrad_blocks(long long npix) { return (int)std::min<long long>(1024, std::max<long long>(1, npix / 128)); }
+// (the MFMA experiment takes chunks of npix / G pixels, 16-pixel aligned)
+int conv_wgrad_blocks(long long npix) { return (int)std::min<long long>(2048, std::max<long long>(1, (npix + 63) / 64)); }
 
 void conv_wgrad(const float* in, const float* dout, float* part, float* dw, float* db, int B, int H, int W, int ci,
                 int co, bool relu_in, hipStream_t st, bool defer_sum) {

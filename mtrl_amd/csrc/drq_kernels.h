@@ -31,7 +31,7 @@ void aug_draw(unsigned long long seed, unsigned long long ctr, int B, int pad, i
               int* crop_n, float* noise_n, hipStream_t st);
 bool conv_supported(int ci, int co);
 extern int g_drq_fwd_g, g_drq_bwd_g;  // conv channel groups per lane, 0: the engine's choice (experiments)
-extern int g_drq_mfma;  // f32-MFMA convs: bit 1 forward, 2 data grad, 4 weight grad (default 7)
+extern int g_drq_mfma;  // f32-MFMA convs (experiment): bit 1 forward, 2 data grad, 4 weight grad (default 0)
 // 3x3 / stride 1 / SAME on NHWC, kernel [3][3][ci][co]; relu_in applies ReLU to the input, res
 // (nullable) is added to the output.  w2 / bias2 (nullable): images [B1, B) use that second
 // parameter set (one launch over the online and the target passes)

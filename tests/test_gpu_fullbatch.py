@@ -403,3 +403,57 @@ def test_lane_mode():
     assert r.returncode == 0 and "modes 1 [1, 1, 1] 1" in r.stdout
     r = _child(code, child_env(16, lanes=False))
     assert r.returncode == 0 and "modes 1 [1, 1, 1] 1" in r.stdout
+
+
+def _drift_run(T, W, prec, chunks):
+    """Logs after each chunk of device-sampled eager steps (same start, stream and noise as
+    _device_steps)."""
+    from mtrl_amd import _lib as L
+    from mtrl_amd.engine import MTSACEngine, make_config
+    from mtrl_amd.init import init_mtsac
+
+    a0, c0 = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=4, task_begin=0, task_count=T)
+    e = MTSACEngine(make_config(num_tasks=T, task_begin=0, task_count=T, obs_dim=39 + T, actor_width=W,
+                                critic_width=W, batch_per_task=128, capacity=512, precision=prec))
+    e.set_params(L.ACTOR, a0)
+    e.set_params(L.CRITIC, c0)
+    e.set_params(L.CRITIC_TARGET, c0)
+    e.buffer_fill_synthetic(77)
+    e.seed_rng(5)
+    e.enable_graph(False)
+    out = []
+    for k in chunks:
+        e.update_many(k)
+        out.append((e.logs(), e.get_params(L.CRITIC).astype(np.float64), e.get_params(L.ACTOR).astype(np.float64)))
+    e.close()
+    return out
+
+
+@pytest.mark.parametrize("T,W,chunks", [(10, 400, (1, 9, 40, 100, 150)), (50, 2048, (1, 9, 50))],
+                         ids=["mt10_w400_300", "s3_60"])
+def test_split2h_long_run_drift_like_split3(T, W, chunks):
+    """Many device-sampled steps: split2h's exponents come from bounds the producers record step after
+    step (weights through the Adam step bound, activations and grads through their partial maxima), so
+    a long run is where a bound that fails to hold would show (an fp16 overflow turns a step into inf /
+    NaN): every log stays finite.  Both split precisions are fp32-accurate with their own summation
+    orders, so each drifts from the exact-fp32 path (precision fp32: FMA GEMMs) by the chaotic growth
+    of last-bit differences; the bar is on the parameters (relative L2 distance to the fp32 run), which
+    average that growth over 10^7 entries: split2h's stays within 4x split3's at every checkpoint."""
+    runs = {p: _drift_run(T, W, p, chunks) for p in (0, 1, 3)}
+    for p, r in runs.items():
+        for lg, _, _ in r:
+            assert all(np.isfinite(v) for v in lg.values()), (p, lg)
+    n = 0
+    for i, k in enumerate(chunks):
+        n += k
+        ref = runs[0][i]
+        row = {}
+        for p in (1, 3):
+            lg, c, a = runs[p][i]
+            row[p] = (max(np.linalg.norm(c - ref[1]) / np.linalg.norm(ref[1]),
+                          np.linalg.norm(a - ref[2]) / np.linalg.norm(ref[2])),
+                      {kk: abs(lg[kk] - ref[0][kk]) / max(abs(ref[0][kk]), 1e-6) for kk in LOSS_KEYS})
+        print(f"T={T} W={W} step {n}: param drift vs fp32 split3 {row[1][0]:.2e} split2h {row[3][0]:.2e}; "
+              f"loss drift split3 " + " ".join(f"{v:.1e}" for v in row[1][1].values()) +
+              " split2h " + " ".join(f"{v:.1e}" for v in row[3][1].values()))
+        assert row[3][0] <= 4 * row[1][0] + 1e-7, (n, row)

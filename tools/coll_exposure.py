@@ -1,0 +1,99 @@
+"""Exposed collective time per bucket of one rank of an N-GPU MT50/W2048 job, on ONE GPU (DESIGN.md
+section 4).  Two modes:
+
+  run  T_LOCAL GBPS PRECISION   eager pipelined steps of the rank's task shard with the modelled trunk
+                                all-reduce (mtsac_debug_set_collective_model: at every RCCL point a delay of
+                                2 (N - 1) / N x bucket bytes over GBPS, on the collective stream); run it
+                                under rocprofv3 --kernel-trace
+  parse TRACE.csv               per bucket (cm_delay_kernel launch, in issue order) of the last full steps:
+                                its modelled length, how much of it the compute streams cover, and the
+                                exposed rest; plus the step wall time
+
+usage: python tools/coll_exposure.py run 7 150 split2h
+       python tools/coll_exposure.py parse kernel_trace.csv"""
+import csv
+import sys
+
+# the modelled collective launches one delay per bucket with a nonzero modelled time (the head |p|^2
+# pair, 8 bytes, rounds to none): 8 per step, in this order
+BUCKETS = ["critic layer 2", "critic layer 1", "critic layer 0", "critic scalar tail", "actor layer 2",
+           "actor layer 1", "actor layer 0", "actor scalar tail"]
+
+
+def run(tl, gbps, prec):
+    import os
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from mtrl_amd import _lib as L
+    from mtrl_amd.engine import MTSACEngine, make_config
+    from mtrl_amd.init import init_mtsac
+
+    T, W = 50, 2048
+    nr = {7: 8, 13: 4, 25: 2}.get(tl, 8)
+    p = {"split3": 1, "bf16": 2, "split2h": 3}[prec]
+    cfg = make_config(num_tasks=T, task_begin=0, task_count=tl, obs_dim=39 + T, actor_width=W, critic_width=W,
+                      batch_per_task=128, capacity=20_000, clip=0, precision=p)
+    eng = MTSACEngine(cfg, device=0)
+    actor, critic = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=1, task_begin=0, task_count=tl)
+    eng.set_params(L.ACTOR, actor)
+    eng.set_params(L.CRITIC, critic)
+    eng.set_params(L.CRITIC_TARGET, critic)
+    eng.buffer_fill_synthetic(1234)
+    eng.seed_rng(1)
+    eng.enable_graph(False)
+    L.check(eng.lib.mtsac_debug_set_collective_model(eng._h, nr, gbps, 0))
+    eng.lib.mtsac_debug_set_pipeline(eng._h, 1)
+    eng.update_many(4)
+    eng.synchronize()
+    eng.update_many(12)
+    eng.synchronize()
+    eng.close()
+    print(f"ran T_local={tl} N={nr} bus {gbps} GB/s {prec}")
+
+
+def union(iv):
+    tot, cur = 0, None
+    for s, e in sorted(iv):
+        if cur is None or s > cur[1]:
+            if cur:
+                tot += cur[1] - cur[0]
+            cur = [s, e]
+        else:
+            cur[1] = max(cur[1], e)
+    return tot + (cur[1] - cur[0] if cur else 0)
+
+
+def parse(path):
+    rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                  for r in csv.DictReader(open(path)))
+    delays = [(s, e) for s, e, n in rows if "cm_delay" in n]
+    comp = [(s, e) for s, e, n in rows if "cm_" not in n]
+    nb = len(BUCKETS)
+    big = max(e - s for s, e in delays)
+    # a step's first bucket: the first of two back-to-back critic hidden-layer buckets (the longest)
+    i0 = next(i for i in range(len(delays) - 1)
+              if delays[i][1] - delays[i][0] > 0.9 * big and delays[i + 1][1] - delays[i + 1][0] > 0.9 * big)
+    cycles = [delays[i:i + nb] for i in range(i0, len(delays) - nb + 1, nb)][1:]  # skip the first (warm)
+    per = [[] for _ in BUCKETS]
+    for cyc in cycles:
+        for j, (s, e) in enumerate(cyc):
+            cov = union([(max(s, cs), min(e, ce)) for cs, ce in comp if cs < e and ce > s])
+            per[j].append((e - s, cov))
+    firsts = [c[0][0] for c in cycles]
+    wall = (firsts[-1] - firsts[0]) / (len(firsts) - 1) / 1e3
+    print(f"steps {len(cycles)}: wall {wall:.1f} us per step (first-bucket to first-bucket)")
+    print(f"{'bucket':20s} {'modelled us':>11s} {'covered us':>11s} {'exposed us':>11s}")
+    tot = 0.0
+    for name, v in zip(BUCKETS, per):
+        m = sum(x for x, _ in v) / len(v) / 1e3
+        c = sum(y for _, y in v) / len(v) / 1e3
+        tot += m - c
+        print(f"{name:20s} {m:11.1f} {c:11.1f} {m - c:11.1f}")
+    print(f"{'sum':20s} {'':11s} {'':11s} {tot:11.1f}")
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "run":
+        run(int(sys.argv[2]), float(sys.argv[3]), sys.argv[4])
+    else:
+        parse(sys.argv[2])

@@ -2,7 +2,7 @@
 slowest rank's tasks: 25 / 13 / 7 for N = 2 / 4 / 8) with the modelled trunk all-reduce
 (mtsac_debug_set_collective_model: at every RCCL point a delay of 2 (N - 1) / N x bucket bytes over an
 assumed bus bandwidth, on the collective stream, held by 8 workgroups), whole vs pipelined steps.
-usage: python tools/shard_model.py [GBPS ...]   (default 150 300; 0 = no collective)"""
+usage: python tools/shard_model.py [GBPS ...] [split3|split2h|bf16]   (default 0 300 150; 0 = no collective)"""
 import sys
 import time
 
@@ -12,10 +12,12 @@ from mtrl_amd.engine import MTSACEngine, make_config  # noqa: E402
 from mtrl_amd.init import init_mtsac  # noqa: E402
 
 T, W = 50, 2048
-gbps_list = [float(x) for x in (sys.argv[1:] or ["0", "300", "150"])]
+PREC = {"split3": 1, "bf16": 2, "split2h": 3}
+prec = next((PREC[a] for a in sys.argv[1:] if a in PREC), 1)
+gbps_list = [float(x) for x in ([a for a in sys.argv[1:] if a not in PREC] or ["0", "300", "150"])]
 for nr, tl in ((8, 7), (4, 13), (2, 25)):
     cfg = make_config(num_tasks=T, task_begin=0, task_count=tl, obs_dim=39 + T, actor_width=W, critic_width=W,
-                      batch_per_task=128, capacity=20_000, clip=0, precision=1)
+                      batch_per_task=128, capacity=20_000, clip=0, precision=prec)
     eng = MTSACEngine(cfg, device=0)
     actor, critic = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=1, task_begin=0, task_count=tl)
     eng.set_params(L.ACTOR, actor)
