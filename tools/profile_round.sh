@@ -4,7 +4,7 @@
 #   pmc_traffic.json              : per-family HBM bytes per launch (tools/pmc_traffic.py)
 set -o pipefail
 TAG=${1:-r1}
-PREC=${2:-split3}  # the default bench's precision (its PMC family keys)
+PREC=${2:-split2h}  # the default bench's precision (its PMC family keys)
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
 mkdir -p $O
