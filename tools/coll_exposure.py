@@ -14,10 +14,10 @@ usage: python tools/coll_exposure.py run 7 150 split2h
 import csv
 import sys
 
-# the modelled collective launches one delay per bucket with a nonzero modelled time (the head |p|^2
-# pair, 8 bytes, rounds to none): 8 per step, in this order
-BUCKETS = ["critic layer 2", "critic layer 1", "critic layer 0", "critic scalar tail", "actor layer 2",
-           "actor layer 1", "actor layer 0", "actor scalar tail"]
+# the modelled collective launches one delay per bucket whose modelled time rounds to >= one 10-ns
+# tick (the scalar tails only at low bandwidths, the head |p|^2 pair never), in this order per step
+BUCKETS = ["critic layer 2", "critic layer 1", "critic layer 0 + tail", "actor layer 2", "actor layer 1",
+           "actor layer 0 + tail"]
 
 
 def run(tl, gbps, prec):
@@ -68,28 +68,46 @@ def parse(path):
                   for r in csv.DictReader(open(path)))
     delays = [(s, e) for s, e, n in rows if "cm_delay" in n]
     comp = [(s, e) for s, e, n in rows if "cm_" not in n]
-    nb = len(BUCKETS)
     big = max(e - s for s, e in delays)
-    # a step's first bucket: the first of two back-to-back critic hidden-layer buckets (the longest)
-    i0 = next(i for i in range(len(delays) - 1)
-              if delays[i][1] - delays[i][0] > 0.9 * big and delays[i + 1][1] - delays[i + 1][0] > 0.9 * big)
-    cycles = [delays[i:i + nb] for i in range(i0, len(delays) - nb + 1, nb)][1:]  # skip the first (warm)
+    # classify by modelled length: critic hidden layers ~big, actor hidden layers ~big / 2 (one member),
+    # the rest small; a step starts at its first critic hidden-layer bucket
+    steps, cur = [], None
+    for s, e in delays:
+        d = e - s
+        kind = 0 if d > 0.75 * big else 1 if d > 0.35 * big else 2
+        if kind == 0 and (cur is None or cur["phase"] > 0):
+            cur = {"phase": 0, "b": [[] for _ in BUCKETS], "n0": 0, "n1": 0, "first": s}
+            steps.append(cur)
+        if cur is None:
+            continue
+        if kind == 0:
+            j = min(cur["n0"], 1)
+            cur["n0"] += 1
+        elif kind == 1:
+            cur["phase"] = 1
+            j = 3 + min(cur["n1"], 1)
+            cur["n1"] += 1
+        else:
+            j = 2 if cur["phase"] == 0 else 5
+        cur["b"][j].append((s, e))
+    steps = [st for st in steps[1:-1] if st["n0"] == 2 and st["n1"] == 2]  # whole steps, the first skipped
     per = [[] for _ in BUCKETS]
-    for cyc in cycles:
-        for j, (s, e) in enumerate(cyc):
-            cov = union([(max(s, cs), min(e, ce)) for cs, ce in comp if cs < e and ce > s])
-            per[j].append((e - s, cov))
-    firsts = [c[0][0] for c in cycles]
+    for st in steps:
+        for j, iv in enumerate(st["b"]):
+            m = sum(e - s for s, e in iv)
+            cov = sum(union([(max(s, cs), min(e, ce)) for cs, ce in comp if cs < e and ce > s]) for s, e in iv)
+            per[j].append((m, cov))
+    firsts = [st["first"] for st in steps]
     wall = (firsts[-1] - firsts[0]) / (len(firsts) - 1) / 1e3
-    print(f"steps {len(cycles)}: wall {wall:.1f} us per step (first-bucket to first-bucket)")
-    print(f"{'bucket':20s} {'modelled us':>11s} {'covered us':>11s} {'exposed us':>11s}")
+    print(f"steps {len(steps)}: wall {wall:.1f} us per step (first bucket to first bucket)")
+    print(f"{'bucket':22s} {'modelled us':>11s} {'covered us':>11s} {'exposed us':>11s}")
     tot = 0.0
     for name, v in zip(BUCKETS, per):
         m = sum(x for x, _ in v) / len(v) / 1e3
         c = sum(y for _, y in v) / len(v) / 1e3
         tot += m - c
-        print(f"{name:20s} {m:11.1f} {c:11.1f} {m - c:11.1f}")
-    print(f"{'sum':20s} {'':11s} {'':11s} {tot:11.1f}")
+        print(f"{name:22s} {m:11.1f} {c:11.1f} {m - c:11.1f}")
+    print(f"{'sum':22s} {'':11s} {'':11s} {tot:11.1f}")
 
 
 if __name__ == "__main__":
