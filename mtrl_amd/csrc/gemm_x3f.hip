@@ -69,9 +69,18 @@ static long long bf16_workgroups(int M, int N, int batch) {
 // ablations only: at the S3 shape its MFMA + LDS skeleton is 3-4 % faster, but with one wave per
 // SIMD the operand loads hide worse and the full kernel is 2 % (split3, 208 rows) to 20 % (bf16,
 // 208 rows vs 400) slower (profiles/r3_x3f_ablate.txt).
+// tile order inside an XCD's run (experiments; SplitGemmParams::order): row tiles fastest measured
+// 2.5 % slower at S3 split2h than column tiles fastest (profiles/r4h_*)
+static const int g_x3f_order = [] {
+  const char* e = getenv("MTSAC_X3F_ORDER");
+  return e ? atoi(e) : 0;
+}();
+
 template <int EPI, bool C_OUT, bool P_OUT, bool MASK16, int TAG = 0>
-void launch(const SplitGemmParams& p, dim3 grid, hipStream_t st, int bm) {
+void launch(const SplitGemmParams& p0, dim3 grid, hipStream_t st, int bm) {
   const dim3 blk(512);
+  SplitGemmParams p = p0;
+  if (g_x3f_order) p.order = g_x3f_order;
   if (p.np == 2) {  // split2h: two fp16 planes, 3 products
     hipLaunchKernelGGL((gemm_x3f_kernel<BM0, EPI, C_OUT, P_OUT, MASK16, TAG, 2>), grid, blk, 0, st, p);
     return;

@@ -117,7 +117,8 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   const int sl = FIN ? lin % nsplit : lin / tiles;
   lin = FIN ? lin / nsplit : lin - sl * tiles;
   const int tile_id = lin;
-  const int by = lin % ny, bx = (lin / ny) % nx, z = lin / (ny * nx);
+  const int by = p.order ? (lin / nx) % ny : lin % ny, bx = p.order ? lin % nx : (lin / ny) % nx;
+  const int z = lin / (ny * nx);
   const int m0 = bx * BM, n0 = by * BN;
   const int k0 = nsplit > 1 ? sl * p.kchunk : 0;
   const __bf16* __restrict__ A = p.A + z * p.sA + k0;

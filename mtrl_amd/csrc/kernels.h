@@ -103,6 +103,8 @@ struct SplitGemmParams {
   float* ws;
   int dbg;                // experiments only: bit0 skip steady-state loads, bit1 skip MFMA
   int tag;                // 1: input-layer launch (separate kernel symbol for profiles)
+  int order;              // gemm_x3f tile order inside an XCD's run: 0 column tiles fastest, 1 row tiles
+                          // fastest (experiments: MTSAC_X3F_ORDER)
   int np;                 // operand planes the products read: 3 (0 = default; fp32-accurate split) or 1
                           // (precision bf16: the high plane only, one MFMA per product)
   float* dbp;             // gemm_x3f: column sums of the epilogue's output per row tile, [z][row tiles][N]

@@ -495,20 +495,50 @@ __global__ __launch_bounds__(1024) void reduce_rows_kernel(RowPtrs in, int n_in,
 // one block of 16 waves, wave w over the global tasks w, w + 16, ...; after the barrier wave 0
 // sums the per-task loss terms in task order
 // the per-task sums of waves [0, nw): wave w takes global tasks w, w + nw, ...
+// Four tasks per wave at a time, every load unconditional (clamped index, value selected after): a
+// load under a branch was waited for one task at a time (three dependent round trips per task).
 __device__ void alpha_tasks(const AlphaParams& a, int wave, int nw) {
   const int lane = threadIdx.x & 63;
-  for (int tg = wave; tg < a.T_glob; tg += nw) {
-    const int t = tg - a.task_begin;
-    float s = 0.f;
-    if (t >= 0 && t < a.T_l) {
-      const int n = a.counts[t];
-      const int* rl = a.rows + (long long)t * a.max_rows;
-      for (int j = lane; j < n; j += 64) s += a.logpi[rl[j]] + a.target_entropy;
-      s = wsumf(s);
+  constexpr int U = 4;
+  for (int tg0 = wave; tg0 < a.T_glob; tg0 += U * nw) {
+    int tl[U], n[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = tg0 + u * nw - a.task_begin;
+      ok[u] = tg0 + u * nw < a.T_glob && t >= 0 && t < a.T_l;
+      tl[u] = ok[u] ? t : 0;
+      const int c = a.counts[tl[u]];
+      n[u] = ok[u] ? c : 0;
     }
+    int nmax = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) nmax = max(nmax, n[u]);  // wave-uniform
+    float s[U] = {0.f, 0.f, 0.f, 0.f};
+    for (int j0 = 0; j0 < nmax; j0 += 64) {
+      const int j = j0 + lane;
+      int r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rr = a.rows[(long long)tl[u] * a.max_rows + min(j, a.max_rows - 1)];
+        r[u] = j < n[u] ? rr : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float lp = a.logpi[r[u]];
+        s[u] += j < n[u] ? lp + a.target_entropy : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) s[u] = wsumf(s[u]);
     if (lane == 0) {
-      a.grad[tg] = (t >= 0 && t < a.T_l) ? -s / (float)a.B_glob : 0.f;
-      a.task_loss[tg] = (t >= 0 && t < a.T_l) ? -a.log_alpha[tg] * s : 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int tg = tg0 + u * nw;
+        if (tg >= a.T_glob) continue;
+        a.grad[tg] = ok[u] ? -s[u] / (float)a.B_glob : 0.f;
+        a.task_loss[tg] = ok[u] ? -a.log_alpha[tg] * s[u] : 0.f;
+      }
     }
   }
 }
@@ -582,10 +612,33 @@ __device__ void write_logs_wave(const LogParams& p) {
 // temperature Adam, the logs and the step counter.
 __global__ __launch_bounds__(1024) void step_finish_kernel(StepFinish f) {
   __shared__ double s[48];  // [8 k + w] row sum k of wave 8 + w; [24 + 2 w + {0,1}] trunk / head |p|^2 of wave 8 + w
+  __shared__ float wm[3][8][2];  // split2h: [job][wave 8 + w][heads, trunk] partial weight maxima
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (wave < 8) {
     if (f.alpha_grad) alpha_tasks(f.alpha, wave, 8);
   } else {
+    {  // split2h: the optimizer's per-block weight maxima, strided over waves 8-15 (loads outside any
+       // branch: a load under a condition was waited for one iteration at a time)
+      const int u = threadIdx.x - 512, wl = wave - 8;
+      for (int j = 0; j < f.nwmax; ++j) {
+        const WeightMaxJob& w = f.wmax[j];
+        float mh = 0.f, mt = 0.f;
+        for (int i = u; i < w.n; i += 512) {
+          const float v = w.parts[i];
+          mh = i < w.nh ? fmaxf(mh, v) : mh;
+          mt = i < w.nh ? mt : fmaxf(mt, v);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          mh = fmaxf(mh, __shfl_xor(mh, o));
+          mt = fmaxf(mt, __shfl_xor(mt, o));
+        }
+        if (lane == 0) {
+          wm[j][wl][0] = mh;
+          wm[j][wl][1] = mt;
+        }
+      }
+    }
     const int u = threadIdx.x - 512, wl = wave - 8;
     double r[3] = {0.0, 0.0, 0.0};
 #pragma unroll
@@ -642,14 +695,9 @@ __global__ __launch_bounds__(1024) void step_finish_kernel(StepFinish f) {
   for (int j = 0; j < f.nwmax; ++j) {
     const WeightMaxJob& w = f.wmax[j];
     float mh = 0.f, mt = 0.f;
-    for (int i = lane; i < w.n; i += 64) {
-      if (i < w.nh) mh = fmaxf(mh, w.parts[i]);
-      else mt = fmaxf(mt, w.parts[i]);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      mh = fmaxf(mh, __shfl_xor(mh, o));
-      mt = fmaxf(mt, __shfl_xor(mt, o));
+    for (int q = 0; q < 8; ++q) {
+      mh = fmaxf(mh, wm[j][q][0]);
+      mt = fmaxf(mt, wm[j][q][1]);
     }
     if (lane == 0) {
       if (w.nh < 0) {
