@@ -96,6 +96,17 @@ def pmc_traffic(precision, family, workload):
     return None, None
 
 
+def build_stamps():
+    """Provenance of the measured library: the source hash stamped into libmtsac.so at link time and
+    the hash of the sources in this tree (mtrl_amd/_lib.py refuses a library whose stamp differs)."""
+    try:
+        from mtrl_amd import _lib as L
+
+        return {"lib_stamp": L.load().mtsac_build_stamp().decode(), "source_stamp": L.source_stamp()}
+    except Exception as e:  # pragma: no cover - reported, not fatal for a dry run
+        return {"error": str(e)}
+
+
 def algorithmic_flops(T, W, n=128, A=4):
     """GEMM flops of one step counting only each row's own head."""
     B = n * T
@@ -368,6 +379,7 @@ def main():
         "config": {"workload": desc, "num_tasks": T, "width": W, "batch_per_task": 128, "global_batch": 128 * T,
                    "parallelism": f"task-shard{world}" if world > 1 else "single", "precision": args.precision,
                    "task_shards": shards, "allreduce_bytes_per_step": ar_bytes},
+        "build": build_stamps(),
     }
     if args.dry_run:
         import torch

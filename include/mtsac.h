@@ -140,6 +140,10 @@ typedef struct mtsac_engine mtsac_engine;
 
 const char* mtsac_last_error(void);
 int mtsac_abi_version(void);
+/* Build provenance: the first 16 hex digits of the sha256 of the sources the library was built from
+ * (the .hip, .cpp and .h files of mtrl_amd/csrc and the .h files of include, in sorted relative-path
+ * order, concatenated; mtrl_amd/csrc/Makefile). */
+const char* mtsac_build_stamp(void);
 void mtsac_default_config(mtsac_config* cfg, int32_t num_tasks);
 
 int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out);

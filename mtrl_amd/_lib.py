@@ -99,6 +99,7 @@ PD = ctypes.POINTER(ctypes.c_double)
 SIGNATURES = {
     "mtsac_last_error": (ctypes.c_char_p, []),
     "mtsac_abi_version": (ctypes.c_int, []),
+    "mtsac_build_stamp": (ctypes.c_char_p, []),
     "mtsac_default_config": (None, [ctypes.POINTER(Config), I32]),
     "mtsac_create": (ctypes.c_int, [ctypes.POINTER(Config), ctypes.c_int, ctypes.POINTER(P)]),
     "mtsac_destroy": (None, [P]),
@@ -214,6 +215,23 @@ SIGNATURES.update({
     "drq_synchronize": (ctypes.c_int, [P]),
 })
 
+def source_stamp() -> str | None:
+    """sha256 (first 16 hex digits) of the engine sources as mtrl_amd/csrc/Makefile stamps them into the
+    library: csrc/*.hip, *.cpp, *.h and include/*.h in sorted path order (as make's $(sort) orders
+    the relative paths), concatenated; None when the sources are not in the tree."""
+    import hashlib
+
+    csrc = pathlib.Path(__file__).resolve().parent / "csrc"
+    if not csrc.is_dir():
+        return None
+    rel = [f.name for pat in ("*.hip", "*.cpp", "*.h") for f in csrc.glob(pat)]
+    rel += ["../../include/" + f.name for f in (csrc / ".." / ".." / "include").glob("*.h")]
+    h = hashlib.sha256()
+    for r in sorted(rel):
+        h.update((csrc / r).read_bytes())
+    return h.hexdigest()[:16]
+
+
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
 
 _lib = None
@@ -247,6 +265,10 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         fn.argtypes = args
     if lib.mtsac_abi_version() != 1:
         raise MTSACLibraryError("libmtsac ABI version mismatch")
+    built, tree = lib.mtsac_build_stamp().decode(), source_stamp()
+    if tree is not None and built != tree and os.environ.get("MTSAC_ALLOW_STALE_LIB") != "1":
+        raise MTSACLibraryError(f"{p} was built from other sources (stamp {built}) than the tree's ({tree}): "
+                                "rebuild it (python -c 'import __graft_entry__ as g; g.build()')")
     if path is None:
         _lib = lib
     return lib

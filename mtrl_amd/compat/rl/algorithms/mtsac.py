@@ -86,7 +86,7 @@ class MTSAC(OffPolicyAlgorithm):
 
     # ------------------------------------------------------------------ construction
     @staticmethod
-    def initialize(config: MTSACConfig, env_config, seed: int = 1, *, precision: str = "split3",
+    def initialize(config: MTSACConfig, env_config, seed: int = 1, *, precision: str = "split2h",
                    device: int = 0) -> "MTSAC":
         if config.critic_config.use_classification:
             raise NotImplementedError("classification critics are outside the MTSAC MSE path")

@@ -89,7 +89,11 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   constexpr int PW = (ABL & 512) ? P0 : PMAX - 1;  // pieces every wave has issued after B(kt, 1)
   // the epilogue reuses the ring as scratch: two 16 x (BN + 4) fp32 row-block images + 8 x BN
   // column-sum partials -- more than the ring of the short one-plane tiles holds
-  constexpr int EPI_LDS = (2 * 16 * (BN + 4) + WV * BN + 16) * 4;  // + the split2h max scratch
+  // EG 16-row blocks per epilogue barrier: 2 for the plane kernels without the in-launch finish (the
+  // per-block barrier chain, not the store bandwidth, bounds an epilogue-heavy launch such as the
+  // input layer's), 1 otherwise
+  constexpr int EG = (!FIN && NP >= 2) ? 2 : 1;
+  constexpr int EPI_LDS = (2 * EG * 16 * (BN + 4) + WV * BN + 16) * 4;  // + the split2h max scratch
   constexpr int SMEM0 = 2 * STAGE > EPI_LDS ? 2 * STAGE : EPI_LDS;
   constexpr int SMEM = SMEM0 + (FIN ? 16 : 0);  // FIN: the 'last slice' word after the scratch
   static_assert(BM % 16 == 0 && SMEM <= 160 * 1024, "tile");
@@ -253,7 +257,7 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   // split2h: unscale the products, and the output planes' exponent from the bound (every workgroup
   // alike); the scratch for the maxima sits past the epilogue's images and column-sum partials
   float unscale = 1.f, oscale = 1.f;
-  float* mscr = img + 2 * 16 * TS + WV * BN;
+  float* mscr = img + 2 * EG * 16 * TS + WV * BN;
   if constexpr (NP == 2) {
     unscale = exp2i(-p.ra->e) * exp2i(-p.rb->e);
     if (P_OUT && !FIN) {
@@ -340,14 +344,24 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   };
   if (two) prefetch(0);
 #pragma unroll
-  for (int i = 0; i < TI; ++i) {
-    if (two && i > 0 && i % PB == 0) prefetch(i);
-    float* tb = img + (i & 1) * 16 * TS;
+  for (int i0 = 0; i0 < TI; i0 += EG) {
+    float* tb0 = img + ((i0 / EG) & 1) * EG * 16 * TS;
 #pragma unroll
-    for (int j = 0; j < JB; ++j)
+    for (int g = 0; g < EG; ++g) {
+      if (i0 + g >= TI) break;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) tb[(4 * (lane >> 4) + r) * TS + 16 * JB * wave + 16 * j + (lane & 15)] = acc[i][j][r];
+      for (int j = 0; j < JB; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          tb0[(16 * g + 4 * (lane >> 4) + r) * TS + 16 * JB * wave + 16 * j + (lane & 15)] = acc[i0 + g][j][r];
+    }
     __syncthreads();
+#pragma unroll
+    for (int g = 0; g < EG; ++g) {
+    const int i = i0 + g;
+    if (i >= TI) break;
+    if (two && i > 0 && i % PB == 0) prefetch(i);
+    float* tb = tb0 + g * 16 * TS;
 #pragma unroll
     for (int rp = 0; rp < RP; ++rp) {
     const int orow = 2 * (wave + WV * rp) + (lane >> 5);
@@ -442,13 +456,14 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
       }
     }
     }  // row pairs
+    }  // row blocks of the group
   }
   if constexpr (NP == 2 && P_OUT && !FIN) {  // this workgroup's max |out|: the next producer's bound input
     const float m = block_max_val(omx, mscr);
     if (t == 0 && blockIdx.x < PLANE_REC_PARTS) p.rc->amax[blockIdx.x] = m;
   }
   if (p.dbp) {  // the tile's column sums: lanes l, l + 32 of every wave hold the same 8 columns
-    float* red = img + 2 * 16 * TS;  // [WV waves][256]
+    float* red = img + 2 * EG * 16 * TS;  // [WV waves][256]
 #pragma unroll
     for (int c = 0; c < 8; ++c) csum[c] += __shfl_xor(csum[c], 32);
     if (lane < 32) {
