@@ -242,7 +242,7 @@ struct mtsac_engine {
   float* tparts = nullptr;
   int wgrid[2] = {}, wbh[2] = {};  // the last optimizer launch's grid and head blocks per network
   RecRef* act_rec(__bf16** actp) {
-    return actp == hap ? r_ac[0] : actp == hcp ? r_ac[1] : actp == hctp ? r_ac[2] : nullptr;
+    return actp == hap || actp == hap_s2 ? r_ac[0] : actp == hcp ? r_ac[1] : actp == hctp ? r_ac[2] : nullptr;
   }
   RecRef* dz_rec(__bf16** dzp) { return dzp == dzap ? r_dz[0] : dzp == dzcp ? r_dz[1] : nullptr; }
   RecRef& w_rec(const Net& net, int which) { return r_w[&net == &critic ? 1 : 0][which]; }
@@ -273,6 +273,7 @@ struct mtsac_engine {
     g.bias_in_b = bias_in_b ? 1 : 0;
   }
   __bf16* hap[MAXD] = {};
+  __bf16* hap_s2[MAXD] = {};  // = hap[i] + krows * ald: the s' rows of the actor's hidden planes
   __bf16* hcp[MAXD] = {};
   __bf16* hctp[MAXD] = {};
   __bf16* dzap[MAXD] = {};
@@ -287,8 +288,17 @@ struct mtsac_engine {
   __bf16* in_planes(const float* X) const {
     for (const InPlanes& q : inp)
       if (q.x == X) return q.p;
+    if (X == xan && inp[0].p) return inp[0].p + actor.krows * actor.xld;  // the s' rows of xa's planes
     return nullptr;
   }
+  // Split actor forward (device collective, eager one stream): the s' rows (a' for the TD target) run
+  // before the critic loss as always, the s rows (pi(s) for the actor loss) beside the critic's trunk
+  // all-reduce -- the one stretch of the step where nothing else may run (the rest needs the updated
+  // critic).  MTSAC_SPLIT_ACTOR=0 / 1 forces either form.
+  int split_actor_req = [] {
+    const char* v = getenv("MTSAC_SPLIT_ACTOR");
+    return v ? atoi(v) : -1;
+  }();
   float *logpi_n = nullptr, *logpi = nullptr, *y = nullptr, *dq = nullptr, *row_a = nullptr, *row_b = nullptr,
         *row_c = nullptr, *alpha_w = nullptr, *cache = nullptr, *dout_a = nullptr;
   float* partials = nullptr;
@@ -1124,8 +1134,11 @@ struct mtsac_engine {
   // on lane 4 as soon as its weight grad is done, overlapping the rest of the backward; the
   // buckets form one chain (every rank issues its collectives in the same order).  Layer 0 and
   // the scalar tail follow in the optimizer segment (reduce_rest).
+  // pre_join (may be empty): segments issued after the last weight grad and before the join that
+  // waits for the all-reduce buckets (the split actor forward, beside the critic's collective)
+  template <class PJ = void (*)()>
   int backward_segs(Net& net, const float* params, const float* X, int ldx, float** acts, __bf16** actp, float** dz,
-                    __bf16** dzp, int d_top, int w_prev, int M) {
+                    __bf16** dzp, int d_top, int w_prev, int M, PJ pre_join = [] {}) {
     int dprev = d_top, wprev = w_prev, rprev = -1;
     const bool bucket = sharded() && net.depth > 1;
     for (int i = net.depth - 1; i >= 0; --i) {
@@ -1137,6 +1150,7 @@ struct mtsac_engine {
       }
       if (i > 0) dprev = seg({dprev}, 1, [&, i] { dgrad_layer(net, params, acts, actp, dz, dzp, i, M); });
     }
+    pre_join();
     if (rprev >= 0) return seg({dprev, wprev, rprev}, 1, [] {});  // join point
     return seg({dprev, wprev}, 1, [] {});
   }
@@ -1241,7 +1255,33 @@ struct mtsac_engine {
     // ONE actor forward over [s | s'] with the pre-update actor: update_critic samples a' ~ pi(.|s')
     // (mtsac.py:525-528) and update_actor a ~ pi(.|s) (:640-642) from the same parameters, so the
     // two row blocks share every trunk GEMM (rows krows.. are s'; the pad rows between are zeros)
+    const bool split_af = split_actor_req > 0 || (split_actor_req < 0 && dev_collective() && one_stream && !build &&
+                                                  !timing_serial && !lanes_alt);
+    auto pi_s = [&](PolicyParams& q) {  // pi(s): the actor-loss half of the policy heads
+      q = pp;
+      q.head = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
+      q.eps = device_noise ? nullptr : eps_c;
+      q.stream_id = 2;
+      q.a_out = xcp;
+      q.a_planes = in_planes(xcp);
+      q.ap_rec = h2 ? r_in[inset_cur].d : nullptr;
+      q.logpi = logpi;
+      q.cache = cache;
+    };
     const int s_af = seg({s_in}, ol ? 0 : 2, [&] {
+      if (split_af) {  // the s' rows only: a' ~ pi(.|s') for the TD target
+        trunk_forward(actor, actor.p, 0, xan, ld_a, han, hap_s2, Bl);
+        PolicyParams qn = pp;
+        qn.head = head(actor, actor.p, han[actor.depth - 1], Bl, task);
+        qn.eps = device_noise ? nullptr : eps_n;
+        qn.stream_id = 1;
+        qn.a_out = xcn;
+        qn.a_planes = in_planes(xcn);
+        qn.ap_rec = h2 ? r_in[inset_cur].d : nullptr;
+        qn.logpi = logpi_n;
+        policy_head(qn, cur);
+        return;
+      }
       trunk_forward(actor, actor.p, 0, xa, ld_a, ha, hap, Ma);
       PolicyParams q = pp;
       q.head = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
@@ -1309,7 +1349,16 @@ struct mtsac_engine {
       if (!c_both)
         head_backward_weight(chp, dq, Bl, counts, rows, Bl, critic.g + critic.off_hW, critic.g + critic.off_hb, cur);
     });
-    const int s_cb = backward_segs(critic, critic.p, xc, ld_c, hc, hcp, dzc, dzcp, s_cl, s_chw, Bl);
+    int s_afs = s_af;
+    const int s_cb = backward_segs(critic, critic.p, xc, ld_c, hc, hcp, dzc, dzcp, s_cl, s_chw, Bl, [&] {
+      if (split_af)  // the s rows beside the critic's all-reduce
+        s_afs = seg({s_in}, 1, [&] {
+          trunk_forward(actor, actor.p, 0, xa, ld_a, ha, hap, Bl);
+          PolicyParams q;
+          pi_s(q);
+          policy_head(q, cur);
+        });
+    });
     // reduce over shards, clip + Adam + Polyak (mtsac.py:599-613)
     const int s_co = seg({s_cb}, 1, [&] {
       if (sharded()) head_sq(critic);  // the heads' |g|^2 into the all-reduced scalar tail
@@ -1319,7 +1368,7 @@ struct mtsac_engine {
       refresh_wt(critic, critic.tgt, 1, cur, true);
     });
     // actor loss through the UPDATED critic (mtsac.py:659-691)
-    const int s_ap = seg({s_co, s_af}, 1, [&] {
+    const int s_ap = seg({s_co, s_af, s_afs}, 1, [&] {
       trunk_forward(critic, critic.p, 0, xcp, ld_c, hc, hcp, Bl);
       CriticHeadParams c = ch;
       c.head = head(critic, critic.p, hc[critic.depth - 1], Bl, task);
@@ -2014,6 +2063,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
       const size_t np = (size_t)net->E * 3 * net->aps();
       for (int i = 0; i + 1 < net->depth; ++i) {
         if ((rc = e->alloc(cr ? &e->hcp[i] : &e->hap[i], np))) return bad(rc);
+        if (!cr) e->hap_s2[i] = e->hap[i] + net->krows * net->ald;
         if (cr && (rc = e->alloc(&e->hctp[i], np))) return bad(rc);
       }
       // dz[0] planes (in_wgrad_planes): the input layer's weight grad (K = B, M = in_dim) on k-major

@@ -6,6 +6,10 @@
 
 #include "gemm_x3p_impl.h"
 
+#ifndef X3F_EPI_GROUP
+#define X3F_EPI_GROUP 2  // 16-row blocks per epilogue barrier in the plane kernels (4 measured equal: profiles/r4k_*)
+#endif
+
 namespace mtsac {
 namespace x3fk {
 
@@ -92,7 +96,7 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   // EG 16-row blocks per epilogue barrier: 2 for the plane kernels without the in-launch finish (the
   // per-block barrier chain, not the store bandwidth, bounds an epilogue-heavy launch such as the
   // input layer's), 1 otherwise
-  constexpr int EG = (!FIN && NP >= 2) ? 2 : 1;
+  constexpr int EG = (!FIN && NP >= 2) ? X3F_EPI_GROUP : 1;
   constexpr int EPI_LDS = (2 * EG * 16 * (BN + 4) + WV * BN + 16) * 4;  // + the split2h max scratch
   constexpr int SMEM0 = 2 * STAGE > EPI_LDS ? 2 * STAGE : EPI_LDS;
   constexpr int SMEM = SMEM0 + (FIN ? 16 : 0);  // FIN: the 'last slice' word after the scratch
