@@ -1255,8 +1255,12 @@ struct mtsac_engine {
     // ONE actor forward over [s | s'] with the pre-update actor: update_critic samples a' ~ pi(.|s')
     // (mtsac.py:525-528) and update_actor a ~ pi(.|s) (:640-642) from the same parameters, so the
     // two row blocks share every trunk GEMM (rows krows.. are s'; the pad rows between are zeros)
+    // auto: with a device collective, on shards of <= 2048 rows, where the critic's buckets outlast its
+    // backward (MT50 at N >= 4); at N = 2 (3200 rows) the buckets hide in the backward and the halved
+    // actor GEMMs only cost (profiles/r4l_shard_model_*.txt: N = 8 -58 us, N = 4 -17 us, N = 2 +167 us
+    // per step at 300 GB/s)
     const bool split_af = split_actor_req > 0 || (split_actor_req < 0 && dev_collective() && one_stream && !build &&
-                                                  !timing_serial && !lanes_alt);
+                                                  !timing_serial && !lanes_alt && Bl <= 2048);
     auto pi_s = [&](PolicyParams& q) {  // pi(s): the actor-loss half of the policy heads
       q = pp;
       q.head = head(actor, actor.p, ha[actor.depth - 1], Bl, task);
