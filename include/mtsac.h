@@ -225,6 +225,22 @@ int mtsac_comm_nranks(mtsac_engine* h, int32_t* nranks);
  * Disables hipGraph replay for this engine.  fn == NULL removes it. */
 typedef int (*mtsac_allreduce_fn)(void* user, float* device_buffer, int64_t count);
 int mtsac_set_allreduce_hook(mtsac_engine* h, mtsac_allreduce_fn fn, void* user);
+/* The same with the sharded optimizer's collectives too: fn(user, op, device_buffer, count), op 0 =
+ * all-reduce (sum), 1 = reduce-scatter in place (rank r's shard [r count / world, (r + 1) count / world)
+ * of the buffer must hold the element-wise sum over all ranks; the rest is left undefined), 2 =
+ * all-gather in place (every rank's shard of the buffer from its owner).  rank / world: this engine's
+ * place in the group.  Replaces an all-reduce hook; fn == NULL removes it. */
+typedef int (*mtsac_collective_fn)(void* user, int32_t op, float* device_buffer, int64_t count);
+int mtsac_set_collective_hook(mtsac_engine* h, mtsac_collective_fn fn, void* user, int32_t rank, int32_t world);
+/* Sharded trunk optimizer (ZeRO-1 style) for task-sharded runs (reference OptimizerConfig.spawn /
+ * TrainState.apply_gradients, mtrl/config/optim.py:26-43, mtrl/rl/algorithms/utils.py:11-46): every trunk
+ * bucket is reduce-scattered instead of all-reduced, the global clip norm comes from an all-reduced
+ * |g|^2, each rank runs Adam on its 1/world of the trunk, the new trunk is all-gathered and every
+ * rank writes its own GEMM planes and Polyak target from it.  on: 1 / 0; active only with a device
+ * collective (RCCL, the modelled one) or a collective hook, and when world divides every bucket into
+ * whole float4s (else the all-reduce path runs).  The Adam moments then live sharded: get_params of
+ * a moment returns this rank's shards current, the rest stale.  Default off (MTSAC_ZERO=1 turns it on). */
+int mtsac_set_sharded_optimizer(mtsac_engine* h, int32_t on);
 /* plain device/host copy helper for hooks written in a host language (hipMemcpyDefault) */
 int mtsac_memcpy(void* dst, const void* src, int64_t bytes);
 

@@ -135,6 +135,8 @@ SIGNATURES = {
     "mtsac_get_noise_state": (ctypes.c_int, [P, P, P]),
     "mtsac_set_noise_state": (ctypes.c_int, [P, ctypes.c_uint64, ctypes.c_uint64]),
     "mtsac_set_allreduce_hook": (ctypes.c_int, [P, ctypes.c_void_p, P]),
+    "mtsac_set_collective_hook": (ctypes.c_int, [P, ctypes.c_void_p, P, ctypes.c_int32, ctypes.c_int32]),
+    "mtsac_set_sharded_optimizer": (ctypes.c_int, [P, ctypes.c_int32]),
     "mtsac_memcpy": (ctypes.c_int, [P, P, I64]),
     "mtsac_set_timing": (ctypes.c_int, [P, I32]),
     "mtsac_get_timing": (ctypes.c_int, [P, I32, PD, PI32, PD]),
@@ -233,6 +235,7 @@ def source_stamp() -> str | None:
 
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
+COLLECTIVE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64)
 
 _lib = None
 

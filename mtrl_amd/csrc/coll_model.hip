@@ -42,11 +42,13 @@ double coll_model_us(long long bytes, int nranks, double bus_gbps) {
   return 2.0 * (nranks - 1) / nranks * (double)bytes / (bus_gbps * 1e3);  // bytes / (GB/s) = ns
 }
 
+// scale: the share of an all-reduce's link time the collective takes (0.5: a reduce-scatter or an
+// all-gather, (N - 1) / N of the bucket each)
 void coll_model_allreduce(float* buf, long long count, int nranks, double bus_gbps, int blocks, float* shadow,
-                          hipStream_t st) {
+                          hipStream_t st, double scale) {
   const int g = (int)std::min<long long>(1024, std::max<long long>(1, (count + 255) / 256));
   if (shadow) hipLaunchKernelGGL(cm_poison_kernel, dim3(g), dim3(256), 0, st, buf, shadow, count);
-  const double us = coll_model_us(count * 4, nranks, bus_gbps);
+  const double us = scale * coll_model_us(count * 4, nranks, bus_gbps);
   const unsigned long long ticks = (unsigned long long)(us * 100.0 + 0.5);  // 100 MHz: 10 ns per tick
   if (ticks > 0) hipLaunchKernelGGL(cm_delay_kernel, dim3(std::max(1, blocks)), dim3(64), 0, st, ticks);
   if (shadow) hipLaunchKernelGGL(cm_restore_kernel, dim3(g), dim3(256), 0, st, buf, shadow, count);

@@ -340,6 +340,18 @@ struct mtsac_engine {
   int nranks = 1, rank = 0;
   mtsac_allreduce_fn hook = nullptr;
   void* hook_user = nullptr;
+  // collective hook with the sharded optimizer's ops (mtsac_set_collective_hook)
+  mtsac_collective_fn chook = nullptr;
+  void* chook_user = nullptr;
+  int hook_rank = 0, hook_world = 1;
+  // sharded trunk optimizer (ZeRO-1 style, optimize_zero): requested / in force for this step [actor, critic]
+  int zero_req = [] {
+    const char* v = getenv("MTSAC_ZERO");
+    return v ? atoi(v) : 0;
+  }();
+  bool zstep[2] = {false, false};
+  float* zparts = nullptr;  // shard |g|^2 partials
+  float* zscr = nullptr;    // the shard Adam launch's |p|^2 partials (the refresh launch's are the ones used)
   std::string comm_error;
   // timing
   bool timing = false;
@@ -935,31 +947,77 @@ struct mtsac_engine {
     return hp;
   }
 
-  void allreduce(float* buf, size_t count) {
-    if (comm == nullptr && cmodel.nranks > 1) {
+  void allreduce(float* buf, size_t count) { coll(0, buf, count); }
+
+  // op 0: all-reduce (sum); 1: reduce-scatter in place (this rank's shard of buf holds the sum);
+  // 2: all-gather in place (every rank's shard from its owner).  On the current stream.
+  void coll(int op, float* buf, size_t count) {
+    if (comm == nullptr && cmodel.nranks > 1) {  // one GPU: the link time of the op, the data as they are
       coll_model_allreduce(buf, (long long)count, cmodel.nranks, cmodel.gbps, cmodel.blocks,
-                           cmodel.poison ? cm_shadow : nullptr, cur);
+                           cmodel.poison ? cm_shadow : nullptr, cur, op == 0 ? 1.0 : 0.5);
       return;
     }
     if (comm != nullptr) {
-      ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm, cur);
+      const size_t sh = count / (size_t)nranks;
+      ncclResult_t r = op == 0   ? ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm, cur)
+                       : op == 1 ? ncclReduceScatter(buf, buf + (size_t)rank * sh, sh, ncclFloat32, ncclSum, comm, cur)
+                                 : ncclAllGather(buf + (size_t)rank * sh, buf, sh, ncclFloat32, comm, cur);
       while (r == ncclInProgress) {  // non-blocking communicator: the enqueue completes asynchronously
         std::this_thread::sleep_for(std::chrono::microseconds(20));
         if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) break;
       }
-      if (r != ncclSuccess) comm_error = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
+      if (r != ncclSuccess) comm_error = std::string("RCCL collective ") + std::to_string(op) + ": " + ncclGetErrorString(r);
       return;
     }
-    if (hook) {
+    if (chook || hook) {
       if (hipStreamSynchronize(cur) != hipSuccess) {
-        comm_error = "stream sync before all-reduce hook failed";
+        comm_error = "stream sync before the collective hook failed";
         return;
       }
-      if (hook(hook_user, buf, (int64_t)count) != 0) comm_error = "all-reduce hook failed";
+      if (chook) {
+        if (chook(chook_user, op, buf, (int64_t)count) != 0) comm_error = "collective hook failed";
+      } else if (op != 0) {
+        comm_error = "an all-reduce hook cannot reduce-scatter / all-gather";
+      } else if (hook(hook_user, buf, (int64_t)count) != 0) {
+        comm_error = "all-reduce hook failed";
+      }
     }
   }
 
-  bool sharded() const { return comm != nullptr || hook != nullptr || cmodel.nranks > 1; }
+  bool sharded() const { return comm != nullptr || hook != nullptr || chook != nullptr || cmodel.nranks > 1; }
+  int coll_world() const { return comm ? nranks : cmodel.nranks > 1 ? cmodel.nranks : chook ? hook_world : 1; }
+  int coll_rank() const { return comm ? rank : chook ? hook_rank : 0; }
+
+  // the trunk's all-reduce buckets of a network in issue order: hidden layers top-down (b_i, W_i), then
+  // layer 0 (b_0, W_0); the whole trunk for a one-layer net
+  int zero_buckets(const Net& net, long long* b, long long* e) const {
+    int k = 0;
+    if (net.depth <= 1) {
+      b[0] = net.trunk_off;
+      e[0] = net.n_flat;
+      return 1;
+    }
+    for (int i = net.depth - 1; i >= 1; --i) {
+      b[k] = net.off_b[i];
+      e[k++] = (i + 1 < net.depth) ? net.off_b[i + 1] : net.n_flat;
+    }
+    b[k] = net.trunk_off;
+    e[k++] = net.off_b[1];
+    return k;
+  }
+  // the sharded optimizer applies: requested, a device collective or a collective hook with world > 1,
+  // and world divides every bucket into whole float4s
+  bool zero_ok(const Net& net) const {
+    const int W = coll_world();
+    if (zero_req <= 0 || W <= 1 || !(comm || cmodel.nranks > 1 || chook) || zparts == nullptr) return false;
+    long long b[MAXD + 1], e[MAXD + 1];
+    const int n = zero_buckets(net, b, e);
+    if (n > 8) return false;
+    for (int i = 0; i < n; ++i)
+      if ((e[i] - b[i]) % (4LL * W) != 0) return false;
+    return true;
+  }
+  bool zero_of(const Net& net) const { return zstep[&net == &critic ? 1 : 0]; }
 
   // clip + Adam (+ Polyak) over one network; gradient already complete (and reduced).  Two launches
   // (optim.hip sumsq2 + adam_fused): the |g|^2 partials (and the Adam count), then one update pass
@@ -968,11 +1026,120 @@ struct mtsac_engine {
   // on every rank); sharded, the heads' |g|^2 is the all-reduced scalar head_sq() left in the tail.
   // |p_new|^2 partials stay per network and are summed in the last segment (norms_and_logs).
   void optimize(Net& net, float lr, float max_norm, bool polyak, int slot) {
+    if (zero_of(net)) {
+      optimize_zero(net, lr, max_norm, polyak, slot);
+      return;
+    }
     float* extra = net.g + net.n_flat;
     int gh = 0;
     const int gt = sumsq2(sharded() ? nullptr : net.g, net.trunk_off, net.g + net.trunk_off, net.n_flat - net.trunk_off,
                           net.hparts, net.gparts, net.sc, &gh, cur);
-    AdamParams a{};
+    AdamParams a{}, at{};
+    TileParams tp{};
+    opt_params(net, lr, polyak, a, at, tp);
+    FusedOpt f{};
+    f.gparts = net.gparts;
+    f.ng = gt;
+    f.hparts = net.hparts;
+    f.nh = gh;
+    f.head_sq = sharded() ? extra + 0 : nullptr;
+    f.max_norm = max_norm;
+    f.ph = net.pph;
+    f.pt = net.ppt;
+    adam_fused(a, at, tp, f, cur);
+    net.n_pph = f.bh;
+    net.n_ppt = f.bt + f.btile;
+    wgrid[&net == &critic ? 1 : 0] = f.bh + f.bt + f.btile;
+    wbh[&net == &critic ? 1 : 0] = f.bh;
+    if (sharded()) sum_partials(net.pph, f.bh, pn + 2 + slot, cur);  // the heads' |p|^2, all-reduced later
+  }
+
+  // Sharded trunk optimizer (ZeRO-1 style, mtsac_set_sharded_optimizer).  The trunk buckets were
+  // reduce-scattered (backward_segs, reduce_rest); the heads' |g|^2 is in the scalar tail (head_sq).
+  //   1. |g|^2 of this rank's shards into the tail, the tail all-reduced: the global clip norm;
+  //   2. Adam on the heads (+ their Polyak) and on this rank's trunk shards only (fp32, no planes);
+  //   3. the new trunk all-gathered, bucket by bucket;
+  //   4. a refresh pass over heads and trunk without the Adam step: the trunk's Polyak target, the GEMM
+  //      planes, |p_new|^2 partials and (split2h) weight maxima, exactly as the fused optimizer leaves them.
+  void optimize_zero(Net& net, float lr, float max_norm, bool polyak, int slot) {
+    float* extra = net.g + net.n_flat;
+    const int W = coll_world(), R = coll_rank();
+    long long bb[MAXD + 1], be[MAXD + 1];
+    const int nb = zero_buckets(net, bb, be);
+    ShardRanges sr{};
+    long long lo[MAXD + 1], hi[MAXD + 1];  // this rank's shards, relative to the trunk start (floats)
+    for (int k = 0; k < nb; ++k) {
+      const long long sh = (be[k] - bb[k]) / W;
+      lo[k] = bb[k] + R * sh - net.trunk_off;
+      hi[k] = lo[k] + sh;
+      sr.b[k] = (bb[k] + R * sh) / 4;
+      sr.e[k] = (bb[k] + R * sh + sh) / 4;
+    }
+    sr.n = nb;
+    shard_sumsq_add(net.g, sr, zparts, extra + 0, net.sc, cur);  // bumps the Adam count too
+    allreduce(extra, (size_t)EXTRA);
+    AdamParams a{}, at{};
+    TileParams tp{};
+    opt_params(net, lr, polyak, a, at, tp);
+    // 2. the shard update: heads as always; the trunk elementwise over the shards only (everything else
+    // skipped), no tiles, no planes, no Polyak, no maxima
+    AdamParams as = at;
+    as.target = nullptr;
+    as.nseg = 0;
+    as.h2 = WeightH2{};
+    as.nskip = 0;
+    {
+      int ord[MAXD + 1];
+      for (int k = 0; k < nb; ++k) ord[k] = k;
+      std::sort(ord, ord + nb, [&](int x, int y) { return lo[x] < lo[y]; });
+      long long prev = 0;
+      for (int q = 0; q < nb; ++q) {
+        const int k = ord[q];
+        if (lo[k] > prev) {
+          as.skip_b[as.nskip] = prev / 4;
+          as.skip_e[as.nskip++] = lo[k] / 4;
+        }
+        prev = hi[k];
+      }
+      const long long n = net.n_flat - net.trunk_off;
+      if (prev < n) {
+        as.skip_b[as.nskip] = prev / 4;
+        as.skip_e[as.nskip++] = (n + 3) / 4;
+      }
+    }
+    AdamParams ah = a;
+    ah.h2 = WeightH2{};
+    TileParams none{};
+    FusedOpt f{};
+    f.head_sq = extra + 0;  // the all-reduced heads + trunk |g|^2
+    f.max_norm = max_norm;
+    f.ph = zscr;
+    f.pt = zscr + FUSED_HEAD_PARTS;
+    adam_fused(ah, as, none, f, cur);
+    // 3. the new trunk from its owners
+    for (int k = nb - 1; k >= 0; --k) coll(2, net.p + bb[k], (size_t)(be[k] - bb[k]));  // layer 0 first
+    // 4. refresh: no Adam step; heads without Polyak (done above), the trunk with it
+    AdamParams hr = a, tr = at;
+    hr.refresh = 1;
+    hr.target = nullptr;
+    tr.refresh = 1;
+    FusedOpt g{};
+    g.head_sq = extra + 0;
+    g.max_norm = max_norm;
+    g.ph = net.pph;
+    g.pt = net.ppt;
+    adam_fused(hr, tr, tp, g, cur);
+    net.n_pph = g.bh;
+    net.n_ppt = g.bt + g.btile;
+    wgrid[&net == &critic ? 1 : 0] = g.bh + g.bt + g.btile;
+    wbh[&net == &critic ? 1 : 0] = g.bh;
+    if (sharded()) sum_partials(net.pph, g.bh, pn + 2 + slot, cur);
+  }
+
+  // the fused optimizer's operands of one network: heads (a), trunk elementwise leaves (at) and the
+  // trunk's kernel tiles with their planes (tp)
+  void opt_params(Net& net, float lr, bool polyak, AdamParams& a, AdamParams& at, TileParams& tp) {
+    a = AdamParams{};
     a.p = net.p;
     a.m = net.m;
     a.v = net.v;
@@ -994,14 +1161,14 @@ struct mtsac_engine {
       a.h2.tparts = polyak ? tparts : nullptr;
     }
     a.n = net.trunk_off;  // heads
-    AdamParams at = a;    // trunk
+    at = a;               // trunk
     at.p += net.trunk_off;
     at.m += net.trunk_off;
     at.v += net.trunk_off;
     at.g += net.trunk_off;
     if (at.target) at.target += net.trunk_off;
     at.n = net.n_flat - net.trunk_off;
-    TileParams tp{};
+    tp = TileParams{};
     if (tiles_fusable(net)) {  // kernel leaves in tiles: natural + transposed planes from the update
       for (int i = 0; i < net.depth; ++i) {
         TileLeaf& lf = tp.leaf[tp.n++];
@@ -1031,21 +1198,6 @@ struct mtsac_engine {
           at.seg[at.nseg++] = PlaneSeg{net.off_W[i] - net.trunk_off, net.ms_W[i], net.E, net.wp[1][i], net.kps(i), 1};
       }
     }
-    FusedOpt f{};
-    f.gparts = net.gparts;
-    f.ng = gt;
-    f.hparts = net.hparts;
-    f.nh = gh;
-    f.head_sq = sharded() ? extra + 0 : nullptr;
-    f.max_norm = max_norm;
-    f.ph = net.pph;
-    f.pt = net.ppt;
-    adam_fused(a, at, tp, f, cur);
-    net.n_pph = f.bh;
-    net.n_ppt = f.bt + f.btile;
-    wgrid[&net == &critic ? 1 : 0] = f.bh + f.bt + f.btile;
-    wbh[&net == &critic ? 1 : 0] = f.bh;
-    if (sharded()) sum_partials(net.pph, f.bh, pn + 2 + slot, cur);  // the heads' |p|^2, all-reduced later
   }
 
   // gemm_x3f / gemm_x3s nets: every plane the GEMMs read comes out of the tiled update
@@ -1145,8 +1297,9 @@ struct mtsac_engine {
       wprev = seg({dprev, wprev}, 3, [&, i] { wgrad_layer(net, X, ldx, acts, actp, dz, dzp, i, M); });
       if (bucket && i > 0) {
         const long long b = net.off_b[i], e = (i + 1 < net.depth) ? net.off_b[i + 1] : net.n_flat;
-        rprev = rprev < 0 ? seg({wprev}, 4, [&, b, e] { allreduce(net.g + b, (size_t)(e - b)); })
-                          : seg({wprev, rprev}, 4, [&, b, e] { allreduce(net.g + b, (size_t)(e - b)); });
+        const int op = zero_of(net) ? 1 : 0;  // the sharded optimizer reduce-scatters
+        rprev = rprev < 0 ? seg({wprev}, 4, [&, b, e, op] { coll(op, net.g + b, (size_t)(e - b)); })
+                          : seg({wprev, rprev}, 4, [&, b, e, op] { coll(op, net.g + b, (size_t)(e - b)); });
       }
       if (i > 0) dprev = seg({dprev}, 1, [&, i] { dgrad_layer(net, params, acts, actp, dz, dzp, i, M); });
     }
@@ -1158,6 +1311,11 @@ struct mtsac_engine {
   // the trunk-gradient all-reduce left after backward_segs: everything, or (buckets) layer 0 and
   // the scalar tail
   void reduce_rest(Net& net) {
+    if (zero_of(net)) {  // layer 0's bucket (the whole trunk of a one-layer net); the tail in optimize_zero
+      const long long e = net.depth > 1 ? net.off_b[1] : net.n_flat;
+      coll(1, net.g + net.trunk_off, (size_t)(e - net.trunk_off));
+      return;
+    }
     if (sharded() && net.depth > 1) {
       allreduce(net.g + net.trunk_off, (size_t)(net.off_b[1] - net.trunk_off));
       allreduce(net.g + net.n_flat, (size_t)EXTRA);
@@ -1201,6 +1359,8 @@ struct mtsac_engine {
     rows = device_batch ? s_rows : inset[inset_cur].rows;
     if (!ev_rotate) ev_next = 0;
     segs.clear();
+    zstep[0] = zero_ok(actor);
+    zstep[1] = zero_ok(critic);
     const float* twp = cfg.use_task_weights ? tw : nullptr;
     PolicyParams pp{};
     pp.seed = cfg.noise_seed;
@@ -2098,6 +2258,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   if ((rc = e->alloc(&e->cache, (size_t)B * 5 * e->A))) return bad(rc);
   if ((rc = e->alloc(&e->dout_a, (size_t)B * 2 * e->A))) return bad(rc);
   if ((rc = e->alloc(&e->partials, 2 * PART))) return bad(rc);  // elementwise + tiled update
+  if ((rc = e->alloc(&e->zparts, 256)) || (rc = e->alloc(&e->zscr, 2048))) return bad(rc);  // sharded optimizer
   if ((rc = e->alloc(&e->pn, 4))) return bad(rc);
   if ((rc = e->alloc(&e->log_alpha, e->T_g))) return bad(rc);
   if ((rc = e->alloc(&e->la_m, e->T_g))) return bad(rc);
@@ -2641,11 +2802,11 @@ int mtsac_task_gradient_stats(mtsac_engine* h, int which, const float* threshold
 int mtsac_update_many(mtsac_engine* h, int32_t steps) {
   if (!h) return fail(-22, "null engine");
   if (steps <= 0) return 0;
-  if (!h->use_graph || h->timing || h->hook) {  // events / host hooks need eager issue
+  if (!h->use_graph || h->timing || h->hook || h->chook) {  // events / host hooks need eager issue
     h->tl_next = 0;  // timing records every launch of this call
     // consecutive steps overlap (the last one joins every lane into the main stream); host hooks
     // (the bring-your-own all-reduce, which blocks the issuing thread) keep whole steps
-    const bool pipe = !h->hook && h->pipeline_on();
+    const bool pipe = !h->hook && !h->chook && h->pipeline_on();
     for (int s = 0; s < steps; ++s) h->step(true, true, pipe, s + 1 == steps);
     HIP_TRY(hipGetLastError());
     return 0;
@@ -2857,6 +3018,24 @@ int mtsac_set_allreduce_hook(mtsac_engine* h, mtsac_allreduce_fn fn, void* user)
   if (!h) return fail(-22, "null engine");
   h->hook = fn;
   h->hook_user = user;
+  if (fn) h->chook = nullptr;
+  return 0;
+}
+
+int mtsac_set_collective_hook(mtsac_engine* h, mtsac_collective_fn fn, void* user, int32_t rank, int32_t world) {
+  if (!h) return fail(-22, "null engine");
+  if (fn && (world < 1 || rank < 0 || rank >= world)) return fail(-22, "bad rank / world");
+  h->chook = fn;
+  h->chook_user = user;
+  h->hook_rank = fn ? rank : 0;
+  h->hook_world = fn ? world : 1;
+  if (fn) h->hook = nullptr;
+  return 0;
+}
+
+int mtsac_set_sharded_optimizer(mtsac_engine* h, int32_t on) {
+  if (!h) return fail(-22, "null engine");
+  h->zero_req = on ? 1 : 0;
   return 0;
 }
 
@@ -2912,7 +3091,7 @@ int mtsac_debug_set_pipeline(mtsac_engine* h, int32_t on) {
 
 int mtsac_debug_set_collective_model(mtsac_engine* h, int32_t nranks, double bus_gbps, int32_t flags) {
   if (!h) return fail(-22, "null engine");
-  if (h->comm || h->hook) return fail(-16, "a communicator or all-reduce hook is installed");
+  if (h->comm || h->hook || h->chook) return fail(-16, "a communicator or collective hook is installed");
   if (nranks < 1 || (nranks > 1 && !(bus_gbps > 0.0))) return fail(-22, "nranks >= 1 and bus_gbps > 0");
   HIP_TRY(hipStreamSynchronize(h->st));
   h->cmodel.nranks = nranks;

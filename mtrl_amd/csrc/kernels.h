@@ -374,7 +374,7 @@ void reduce_rows(const float* const* ins, int n_in, int B, float* out, hipStream
 // workgroups on the stream; shadow non-null: the bucket is NaN until the delay is over
 double coll_model_us(long long bytes, int nranks, double bus_gbps);
 void coll_model_allreduce(float* buf, long long count, int nranks, double bus_gbps, int blocks, float* shadow,
-                          hipStream_t st);
+                          hipStream_t st, double scale = 1.0);
 // partial sums of squares of x[0..n) into partials[grid]; returns grid size used
 int sumsq_partials(const float* x, long long n, float* partials, int max_blocks, hipStream_t st);
 // optimizer scalars: sums partials, computes norm and clip scale
@@ -420,6 +420,8 @@ struct AdamParams {
   int nskip;            // float4 ranges [skip_b, skip_e) of p left to adam_update_tiles
   long long skip_b[MAX_PLANE_SEGS], skip_e[MAX_PLANE_SEGS];
   WeightH2 h2;          // np == 2
+  int refresh;          // 1: no Adam step -- p is already the new value (the sharded optimizer's all-gathered
+                        // trunk); Polyak (target non-null), planes, |p|^2 and maxima as usual
 };
 // p_partials accumulate |p_new|^2 over [norm_from, n) only (the replicated trunk range)
 int adam_update(const AdamParams& a, float max_norm, long long norm_from, int max_blocks, hipStream_t st);
@@ -466,6 +468,13 @@ struct FusedOpt {
 int sumsq2(const float* h, long long nh, const float* t, long long nt, float* hparts, float* tparts, OptScalars* sc,
            int* gh_out, hipStream_t st);
 void adam_fused(const AdamParams& ah, const AdamParams& at, const TileParams& tp, FusedOpt& f, hipStream_t st);
+// Sharded trunk optimizer (ZeRO-1, engine.cpp optimize_zero): |g|^2 over this rank's shard of every
+// reduce-scattered bucket, added to *out (partials summed in a fixed order), and the Adam count bumped
+struct ShardRanges {
+  long long b[8], e[8];  // float4 index ranges of g
+  int n;
+};
+void shard_sumsq_add(const float* g, const ShardRanges& r, float* partials, float* out, OptScalars* sc, hipStream_t st);
 struct PnormParts {  // [0] critic, [1] actor
   const float* pt[2]; int nt[2];
   const float* ph[2]; int nh[2];

@@ -135,31 +135,37 @@ __device__ inline float adam_elems(const AdamParams& a, const AdamConsts& k, lon
     bool skip = false;
     for (int q = 0; q < a.nskip; ++q) skip |= i >= a.skip_b[q] && i < a.skip_e[q];
     if (skip) continue;  // a tiled leaf (adam_tiles)
-    float4 g = g4[i], p = p4[i], m = m4[i], v = v4[i];
-    float* gp = &g.x;
+    float4 p = p4[i];
     float* pp = &p.x;
-    float* mp = &m.x;
-    float* vp = &v.x;
     float sq = 0.f;
+    if (a.refresh) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      float gk = gp[c];
-      if (k.clip) gk = (gk / k.gn) * k.max_norm;
-      mp[c] = k.omb1 * gk + a.b1 * mp[c];
-      vp[c] = k.omb2 * (gk * gk) + a.b2 * vp[c];
-      const float mh = mp[c] / k.bc1;
-      const float vh = vp[c] / k.bc2;
-      const float u = mh / (sqrtf(vh) + a.eps);
-      pp[c] = pp[c] + u * k.neg_lr;
-      sq += pp[c] * pp[c];
+      for (int c = 0; c < 4; ++c) sq += pp[c] * pp[c];
+    } else {
+      float4 g = g4[i], m = m4[i], v = v4[i];
+      float* gp = &g.x;
+      float* mp = &m.x;
+      float* vp = &v.x;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float gk = gp[c];
+        if (k.clip) gk = (gk / k.gn) * k.max_norm;
+        mp[c] = k.omb1 * gk + a.b1 * mp[c];
+        vp[c] = k.omb2 * (gk * gk) + a.b2 * vp[c];
+        const float mh = mp[c] / k.bc1;
+        const float vh = vp[c] / k.bc2;
+        const float u = mh / (sqrtf(vh) + a.eps);
+        pp[c] = pp[c] + u * k.neg_lr;
+        sq += pp[c] * pp[c];
+      }
+      p4[i] = p;
+      m4[i] = m;
+      v4[i] = v;
     }
     if (i >= norm_from4) acc += sq;  // |p|^2 of the replicated (trunk) range only
     pmx = fmaxf(pmx, fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fmaxf(fabsf(p.z), fabsf(p.w))));
-    p4[i] = p;
-    m4[i] = m;
-    v4[i] = v;
     float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (POLYAK) {
+    if (POLYAK && t4 != nullptr) {
       t = t4[i];
       t.x = a.tau * p.x + k.omtau * t.x;
       t.y = a.tau * p.y + k.omtau * t.y;
@@ -248,29 +254,37 @@ __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, co
       float4 p = make_float4(0.f, 0.f, 0.f, 0.f), tv = p;
       if (r < lf.rows && c < lf.cols) {
         const long long i4 = (base + (long long)r * lf.cols + c) >> 2;
-        float4 g = reinterpret_cast<const float4*>(a.g)[i4];
-        float4 m = reinterpret_cast<float4*>(a.m)[i4], v = reinterpret_cast<float4*>(a.v)[i4];
         p = reinterpret_cast<float4*>(a.p)[i4];
-        float* gp = &g.x;
         float* pp = &p.x;
-        float* mp = &m.x;
-        float* vp = &v.x;
+        if (a.refresh) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float gk = gp[q];
-          if (k.clip) gk = (gk / k.gn) * k.max_norm;
-          mp[q] = k.omb1 * gk + a.b1 * mp[q];
-          vp[q] = k.omb2 * (gk * gk) + a.b2 * vp[q];
-          const float mh = mp[q] / k.bc1;
-          const float vh = vp[q] / k.bc2;
-          const float u = mh / (sqrtf(vh) + a.eps);
-          pp[q] = pp[q] + u * k.neg_lr;
-          acc += pp[q] * pp[q];
-          pmx = fmaxf(pmx, fabsf(pp[q]));
+          for (int q = 0; q < 4; ++q) {
+            acc += pp[q] * pp[q];
+            pmx = fmaxf(pmx, fabsf(pp[q]));
+          }
+        } else {
+          float4 g = reinterpret_cast<const float4*>(a.g)[i4];
+          float4 m = reinterpret_cast<float4*>(a.m)[i4], v = reinterpret_cast<float4*>(a.v)[i4];
+          float* gp = &g.x;
+          float* mp = &m.x;
+          float* vp = &v.x;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float gk = gp[q];
+            if (k.clip) gk = (gk / k.gn) * k.max_norm;
+            mp[q] = k.omb1 * gk + a.b1 * mp[q];
+            vp[q] = k.omb2 * (gk * gk) + a.b2 * vp[q];
+            const float mh = mp[q] / k.bc1;
+            const float vh = vp[q] / k.bc2;
+            const float u = mh / (sqrtf(vh) + a.eps);
+            pp[q] = pp[q] + u * k.neg_lr;
+            acc += pp[q] * pp[q];
+            pmx = fmaxf(pmx, fabsf(pp[q]));
+          }
+          reinterpret_cast<float4*>(a.p)[i4] = p;
+          reinterpret_cast<float4*>(a.m)[i4] = m;
+          reinterpret_cast<float4*>(a.v)[i4] = v;
         }
-        reinterpret_cast<float4*>(a.p)[i4] = p;
-        reinterpret_cast<float4*>(a.m)[i4] = m;
-        reinterpret_cast<float4*>(a.v)[i4] = v;
         if (POLYAK) {
           tv = reinterpret_cast<float4*>(a.target)[i4];
           tv.x = a.tau * p.x + k.omtau * tv.x;
@@ -444,6 +458,35 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(AdamParams ah, AdamPara
       }
     }
   }
+}
+
+// the sharded optimizer's |g|^2: per block over this rank's shard ranges; block 0 bumps the Adam count
+__global__ __launch_bounds__(256) void shard_sumsq_kernel(const float* __restrict__ g, ShardRanges r,
+                                                          float* __restrict__ part, OptScalars* sc) {
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  float acc = 0.f;
+  for (int q = 0; q < r.n; ++q)
+    for (long long i = r.b[q] + (long long)blockIdx.x * 256 + threadIdx.x; i < r.e[q]; i += (long long)gridDim.x * 256) {
+      const float4 v = g4[i];
+      acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+  acc = block_sum256(acc);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = acc;
+    if (blockIdx.x == 0) sc->count += 1;
+  }
+}
+
+// *out += sum(partials) in a fixed order (one block, double accumulation)
+__global__ __launch_bounds__(256) void sum_partials_add_kernel(const float* __restrict__ partials, int nparts,
+                                                               float* __restrict__ out) {
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) acc += (double)partials[i];
+  acc = wsumd(acc);
+  __shared__ double s[4];
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = (float)((double)*out + ((s[0] + s[1]) + (s[2] + s[3])));
 }
 
 // |g|^2 partials of a network: blocks [0, gh) over the heads' range, [gh, gh + gt) over the trunk's;
@@ -809,6 +852,15 @@ void adam_fused(const AdamParams& ah, const AdamParams& at, const TileParams& tp
     hipLaunchKernelGGL(adam_fused_kernel<true>, grid, dim3(256), 0, st, ah, at, tp, f);
   else
     hipLaunchKernelGGL(adam_fused_kernel<false>, grid, dim3(256), 0, st, ah, at, tp, f);
+}
+
+void shard_sumsq_add(const float* g, const ShardRanges& r, float* partials, float* out, OptScalars* sc,
+                     hipStream_t st) {
+  long long n4 = 0;
+  for (int q = 0; q < r.n; ++q) n4 += r.e[q] - r.b[q];
+  const int G = (int)std::max<long long>(1, std::min<long long>(256, (n4 + 1023) / 1024));
+  hipLaunchKernelGGL(shard_sumsq_kernel, dim3(G), dim3(256), 0, st, g, r, partials, sc);
+  hipLaunchKernelGGL(sum_partials_add_kernel, dim3(1), dim3(256), 0, st, partials, G, out);
 }
 
 void sum_partials(const float* partials, int nparts, float* out, hipStream_t st) {

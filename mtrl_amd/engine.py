@@ -314,6 +314,33 @@ class MTSACEngine:
         self._hook = _lib.ALLREDUCE_FN(tramp)
         check(self.lib.mtsac_set_allreduce_hook(self._h, ctypes.cast(self._hook, ctypes.c_void_p), None))
 
+    def set_collective_hook(self, fn, rank: int, world: int) -> None:
+        """``fn(op, device_ptr, count)``: op 0 all-reduce (sum), 1 reduce-scatter in place (this rank's
+        shard [rank count / world, (rank + 1) count / world) must hold the sum), 2 all-gather in place
+        (include/mtsac.h mtsac_set_collective_hook)."""
+        if fn is None:
+            self._hook = None
+            check(self.lib.mtsac_set_collective_hook(self._h, None, None, 0, 1))
+            return
+
+        def tramp(_user, op, ptr, count):
+            try:
+                fn(op, ptr, count)
+                return 0
+            except Exception:  # pragma: no cover - reported through the engine
+                import traceback
+
+                traceback.print_exc()
+                return -1
+
+        self._hook = _lib.COLLECTIVE_FN(tramp)
+        check(self.lib.mtsac_set_collective_hook(self._h, ctypes.cast(self._hook, ctypes.c_void_p), None, rank, world))
+
+    def set_sharded_optimizer(self, on: bool) -> None:
+        """ZeRO-1-style sharded trunk optimizer for task-sharded runs (include/mtsac.h
+        mtsac_set_sharded_optimizer): reduce-scatter, Adam on 1/world of the trunk, all-gather."""
+        check(self.lib.mtsac_set_sharded_optimizer(self._h, 1 if on else 0))
+
     # ------------------------------------------------------------------ measurement
     def set_timing(self, on: bool, serial: bool = False) -> None:
         """HIP-event timing of every GEMM launch of the next update call(s); serial=True runs

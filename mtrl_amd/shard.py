@@ -69,6 +69,36 @@ class InProcessAllReduce:
         return fn
 
 
+class InProcessCollectives(InProcessAllReduce):
+    """All-reduce, reduce-scatter and all-gather between engines on threads of one process, for
+    :meth:`MTSACEngine.set_collective_hook` (the sharded optimizer's collectives).  Host-staged."""
+
+    def collective_hook(self, rank: int):
+        lib = _lib.load()
+        world = self.world
+
+        def fn(op: int, ptr: int, count: int) -> None:
+            host = np.empty(count, np.float32)
+            _lib.check(lib.mtsac_memcpy(host.ctypes.data, ptr, count * 4))
+            self.bufs[rank] = host
+            if self.barrier.wait() == 0:
+                if op == 2:  # all-gather: shard r from rank r
+                    sh = count // world
+                    acc = np.empty(count, np.float32)
+                    for r, b in enumerate(self.bufs):
+                        acc[r * sh:(r + 1) * sh] = b[r * sh:(r + 1) * sh]
+                else:  # all-reduce / reduce-scatter: the sum (rank order), written whole
+                    acc = self.bufs[0].copy()
+                    for b in self.bufs[1:]:
+                        acc += b
+                self.total = acc
+            self.barrier.wait()
+            _lib.check(lib.mtsac_memcpy(ptr, self.total.ctypes.data, count * 4))
+            self.barrier.wait()
+
+        return fn
+
+
 def allreduce_floats_per_step(obs_dim: int, action_dim: int, actor_width: int, actor_depth: int, critic_width: int,
                               critic_depth: int, num_critics: int) -> int:
     """Floats one rank all-reduces per gradient step: each network's contiguous trunk range

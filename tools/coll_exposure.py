@@ -5,6 +5,8 @@ section 4).  Two modes:
                                 all-reduce (mtsac_debug_set_collective_model: at every RCCL point a delay of
                                 2 (N - 1) / N x bucket bytes over GBPS, on the collective stream); run it
                                 under rocprofv3 --kernel-trace
+  classes TRACE.csv [N]         any bucketing (the sharded optimizer's too): modelled and exposed time per
+                                step by op class (N = critic hidden-layer ops per step: 2, or 4 sharded)
   parse TRACE.csv               per bucket (cm_delay_kernel launch, in issue order) of the last full steps:
                                 its modelled length, how much of it the compute streams cover, and the
                                 exposed rest; plus the step wall time
@@ -110,8 +112,42 @@ def parse(path):
     print(f"{'sum':22s} {'':11s} {'':11s} {tot:11.1f}")
 
 
+def parse_classes(path, per_step_big):
+    """Any bucketing (the sharded optimizer's reduce-scatters and all-gathers too): the delays by
+    modelled-length class -- critic hidden-layer ops (the longest), actor hidden-layer ops (about half),
+    the rest -- their modelled and exposed time per step; per_step_big = critic hidden-layer ops per step
+    (2 all-reduce, 4 reduce-scatter + all-gather)."""
+    rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                  for r in csv.DictReader(open(path)))
+    delays = [(s, e) for s, e, n in rows if "cm_delay" in n]
+    comp = [(s, e) for s, e, n in rows if "cm_" not in n]
+    big = max(e - s for s, e in delays)
+    firsts = [s for s, e in delays if e - s > 0.75 * big]
+    # skip the warm-up step and the last (partial) one
+    t0, t1 = firsts[per_step_big], firsts[-per_step_big]
+    out = {"critic hidden-layer ops": [0.0, 0.0], "actor hidden-layer ops": [0.0, 0.0], "other": [0.0, 0.0]}
+    for s, e in delays:
+        if not (t0 <= s < t1):
+            continue
+        d = e - s
+        k = "critic hidden-layer ops" if d > 0.75 * big else "actor hidden-layer ops" if d > 0.35 * big else "other"
+        cov = union([(max(s, cs), min(e, ce)) for cs, ce in comp if cs < e and ce > s])
+        out[k][0] += d
+        out[k][1] += d - cov
+    steps = sum(1 for f in firsts if t0 <= f < t1) / per_step_big
+    print(f"steps {steps:.0f}: wall {(t1 - t0) / steps / 1e3:.1f} us per step")
+    print(f"{'class':26s} {'modelled us':>11s} {'exposed us':>11s}   (per step)")
+    tot = 0.0
+    for k, (m, x) in out.items():
+        tot += x
+        print(f"{k:26s} {m / steps / 1e3:11.1f} {x / steps / 1e3:11.1f}")
+    print(f"{'sum':26s} {'':11s} {tot / steps / 1e3:11.1f}")
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "run":
         run(int(sys.argv[2]), float(sys.argv[3]), sys.argv[4])
+    elif sys.argv[1] == "classes":
+        parse_classes(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 2)
     else:
         parse(sys.argv[2])
