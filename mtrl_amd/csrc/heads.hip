@@ -106,6 +106,11 @@ __device__ inline void policy_finish(const PolicyParams& p, int b, int t, const 
   const HeadParams& hp = p.head;
   const int A = p.A;
   float term = 0.f;
+  // the row's loads before the lane test (a load inside it was waited for at the branch's end, one
+  // round trip per row): lanes >= A read lane 0's entries and drop them
+  const int lj = lane < A ? lane : 0;
+  const float bmu = hp.bh[t * HD + lj], bls = hp.bh[t * HD + A + lj];
+  const float eps_in = p.eps != nullptr ? p.eps[(long long)b * A + lj] : 0.f;
   if (lane < A) {
     // pick acc[j], acc[A+j] with a static unroll
     float mu = 0.f, ls = 0.f;
@@ -114,11 +119,11 @@ __device__ inline void policy_finish(const PolicyParams& p, int b, int t, const 
       if (o == lane) mu = acc[o];
       if (o == lane + A) ls = acc[o];
     }
-    mu += hp.bh[t * HD + lane];
-    ls += hp.bh[t * HD + A + lane];
+    mu += bmu;
+    ls += bls;
     float eps;
     if (p.eps != nullptr) {
-      eps = p.eps[(long long)b * A + lane];
+      eps = eps_in;
     } else {
       float nz[4];
       normal4(p.seed, p.stream_id + 16u * (uint32_t)(lane >> 2), *p.counter, (uint32_t)b, nz);
@@ -227,8 +232,19 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
   const HeadParams& hp = p.head;
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
   float dqmax = 0.f;
-  for (int b = wid; b < hp.B; b += gridDim.x * 4) {
-  const int t = hp.task[b];
+  const int stride = gridDim.x * 4;
+  int t_next = wid < hp.B ? hp.task[wid] : 0;  // the next row's task, loaded one row ahead
+  for (int b = wid; b < hp.B; b += stride) {
+  const int t = t_next;
+  if (b + stride < hp.B) t_next = hp.task[b + stride];
+  // the row's scalars, loaded by every lane before the head dot products (a load inside the lane-0
+  // tail below was waited for one at a time, several round trips per row)
+  const float la_t = p.log_alpha[p.task_begin + t];
+  const float w_t = p.tw != nullptr ? p.tw[b] : 1.f;
+  const float lp_b = (p.mode != CH_CRITIC || p.fused_target) ? p.logpi[b] : 0.f;
+  const float rew_b = (p.mode == CH_TARGET || p.fused_target) ? p.rew[b] : 0.f;
+  const float done_b = (p.mode == CH_TARGET || p.fused_target) ? p.done[b] : 0.f;
+  const float y_b = (p.mode == CH_CRITIC && !p.fused_target) ? p.y[b] : 0.f;
   float q[4];
   const int E = hp.E;
   for (int e = 0; e < E; ++e) {
@@ -246,14 +262,13 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
     }
   }
   if (lane != 0) continue;
-  const float alpha = expf(p.log_alpha[p.task_begin + t]);  // exp(onehot . log_alpha), mtsac.py:60-63
-  float w = 1.f;
-  if (p.tw != nullptr) w = p.tw[b];  // T * softmax(-log_alpha)[t] (mtsac.py:103-113)
+  const float alpha = expf(la_t);  // exp(onehot . log_alpha), mtsac.py:60-63
+  const float w = w_t;             // T * softmax(-log_alpha)[t] (mtsac.py:103-113), or 1
   auto td_target = [&](const float* qq) {
     float mn = qq[0];
     for (int e = 1; e < E; ++e) mn = fminf(mn, qq[e]);
-    const float mnext = mn - alpha * p.logpi[b];
-    float y = p.rew[b] + (1.0f - p.done[b]) * p.gamma * mnext;  // mtsac.py:547-553
+    const float mnext = mn - alpha * lp_b;
+    float y = rew_b + (1.0f - done_b) * p.gamma * mnext;  // mtsac.py:547-553
     if (p.clip) y = fminf(fmaxf(y, -5000.f), 5000.f);
     p.y_out[b] = y;
     return y;
@@ -261,7 +276,7 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
   if (p.mode == CH_TARGET) {
     td_target(q);
   } else if (p.mode == CH_CRITIC) {
-    const float y = p.fused_target ? td_target(qt) : p.y[b];
+    const float y = p.fused_target ? td_target(qt) : y_b;
     float sq = 0.f, qs = 0.f;
     for (int e = 0; e < E; ++e) {
       float qc = q[e], dcl = 1.f;
@@ -288,7 +303,7 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
       p.dq[e * hp.B + b] = g;
       dqmax = fmaxf(dqmax, fabsf(g));
     }
-    p.row_a[b] = w * (alpha * p.logpi[b] - mn);
+    p.row_a[b] = w * (alpha * lp_b - mn);
     p.alpha_w[b] = w * alpha * p.inv_norm;
   }
   }  // rows
@@ -303,10 +318,10 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
 // grad needs no pass over an fp32 dz.  dz (fp32) may be null.
 constexpr int HB_RS = 4;
 
+// the masked data grad of row b at columns w .. w + 3 (loads only)
 template <int HD>
-__device__ inline float4 head_bwd_row(const HeadParams& hp, const float* __restrict__ dout, long long s_dout, int e,
-                                      int b, int w, const float (&wt)[4][HD], float* __restrict__ dz,
-                                      const PlaneOut& po) {
+__device__ inline float4 head_bwd_val(const HeadParams& hp, const float* __restrict__ dout, long long s_dout, int e,
+                                      int b, int w, const float (&wt)[4][HD]) {
   const float* d = dout + e * s_dout + (long long)b * HD;
   float g[4];
 #pragma unroll
@@ -316,13 +331,20 @@ __device__ inline float4 head_bwd_row(const HeadParams& hp, const float* __restr
     for (int o = 0; o < HD; ++o) s += d[o] * wt[k][o];
     g[k] = s;
   }
-  const long long off = e * hp.sh + (long long)b * hp.W + w;
-  const float4 h = *reinterpret_cast<const float4*>(hp.h + off);
+  const float4 h = *reinterpret_cast<const float4*>(hp.h + e * hp.sh + (long long)b * hp.W + w);
   float4 out;
   out.x = h.x > 0.f ? g[0] : 0.f;
   out.y = h.y > 0.f ? g[1] : 0.f;
   out.z = h.z > 0.f ? g[2] : 0.f;
   out.w = h.w > 0.f ? g[3] : 0.f;
+  return out;
+}
+
+// its stores: fp32 dz (if any) and the GEMM planes
+template <int HD>
+__device__ inline void head_bwd_put(const HeadParams& hp, int e, int b, int w, float4 out, float* __restrict__ dz,
+                                    const PlaneOut& po) {
+  const long long off = e * hp.sh + (long long)b * hp.W + w;
   if (dz) *reinterpret_cast<float4*>(dz + off) = out;
   if (po.p && po.rc) {  // split2h: fp16 planes at the bound's exponent (oscale folded into po.kmul below)
     const float v[4] = {out.x, out.y, out.z, out.w};
@@ -355,6 +377,14 @@ __device__ inline float4 head_bwd_row(const HeadParams& hp, const float* __restr
     *reinterpret_cast<bf16x4*>(q + po.ps) = pm;
     *reinterpret_cast<bf16x4*>(q + 2 * po.ps) = pl;
   }
+}
+
+template <int HD>
+__device__ inline float4 head_bwd_row(const HeadParams& hp, const float* __restrict__ dout, long long s_dout, int e,
+                                      int b, int w, const float (&wt)[4][HD], float* __restrict__ dz,
+                                      const PlaneOut& po) {
+  const float4 out = head_bwd_val<HD>(hp, dout, s_dout, e, b, w, wt);
+  head_bwd_put<HD>(hp, e, b, w, out, dz, po);
   return out;
 }
 
@@ -388,19 +418,24 @@ __device__ inline void head_bwd_data_body(const HeadParams& hp, const float* __r
       for (int o = 0; o < HD; ++o) wt[k][o] = Wt[k * HD + o];
   }
   float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (ok) {
-    constexpr int STRIDE = 4 * HB_RS;
-    int j = 4 * rs + rl;
-    for (; j + STRIDE < n; j += 2 * STRIDE) {
-      const int b0 = rw[j], b1 = rw[j + STRIDE];
-      const float4 o0 = head_bwd_row<HD>(hp, dout, s_dout, e, b0, w, wt, dz, po);
-      const float4 o1 = head_bwd_row<HD>(hp, dout, s_dout, e, b1, w, wt, dz, po);
-      cs.x += o0.x; cs.y += o0.y; cs.z += o0.z; cs.w += o0.w;
-      cs.x += o1.x; cs.y += o1.y; cs.z += o1.z; cs.w += o1.w;
-    }
-    if (j < n) {
-      const float4 o0 = head_bwd_row<HD>(hp, dout, s_dout, e, rw[j], w, wt, dz, po);
-      cs.x += o0.x; cs.y += o0.y; cs.z += o0.z; cs.w += o0.w;
+  if (ok && n > 0) {
+    // CH rows per batch: their row indices, then their loads, all unconditional (clamped to the last
+    // row) so they are in flight together; the stores and sums of the rows past n are dropped.  Rows
+    // are added in ascending j as before.
+    constexpr int STRIDE = 4 * HB_RS, CH = 4;
+    for (int j0 = 4 * rs + rl; j0 < n; j0 += CH * STRIDE) {
+      int bb[CH];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) bb[u] = rw[min(j0 + u * STRIDE, n - 1)];
+      float4 o[CH];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) o[u] = head_bwd_val<HD>(hp, dout, s_dout, e, bb[u], w, wt);
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        if (j0 + u * STRIDE >= n) break;
+        head_bwd_put<HD>(hp, e, bb[u], w, o[u], dz, po);
+        cs.x += o[u].x; cs.y += o[u].y; cs.z += o[u].z; cs.w += o[u].w;
+      }
     }
   }
   if (dbp == nullptr) return;
@@ -592,7 +627,9 @@ __global__ __launch_bounds__(256) void head_bwd_both_kernel(HeadParams hp, const
 // AG_RW rows per wavefront: the critic layer-0 kernel rows (A x Wc) are read once per AG_RW rows
 // (4, or fewer on small task shards, see rows_per_wave).  Per row the sums run over the lane's w
 // (16-B chunks 4l + 256i when Wc % 4 == 0, else l + 64i), then over the wave.
-template <int AG_RW>
+// AM: action dimensions held per row -- 4 (MetaWorld: no run-time test around the weight loads, which
+// were otherwise waited for one at a time) or 8 (any A <= 8)
+template <int AG_RW, int AM>
 __global__ __launch_bounds__(256) void action_grad_kernel(ActionGradParams p) {
   const int lane = threadIdx.x & 63;
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -605,26 +642,27 @@ __global__ __launch_bounds__(256) void action_grad_kernel(ActionGradParams p) {
   int rows[AG_RW];
 #pragma unroll
   for (int r = 0; r < AG_RW; ++r) rows[r] = min(b0 + r, p.B - 1);
-  float ga[AG_RW][8];
+  float ga[AG_RW][AM];
 #pragma unroll
   for (int r = 0; r < AG_RW; ++r)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ga[r][j] = 0.f;
+    for (int j = 0; j < AM; ++j) ga[r][j] = 0.f;
   for (int e = 0; e < p.E; ++e) {
     const float* dz = p.dz1 + e * p.s_dz;
     const float* W0 = p.W0 + e * p.s_W0;
     if ((p.Wc & 3) == 0) {  // 16-B loads: lane l takes w = 4l + 256i .. +3
 #pragma unroll 2
       for (int w = 4 * lane; w < p.Wc; w += 256) {
-        float4 wv[8];
+        float4 wv[AM];
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          wv[j] = j < A ? *reinterpret_cast<const float4*>(W0 + (long long)j * p.Wc + w) : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < AM; ++j)
+          wv[j] = (AM == 4 || j < A) ? *reinterpret_cast<const float4*>(W0 + (long long)j * p.Wc + w)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int r = 0; r < AG_RW; ++r) {
           const float4 g = *reinterpret_cast<const float4*>(dz + (long long)rows[r] * p.Wc + w);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
+          for (int j = 0; j < AM; ++j) {
             float a = ga[r][j];
             a += g.x * wv[j].x;
             a += g.y * wv[j].y;
@@ -637,31 +675,41 @@ __global__ __launch_bounds__(256) void action_grad_kernel(ActionGradParams p) {
       continue;
     }
     for (int w = lane; w < p.Wc; w += 64) {
-      float wv[8];
+      float wv[AM];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) wv[j] = j < A ? W0[(long long)j * p.Wc + w] : 0.f;
+      for (int j = 0; j < AM; ++j) wv[j] = (AM == 4 || j < A) ? W0[(long long)j * p.Wc + w] : 0.f;
 #pragma unroll
       for (int r = 0; r < AG_RW; ++r) {
         const float g = dz[(long long)rows[r] * p.Wc + w];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ga[r][j] += g * wv[j];
+        for (int j = 0; j < AM; ++j) ga[r][j] += g * wv[j];
       }
     }
   }
   float omx = 0.f;
+  // every row's cache entries and temperature weight first (loads outside the row / lane tests)
+  const int lj = lane < A ? lane : 0;
+  float c_ls[AG_RW], c_a[AG_RW], c_eps[AG_RW], c_lp[AG_RW];
+#pragma unroll
+  for (int r = 0; r < AG_RW; ++r) {
+    const float* c = p.cache + (long long)rows[r] * 5 * A;
+    c_ls[r] = c[A + lj];
+    c_a[r] = c[3 * A + lj];
+    c_eps[r] = c[4 * A + lj];
+    c_lp[r] = p.alpha_w[rows[r]];
+  }
 #pragma unroll
   for (int r = 0; r < AG_RW; ++r) {
     const int b = b0 + r;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ga[r][j] = j < A ? wsum(ga[r][j]) : 0.f;
+    for (int j = 0; j < AM; ++j) ga[r][j] = j < A ? wsum(ga[r][j]) : 0.f;
     if (b >= p.B || lane >= A) continue;
     float g_a = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+    for (int j = 0; j < AM; ++j)
       if (j == lane) g_a = ga[r][j];
-    const float* c = p.cache + (long long)b * 5 * A;
-    const float ls = c[A + lane], a = c[3 * A + lane], eps = c[4 * A + lane];
-    const float g_logpi = p.alpha_w[b];
+    const float ls = c_ls[r], a = c_a[r], eps = c_eps[r];
+    const float g_logpi = c_lp[r];
     const float sigma = expf(fminf(fmaxf(ls, p.ls_min), p.ls_max));
     const float g_x = g_a * (1.0f - a * a) + g_logpi * 2.0f * a;  // d logpi/dx = 2 tanh(x)
     const float g_ls = (g_x * sigma * eps - g_logpi) * clip_grad(ls, p.ls_min, p.ls_max);
@@ -810,9 +858,13 @@ void action_grad(const ActionGradParams& p, hipStream_t st) {
   const int rw = rows_per_wave((p.B + 3) / 4);
   const dim3 grid((unsigned)((p.B + 4 * rw - 1) / (4 * rw)));
   if (p.dout_parts) *p.dout_parts = std::min<int>(4 * (int)grid.x, PLANE_REC_PARTS);
-  if (rw == 4) hipLaunchKernelGGL(action_grad_kernel<4>, grid, dim3(256), 0, st, p);
-  else if (rw == 2) hipLaunchKernelGGL(action_grad_kernel<2>, grid, dim3(256), 0, st, p);
-  else hipLaunchKernelGGL(action_grad_kernel<1>, grid, dim3(256), 0, st, p);
+#define AGL(AMV)                                                                                  \
+  if (rw == 4) hipLaunchKernelGGL((action_grad_kernel<4, AMV>), grid, dim3(256), 0, st, p);        \
+  else if (rw == 2) hipLaunchKernelGGL((action_grad_kernel<2, AMV>), grid, dim3(256), 0, st, p);   \
+  else hipLaunchKernelGGL((action_grad_kernel<1, AMV>), grid, dim3(256), 0, st, p);
+  if (p.A == 4) { AGL(4) }
+  else { AGL(8) }
+#undef AGL
 }
 
 void row_alpha(const int* task, int task_begin, const float* log_alpha, int T_glob, int B, int use_task_weights,
