@@ -1237,7 +1237,8 @@ struct mtsac_engine {
     cur_lane = lane;
     if (build) {
       std::vector<hipGraphNode_t> dn;
-      for (int d : deps) dn.push_back(segs[d].node);
+      for (int d : deps)  // a repeated dependency (s_afs = s_af unsplit) is an invalid graph edge list
+        if (std::find(dn.begin(), dn.end(), segs[d].node) == dn.end()) dn.push_back(segs[d].node);
       hipGraph_t g = nullptr;
       hipError_t r = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
       cur = st;

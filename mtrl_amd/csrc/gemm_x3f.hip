@@ -126,6 +126,8 @@ void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t s
     if (wv4) ablate_at<BM0, 1, 4>(p, abl, grid, st);
     else if (short8) ablate_at<BM0, 1, 8>(p, abl, grid, st);
     else ablate_at<400, 1, 8>(p, abl, grid, st);
+  } else if (p.np == 2) {  // split2h: 8 waves (the 4-wave form is not instantiated for it)
+    ablate_at<BM0, 2, 8>(p, abl, grid, st);
   } else if (wv4) {
     ablate_at<BM0, 3, 4>(p, abl, grid, st);
   } else if (abl == 4 || abl == 128 || abl == 512) {
