@@ -232,19 +232,8 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
   const HeadParams& hp = p.head;
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
   float dqmax = 0.f;
-  const int stride = gridDim.x * 4;
-  int t_next = wid < hp.B ? hp.task[wid] : 0;  // the next row's task, loaded one row ahead
-  for (int b = wid; b < hp.B; b += stride) {
-  const int t = t_next;
-  if (b + stride < hp.B) t_next = hp.task[b + stride];
-  // the row's scalars, loaded by every lane before the head dot products (a load inside the lane-0
-  // tail below was waited for one at a time, several round trips per row)
-  const float la_t = p.log_alpha[p.task_begin + t];
-  const float w_t = p.tw != nullptr ? p.tw[b] : 1.f;
-  const float lp_b = (p.mode != CH_CRITIC || p.fused_target) ? p.logpi[b] : 0.f;
-  const float rew_b = (p.mode == CH_TARGET || p.fused_target) ? p.rew[b] : 0.f;
-  const float done_b = (p.mode == CH_TARGET || p.fused_target) ? p.done[b] : 0.f;
-  const float y_b = (p.mode == CH_CRITIC && !p.fused_target) ? p.y[b] : 0.f;
+  for (int b = wid; b < hp.B; b += gridDim.x * 4) {
+  const int t = hp.task[b];
   float q[4];
   const int E = hp.E;
   for (int e = 0; e < E; ++e) {
@@ -262,13 +251,14 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
     }
   }
   if (lane != 0) continue;
-  const float alpha = expf(la_t);  // exp(onehot . log_alpha), mtsac.py:60-63
-  const float w = w_t;             // T * softmax(-log_alpha)[t] (mtsac.py:103-113), or 1
+  const float alpha = expf(p.log_alpha[p.task_begin + t]);  // exp(onehot . log_alpha), mtsac.py:60-63
+  float w = 1.f;
+  if (p.tw != nullptr) w = p.tw[b];  // T * softmax(-log_alpha)[t] (mtsac.py:103-113)
   auto td_target = [&](const float* qq) {
     float mn = qq[0];
     for (int e = 1; e < E; ++e) mn = fminf(mn, qq[e]);
-    const float mnext = mn - alpha * lp_b;
-    float y = rew_b + (1.0f - done_b) * p.gamma * mnext;  // mtsac.py:547-553
+    const float mnext = mn - alpha * p.logpi[b];
+    float y = p.rew[b] + (1.0f - p.done[b]) * p.gamma * mnext;  // mtsac.py:547-553
     if (p.clip) y = fminf(fmaxf(y, -5000.f), 5000.f);
     p.y_out[b] = y;
     return y;
@@ -276,7 +266,7 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
   if (p.mode == CH_TARGET) {
     td_target(q);
   } else if (p.mode == CH_CRITIC) {
-    const float y = p.fused_target ? td_target(qt) : y_b;
+    const float y = p.fused_target ? td_target(qt) : p.y[b];
     float sq = 0.f, qs = 0.f;
     for (int e = 0; e < E; ++e) {
       float qc = q[e], dcl = 1.f;
@@ -303,7 +293,7 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
       p.dq[e * hp.B + b] = g;
       dqmax = fmaxf(dqmax, fabsf(g));
     }
-    p.row_a[b] = w * (alpha * lp_b - mn);
+    p.row_a[b] = w * (alpha * p.logpi[b] - mn);
     p.alpha_w[b] = w * alpha * p.inv_norm;
   }
   }  // rows
