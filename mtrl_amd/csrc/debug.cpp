@@ -52,7 +52,8 @@ void plane_geom(int rows, int K, bool kmajor, long long& ld, long long& ps) {
   ps = (kmajor ? up32(K) : (long long)rows) * ld;
 }
 
-void split_into(const float* dsrc, int rows, int K, bool kmajor, __bf16* out, const int* e2h = nullptr) {
+void split_into(const float* dsrc, int rows, int K, bool kmajor, __bf16* out, const int* e2h = nullptr,
+                bool frag = false) {
   long long ld, ps;
   plane_geom(rows, K, kmajor, ld, ps);
   SplitParams s{};
@@ -66,6 +67,7 @@ void split_into(const float* dsrc, int rows, int K, bool kmajor, __bf16* out, co
   s.po = ps;
   s.out_cols = (int)ld;
   s.e2h = e2h;
+  s.frag = frag ? 1 : 0;
   split_planes(s, false, 1, nullptr);
 }
 
@@ -197,8 +199,10 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
   const bool autosplit = (epi >> 11) & 1;     // split-K by the launcher's own choice (workspace given)
   const bool fin = (epi >> 12) & 1;           // ... with arrival counters: the in-launch finish
   const bool h2 = (epi >> 13) & 1;            // precision split2h: fp16 planes scaled per tensor
+  const bool bfrag = (epi >> 14) & 1;         // B planes in the fragment layout (N % 16 == 0)
   epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || !A || !B || !C) return -22;
+  if (bfrag && N % 16 != 0) return -22;
   DevBuf d;
   const size_t nA = (size_t)M * K * batch, nB = (size_t)N * K * batch, nC = (size_t)M * N * batch;
   // split2h: records of A, B (its max covering the bias, as a trunk record does), the mask and C
@@ -252,7 +256,9 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
     s.x = dB + (size_t)z * N * K; s.rows = N;
     s.out = Bp + (size_t)z * 3 * N * Kp; s.po = (long long)N * Kp; s.out_rows = N;
     s.e2h = h2 ? &rec[1].e : nullptr;
+    s.frag = bfrag ? 1 : 0;
     split_planes(s, false, 1, nullptr);
+    s.frag = 0;
     if (m16) {  // planes of the mask, row stride N
       s.x = dmask + (size_t)z * M * N; s.ldx = N; s.rows = M; s.cols = N;
       s.out = dM16 + (size_t)z * 3 * M * N; s.ldo = N; s.po = (long long)M * N; s.out_rows = M; s.out_cols = N;
@@ -263,6 +269,7 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
   SplitGemmParams g{};
   g.A = Ap; g.lda = Kp; g.pA = (long long)M * Kp; g.sA = 3 * g.pA;
   g.B = Bp; g.ldb = Kp; g.pB = (long long)N * Kp; g.sB = 3 * g.pB;
+  g.b_frag = bfrag ? 1 : 0;
   g.C = dC; g.ldc = N; g.sC = (long long)M * N;
   g.bias = dbias; g.sBias = N;
   g.mask = dmask; g.ldm = N; g.sMask = (long long)M * N;
@@ -335,6 +342,7 @@ int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int 
   const bool autosplit = (epi >> 11) & 1;     // split-K by the launcher's own choice (workspace given)
   const bool fin = (epi >> 12) & 1;           // ... with arrival counters: the in-launch finish
   const bool h2 = (epi >> 13) & 1;            // precision split2h (exponents 0: operands in [-1, 1])
+  const bool bfrag = (epi >> 14) & 1;         // gemm_x3f: B planes in the fragment layout
   epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || iters < 1 || !ms_per_launch) return -22;
   DevBuf d;
@@ -360,7 +368,7 @@ int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int 
   if (!Ap || !Bp) return -12;
   for (int z = 0; z < batch; ++z) {
     split_into(fa, M, (int)Kp, false, Ap + 3 * pa * z, h2 ? &rec[0].e : nullptr);
-    split_into(fb, N, (int)Kp, bk, Bp + 3 * pb * z, h2 ? &rec[1].e : nullptr);
+    split_into(fb, N, (int)Kp, bk, Bp + 3 * pb * z, h2 ? &rec[1].e : nullptr, bfrag && !bk);
   }
   SplitGemmParams g{};
   if (h2) {
@@ -370,6 +378,7 @@ int mtsac_debug_gemm_fwd_bench(int which, int epi, int batch, int M, int N, int 
   }
   g.A = Ap; g.lda = lda; g.pA = pa; g.sA = 3 * pa;
   g.B = Bp; g.ldb = ldb; g.pB = pb; g.sB = 3 * pb; g.b_kmajor = bk;
+  g.b_frag = bfrag && !bk ? 1 : 0;
   g.C = C; g.ldc = N; g.sC = (long long)M * N;
   g.bias = bias; g.sBias = N;
   g.mask = C; g.ldm = N; g.sMask = (long long)M * N;

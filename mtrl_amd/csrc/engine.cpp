@@ -35,6 +35,7 @@ using namespace mtsac;
 namespace {
 
 thread_local std::string g_last_error;
+int g_bfrag_mode = -1;  // mtsac_debug_set_bfrag: -1 by shape (and MTSAC_BFRAG), 0 off, 1 allowed
 
 int fail(int code, const std::string& msg) {
   g_last_error = msg;
@@ -81,6 +82,10 @@ struct Net {
   // activations then keep planes only (their ReLU mask is read from the high plane)
   bool x3f = false;
   __bf16* wtp[2][MAXD] = {};
+  // the GEMM-read weight planes (wtp, and wp for the data grad) in the fragment layout
+  // (gemm_common.h frag_off: gemm_x3f's B wave loads read whole lines); set when every trunk GEMM
+  // that reads them runs on gemm_x3f (B rows fill >= 192 row x column tiles, no fallback kernel)
+  bool bfrag = false;
   // column-sum partials of dz[i] written by the pass that produces it (head backward, gemm_x3f data
   // grad): [E][chunks][width]; dbp_chunks[i] > 0 when the current step's dz[i] came with them
   float* dbp[MAXD] = {};
@@ -560,6 +565,8 @@ struct mtsac_engine {
                                        (p.C ? "true" : "false") + ", " + (p.Cp ? "true" : "false") + ", " +
                                        (p.mask16 ? "true" : "false") + ", " + (tagged ? "8" : "0") + ", " +
                                        std::to_string(p.np == 0 ? 3 : p.np) + ">";
+    } else if (p.b_frag) {  // only gemm_x3f reads the fragment layout (Net::bfrag promised it takes the shape)
+      comm_error = "B planes in the fragment layout and a shape gemm_x3f does not take";
     } else if (gemm_x3s_ok(p, epi, batch)) {
       gemm_x3s(p, epi, batch, cur);
       const bool tagged = epi == EPI_BIAS_RELU && p.tag == 1 && p.Cp && !p.C;
@@ -655,6 +662,7 @@ struct mtsac_engine {
         g.ldb = net.wtk(i);
         g.pB = net.wtps(i);
         g.sB = 3 * net.wtps(i);
+        g.b_frag = net.bfrag ? 1 : 0;
         if (last) {  // the heads read fp32
           g.C = acts[i];
           g.ldc = net.width;
@@ -769,6 +777,7 @@ struct mtsac_engine {
       sp.out_cols = (int)net.wld;
       sp.out = net.wp[which][i];
       sp.e2h = h2 ? &w_rec(net, which).d->e : nullptr;  // split2h: the exponent the optimizer / set_params chose
+      sp.frag = net.bfrag ? 1 : 0;
       if (!(fused && planes_fusable(net))) split_planes(sp, false, net.E, s);
       if (net.x3f) {  // W_i^T planes for the gemm_x3f forward (zeros past the in-dim)
         SplitParams st{};
@@ -784,6 +793,7 @@ struct mtsac_engine {
         st.out_rows = net.width;
         st.out_cols = (int)net.wtk(i);
         st.e2h = sp.e2h;
+        st.frag = sp.frag;
         split_planes(st, true, net.E, s);
       }
     }
@@ -868,6 +878,7 @@ struct mtsac_engine {
       g.ldb = net.wld;
       g.pB = net.wps();
       g.sB = 3 * net.wps();
+      g.b_frag = net.bfrag ? 1 : 0;
       g.C = dz[i - 1];
       g.ldc = net.width;
       g.sC = (long long)M * net.width;
@@ -1188,6 +1199,7 @@ struct mtsac_engine {
         lf.tr[1] = polyak ? net.wtp[1][i] : nullptr;
         lf.tr_ld = net.wtk(i);
         lf.tr_ps = net.wtps(i);
+        lf.frag = net.bfrag ? 1 : 0;
         at.skip_b[at.nskip] = lf.off / 4;
         at.skip_e[at.nskip++] = (lf.off + lf.ms * net.E) / 4;
       }
@@ -2143,6 +2155,14 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
                ((net->ald % 64 == 0 && gemm_x3f_tiles(M_fwd, net->width, net->E) >= x3f_min_tiles) ||
                 (net->ald <= 512 && e->B <= 2048));
     if (net->x3f) net->xld = align_up(net->in_dim, 64);  // gemm_x3f steps K by 64
+    static const int bfrag_env = [] {  // MTSAC_BFRAG=0: row-major weight planes (experiments)
+      const char* v = getenv("MTSAC_BFRAG");
+      return v ? atoi(v) : 1;
+    }();
+    const int bfrag_req = g_bfrag_mode >= 0 ? g_bfrag_mode : bfrag_env;
+    // every forward (>= B rows) and data grad (B rows) of this net fills >= 192 gemm_x3f tiles
+    net->bfrag = net->x3f && bfrag_req != 0 && net->depth <= MAX_TILE_LEAVES && net->width % 16 == 0 && net->ald % 64 == 0 &&
+                 gemm_x3f_tiles(e->B, net->width, 1) >= 192;
     for (int w = 0; w < (net == &e->critic ? 2 : 1); ++w)
       for (int i = 0; i < net->depth; ++i) {
         if (!e->planes) {
@@ -3125,6 +3145,17 @@ int mtsac_debug_force_one_stream(mtsac_engine* h, int32_t on) {
   h->force_one = on != 0;
   mtsac_engine::relane(r);
   return 0;
+}
+
+int mtsac_debug_set_bfrag(int32_t mode) {
+  if (mode < -1 || mode > 1) return fail(-22, "bfrag mode is -1, 0 or 1");
+  g_bfrag_mode = mode;
+  return 0;
+}
+
+int mtsac_debug_bfrag(mtsac_engine* h) {
+  if (!h) return fail(-22, "null engine");
+  return (h->actor.bfrag ? 1 : 0) | (h->critic.bfrag ? 2 : 0);
 }
 
 int mtsac_debug_lane_mode(mtsac_engine* h) {

@@ -64,6 +64,14 @@ struct TileOut {
 // zero keeps the smallest fp16 subnormal in l, so 'x > 0 <=> h > 0 or l > 0' holds exactly (the
 // ReLU mask of the data grad reads the planes).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// ---- the fragment layout of a B plane [rows][ldk] (ldk % 32 == 0, rows padded to 16): element
+// (n, k) of fragment (n / 16, k / 32) -- 512 elements, 1 KB, contiguous in (n / 16, k / 32) order --
+// at lane (n % 16) + 16 ((k / 8) % 4), element k % 8: the lane order of a v_mfma_*_16x16x32 B
+// operand, so one wave load of a fragment reads 8 whole lines (row-major planes: 16 half lines)
+__host__ __device__ inline long long frag_off(long long n, long long k, long long ldk) {
+  return (((n >> 4) * (ldk >> 5) + (k >> 5)) << 9) + (((n & 15) + 16 * ((k >> 3) & 3)) << 3) + (k & 7);
+}
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 __device__ inline void split2h_dev(float x, float s, _Float16& h, _Float16& l) {

@@ -126,8 +126,9 @@ void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t s
     if (wv4) ablate_at<BM0, 1, 4>(p, abl, grid, st);
     else if (short8) ablate_at<BM0, 1, 8>(p, abl, grid, st);
     else ablate_at<400, 1, 8>(p, abl, grid, st);
-  } else if (p.np == 2) {  // split2h: 8 waves (the 4-wave form is not instantiated for it)
-    ablate_at<BM0, 2, 8>(p, abl, grid, st);
+  } else if (p.np == 2) {  // split2h: 8 waves, or (+ 1000) 4 waves x 64-column slabs
+    if (wv4) ablate_at<BM0, 2, 4>(p, abl, grid, st);
+    else ablate_at<BM0, 2, 8>(p, abl, grid, st);
   } else if (wv4) {
     ablate_at<BM0, 3, 4>(p, abl, grid, st);
   } else if (abl == 4 || abl == 128 || abl == 512) {
@@ -250,7 +251,8 @@ bool gemm_x3f_ok(const SplitGemmParams& p, int epi, int batch) {
   return !p.a_kmajor && !p.b_kmajor && p.K % x3fk::KS == 0 && p.N % 8 == 0 && p.lda % 8 == 0 && p.ldb % 8 == 0 &&
          (!p.C || p.ldc % 4 == 0) && (!p.Cp || p.ldcp % 8 == 0) && (epi != EPI_RELU_MASK || p.ldm % 8 == 0) &&
          (epi != EPI_STORE) && x3f_workgroups(p, epi, batch) >= 192 &&
-         (p.C || p.Cp) && (long long)p.N * p.ldb * 2 < (1ll << 31);
+         (p.C || p.Cp) && (long long)p.N * p.ldb * 2 < (1ll << 31) &&
+         (!p.b_frag || (p.N % 16 == 0 && p.ldb % 32 == 0));
 }
 
 int gemm_x3f(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {

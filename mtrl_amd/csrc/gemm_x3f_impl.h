@@ -130,7 +130,9 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   const int m0 = bx * BM, n0 = by * BN;
   const int k0 = nsplit > 1 ? sl * p.kchunk : 0;
   const __bf16* __restrict__ A = p.A + z * p.sA + k0;
-  const __bf16* B = p.B + z * p.sB + k0;
+  // B planes in the fragment layout (p.b_frag, frag_off): k advances 16 elements per k (512 per 32)
+  const int bks = p.b_frag ? 16 : 1;
+  const __bf16* B = p.B + z * p.sB + (long long)bks * k0;
   const int nk = (nsplit > 1 ? min(p.kchunk, p.K - k0) : p.K) / KS;
 
   // ---- A: LDS-DMA piece j of the stage at k0 into stage buffer `st` (byte address)
@@ -160,12 +162,17 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
     int n = n0 + 16 * JB * wave + 16 * j + (lane & 15);
     n = n < p.N ? n : p.N - 1;
     boff[j] = (unsigned)(((long long)n * p.ldb + 8 * (lane >> 4)) * 2);
+    if (p.b_frag) {  // the fragment of columns nb .. nb + 15 at k = 0: this lane's 16 B of its 1 KB
+      int nb = (n0 + 16 * JB * wave + 16 * j) >> 4;
+      nb = nb < (p.N >> 4) ? nb : (p.N >> 4) - 1;  // N % 16 == 0 (gemm_x3f_ok)
+      boff[j] = (unsigned)(((long long)nb * (p.ldb >> 5) * 512 + 8 * lane) * 2);
+    }
     if (ABL & 64) boff[j] = (unsigned)((long long)(n0 + 16 * JB * wave + 16 * j) * p.ldb * 2 + 16 * lane);
   }
   auto bload = [&](bf16x8 (&b)[JB][NP], int k) {  // the 32-deep half step at k
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
-      const __bf16* base = B + q * p.pB + k;
+      const __bf16* base = B + q * p.pB + bks * k;
 #pragma unroll
       for (int j = 0; j < JB; ++j) b[j][q] = gload_frag(base, boff[j]);
     }

@@ -52,12 +52,12 @@ __global__ __launch_bounds__(256) void split_kernel(SplitParams s) {
       v = tile[b][a];
       const int orow = c0 + a, ocol = r0 + b;
       if (orow >= s.out_rows || ocol >= s.out_cols) continue;
-      o = (long long)orow * s.ldo + ocol;
+      o = s.frag ? frag_off(orow, ocol, s.ldo) : (long long)orow * s.ldo + ocol;
     } else {
       v = tile[a][b];
       const int orow = r0 + a, ocol = c0 + b;
       if (orow >= s.out_rows || ocol >= s.out_cols) continue;
-      o = (long long)orow * s.ldo + ocol;
+      o = s.frag ? frag_off(orow, ocol, s.ldo) : (long long)orow * s.ldo + ocol;
     }
     if (s.e2h) {
       _Float16 h, l;
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void split_rows_kernel(SplitParams s, long lon
       split2h_dev(v[j], sc, a, b);
       h[j] = a; l[j] = b;
     }
-    __bf16* o = s.out + z * s.so + (long long)r * s.ldo + c;
+    __bf16* o = s.out + z * s.so + (s.frag ? frag_off(r, c, s.ldo) : (long long)r * s.ldo + c);
     *reinterpret_cast<f16x4*>(o) = h;
     *reinterpret_cast<f16x4*>(o + s.po) = l;
     return;
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void split_rows_kernel(SplitParams s, long lon
     split3_dev(v[j], a, b, cc);
     h[j] = a; m[j] = b; l[j] = cc;
   }
-  __bf16* o = s.out + z * s.so + (long long)r * s.ldo + c;
+  __bf16* o = s.out + z * s.so + (s.frag ? frag_off(r, c, s.ldo) : (long long)r * s.ldo + c);
   *reinterpret_cast<bf16x4_t*>(o) = h;
   *reinterpret_cast<bf16x4_t*>(o + s.po) = m;
   *reinterpret_cast<bf16x4_t*>(o + 2 * s.po) = l;

@@ -372,6 +372,7 @@ int gemm_x3s_ti(int M, int N, int batch) {
 }
 
 bool gemm_x3s_ok(const SplitGemmParams& p, int epi, int batch) {
+  if (p.b_frag) return false;  // row-major B planes only
   auto fits = [](long long rows, long long ld, long long plane_stride) {  // 32-bit byte offsets
     return 2 * (rows * ld + 2 * plane_stride) < (1ll << 31);
   };

@@ -105,6 +105,8 @@ struct SplitGemmParams {
   int tag;                // 1: input-layer launch (separate kernel symbol for profiles)
   int order;              // gemm_x3f tile order inside an XCD's run: 0 column tiles fastest, 1 row tiles
                           // fastest (experiments: MTSAC_X3F_ORDER)
+  int b_frag;             // gemm_x3f: B planes in the fragment layout (frag_off: every 16-row x 32-k
+                          // MFMA fragment 1 KB contiguous, so a B wave load reads 8 whole lines)
   int np;                 // operand planes the products read: 3 (0 = default; fp32-accurate split) or 1
                           // (precision bf16: the high plane only, one MFMA per product)
   float* dbp;             // gemm_x3f: column sums of the epilogue's output per row tile, [z][row tiles][N]
@@ -174,6 +176,7 @@ struct SplitParams {
   long long ldo, po, so;
   int out_rows, out_cols;
   const int* e2h;  // non-null: precision split2h, two fp16 planes of x * 2^(*e2h) (gemm_common.h split2h_dev)
+  int frag;        // out planes in the fragment layout (gemm_common.h frag_off; ldo % 32 == 0, out_rows % 16 == 0)
 };
 void split_planes(const SplitParams& s, bool transpose, int batch, hipStream_t st);
 // db[z][c] = sum_r x[z][r][c] (deterministic two-pass; part holds batch*COLSUM_CHUNKS*cols floats)
@@ -439,6 +442,7 @@ struct TileLeaf {
   long long nat_ld, nat_ps;
   __bf16* tr[2];
   long long tr_ld, tr_ps;
+  int frag;  // nat and tr planes in the fragment layout (gemm_common.h frag_off)
 };
 constexpr int MAX_TILE_LEAVES = 8;
 struct TileParams {

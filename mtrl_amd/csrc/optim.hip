@@ -307,7 +307,7 @@ __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, co
               split2h_dev(src[q], w ? hs.st : hs.sw, x0, x1);
               h2h[q] = x0; h2l[q] = x1;
             }
-            __bf16* dst = np_ + e * 3 * lf.nat_ps + (long long)r * lf.nat_ld + c;
+            __bf16* dst = np_ + e * 3 * lf.nat_ps + (lf.frag ? frag_off(r, c, lf.nat_ld) : (long long)r * lf.nat_ld + c);
             *reinterpret_cast<f16x4*>(dst) = h2h;
             *reinterpret_cast<f16x4*>(dst + lf.nat_ps) = h2l;
             continue;
@@ -319,7 +319,7 @@ __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, co
             split3_dev(src[q], x0, x1, x2);
             h[q] = x0; mm[q] = x1; l[q] = x2;
           }
-          __bf16* dst = np_ + e * 3 * lf.nat_ps + (long long)r * lf.nat_ld + c;
+          __bf16* dst = np_ + e * 3 * lf.nat_ps + (lf.frag ? frag_off(r, c, lf.nat_ld) : (long long)r * lf.nat_ld + c);
           *reinterpret_cast<bf16x4_t*>(dst) = h;
           if (a.np != 1) {
             *reinterpret_cast<bf16x4_t*>(dst + lf.nat_ps) = mm;
@@ -342,7 +342,9 @@ __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, co
         for (int w = 0; w < 2; ++w) {
           __bf16* tp_ = lf.tr[w];
           if (tp_ == nullptr || (w == 1 && !POLYAK)) continue;
-          __bf16* dst = tp_ + e * 3 * lf.tr_ps + (long long)o * lf.tr_ld + kk;
+          // the two 8-k halves: adjacent, or (fragment layout) 16 lanes = 128 elements apart
+          __bf16* dst = tp_ + e * 3 * lf.tr_ps + (lf.frag ? frag_off(o, kk, lf.tr_ld) : (long long)o * lf.tr_ld + kk);
+          const int hs8 = lf.frag ? 128 : 8;
           if (a.np == 2) {  // split2h planes
             f16x8 h2h[2], h2l[2];
 #pragma unroll
@@ -355,8 +357,8 @@ __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, co
 #pragma unroll
             for (int hh = 0; hh < 2; ++hh) {
               if (kk + 8 * hh >= lf.tr_ld) break;
-              *reinterpret_cast<f16x8*>(dst + 8 * hh) = h2h[hh];
-              *reinterpret_cast<f16x8*>(dst + lf.tr_ps + 8 * hh) = h2l[hh];
+              *reinterpret_cast<f16x8*>(dst + hs8 * hh) = h2h[hh];
+              *reinterpret_cast<f16x8*>(dst + lf.tr_ps + hs8 * hh) = h2l[hh];
             }
             continue;
           }
@@ -371,10 +373,10 @@ __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, co
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
             if (kk + 8 * hh >= lf.tr_ld) break;
-            *reinterpret_cast<bf16x8*>(dst + 8 * hh) = h[hh];
+            *reinterpret_cast<bf16x8*>(dst + hs8 * hh) = h[hh];
             if (a.np != 1) {
-              *reinterpret_cast<bf16x8*>(dst + lf.tr_ps + 8 * hh) = mm[hh];
-              *reinterpret_cast<bf16x8*>(dst + 2 * lf.tr_ps + 8 * hh) = l[hh];
+              *reinterpret_cast<bf16x8*>(dst + lf.tr_ps + hs8 * hh) = mm[hh];
+              *reinterpret_cast<bf16x8*>(dst + 2 * lf.tr_ps + hs8 * hh) = l[hh];
             }
           }
         }

@@ -195,7 +195,7 @@ def test_full_batch_modelled_collective_matches_oracle():
     e.close()
 
 
-def _device_steps(T, tc, W, prec, steps, pipe, model=0, calls=None):
+def _device_steps(T, tc, W, prec, steps, pipe, model=0, calls=None, info=None):
     """Logs, parameters, moments, index-stream and noise state after device-sampled eager steps."""
     from mtrl_amd import _lib as L
     from mtrl_amd.engine import MTSACEngine, make_config
@@ -213,6 +213,8 @@ def _device_steps(T, tc, W, prec, steps, pipe, model=0, calls=None):
     if model:
         assert e.lib.mtsac_debug_set_collective_model(e._h, 8, 300.0, 1) == 0
     e.lib.mtsac_debug_set_pipeline(e._h, pipe)
+    if info is not None:
+        info["bfrag"] = e.lib.mtsac_debug_bfrag(e._h)
     for k in calls or (steps,):
         e.update_many(k)
     out = (e.logs(), [e.get_params(w) for w in (L.ACTOR, L.CRITIC, L.CRITIC_TARGET, L.LOG_ALPHA, L.ACTOR_ADAM_MU,
@@ -241,6 +243,26 @@ def test_pipelined_steps_equal_whole_steps(T, tc, W, prec, model):
     and index-stream / noise state of 4 whole steps.  The modelled cases take the sharded path with
     the device collective (NaN-poisoned buckets) on its own stream, as an 8-GPU rank does."""
     _assert_same(_device_steps(T, tc, W, prec, 4, 0, model), _device_steps(T, tc, W, prec, 4, 1, model))
+
+
+@pytest.mark.parametrize("prec", [3, 1, 2], ids=["split2h", "split3", "bf16"])
+def test_fragment_layout_weights_equal_row_major(prec):
+    """S3: the weight planes the trunk GEMMs read (W^T for the forward, W for the data grad) in the
+    fragment layout (gemm_common.h frag_off; the optimizer's tile pass and the set_params split write
+    them so) give bitwise the logs, parameters, moments and stream states of row-major planes over
+    3 device-sampled steps; and S3 does take the fragment layout (both networks)."""
+    from mtrl_amd import _lib as L
+
+    lib = L.load()
+    info_off, info_on = {}, {}
+    try:
+        assert lib.mtsac_debug_set_bfrag(0) == 0
+        a = _device_steps(50, 50, 2048, prec, 3, 0, info=info_off)
+    finally:
+        lib.mtsac_debug_set_bfrag(-1)
+    b = _device_steps(50, 50, 2048, prec, 3, 0, info=info_on)
+    assert info_off["bfrag"] == 0 and info_on["bfrag"] == 3, (info_off, info_on)
+    _assert_same(a, b)
 
 
 _PIPE_LANES_CHILD = """

@@ -253,3 +253,37 @@ def test_split2h_products(E, M, N, K, epi, m16, scale_a, spread):
     lim = 2.0 ** -21 * np.abs(C) + 1.01 * 2.0 ** (-24 - e)
     print("planes: e", e, "worst |planes - C| / limit", float((dev / lim).max()))
     assert np.all(dev <= lim)
+
+
+@pytest.mark.parametrize("E,M,N,K,epi,m16,prec,split", [(1, 6400, 2048, 2048, 1, False, "split2h", False),
+                                                        (2, 6400, 2048, 256, 2, True, "split2h", False),
+                                                        (2, 6300, 2032, 192, 1, False, "split3", False),
+                                                        (2, 6400, 2048, 512, 2, True, "bf16", False),
+                                                        (2, 896, 2048, 2048, 1, False, "split2h", True),
+                                                        (2, 768, 2048, 2048, 2, True, "split3", True)],
+                         ids=["s3_fwd_h2", "dgrad_m16_h2", "ragged_split3", "dgrad_bf16", "shard7_splitk_h2",
+                              "shard6_splitk_split3_dgrad"])
+def test_fragment_layout_b_bitwise(E, M, N, K, epi, m16, prec, split):
+    """B planes in the fragment layout (gemm_common.h frag_off: each 16-row x 32-k MFMA fragment 1 KB
+    contiguous, the engine's weight planes at S3) give the row-major planes' outputs bit for bit:
+    the same products in the same order, only the addresses differ."""
+    from mtrl_amd import _lib as L
+
+    lib = L.load()
+    rng = np.random.default_rng(M + K + N)
+    A = rng.standard_normal((E, M, K)).astype(np.float32)
+    B = (rng.standard_normal((E, N, K)) / np.sqrt(K)).astype(np.float32)
+    bias = rng.standard_normal((E, N)).astype(np.float32) * 0.1
+    mask = np.maximum(rng.standard_normal((E, M, N)), 0).astype(np.float32)
+    p = lambda a: np.ascontiguousarray(a, np.float32).ctypes.data
+    flags = {"split2h": 8192, "split3": 0, "bf16": 1024}[prec] | (256 if m16 else 0) | (2048 if split else 0)
+    out = []
+    for frag in (0, 16384):
+        C = np.zeros((E, M, N), np.float32)
+        Cs = np.zeros((E, M, N), np.float32)
+        L.check(lib.mtsac_debug_gemm_x3f(epi | flags | frag, E, M, N, K, p(A), p(B), C.ctypes.data, p(bias), p(mask),
+                                         Cs.ctypes.data))
+        out.append((C, Cs))
+    np.testing.assert_array_equal(out[1][0], out[0][0])
+    np.testing.assert_array_equal(out[1][1], out[0][1])
+    assert np.abs(out[1][0]).max() > 0
