@@ -82,7 +82,7 @@ int mtsac_debug_set_pipeline(struct mtsac_engine* engine, int32_t on);
 int mtsac_debug_lane_mode(struct mtsac_engine* engine);
 /* Weight planes in the fragment layout (gemm_x3f B operand, engine.cpp Net::bfrag): mode -1 (the
  * default) decides by shape (MTSAC_BFRAG=0 turns it off), 0 / 1 forces it off / allows it, for
- * engines created afterwards.  mtsac_debug_bfrag: bit 0 actor, bit 1 critic of this engine. */
+ * engines created afterwards.  mtsac_debug_bfrag: bit i actor layer i, bit 8 + i critic layer i. */
 int mtsac_debug_set_bfrag(int32_t mode);
 int mtsac_debug_bfrag(struct mtsac_engine* engine);
 /* on != 0: this engine issues on one stream whatever MTSAC_LANES asks, and is not counted by the

@@ -82,10 +82,10 @@ struct Net {
   // activations then keep planes only (their ReLU mask is read from the high plane)
   bool x3f = false;
   __bf16* wtp[2][MAXD] = {};
-  // the GEMM-read weight planes (wtp, and wp for the data grad) in the fragment layout
-  // (gemm_common.h frag_off: gemm_x3f's B wave loads read whole lines); set when every trunk GEMM
-  // that reads them runs on gemm_x3f (B rows fill >= 192 row x column tiles, no fallback kernel)
-  bool bfrag = false;
+  // layer i's GEMM-read weight planes (wtp[.][i], and wp[.][i] for the data grad) in the fragment
+  // layout (gemm_common.h frag_off: gemm_x3f's B wave loads read whole lines); set when every GEMM
+  // that reads them runs on gemm_x3f (engine frag_probe; no other kernel reads the layout)
+  bool bfrag[MAXD] = {};
   // column-sum partials of dz[i] written by the pass that produces it (head backward, gemm_x3f data
   // grad): [E][chunks][width]; dbp_chunks[i] > 0 when the current step's dz[i] came with them
   float* dbp[MAXD] = {};
@@ -322,6 +322,70 @@ struct mtsac_engine {
     return on ? cnt_lane[cur_lane] : nullptr;
   }
   int cur_lane = 0;
+
+  // Net::bfrag[li]: every GEMM that reads layer li's weight planes takes gemm_x3f (no other kernel
+  // reads the fragment layout).  The step's parameter sets (trunk_forward's x3f branch, dgrad_layer),
+  // probed with placeholder pointers after the workspaces exist; a mismatch with the step surfaces
+  // as gemmp's error, never as a silent fallback.
+  bool frag_probe(const Net& net, int li) {
+    static float f_;
+    static __bf16 h_;
+    float* F = &f_;
+    __bf16* H = &h_;
+    const bool is_actor = &net == &actor;
+    auto base = [&](int M, long long K, long long ldb) {
+      SplitGemmParams g{};
+      g.np = np;
+      g.lda = K;
+      g.ldb = ldb;
+      g.M = M;
+      g.N = net.width;
+      g.K = (int)K;
+      g.splits = -1;
+      g.ws = ws_lane[0];
+      g.cnt = fin_cnt();
+      g.b_frag = 1;
+      return g;
+    };
+    std::vector<int> fwd_rows = {B};
+    if (is_actor) fwd_rows.push_back((int)(net.krows + B));  // the merged [s | s'] forward
+    for (int M : fwd_rows)
+      for (int i = li; i == li; ++i) {
+        SplitGemmParams g = base(M, net.wtk(i), net.wtk(i));
+        g.bias = F;
+        if (i == net.depth - 1) {
+          g.C = F;
+          g.ldc = net.width;
+        } else {
+          g.Cp = H;
+          g.ldcp = net.ald;
+        }
+        if (!gemm_x3f_ok(g, EPI_BIAS_RELU, net.E)) return false;
+      }
+    for (int want_db = 0; want_db < 2; ++want_db)
+      for (int i = li; i == li && i > 0; ++i) {
+        SplitGemmParams g = base(B, net.ald, net.wld);
+        g.C = F;
+        g.ldc = net.width;
+        g.mask16 = H;
+        g.ldm = (int)net.ald;
+        if (i - 1 >= 1 || want_db) {
+          g.Cp = H;
+          g.ldcp = net.ald;
+        }
+        bool ok = false;
+        if (g.Cp && want_db) {
+          SplitGemmParams q = g;
+          q.C = nullptr;
+          q.dbp = F;
+          ok = gemm_x3f_ok(q, EPI_RELU_MASK, net.E);
+        } else if (g.Cp) {
+          g.C = nullptr;
+        }
+        if (!ok && !gemm_x3f_ok(g, EPI_RELU_MASK, net.E)) return false;
+      }
+    return true;
+  }
   float* pn = nullptr;  // [critic trunk |p|^2, actor trunk, critic heads, actor heads]
   float* log_alpha = nullptr;
   float *la_m = nullptr, *la_v = nullptr;
@@ -662,7 +726,7 @@ struct mtsac_engine {
         g.ldb = net.wtk(i);
         g.pB = net.wtps(i);
         g.sB = 3 * net.wtps(i);
-        g.b_frag = net.bfrag ? 1 : 0;
+        g.b_frag = net.bfrag[i] ? 1 : 0;
         if (last) {  // the heads read fp32
           g.C = acts[i];
           g.ldc = net.width;
@@ -777,7 +841,7 @@ struct mtsac_engine {
       sp.out_cols = (int)net.wld;
       sp.out = net.wp[which][i];
       sp.e2h = h2 ? &w_rec(net, which).d->e : nullptr;  // split2h: the exponent the optimizer / set_params chose
-      sp.frag = net.bfrag ? 1 : 0;
+      sp.frag = net.bfrag[i] ? 1 : 0;
       if (!(fused && planes_fusable(net))) split_planes(sp, false, net.E, s);
       if (net.x3f) {  // W_i^T planes for the gemm_x3f forward (zeros past the in-dim)
         SplitParams st{};
@@ -878,7 +942,7 @@ struct mtsac_engine {
       g.ldb = net.wld;
       g.pB = net.wps();
       g.sB = 3 * net.wps();
-      g.b_frag = net.bfrag ? 1 : 0;
+      g.b_frag = net.bfrag[i] ? 1 : 0;
       g.C = dz[i - 1];
       g.ldc = net.width;
       g.sC = (long long)M * net.width;
@@ -1199,7 +1263,7 @@ struct mtsac_engine {
         lf.tr[1] = polyak ? net.wtp[1][i] : nullptr;
         lf.tr_ld = net.wtk(i);
         lf.tr_ps = net.wtps(i);
-        lf.frag = net.bfrag ? 1 : 0;
+        lf.frag = net.bfrag[i] ? 1 : 0;
         at.skip_b[at.nskip] = lf.off / 4;
         at.skip_e[at.nskip++] = (lf.off + lf.ms * net.E) / 4;
       }
@@ -2160,9 +2224,10 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
       return v ? atoi(v) : 1;
     }();
     const int bfrag_req = g_bfrag_mode >= 0 ? g_bfrag_mode : bfrag_env;
-    // every forward (>= B rows) and data grad (B rows) of this net fills >= 192 gemm_x3f tiles
-    net->bfrag = net->x3f && bfrag_req != 0 && net->depth <= MAX_TILE_LEAVES && net->width % 16 == 0 && net->ald % 64 == 0 &&
-                 gemm_x3f_tiles(e->B, net->width, 1) >= 192;
+    // candidates; frag_probe (after the workspaces) keeps those whose every trunk GEMM is gemm_x3f's
+    const bool cand = net->x3f && bfrag_req != 0 && net->depth <= MAX_TILE_LEAVES && net->width % 16 == 0 &&
+                      net->ald % 64 == 0 && net->wld % 32 == 0;
+    for (int i = 0; i < net->depth; ++i) net->bfrag[i] = cand;
     for (int w = 0; w < (net == &e->critic ? 2 : 1); ++w)
       for (int i = 0; i < net->depth; ++i) {
         if (!e->planes) {
@@ -2193,6 +2258,9 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     for (int*& c : e->cnt_lane)
       if ((rc = e->alloc(&c, (size_t)GEMM_X3F_CNT))) return bad(rc);
   }
+  for (Net* net : {&e->actor, &e->critic})
+    for (int i = 0; i < net->depth; ++i)
+      if (net->bfrag[i]) net->bfrag[i] = e->frag_probe(*net, i);
 
   const int B = e->B;
   if ((rc = e->alloc(&e->store, (size_t)c.capacity * e->T_l * e->R))) return bad(rc);
@@ -3155,7 +3223,9 @@ int mtsac_debug_set_bfrag(int32_t mode) {
 
 int mtsac_debug_bfrag(mtsac_engine* h) {
   if (!h) return fail(-22, "null engine");
-  return (h->actor.bfrag ? 1 : 0) | (h->critic.bfrag ? 2 : 0);
+  int m = 0;
+  for (int i = 0; i < MAXD && i < 8; ++i) m |= (h->actor.bfrag[i] ? 1 << i : 0) | (h->critic.bfrag[i] ? 256 << i : 0);
+  return m;
 }
 
 int mtsac_debug_lane_mode(mtsac_engine* h) {

@@ -245,23 +245,33 @@ def test_pipelined_steps_equal_whole_steps(T, tc, W, prec, model):
     _assert_same(_device_steps(T, tc, W, prec, 4, 0, model), _device_steps(T, tc, W, prec, 4, 1, model))
 
 
-@pytest.mark.parametrize("prec", [3, 1, 2], ids=["split2h", "split3", "bf16"])
-def test_fragment_layout_weights_equal_row_major(prec):
-    """S3: the weight planes the trunk GEMMs read (W^T for the forward, W for the data grad) in the
-    fragment layout (gemm_common.h frag_off; the optimizer's tile pass and the set_params split write
-    them so) give bitwise the logs, parameters, moments and stream states of row-major planes over
-    3 device-sampled steps; and S3 does take the fragment layout (both networks)."""
+@pytest.mark.parametrize("T,tc,prec,model", [(50, 50, 3, 0), (50, 50, 1, 0), (50, 50, 2, 0), (10, 10, 3, 0),
+                                             (50, 7, 3, 0), (50, 7, 3, 1), (50, 13, 1, 0)],
+                         ids=["s3_split2h", "s3_split3", "s3_bf16", "mt10_w2048_split2h", "mt50_shard7_split2h",
+                              "mt50_shard7_modelled_split2h", "mt50_shard13_split3"])
+def test_fragment_layout_weights_equal_row_major(T, tc, prec, model):
+    """W = 2048: the weight planes the trunk GEMMs read (W^T for the forward, W for the data grad) in
+    the fragment layout (gemm_common.h frag_off; the optimizer's tile pass and the set_params split
+    write them so) give bitwise the logs, parameters, moments and stream states of row-major planes
+    over 3 device-sampled steps.  A layer's planes take the layout only where every GEMM reading them
+    runs on gemm_x3f (engine.cpp frag_probe): every layer at S3, the critic's hidden layers on
+    MT10 and the task shards."""
     from mtrl_amd import _lib as L
 
     lib = L.load()
     info_off, info_on = {}, {}
     try:
         assert lib.mtsac_debug_set_bfrag(0) == 0
-        a = _device_steps(50, 50, 2048, prec, 3, 0, info=info_off)
+        a = _device_steps(T, tc, 2048, prec, 3, 0, model, info=info_off)
     finally:
         lib.mtsac_debug_set_bfrag(-1)
-    b = _device_steps(50, 50, 2048, prec, 3, 0, info=info_on)
-    assert info_off["bfrag"] == 0 and info_on["bfrag"] == 3, (info_off, info_on)
+    b = _device_steps(T, tc, 2048, prec, 3, 0, model, info=info_on)
+    print("bfrag mask (bit i actor layer i, bit 8 + i critic layer i):", hex(info_on["bfrag"]))
+    assert info_off["bfrag"] == 0, info_off
+    if tc == 50:  # S3: every layer of both networks
+        assert info_on["bfrag"] == 0x707, hex(info_on["bfrag"])
+    else:  # the critic's hidden layers at least (gemm_x3f + split-K; others may run on gemm_x3p)
+        assert info_on["bfrag"] & 0x600 == 0x600, hex(info_on["bfrag"])
     _assert_same(a, b)
 
 
