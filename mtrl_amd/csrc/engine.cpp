@@ -86,6 +86,9 @@ struct Net {
   // layout (gemm_common.h frag_off: gemm_x3f's B wave loads read whole lines); set when every GEMM
   // that reads them runs on gemm_x3f (engine frag_probe; no other kernel reads the layout)
   bool bfrag[MAXD] = {};
+  // the actor's head kernel transposed per task ([T_l][hd][W], heads.hip HeadParams::WhT): the policy
+  // heads' weight loads read whole lines; rewritten with the planes after every write of p
+  float* whT = nullptr;
   // column-sum partials of dz[i] written by the pass that produces it (head backward, gemm_x3f data
   // grad): [E][chunks][width]; dbp_chunks[i] > 0 when the current step's dz[i] came with them
   float* dbp[MAXD] = {};
@@ -821,6 +824,7 @@ struct mtsac_engine {
   // after every write of params: Net::wt[which] (fp32) or the planes wp[which] (split3);
   // fused: the optimizer already wrote them (see optimize())
   void refresh_wt(Net& net, const float* params, int which, hipStream_t s, bool fused = false) {
+    if (which == 0 && net.whT && net.E == 1) head_transpose(params + net.off_hW, T_l, net.width, net.hd, net.whT, s);
     if (fused && tiles_fusable(net)) return;  // the optimizer wrote every plane the GEMMs read
     for (int i = planes ? 0 : 1; i < net.depth; ++i) {
       if (!planes) {
@@ -1010,6 +1014,7 @@ struct mtsac_engine {
     HeadParams hp{};
     hp.h = h;
     hp.Wh = params + net.off_hW;
+    hp.WhT = params == net.p ? net.whT : nullptr;
     hp.bh = params + net.off_hb;
     hp.task = tsk;
     hp.B = M;
@@ -2237,6 +2242,9 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
         if ((rc = e->alloc(&net->wp[w][i], (size_t)net->E * 3 * net->kps(i)))) return bad(rc);
         if (net->x3f && (rc = e->alloc(&net->wtp[w][i], (size_t)net->E * 3 * net->wtps(i)))) return bad(rc);
       }
+    if (net == &e->actor && net->E == 1 && net->width % 4 == 0 &&
+        (rc = e->alloc(&net->whT, (size_t)e->T_l * net->width * net->hd)))
+      return bad(rc);
   }
   {  // split-K workspaces: the largest GEMM that splits, per lane
     long long ws = 0;

@@ -10,6 +10,8 @@
 #include "devrng.h"
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "gemm_common.h"
 #include "kernels.h"
 
@@ -42,14 +44,42 @@ __device__ inline float clip_grad(float v, float lo, float hi) {
 // 16-B loads of h and of the head kernel (L2-resident: W*HD floats per task), several i in
 // flight; otherwise w = l + 64i.  The order is fixed per W, so every kernel that uses this
 // gets bitwise the same head outputs.
+// WtT (nullable, W % 4 == 0): the same kernel transposed, [HD][W] -- lane l's 4 weights of output o
+// are 16 contiguous bytes, so each of the HD loads reads whole lines (from Wt, lanes 4 HD floats
+// apart: every load touches 64 lines); the products and their order are unchanged (bitwise equal)
 template <int HD, int R>
-__device__ inline void rows_dot(const float* const (&h)[R], const float* __restrict__ Wt, int W, float (&acc)[R][HD]) {
+__device__ inline void rows_dot(const float* const (&h)[R], const float* __restrict__ Wt, int W, float (&acc)[R][HD],
+                                const float* __restrict__ WtT = nullptr) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int o = 0; o < HD; ++o) acc[r][o] = 0.f;
-  if ((W & 3) == 0) {
+  if (WtT != nullptr && (W & 3) == 0) {
+#pragma unroll 2
+    for (int w = 4 * lane; w < W; w += 256) {
+      float4 hv[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) hv[r] = *reinterpret_cast<const float4*>(h[r] + w);
+      float wv[4 * HD];  // wv[k HD + o] = Wt[w + k][o], as below
+#pragma unroll
+      for (int o = 0; o < HD; ++o) {
+        const float4 v = *reinterpret_cast<const float4*>(WtT + (long long)o * W + w);
+        wv[o] = v.x; wv[HD + o] = v.y; wv[2 * HD + o] = v.z; wv[3 * HD + o] = v.w;
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int o = 0; o < HD; ++o) {
+          float a = acc[r][o];
+          a += hv[r].x * wv[o];
+          a += hv[r].y * wv[HD + o];
+          a += hv[r].z * wv[2 * HD + o];
+          a += hv[r].w * wv[3 * HD + o];
+          acc[r][o] = a;
+        }
+    }
+  } else if ((W & 3) == 0) {
 #pragma unroll 2
     for (int w = 4 * lane; w < W; w += 256) {
       float4 hv[R];
@@ -173,7 +203,14 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyParams p) {
   if (b >= hp.B) return;
   const int t = hp.task[b];
   float acc[HD];
-  head_dot<HD>(hp.h + (long long)b * hp.W, hp.Wh + (long long)t * hp.W * HD, hp.W, acc);
+  {
+    const float* const hr[1] = {hp.h + (long long)b * hp.W};
+    float a[1][HD];
+    rows_dot<HD, 1>(hr, hp.Wh + (long long)t * hp.W * HD, hp.W, a,
+                    hp.WhT ? hp.WhT + (long long)t * hp.W * HD : nullptr);
+#pragma unroll
+    for (int o = 0; o < HD; ++o) acc[o] = a[0][o];
+  }
   policy_finish<HD>(p, b, t, acc, lane);
 }
 
@@ -200,7 +237,8 @@ __device__ inline void policy_head_grouped_body(const PolicyParams& p) {
     hr[r] = hp.h + (long long)row[r] * hp.W;
   }
   float acc[RW][HD];
-  rows_dot<HD, RW>(hr, hp.Wh + (long long)t * hp.W * HD, hp.W, acc);
+  rows_dot<HD, RW>(hr, hp.Wh + (long long)t * hp.W * HD, hp.W, acc,
+                   hp.WhT ? hp.WhT + (long long)t * hp.W * HD : nullptr);
 #pragma unroll
   for (int r = 0; r < RW; ++r)
     if (j0 + wave * RW + r < n) policy_finish<HD>(p, row[r], t, acc[r], lane);
@@ -220,6 +258,12 @@ __global__ __launch_bounds__(256) void policy_head_pair_kernel(PolicyPair pp) {
 // rows per wave for a launch that would have wgs_at_rw1 workgroups at one row per wave: the largest
 // of 4, 2, 1 that still gives >= 256 workgroups (one per CU)
 static int rows_per_wave(long long wgs_at_rw1) {
+  static const int forced = [] {  // MTSAC_HEAD_RW=1 / 2 / 4: experiments
+    const char* e = getenv("MTSAC_HEAD_RW");
+    const int v = e ? atoi(e) : 0;
+    return v == 1 || v == 2 || v == 4 ? v : 0;
+  }();
+  if (forced) return forced;
   for (int rw = 4; rw > 1; rw >>= 1)
     if (wgs_at_rw1 / rw >= 256) return rw;
   return 1;
@@ -732,7 +776,24 @@ __global__ __launch_bounds__(256) void row_alpha_kernel(const int* __restrict__ 
   }
 }
 
+// WhT[t][o][w] = Wh[t][w][o]: one thread per output element (reads hd-strided, writes whole lines)
+__global__ __launch_bounds__(256) void head_transpose_kernel(const float* __restrict__ Wh, int W, int hd,
+                                                             long long n, float* __restrict__ WhT) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long long per = (long long)W * hd;
+  const long long t = i / per, r = i - t * per;
+  const int o = (int)(r / W), w = (int)(r - (long long)o * W);
+  WhT[i] = Wh[t * per + (long long)w * hd + o];
+}
+
 }  // namespace
+
+void head_transpose(const float* Wh, int T_l, int W, int hd, float* WhT, hipStream_t st) {
+  const long long n = (long long)T_l * W * hd;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(head_transpose_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, Wh, W, hd, n, WhT);
+}
 
 void policy_head(const PolicyParams& p, hipStream_t st) {
   const int hd = p.head.hd;

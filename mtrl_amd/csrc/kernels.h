@@ -253,6 +253,8 @@ void task_rows(const int* task, int B, int T_l, int* counts, int* rows, int max_
 struct HeadParams {
   const float* h;       // [E][B][W] last trunk activation
   const float* Wh;      // [E][T_l][W][hd]
+  const float* WhT;     // [T_l][hd][W]: Wh transposed per task (the actor's, E = 1), or null: the policy
+                        // heads' weight loads then read whole lines (Wh rows are hd floats apart)
   const float* bh;      // [E][T_l][hd]
   const int* task;      // [B]
   int B, W, hd, E;
@@ -285,6 +287,8 @@ struct PolicyParams {
   int max_count;        // bound on counts[] (sizes the grid)
 };
 void policy_head(const PolicyParams& p, hipStream_t st);
+// WhT[t][o][w] = Wh[t][w][o] for T_l tasks (E = 1): the policy heads' copy, after every write of Wh
+void head_transpose(const float* Wh, int T_l, int W, int hd, float* WhT, hipStream_t st);
 // the s and s' heads of the merged actor forward in one launch (grouped form; else two launches)
 struct PolicyPair {
   PolicyParams p[2];
