@@ -256,7 +256,9 @@ __global__ __launch_bounds__(256) void policy_head_pair_kernel(PolicyPair pp) {
 }
 
 // rows per wave for a launch that would have wgs_at_rw1 workgroups at one row per wave: the largest
-// of 4, 2, 1 that still gives >= 256 workgroups (one per CU)
+// of 4, 2, 1 that still gives >= 1024 workgroups (four per CU: the row loads of more waves in flight;
+// S3, serialised: the policy-head pair 68.7 -> 39.8 us at 2 rows per wave instead of 4, the action
+// grad 43.5 -> 30.4 us at 1, profiles/r4t_*)
 static int rows_per_wave(long long wgs_at_rw1) {
   static const int forced = [] {  // MTSAC_HEAD_RW=1 / 2 / 4: experiments
     const char* e = getenv("MTSAC_HEAD_RW");
@@ -265,7 +267,7 @@ static int rows_per_wave(long long wgs_at_rw1) {
   }();
   if (forced) return forced;
   for (int rw = 4; rw > 1; rw >>= 1)
-    if (wgs_at_rw1 / rw >= 256) return rw;
+    if (wgs_at_rw1 / rw >= 1024) return rw;
   return 1;
 }
 
@@ -657,6 +659,145 @@ __global__ __launch_bounds__(256) void head_bwd_both_kernel(HeadParams hp, const
   head_bwd_weight_body<HD>(hp, dout, s_dout, counts, rows, max_rows, dWh, dbh, bx, by, bz, red);
 }
 
+// The head backward's data and weight passes reading h ONCE: block (task t, 256 columns bx, member e),
+// wave g walks the task's rows j = g, g + 4, ... (the weight pass's order) in batches of four, row
+// u of a batch being row slice rs = u of the data pass (j = 4 rs + g + 16 k): per row the masked data
+// grad (planes out), its column sum into the (t, rs) partial, and h dout into the weight grad.  Every
+// output is bitwise the separate passes' (head_bwd_data_body / head_bwd_weight_body): the same
+// products, added in the same order.
+template <int HD>
+__global__ __launch_bounds__(256) void head_bwd_fused_kernel(HeadParams hp, const float* __restrict__ dout,
+                                                             long long s_dout, float* __restrict__ dz, PlaneOut po,
+                                                             float* __restrict__ dbp, const int* __restrict__ counts,
+                                                             const int* __restrict__ rows, int max_rows, int T_l,
+                                                             float* __restrict__ dWh, float* __restrict__ dbh) {
+  constexpr int HDL = HD < HB_RS ? HB_RS : HD;  // the column-sum reduction needs [HB_RS][4][64] float4
+  __shared__ float4 red[4][64][HDL];
+  const int gw = (hp.W + 255) / 256, gy = T_l * HB_RS;
+  const int t = blockIdx.x % T_l, bx = (blockIdx.x / T_l) % gw, e = blockIdx.x / (T_l * gw);
+  if (po.p && po.rc) {  // split2h: as head_bwd_data_body
+    const float md = rec_max(po.rd, po.nd, reinterpret_cast<float*>(&red[0][0][0]));
+    const int ec = plane_exp(po.kmul * md * (po.rw->amax[1] + po.w_add));
+    po.w_add = exp2i(ec);
+    if (blockIdx.x == 0 && threadIdx.x == 0) po.rc->e = ec;
+    __syncthreads();  // the scratch is red: reused below
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int w = bx * 256 + 4 * lane;
+  const bool ok = w < hp.W;
+  const int n = counts[t];
+  const int* rl = rows + (long long)t * max_rows;
+  const float* h = hp.h + e * hp.sh;
+  const float* d = dout + e * s_dout;
+  float wt[4][HD];
+  if (ok) {
+    const float* Wt = hp.Wh + e * hp.sWh + ((long long)t * hp.W + w) * HD;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int o = 0; o < HD; ++o) wt[k][o] = Wt[k * HD + o];
+  }
+  float4 acc[HD], cs[HB_RS];
+#pragma unroll
+  for (int o = 0; o < HD; ++o) acc[o] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int u = 0; u < HB_RS; ++u) cs[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok && n > 0) {
+    for (int j0 = wave; j0 < n; j0 += 4 * HB_RS) {
+      int bb[HB_RS];
+#pragma unroll
+      for (int u = 0; u < HB_RS; ++u) bb[u] = rl[min(j0 + 4 * u, n - 1)];
+      float4 hv[HB_RS];
+      float dv[HB_RS][HD];
+#pragma unroll
+      for (int u = 0; u < HB_RS; ++u) {
+        hv[u] = *reinterpret_cast<const float4*>(h + (long long)bb[u] * hp.W + w);
+#pragma unroll
+        for (int o = 0; o < HD; ++o) dv[u][o] = d[(long long)bb[u] * HD + o];
+      }
+#pragma unroll
+      for (int u = 0; u < HB_RS; ++u) {
+        if (j0 + 4 * u >= n) break;
+        float g[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float s = 0.f;
+#pragma unroll
+          for (int o = 0; o < HD; ++o) s += dv[u][o] * wt[k][o];
+          g[k] = s;
+        }
+        float4 out;
+        out.x = hv[u].x > 0.f ? g[0] : 0.f;
+        out.y = hv[u].y > 0.f ? g[1] : 0.f;
+        out.z = hv[u].z > 0.f ? g[2] : 0.f;
+        out.w = hv[u].w > 0.f ? g[3] : 0.f;
+        head_bwd_put<HD>(hp, e, bb[u], w, out, dz, po);
+        cs[u].x += out.x; cs[u].y += out.y; cs[u].z += out.z; cs[u].w += out.w;
+#pragma unroll
+        for (int o = 0; o < HD; ++o) {
+          const float dvo = dv[u][o];
+          acc[o].x += hv[u].x * dvo;
+          acc[o].y += hv[u].y * dvo;
+          acc[o].z += hv[u].z * dvo;
+          acc[o].w += hv[u].w * dvo;
+        }
+      }
+    }
+  }
+  // weight grad: the four waves in order (head_bwd_weight_body)
+#pragma unroll
+  for (int o = 0; o < HD; ++o) red[wave][lane][o] = acc[o];
+  __syncthreads();
+  if (wave == 0 && ok) {
+    float v[4][HD];
+#pragma unroll
+    for (int o = 0; o < HD; ++o) {
+      const float4 a0 = red[0][lane][o], a1 = red[1][lane][o], a2 = red[2][lane][o], a3 = red[3][lane][o];
+      v[0][o] = a0.x + a1.x + a2.x + a3.x;
+      v[1][o] = a0.y + a1.y + a2.y + a3.y;
+      v[2][o] = a0.z + a1.z + a2.z + a3.z;
+      v[3][o] = a0.w + a1.w + a2.w + a3.w;
+    }
+    float* out = dWh + e * hp.sWh + ((long long)t * hp.W + w) * HD;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int o = 0; o < HD; ++o) out[k * HD + o] = v[k][o];
+  }
+  __syncthreads();
+  // the data grad's column sums per row slice rs: waves (a + b) + c + d (head_bwd_data_body)
+  if (dbp != nullptr) {
+    float4(*cr)[4][64] = reinterpret_cast<float4(*)[4][64]>(&red[0][0][0]);  // [rs][wave][lane]
+#pragma unroll
+    for (int u = 0; u < HB_RS; ++u) cr[u][wave][lane] = cs[u];
+    __syncthreads();
+    if (ok) {  // wave g finishes row slice rs = g
+      const float4 a = cr[wave][0][lane], b = cr[wave][1][lane], c = cr[wave][2][lane], dd = cr[wave][3][lane];
+      *reinterpret_cast<float4*>(dbp + ((long long)e * gy + t * HB_RS + wave) * hp.W + w) =
+          make_float4(((a.x + b.x) + c.x) + dd.x, ((a.y + b.y) + c.y) + dd.y, ((a.z + b.z) + c.z) + dd.z,
+                      ((a.w + b.w) + c.w) + dd.w);
+    }
+    __syncthreads();
+  }
+  if (bx == 0) {  // head bias grad: as head_bwd_weight_body
+    float* part = reinterpret_cast<float*>(&red[0][0][0]);  // >= 256 * HD floats
+#pragma unroll
+    for (int o = 0; o < HD; ++o) {
+      float s = 0.f;
+      for (int j = threadIdx.x; j < n; j += 256) s += d[(long long)rl[j] * HD + o];
+      part[o * 256 + threadIdx.x] = s;
+    }
+    __syncthreads();
+    for (int half = 128; half > 0; half >>= 1) {
+      if (threadIdx.x < half)
+#pragma unroll
+        for (int o = 0; o < HD; ++o) part[o * 256 + threadIdx.x] += part[o * 256 + threadIdx.x + half];
+      __syncthreads();
+    }
+    if (threadIdx.x < HD) dbh[e * hp.sbh + t * HD + threadIdx.x] = part[threadIdx.x * 256];
+  }
+}
+
 // ------------------------------------------------------------------ critic -> action grad -> policy grad
 // AG_RW rows per wavefront: the critic layer-0 kernel rows (A x Wc) are read once per AG_RW rows
 // (4, or fewer on small task shards, see rows_per_wave).  Per row the sums run over the lane's w
@@ -873,10 +1014,18 @@ bool head_backward_both(const HeadParams& hp, const float* dout, long long s_dou
                         hipStream_t st) {
   if (hp.W % 4 != 0) return false;  // the scalar weight kernel: two launches
   const int gw = (hp.W + 255) / 256;
-  const dim3 grid((unsigned)(gw * T_l * HB_RS * hp.E + T_l * gw * hp.E));
-#define HBB_LAUNCH(HDV)                                                                                       \
-  hipLaunchKernelGGL(head_bwd_both_kernel<HDV>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po, dbp, counts, rows, \
-                     max_rows, T_l, dWh, dbh)
+  static const bool split = [] {  // MTSAC_HEAD_BWD_SPLIT=1: the data and weight passes as separate blocks
+    const char* e = getenv("MTSAC_HEAD_BWD_SPLIT");
+    return e && atoi(e) != 0;
+  }();
+  const dim3 grid((unsigned)(split ? gw * T_l * HB_RS * hp.E + T_l * gw * hp.E : T_l * gw * hp.E));
+#define HBB_LAUNCH(HDV)                                                                                         \
+  if (split)                                                                                                    \
+    hipLaunchKernelGGL(head_bwd_both_kernel<HDV>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po, dbp, counts,  \
+                       rows, max_rows, T_l, dWh, dbh);                                                          \
+  else                                                                                                          \
+    hipLaunchKernelGGL(head_bwd_fused_kernel<HDV>, grid, dim3(256), 0, st, hp, dout, s_dout, dz, po, dbp, counts, \
+                       rows, max_rows, T_l, dWh, dbh)
   switch (hp.hd) {
     case 1: HBB_LAUNCH(1); break;
     case 2: HBB_LAUNCH(2); break;

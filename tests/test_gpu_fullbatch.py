@@ -545,3 +545,40 @@ def test_full_batch_8way_sharded_optimizer_matches_oracle(precision, name):
     assert max(frac) < 0.3, frac
     for e in shards:
         e.close()
+
+
+_DIGEST_CHILD = """
+import hashlib
+import sys
+sys.path.insert(0, {root!r})
+sys.path.insert(0, {tests!r})
+import numpy as np
+import test_gpu_fullbatch as t
+a = t._device_steps({T}, {tc}, 2048, 3, 3, 0)
+h = hashlib.sha256()
+h.update(repr(sorted(a[0].items())).encode())
+for x in a[1]:
+    h.update(np.ascontiguousarray(x).tobytes())
+h.update(repr(a[2]).encode())
+h.update(repr(a[3]).encode())
+print("digest", h.hexdigest())
+"""
+
+
+@pytest.mark.parametrize("T,tc", [(50, 50), (50, 7)], ids=["s3_split2h", "mt50_shard7_split2h"])
+def test_head_kernel_forms_bitwise(T, tc):
+    """The head kernels' launch forms are bitwise interchangeable: the fused head backward (data and
+    weight passes reading h once) against the separate passes (MTSAC_HEAD_BWD_SPLIT=1), and the
+    policy / action-grad rows per wave (MTSAC_HEAD_RW=4 against the default): 3 device-sampled
+    steps each in a fresh process (the switches are read once), digests of logs, parameters,
+    moments and stream states equal."""
+    import os
+
+    tests = os.path.dirname(os.path.abspath(__file__))
+    code = _DIGEST_CHILD.format(root=os.path.dirname(tests), tests=tests, T=T, tc=tc)
+    digests = []
+    for extra in ({}, {"MTSAC_HEAD_BWD_SPLIT": "1"}, {"MTSAC_HEAD_RW": "4"}):
+        r = _child(code, dict(os.environ, **extra), timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        digests.append([ln for ln in r.stdout.splitlines() if ln.startswith("digest")][-1])
+    assert digests[0] == digests[1] == digests[2], digests

@@ -1,0 +1,18 @@
+# gpu_r4u.sh -- round-4: fused head backward (h read once) + 4-per-CU rows per wave: bitwise forms
+# test, full GPU suite, S3 bench, serialised S3 / 7-task sums
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r4u
+mkdir -p $O
+R=$GRAFT_REPO_ROOT
+timeout -k 10 600 python -u -m pytest tests/test_gpu_fullbatch.py -q -rf -x -s -k head_kernel_forms --timeout 500 --timeout-method thread > $O/tests_forms.log 2>&1 || exit 1
+timeout -k 10 700 python -u -m pytest tests -m gpu -q -rf -x --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err || exit 1
+cd /tmp && export TMPDIR=/tmp
+for cfg in "50 50 2048 3 s3_split2h" "7 50 2048 3 t7_split2h"; do
+  set -- $cfg
+  timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $R/$O/kt_$5 -o run -- python $R/tools/shard_prof.py $1 $2 $3 $4 > $R/$O/kt_$5.log 2>&1 || exit 1
+  python $R/tools/kernel_sums.py $R/$O/kt_$5/run_kernel_trace.csv 45 > $R/$O/sums_$5.txt || exit 1
+  rm -rf $R/$O/kt_$5
+done
+echo done
