@@ -804,15 +804,9 @@ __global__ __launch_bounds__(256) void head_bwd_fused_kernel(HeadParams hp, cons
 // (16-B chunks 4l + 256i when Wc % 4 == 0, else l + 64i), then over the wave.
 // AM: action dimensions held per row -- 4 (MetaWorld: no run-time test around the weight loads, which
 // were otherwise waited for one at a time) or 8 (any A <= 8)
+// rows b0 .. b0 + AG_RW - 1 of one wave; returns the wave's max |dout| (lanes < A; 0 elsewhere)
 template <int AG_RW, int AM>
-__global__ __launch_bounds__(256) void action_grad_kernel(ActionGradParams p) {
-  const int lane = threadIdx.x & 63;
-  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int b0 = wid * AG_RW;
-  if (b0 >= p.B) {
-    if (p.dout_rec && lane == 0 && wid < PLANE_REC_PARTS) p.dout_rec->amax[wid] = 0.f;
-    return;
-  }
+__device__ inline float action_grad_rows(const ActionGradParams& p, int b0, int lane) {
   const int A = p.A;
   int rows[AG_RW];
 #pragma unroll
@@ -892,10 +886,24 @@ __global__ __launch_bounds__(256) void action_grad_kernel(ActionGradParams p) {
     p.dout[(long long)b * 2 * A + A + lane] = g_ls;
     omx = fmaxf(omx, fmaxf(fabsf(g_x), fabsf(g_ls)));
   }
-  if (p.dout_rec) {  // split2h: this wave's max |dout| (the actor head backward's bound input)
+  return omx;
+}
+
+// grid-stride over wave row groups (the grid is capped at PLANE_REC_PARTS workgroups); split2h: one
+// max |dout| per workgroup (the actor head backward's bound input), every row covered
+template <int AG_RW, int AM>
+__global__ __launch_bounds__(256) void action_grad_kernel(ActionGradParams p) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float omx = 0.f;
+  for (int wid = blockIdx.x * 4 + wave; wid * AG_RW < p.B; wid += gridDim.x * 4)
+    omx = fmaxf(omx, action_grad_rows<AG_RW, AM>(p, wid * AG_RW, lane));
+  if (p.dout_rec) {
+    __shared__ float smx[4];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) omx = fmaxf(omx, __shfl_xor(omx, o));
-    if (lane == 0 && wid < PLANE_REC_PARTS) p.dout_rec->amax[wid] = omx;
+    if (lane == 0) smx[wave] = omx;
+    __syncthreads();
+    if (threadIdx.x == 0) p.dout_rec->amax[blockIdx.x] = fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3]));
   }
 }
 
@@ -1056,8 +1064,8 @@ void head_backward_weight(const HeadParams& hp, const float* dout, long long s_d
 
 void action_grad(const ActionGradParams& p, hipStream_t st) {
   const int rw = rows_per_wave((p.B + 3) / 4);
-  const dim3 grid((unsigned)((p.B + 4 * rw - 1) / (4 * rw)));
-  if (p.dout_parts) *p.dout_parts = std::min<int>(4 * (int)grid.x, PLANE_REC_PARTS);
+  const dim3 grid((unsigned)std::min((p.B + 4 * rw - 1) / (4 * rw), PLANE_REC_PARTS));
+  if (p.dout_parts) *p.dout_parts = (int)grid.x;  // one partial max per workgroup
 #define AGL(AMV)                                                                                  \
   if (rw == 4) hipLaunchKernelGGL((action_grad_kernel<4, AMV>), grid, dim3(256), 0, st, p);        \
   else if (rw == 2) hipLaunchKernelGGL((action_grad_kernel<2, AMV>), grid, dim3(256), 0, st, p);   \
