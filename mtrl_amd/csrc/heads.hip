@@ -70,12 +70,12 @@ __device__ inline void rows_dot(const float* const (&h)[R], const float* __restr
 #pragma unroll
       for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int o = 0; o < HD; ++o) {
+        for (int o = 0; o < HD; ++o) {  // explicit fmas: the same roundings in every R instance
           float a = acc[r][o];
-          a += hv[r].x * wv[o];
-          a += hv[r].y * wv[HD + o];
-          a += hv[r].z * wv[2 * HD + o];
-          a += hv[r].w * wv[3 * HD + o];
+          a = __builtin_fmaf(hv[r].x, wv[o], a);
+          a = __builtin_fmaf(hv[r].y, wv[HD + o], a);
+          a = __builtin_fmaf(hv[r].z, wv[2 * HD + o], a);
+          a = __builtin_fmaf(hv[r].w, wv[3 * HD + o], a);
           acc[r][o] = a;
         }
     }
@@ -94,12 +94,12 @@ __device__ inline void rows_dot(const float* const (&h)[R], const float* __restr
 #pragma unroll
       for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int o = 0; o < HD; ++o) {
+        for (int o = 0; o < HD; ++o) {  // explicit fmas: the same roundings in every R instance
           float a = acc[r][o];
-          a += hv[r].x * wv[o];
-          a += hv[r].y * wv[HD + o];
-          a += hv[r].z * wv[2 * HD + o];
-          a += hv[r].w * wv[3 * HD + o];
+          a = __builtin_fmaf(hv[r].x, wv[o], a);
+          a = __builtin_fmaf(hv[r].y, wv[HD + o], a);
+          a = __builtin_fmaf(hv[r].z, wv[2 * HD + o], a);
+          a = __builtin_fmaf(hv[r].w, wv[3 * HD + o], a);
           acc[r][o] = a;
         }
     }
@@ -109,7 +109,7 @@ __device__ inline void rows_dot(const float* const (&h)[R], const float* __restr
       for (int r = 0; r < R; ++r) {
         const float hv = h[r][w];
 #pragma unroll
-        for (int o = 0; o < HD; ++o) acc[r][o] += hv * Wt[(long long)w * HD + o];
+        for (int o = 0; o < HD; ++o) acc[r][o] = __builtin_fmaf(hv, Wt[(long long)w * HD + o], acc[r][o]);
       }
     }
   }
@@ -272,7 +272,7 @@ static int rows_per_wave(long long wgs_at_rw1) {
 }
 
 // ------------------------------------------------------------------ critic heads + losses
-// grid-stride over rows (one wave per row at a time); split2h: each wave's max |dq| to dq_rec
+// grid-stride over rows (one wave per row at a time); split2h: each workgroup's max |dq| to dq_rec
 __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
   const int lane = threadIdx.x & 63;
   const HeadParams& hp = p.head;
@@ -343,7 +343,12 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
     p.alpha_w[b] = w * alpha * p.inv_norm;
   }
   }  // rows
-  if (p.dq_rec && lane == 0 && wid < PLANE_REC_PARTS) p.dq_rec->amax[wid] = dqmax;
+  if (p.dq_rec) {  // one max per workgroup (lane 0 of each wave holds its wave's)
+    __shared__ float smx[4];
+    if (lane == 0) smx[threadIdx.x >> 6] = dqmax;
+    __syncthreads();
+    if (threadIdx.x == 0) p.dq_rec->amax[blockIdx.x] = fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3]));
+  }
 }
 
 // ------------------------------------------------------------------ head backward (data)
@@ -831,12 +836,12 @@ __device__ inline float action_grad_rows(const ActionGradParams& p, int b0, int 
         for (int r = 0; r < AG_RW; ++r) {
           const float4 g = *reinterpret_cast<const float4*>(dz + (long long)rows[r] * p.Wc + w);
 #pragma unroll
-          for (int j = 0; j < AM; ++j) {
+          for (int j = 0; j < AM; ++j) {  // explicit fmas: the same roundings in every AG_RW instance
             float a = ga[r][j];
-            a += g.x * wv[j].x;
-            a += g.y * wv[j].y;
-            a += g.z * wv[j].z;
-            a += g.w * wv[j].w;
+            a = __builtin_fmaf(g.x, wv[j].x, a);
+            a = __builtin_fmaf(g.y, wv[j].y, a);
+            a = __builtin_fmaf(g.z, wv[j].z, a);
+            a = __builtin_fmaf(g.w, wv[j].w, a);
             ga[r][j] = a;
           }
         }
@@ -851,7 +856,7 @@ __device__ inline float action_grad_rows(const ActionGradParams& p, int b0, int 
       for (int r = 0; r < AG_RW; ++r) {
         const float g = dz[(long long)rows[r] * p.Wc + w];
 #pragma unroll
-        for (int j = 0; j < AM; ++j) ga[r][j] += g * wv[j];
+        for (int j = 0; j < AM; ++j) ga[r][j] = __builtin_fmaf(g, wv[j], ga[r][j]);
       }
     }
   }
@@ -994,8 +999,10 @@ void policy_head_pair(const PolicyParams& a, const PolicyParams& b, hipStream_t 
 }
 
 void critic_head(const CriticHeadParams& p, hipStream_t st) {
-  const int g = std::min((p.head.B + 3) / 4, PLANE_REC_PARTS / 4);  // one max per wave (split2h)
-  if (p.dq_parts) *p.dq_parts = 4 * g;
+  // a wave per row (grid-stride past PLANE_REC_PARTS workgroups: one max per workgroup, split2h);
+  // at S3 6400 rows in flight instead of 2048 waves stepping over three rows each
+  const int g = std::min((p.head.B + 3) / 4, PLANE_REC_PARTS);
+  if (p.dq_parts) *p.dq_parts = g;
   hipLaunchKernelGGL(critic_head_kernel, dim3(g), dim3(256), 0, st, p);
 }
 
