@@ -872,8 +872,11 @@ __device__ inline float action_grad_rows(const ActionGradParams& p, int b0, int 
     c_eps[r] = c[4 * A + lj];
     c_lp[r] = p.alpha_w[rows[r]];
   }
+  // no contraction in the per-row tail: the vectoriser packs rows of the 2- and 4-row instances, and
+  // contracted multiply-adds then round differently per instance (profiles/r4v_head_forms.txt)
 #pragma unroll
   for (int r = 0; r < AG_RW; ++r) {
+#pragma clang fp contract(off)
     const int b = b0 + r;
 #pragma unroll
     for (int j = 0; j < AM; ++j) ga[r][j] = j < A ? wsum(ga[r][j]) : 0.f;
