@@ -282,65 +282,18 @@ __global__ __launch_bounds__(256) void critic_head_kernel(CriticHeadParams p) {
   const int t = hp.task[b];
   float q[4];
   const int E = hp.E;
+  for (int e = 0; e < E; ++e) {
+    float acc[1];
+    head_dot<1>(hp.h + e * hp.sh + (long long)b * hp.W, hp.Wh + e * hp.sWh + (long long)t * hp.W, hp.W, acc);
+    q[e] = acc[0] + hp.bh[e * hp.sbh + t];
+  }
   float qt[4];  // fused_target: the target critic's heads of the same row (same row, same task)
-  if (E == 2 && (hp.W & 3) == 0 && !p.seq_dots) {
-    // the twin critic: the row's 2 (fused target: 4) dot products in ONE pass over w, their loads in
-    // flight together (one after another they were 4 latency-bound passes); each sum keeps head_dot's
-    // per-lane order and fmas, so the results are bitwise the same
+  if (p.fused_target) {
     const HeadParams& th = p.thead;
-    const int nq = p.fused_target ? 4 : 2;
-    const float* hq[4];
-    const float* wq[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const HeadParams& hh = k < 2 ? hp : th;
-      const int e = k & 1;
-      hq[k] = hh.h + e * hh.sh + (long long)b * hh.W;
-      wq[k] = hh.Wh + e * hh.sWh + (long long)t * hh.W;
-    }
-    float a[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-    for (int w = 4 * lane; w < hp.W; w += 256) {
-      float4 hv[4], wv[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (k < nq) {
-          hv[k] = *reinterpret_cast<const float4*>(hq[k] + w);
-          wv[k] = *reinterpret_cast<const float4*>(wq[k] + w);
-        } else {
-          hv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-          wv[k] = hv[k];
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        a[k] = __builtin_fmaf(hv[k].x, wv[k].x, a[k]);
-        a[k] = __builtin_fmaf(hv[k].y, wv[k].y, a[k]);
-        a[k] = __builtin_fmaf(hv[k].z, wv[k].z, a[k]);
-        a[k] = __builtin_fmaf(hv[k].w, wv[k].w, a[k]);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) a[k] = wsum(a[k]);
-    q[0] = a[0] + hp.bh[t];
-    q[1] = a[1] + hp.bh[hp.sbh + t];
-    if (p.fused_target) {
-      qt[0] = a[2] + th.bh[t];
-      qt[1] = a[3] + th.bh[th.sbh + t];
-    }
-  } else {
     for (int e = 0; e < E; ++e) {
       float acc[1];
-      head_dot<1>(hp.h + e * hp.sh + (long long)b * hp.W, hp.Wh + e * hp.sWh + (long long)t * hp.W, hp.W, acc);
-      q[e] = acc[0] + hp.bh[e * hp.sbh + t];
-    }
-    if (p.fused_target) {
-      const HeadParams& th = p.thead;
-      for (int e = 0; e < E; ++e) {
-        float acc[1];
-        head_dot<1>(th.h + e * th.sh + (long long)b * th.W, th.Wh + e * th.sWh + (long long)t * th.W, th.W, acc);
-        qt[e] = acc[0] + th.bh[e * th.sbh + t];
-      }
+      head_dot<1>(th.h + e * th.sh + (long long)b * th.W, th.Wh + e * th.sWh + (long long)t * th.W, th.W, acc);
+      qt[e] = acc[0] + th.bh[e * th.sbh + t];
     }
   }
   if (lane != 0) continue;
@@ -1048,13 +1001,7 @@ void policy_head_pair(const PolicyParams& a, const PolicyParams& b, hipStream_t 
 #undef PHP
 }
 
-void critic_head(const CriticHeadParams& p0, hipStream_t st) {
-  static const int seq = [] {  // MTSAC_CRITIC_HEAD_SEQ=1: the member dot products one after another
-    const char* e = getenv("MTSAC_CRITIC_HEAD_SEQ");
-    return e && atoi(e) != 0 ? 1 : 0;
-  }();
-  CriticHeadParams p = p0;
-  p.seq_dots = seq;
+void critic_head(const CriticHeadParams& p, hipStream_t st) {
   // a wave per row (grid-stride past PLANE_REC_PARTS workgroups: one max per workgroup, split2h);
   // at S3 6400 rows in flight instead of 2048 waves stepping over three rows each
   const int g = std::min((p.head.B + 3) / 4, PLANE_REC_PARTS);

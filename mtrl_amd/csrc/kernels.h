@@ -321,7 +321,6 @@ struct CriticHeadParams {
   float inv_norm;       // 1/(E*B) critic, 1/B actor (global B)
   PlaneRec* dq_rec;     // split2h: per-workgroup max |dq| (the head backward's bound input), or null
   int* dq_parts;        // host: how many the launch wrote
-  int seq_dots;         // set by critic_head: the twin members' dot products one after another (experiments)
 };
 void critic_head(const CriticHeadParams& p, hipStream_t st);
 
