@@ -1032,10 +1032,14 @@ bool head_backward_both(const HeadParams& hp, const float* dout, long long s_dou
                         hipStream_t st) {
   if (hp.W % 4 != 0) return false;  // the scalar weight kernel: two launches
   const int gw = (hp.W + 255) / 256;
-  static const bool split = [] {  // MTSAC_HEAD_BWD_SPLIT=1: the data and weight passes as separate blocks
+  static const bool split_req = [] {  // MTSAC_HEAD_BWD_SPLIT=1: the data and weight passes as separate blocks
     const char* e = getenv("MTSAC_HEAD_BWD_SPLIT");
     return e && atoi(e) != 0;
   }();
+  // the one-pass form has a workgroup per (task, 256 columns, member): below one per CU (task shards,
+  // MT10) the separate passes' 5x more workgroups win (7-task shard: 27 / 18 us one-pass against
+  // 15 / 11 us, profiles/r4u_sums_t7_split2h.txt vs r4g); bitwise the same either way
+  const bool split = split_req || (long long)T_l * gw * hp.E < 256;
   const dim3 grid((unsigned)(split ? gw * T_l * HB_RS * hp.E + T_l * gw * hp.E : T_l * gw * hp.E));
 #define HBB_LAUNCH(HDV)                                                                                         \
   if (split)                                                                                                    \
