@@ -236,10 +236,12 @@ int mtsac_set_collective_hook(mtsac_engine* h, mtsac_collective_fn fn, void* use
  * TrainState.apply_gradients, mtrl/config/optim.py:26-43, mtrl/rl/algorithms/utils.py:11-46): every trunk
  * bucket is reduce-scattered instead of all-reduced, the global clip norm comes from an all-reduced
  * |g|^2, each rank runs Adam on its 1/world of the trunk, the new trunk is all-gathered and every
- * rank writes its own GEMM planes and Polyak target from it.  on: 1 / 0; active only with a device
- * collective (RCCL, the modelled one) or a collective hook, and when world divides every bucket into
- * whole float4s (else the all-reduce path runs).  The Adam moments then live sharded: get_params of
- * a moment returns this rank's shards current, the rest stale.  Default off (MTSAC_ZERO=1 turns it on). */
+ * rank writes its own GEMM planes and Polyak target from it.  on: 1 / 0; active only with an RCCL
+ * communicator or a collective hook (not the one-GPU modelled collective, whose collectives move no data),
+ * with world > 1, at most 7 trunk buckets and world dividing every bucket into whole float4s (else the
+ * all-reduce path runs).  Switching drops a captured step graph.  The Adam moments then live sharded:
+ * get_params of a moment returns this rank's shards current, the rest stale.  Default off (MTSAC_ZERO=1
+ * turns it on). */
 int mtsac_set_sharded_optimizer(mtsac_engine* h, int32_t on);
 /* plain device/host copy helper for hooks written in a host language (hipMemcpyDefault) */
 int mtsac_memcpy(void* dst, const void* src, int64_t bytes);

@@ -80,6 +80,15 @@ int mtsac_debug_set_pipeline(struct mtsac_engine* engine, int32_t on);
  * form needs MTSAC_LANES=1 and enough hardware queues: GPU_MAX_HW_QUEUES as the process started
  * >= 5 per live engine + 3), else 0. */
 int mtsac_debug_lane_mode(struct mtsac_engine* engine);
+/* Guard zones (MTSAC_GUARD_BYTES=n in the environment before the engine is created): n bytes of 0xFF
+ * around every device allocation.  Returns the number of guards a kernel wrote (0 = intact; -95 when
+ * the mode is off); the first few are named in mtsac_last_error. */
+int mtsac_debug_check_guards(struct mtsac_engine* engine);
+/* Step buffer views (diagnostics): snapshot on/off; read id 0 actor top activations, 1 / 2 their
+ * snapshots after the actor forward / the actor-loss pass ([Ma][W]), 3 actor dout ([B][2A]), 4 actor
+ * gradient head leaves.  count must equal the buffer's float count. */
+int mtsac_debug_snapshot(struct mtsac_engine* engine, int32_t on);
+int mtsac_debug_read(struct mtsac_engine* engine, int32_t id, float* dst, int64_t count);
 /* Weight planes in the fragment layout (gemm_x3f B operand, engine.cpp Net::bfrag): mode -1 (the
  * default) decides by shape (MTSAC_BFRAG=0 turns it off), 0 / 1 forces it off / allows it, for
  * engines created afterwards.  mtsac_debug_bfrag: bit i actor layer i, bit 8 + i critic layer i. */

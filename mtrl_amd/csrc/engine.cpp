@@ -447,6 +447,7 @@ struct mtsac_engine {
   std::vector<TimedLaunch> tl;
   size_t tl_next = 0;
   std::vector<void*> allocs;
+  float* dbg_snap[2] = {};  // mtsac_debug_snapshot: ha[top] after the actor forward (0) and after the actor-loss pass (1)
 
   ~mtsac_engine() {
     if (gexec) (void)hipGraphExecDestroy(gexec);
@@ -539,17 +540,41 @@ struct mtsac_engine {
     relane(r);
   }
 
+  // Guard zones (debug, MTSAC_GUARD_BYTES=n): every allocation gets n bytes of 0xFF (a NaN in fp32,
+  // bf16 and fp16 alike) before and after it; mtsac_debug_check_guards reports any guard a kernel wrote
+  // (an out-of-bounds store) -- and an out-of-bounds load inside a guard reads NaN, which the parity
+  // tests see.  Off by default (0 bytes).
+  struct Guard {
+    char* base;
+    size_t bytes;
+    int line;
+  };
+  std::vector<Guard> guards;
+  static size_t guard_bytes() {
+    static const size_t g = [] {
+      const char* e = getenv("MTSAC_GUARD_BYTES");
+      const long long v = e ? atoll(e) : 0;
+      return v > 0 ? (size_t)(v + 255) / 256 * 256 : (size_t)0;
+    }();
+    return g;
+  }
+
   template <typename T>
-  int alloc(T** p, size_t count) {
+  int alloc(T** p, size_t count, int line = __builtin_LINE()) {
     void* q = nullptr;
     size_t bytes = std::max<size_t>(count * sizeof(T), 256);
     bytes = (bytes + 255) / 256 * 256;
-    hipError_t e = hipMalloc(&q, bytes);
+    const size_t G = guard_bytes();
+    hipError_t e = hipMalloc(&q, bytes + 2 * G);
     if (e != hipSuccess) return fail(-12, std::string("hipMalloc failed: ") + hipGetErrorString(e));
-    e = hipMemset(q, 0, bytes);
+    char* b = reinterpret_cast<char*>(q);
+    e = hipMemset(b + G, 0, bytes);
+    if (e == hipSuccess && G) e = hipMemset(b, 0xFF, G);
+    if (e == hipSuccess && G) e = hipMemset(b + G + bytes, 0xFF, G);
     if (e != hipSuccess) return fail(-5, std::string("hipMemset failed: ") + hipGetErrorString(e));
     allocs.push_back(q);
-    *p = reinterpret_cast<T*>(q);
+    if (G) guards.push_back(Guard{b, bytes, line});
+    *p = reinterpret_cast<T*>(b + G);
     return 0;
   }
 
@@ -1089,10 +1114,13 @@ struct mtsac_engine {
   // and world divides every bucket into whole float4s
   bool zero_ok(const Net& net) const {
     const int W = coll_world();
-    if (zero_req <= 0 || W <= 1 || !(comm || cmodel.nranks > 1 || chook) || zparts == nullptr) return false;
+    // not under the modelled collective: its reduce-scatter / all-gather move no data, so Adam would
+    // update shard 0 of every bucket only (timing runs of the sharded optimizer need real ranks)
+    if (zero_req <= 0 || W <= 1 || !(comm || chook) || zparts == nullptr) return false;
     long long b[MAXD + 1], e[MAXD + 1];
     const int n = zero_buckets(net, b, e);
-    if (n > 8) return false;
+    // optimize_zero skips the gaps around this rank's n shards: up to n + 1 ranges in AdamParams::skip_b/_e
+    if (n + 1 > MAX_PLANE_SEGS) return false;
     for (int i = 0; i < n; ++i)
       if ((e[i] - b[i]) % (4LL * W) != 0) return false;
     return true;
@@ -1176,6 +1204,10 @@ struct mtsac_engine {
       for (int q = 0; q < nb; ++q) {
         const int k = ord[q];
         if (lo[k] > prev) {
+          if (as.nskip >= MAX_PLANE_SEGS) {  // zero_ok admits at most MAX_PLANE_SEGS - 1 buckets
+            comm_error = "sharded optimizer: too many skip ranges";
+            return;
+          }
           as.skip_b[as.nskip] = prev / 4;
           as.skip_e[as.nskip++] = lo[k] / 4;
         }
@@ -1183,6 +1215,10 @@ struct mtsac_engine {
       }
       const long long n = net.n_flat - net.trunk_off;
       if (prev < n) {
+        if (as.nskip >= MAX_PLANE_SEGS) {
+          comm_error = "sharded optimizer: too many skip ranges";
+          return;
+        }
         as.skip_b[as.nskip] = prev / 4;
         as.skip_e[as.nskip++] = (n + 3) / 4;
       }
@@ -1547,6 +1583,9 @@ struct mtsac_engine {
       qn.ap_rec = q.ap_rec;
       qn.logpi = logpi_n;
       policy_head_pair(q, qn, cur);
+      if (dbg_snap[0])
+        (void)hipMemcpyAsync(dbg_snap[0], ha[actor.depth - 1], sizeof(float) * Ma * actor.width,
+                             hipMemcpyDeviceToDevice, cur);
     });
     // target critic at (s', a'), TD target (mtsac.py:529-553)
     const bool fuse_td = one_stream || timing_serial;  // lanes: s_tg and s_cf run on two lanes
@@ -1650,6 +1689,9 @@ struct mtsac_engine {
         ag.dout_parts = &r_dout.n;
       }
       action_grad(ag, cur);
+      if (dbg_snap[1])
+        (void)hipMemcpyAsync(dbg_snap[1], ha[actor.depth - 1], sizeof(float) * Ma * actor.width,
+                             hipMemcpyDeviceToDevice, cur);
       if (sharded()) {
         const float* ins[1] = {row_c};
         reduce_rows(ins, 1, Bl, actor.g + actor.n_flat + 1, cur);
@@ -3132,7 +3174,16 @@ int mtsac_set_collective_hook(mtsac_engine* h, mtsac_collective_fn fn, void* use
 
 int mtsac_set_sharded_optimizer(mtsac_engine* h, int32_t on) {
   if (!h) return fail(-22, "null engine");
-  h->zero_req = on ? 1 : 0;
+  const int want = on ? 1 : 0;
+  if (want == h->zero_req) return 0;
+  HIP_TRY(hipStreamSynchronize(h->st));
+  h->zero_req = want;
+  if (h->gexec) {  // the captured step holds the other optimizer form (bucket ops, optimize_zero)
+    (void)hipGraphExecDestroy(h->gexec);
+    (void)hipGraphDestroy(h->graph);
+    h->gexec = nullptr;
+    h->graph = nullptr;
+  }
   return 0;
 }
 
@@ -3234,6 +3285,70 @@ int mtsac_debug_bfrag(mtsac_engine* h) {
   int m = 0;
   for (int i = 0; i < MAXD && i < 8; ++i) m |= (h->actor.bfrag[i] ? 1 << i : 0) | (h->critic.bfrag[i] ? 256 << i : 0);
   return m;
+}
+
+// MTSAC_GUARD_BYTES debug mode: the allocations whose guard zones a kernel wrote; returns their count
+// (0: every guard intact, -95 when the mode is off) and names the first few (source line of the
+// alloc call, side, first written byte) in mtsac_last_error
+int mtsac_debug_check_guards(mtsac_engine* h) {
+  if (!h) return fail(-22, "null engine");
+  const size_t G = mtsac_engine::guard_bytes();
+  if (G == 0) return fail(-95, "guard zones are off (set MTSAC_GUARD_BYTES before the engine is created)");
+  HIP_TRY(hipDeviceSynchronize());
+  std::vector<unsigned char> buf(G);
+  int bad = 0;
+  std::string msg;
+  for (const auto& g : h->guards)
+    for (int side = 0; side < 2; ++side) {
+      HIP_TRY(hipMemcpy(buf.data(), g.base + (side ? G + g.bytes : 0), G, hipMemcpyDeviceToHost));
+      size_t first = G, n = 0;
+      for (size_t i = 0; i < G; ++i)
+        if (buf[i] != 0xFF) {
+          if (first == G) first = i;
+          ++n;
+        }
+      if (n) {
+        ++bad;
+        if (bad <= 8)
+          msg += "alloc@line " + std::to_string(g.line) + " (" + std::to_string(g.bytes) + " B) " +
+                 (side ? "back" : "front") + " guard: " + std::to_string(n) + " bytes written, first at " +
+                 (side ? "+" : "-") + std::to_string(side ? first : G - first) + "; ";
+      }
+    }
+  if (bad) g_last_error = msg;
+  return bad;
+}
+
+// Debug views of step buffers (tools/shard_diag.py).  mtsac_debug_snapshot(on): from the next step on,
+// copy the actor's top activations right after the actor forward and after the actor-loss pass.
+// mtsac_debug_read(id): 0 the actor's top activations now, 1 / 2 the two snapshots ([Ma][W] each),
+// 3 the actor head's output gradient dout ([B][2A]), 4 the actor gradient's head leaves.
+int mtsac_debug_snapshot(mtsac_engine* h, int32_t on) {
+  if (!h) return fail(-22, "null engine");
+  if (on && !h->dbg_snap[0])
+    for (float*& q : h->dbg_snap)
+      if (int rc = h->alloc(&q, (size_t)h->Ma * h->actor.width)) return rc;
+  if (!on) h->dbg_snap[0] = h->dbg_snap[1] = nullptr;  // freed with the engine
+  return 0;
+}
+
+int mtsac_debug_read(mtsac_engine* h, int32_t id, float* dst, int64_t count) {
+  if (!h || !dst) return fail(-22, "null argument");
+  const float* src = nullptr;
+  int64_t n = 0;
+  switch (id) {
+    case 0: src = h->ha[h->actor.depth - 1]; n = (int64_t)h->Ma * h->actor.width; break;
+    case 1: src = h->dbg_snap[0]; n = (int64_t)h->Ma * h->actor.width; break;
+    case 2: src = h->dbg_snap[1]; n = (int64_t)h->Ma * h->actor.width; break;
+    case 3: src = h->dout_a; n = (int64_t)h->B * 2 * h->A; break;
+    case 4: src = h->actor.g; n = h->actor.trunk_off; break;
+    default: return fail(-22, "unknown buffer id");
+  }
+  if (!src) return fail(-22, "buffer not allocated (mtsac_debug_snapshot)");
+  if (count != n) return fail(-22, "count must be " + std::to_string(n));
+  HIP_TRY(hipStreamSynchronize(h->st));
+  HIP_TRY(hipMemcpy(dst, src, sizeof(float) * n, hipMemcpyDeviceToHost));
+  return 0;
 }
 
 int mtsac_debug_lane_mode(mtsac_engine* h) {
