@@ -530,7 +530,7 @@ struct mtsac_engine {
     int laned = 0;
     for (mtsac_engine* e : r.live) laned += e->force_one ? 0 : 1;
     const bool one = !(want && atoi(want) != 0) || laned * LANES + 3 > hwq;
-    for (mtsac_engine* e : r.live) e->one_stream = one || e->force_one;
+    for (mtsac_engine* e : r.live) e->one_stream = one || e->force_one || e->s1 == nullptr;  // no lane streams: created without MTSAC_LANES
   }
   void lane_mode_for() {
     Registry& r = registry();
@@ -1049,6 +1049,11 @@ struct mtsac_engine {
     hp.sWh = net.ms_hW;
     hp.sbh = net.ms_hb;
     hp.sh = (long long)M * net.width;
+    static const int dbg = [] {
+      const char* e = getenv("MTSAC_DBG_HEAD");
+      return e ? atoi(e) : 0;
+    }();
+    hp.dbg = dbg;
     return hp;
   }
 
@@ -2197,8 +2202,33 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
     delete e;
     return r;
   };
-  for (hipStream_t* x : {&e->st, &e->s1, &e->s2, &e->s3, &e->s4, &e->sa})
-    if (hipStreamCreateWithFlags(x, hipStreamNonBlocking) != hipSuccess) return bad(fail(-5, "stream"));
+  // Streams: the main stream, the prefetch stream s2, the collective stream s4 and the buffer-add pack
+  // stream sa -- four, so HIP's default four hardware queues give each its own.  s1 and s3 serve only
+  // the experimental 5-lane form and exist only when it is requested (MTSAC_LANES=1).  Streams beyond
+  // GPU_MAX_HW_QUEUES share hardware queues, and concurrently active streams on a shared queue were
+  // seen to read stale data ("Shared hardware queues").
+  {
+    const char* lw = getenv("MTSAC_LANES");
+    const bool lanes_wanted = lw && atoi(lw) != 0;
+    // diagnostics (MTSAC_CU_SLICE=k:n): this engine's streams run on CU slice k of n only, so engines
+    // sharing one device in a test never share a CU
+    std::vector<uint32_t> cu_mask;
+    if (const char* cs = getenv("MTSAC_CU_SLICE")) {
+      int k = 0, n = 1, ncu = 0;
+      if (sscanf(cs, "%d:%d", &k, &n) == 2 && n >= 1 && k >= 0 && k < n &&
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && ncu > 0) {
+        cu_mask.assign((ncu + 31) / 32, 0u);
+        for (int c = k * ncu / n; c < (k + 1) * ncu / n; ++c) cu_mask[c / 32] |= 1u << (c % 32);
+      }
+    }
+    for (hipStream_t* x : {&e->st, &e->s2, &e->s4, &e->sa, &e->s1, &e->s3}) {
+      if ((x == &e->s1 || x == &e->s3) && !lanes_wanted) continue;
+      const hipError_t r = cu_mask.empty()
+                               ? hipStreamCreateWithFlags(x, hipStreamNonBlocking)
+                               : hipExtStreamCreateWithCUMask(x, (uint32_t)cu_mask.size(), cu_mask.data());
+      if (r != hipSuccess) return bad(fail(-5, "stream"));
+    }
+  }
   e->lane_mode_for();
   e->cur = e->st;
   for (int i = 0; i < 128; ++i) {

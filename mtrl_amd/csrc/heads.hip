@@ -636,6 +636,11 @@ __global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, con
                                                               const int* __restrict__ rows, int max_rows,
                                                               float* __restrict__ dWh, float* __restrict__ dbh) {
   __shared__ float4 red[4][64][HD];
+  if (hp.dbg & 1) {  // diagnostics: drop this CU's L1 before any load (MTSAC_DBG_HEAD=1)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   head_bwd_weight_body<HD>(hp, dout, s_dout, counts, rows, max_rows, dWh, dbh, blockIdx.x, blockIdx.y, blockIdx.z,
                            red);
 }
@@ -652,6 +657,11 @@ __global__ __launch_bounds__(256) void head_bwd_both_kernel(HeadParams hp, const
   __shared__ float4 red[4][64][HD];
   const int gw = (hp.W + 255) / 256, gy = T_l * HB_RS;
   const int nd = gw * gy * hp.E;
+  if (hp.dbg & 1) {  // diagnostics: drop this CU's L1 before any load (MTSAC_DBG_HEAD=1)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   int b = blockIdx.x;
   if (b < nd) {
     const int bx = b % gw, by = (b / gw) % gy, bz = b / (gw * gy);

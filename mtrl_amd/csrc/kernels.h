@@ -259,6 +259,7 @@ struct HeadParams {
   const int* task;      // [B]
   int B, W, hd, E;
   long long sWh, sbh, sh;
+  int dbg;              // diagnostics (MTSAC_DBG_HEAD): 1 = an agent-scope acquire at the start of the head backward blocks
 };
 
 // actor head + tanh-normal sample (networks.py:28-45, distributions.py:6-16)

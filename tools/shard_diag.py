@@ -48,6 +48,8 @@ def leaf_errs(got, ref, shapes, tag):
 
 
 SNAP = False
+CU_SLICE = False  # --cu-slice: engine r runs on CU slice r of 8 (MTSAC_CU_SLICE)
+SNAP0 = {}  # rank -> the first repeat's h after the forward
 
 
 def snap_count(e, i):
@@ -65,9 +67,12 @@ def run_sharded(name, precision, world=8):
     shards = []
     for r in range(world):
         b0, c0 = shard_tasks(T, world, r)
+        if CU_SLICE:
+            os.environ["MTSAC_CU_SLICE"] = f"{r}:{world}"
         e = t._engine(spec, precision, b0, c0)
         t._load(e, st, b0, c0)
         shards.append(e)
+    os.environ.pop("MTSAC_CU_SLICE", None)
     if SNAP:
         for e in shards:
             L.check(e.lib.mtsac_debug_snapshot(e._h, 1))
@@ -114,12 +119,38 @@ def run_sharded(name, precision, world=8):
             off = -(-8 * c0 // 64) * 64  # leaves are 64-float aligned
             eng = bufs[4][off:off + c0 * W * 8].reshape(c0, W, 8).astype(np.float64)
             rel = np.abs(eng - gW).max() / np.abs(gW).max()
+            if rel > 1e-5 and os.environ.get("DIAG_DUMP"):  # the failing rank's operands, for offline analysis
+                os.makedirs(os.environ["DIAG_DUMP"], exist_ok=True)
+                np.savez_compressed(os.path.join(os.environ["DIAG_DUMP"], f"fail_r{r}_{len(SNAP0)}_{np.random.randint(1 << 30)}.npz"),
+                                    h=bufs[0].reshape(-1, W)[:B], dout=bufs[3], eng=bufs[4], c0=c0, n=n)
+            if rel > 1e-5:  # which contributions are wrong: fit D[t, w, :] = c * dout[row, :] per row
+                D = eng - gW
+                tt, ww = np.unravel_index(np.argmax(np.abs(D).max(axis=2)), D.shape[:2])
+                rr = np.arange(n) * c0 + tt
+                dv = D[tt, ww]
+                best = []
+                for row in rr:
+                    dd = d[row]
+                    c = float(dv @ dd) / max(float(dd @ dd), 1e-300)
+                    best.append((float(np.linalg.norm(dv - c * dd)), int(row), c, float(h[row, ww])))
+                best.sort()
+                bad_w = np.flatnonzero(np.abs(D[tt]).max(axis=1) > 1e-5 * np.abs(gW).max())
+                print(f"  rank {r}: worst (t {tt}, w {ww}) D {np.array2string(dv, precision=3)}; bad w of t: {bad_w}; "
+                      f"best single-row fits (resid, row, coef, h[row,w]): {best[:3]} |dv| {np.linalg.norm(dv):.3e}",
+                      flush=True)
             s01 = np.array_equal(bufs[1], bufs[2]) and np.array_equal(bufs[1], bufs[0])
             diffrows = np.unique(np.flatnonzero((bufs[1] != bufs[0]).reshape(-1, W).any(axis=1)))
             diffcols = np.unique(np.flatnonzero((bufs[1] != bufs[0]).reshape(-1, W).any(axis=0)))
             print(f"  rank {r}: h snapshots equal {s01}; head_W grad vs numpy(h_final, dout) max rel {rel:.2e}; "
                   f"h changed after fwd: rows {diffrows[:10]} ({diffrows.size}) cols {diffcols[:10]} ({diffcols.size}); "
                   f"changed after loss pass: {not np.array_equal(bufs[2], bufs[0])}", flush=True)
+            if r in SNAP0:
+                d0 = (bufs[1] != SNAP0[r]).reshape(-1, W)
+                rr, cc = np.nonzero(d0)
+                print(f"  rank {r}: h after fwd vs rep 0: {rr.size} entries differ, rows {np.unique(rr)[:12]}, "
+                      f"cols {np.unique(cc)[:16]}", flush=True)
+            else:
+                SNAP0[r] = bufs[1].copy()
             snaps.append(bufs)
     logs = [e.logs() for e in shards]
     mus = [(e.get_params(L.ACTOR_ADAM_MU), e.get_params(L.CRITIC_ADAM_MU)) for e in shards]
@@ -135,9 +166,12 @@ def main():
     ap.add_argument("--single", action="store_true")
     ap.add_argument("--name", default="s3_mt50_w2048")
     ap.add_argument("--snap", action="store_true", help="snapshot the actor's top activations in the step")
+    ap.add_argument("--cu-slice", action="store_true", help="engine r on CU slice r of 8: no two engines share a CU")
+    ap.add_argument("--alternate", action="store_true", help="alternate --cu-slice on / off between repeats")
     a = ap.parse_args()
-    global SNAP
+    global SNAP, CU_SLICE
     SNAP = a.snap
+    CU_SLICE = a.cu_slice
     spec = t.SHARD_CASES[a.name]
     cfg, st, batch, en, ec, st1, want = t._problem(a.name)
     T, W = spec["T"], spec["W"]
@@ -147,6 +181,10 @@ def main():
     ref_a, ref_c = st1.actor_opt.mu, st1.critic_opt.mu
     first = None
     for rep in range(a.repeats):
+
+        if a.alternate:  # even repeats on CU slices, odd ones unsliced (same box, interleaved)
+            CU_SLICE = rep % 2 == 0
+            print(f"rep {rep}: cu slices {CU_SLICE}", flush=True)
         logs, mus = run_sharded(a.name, a.precision)
         same_ranks = all(lg == logs[0] for lg in logs)
         errs = {k: abs(logs[0][k] - want[k]) / max(abs(want[k]), 1e-30) for k in keys}
