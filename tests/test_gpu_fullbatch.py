@@ -63,14 +63,26 @@ def _problem(name):
     return cfg, st, batch, en, ec, st1, want
 
 
-def _engine(spec, precision, begin=0, count=None):
+def _engine(spec, precision, begin=0, count=None, cu_slice=None):
+    """cu_slice = (k, n): the engine's streams run on CU slice k of n only (MTSAC_CU_SLICE, read at
+    create).  The in-process multi-rank tests give every emulated rank its own CUs, as ranks on their
+    own GPUs have: with all engines' kernels co-resident on every CU, a handful of values of the head
+    backward's cross-wave LDS reduction came out wrong on some boxes ("Eight
+    engines on one device")."""
+    import os
+
     from mtrl_amd.engine import MTSACEngine, make_config
 
     T, W, n = spec["T"], spec["W"], spec["n"]
     c = make_config(num_tasks=T, task_begin=begin, task_count=T if count is None else count, obs_dim=39 + T,
                     actor_width=W, critic_width=W, batch_per_task=n, capacity=n, clip=int(spec["clip"]),
                     precision=precision)
-    e = MTSACEngine(c)
+    if cu_slice is not None:
+        os.environ["MTSAC_CU_SLICE"] = f"{cu_slice[0]}:{cu_slice[1]}"
+    try:
+        e = MTSACEngine(c)
+    finally:
+        os.environ.pop("MTSAC_CU_SLICE", None)
     e.enable_graph(False)
     return e
 
@@ -131,26 +143,20 @@ def test_full_batch_step_matches_oracle(name, precision):
     e.close()
 
 
-@pytest.mark.parametrize("precision", [0, 1, 3], ids=["fp32", "split3", "split2h"])
-@pytest.mark.parametrize("name", ["s3_mt50_w2048", "s4_mt50_w400"])
-def test_full_batch_8way_shard_matches_oracle(precision, name):
-    """The MT50 8-GPU task split (7,7,6,6,6,6,6,6 tasks, 128 rows each) as 8 engines on one
-    device reducing through the in-process hook (same reduction points as RCCL), against
-    the float64 oracle of the unsharded step.  S3 (W=2048) and S4, the literal
-    experiments/mt50_mtmhsac_v2.py width 400 (a shard's trunk GEMMs then run gemm_x3s and the
-    256x128 weight-grad tiles)."""
+def _run_8way(name, precision, world=8):
+    """The MT50 8-GPU task split as 8 engines on one device (each on its own CU slice), one full-batch
+    step through the in-process all-reduce hook; returns the engines (open) and their logs."""
     import threading
 
     from mtrl_amd.shard import InProcessAllReduce, local_rows, shard_tasks
 
-    world = 8
     spec = SHARD_CASES[name]
     cfg, st, batch, en, ec, st1, want = _problem(name)
     T, n = spec["T"], spec["n"]
     shards = []
     for r in range(world):
         b0, c0 = shard_tasks(T, world, r)
-        e = _engine(spec, precision, b0, c0)
+        e = _engine(spec, precision, b0, c0, cu_slice=(r, world))
         _load(e, st, b0, c0)
         shards.append(e)
     group = InProcessAllReduce(world)
@@ -170,13 +176,48 @@ def test_full_batch_8way_shard_matches_oracle(precision, name):
     [t.start() for t in th]
     [t.join() for t in th]
     assert not errs, errs
-    logs = [e.logs() for e in shards]
+    return shards, [e.logs() for e in shards]
+
+
+@pytest.mark.parametrize("precision", [0, 1, 3], ids=["fp32", "split3", "split2h"])
+@pytest.mark.parametrize("name", ["s3_mt50_w2048", "s4_mt50_w400"])
+def test_full_batch_8way_shard_matches_oracle(precision, name):
+    """The MT50 8-GPU task split (7,7,6,6,6,6,6,6 tasks, 128 rows each) as 8 engines on one
+    device reducing through the in-process hook (same reduction points as RCCL), against
+    the float64 oracle of the unsharded step.  S3 (W=2048) and S4, the literal
+    experiments/mt50_mtmhsac_v2.py width 400 (a shard's trunk GEMMs then run gemm_x3s and the
+    256x128 weight-grad tiles)."""
+    from mtrl_amd.shard import shard_tasks
+
+    world = 8
+    spec = SHARD_CASES[name]
+    cfg, st, batch, en, ec, st1, want = _problem(name)
+    shards, logs = _run_8way(name, precision, world)
     assert all(lg == logs[0] for lg in logs)  # every logged scalar is reduced: ranks agree bitwise
     _check_logs(logs[0], want, f"shard8/p{precision}")
     for r, e in enumerate(shards):
-        b0, c0 = shard_tasks(T, world, r)
+        b0, c0 = shard_tasks(spec["T"], world, r)
         _check_params(e, st1, f"shard8/p{precision}/r{r}", b0, c0)
         e.close()
+
+
+def test_full_batch_8way_shard_split2h_deterministic():
+    """the 8-engine S3 split2h step twice in one process (fresh engines, same
+    inputs) gives bitwise the same logs, parameters and Adam moments on every rank."""
+    from mtrl_amd import _lib as L
+
+    outs = []
+    for _ in range(2):
+        shards, logs = _run_8way("s3_mt50_w2048", 3)
+        outs.append((logs, [[e.get_params(w) for w in (L.ACTOR, L.CRITIC, L.CRITIC_TARGET, L.ACTOR_ADAM_MU,
+                                                         L.CRITIC_ADAM_MU, L.ACTOR_ADAM_NU)] for e in shards]))
+        for e in shards:
+            e.close()
+    (la, pa), (lb, pb) = outs
+    assert la == lb, [(r, {k: (a[k], b[k]) for k in a if a[k] != b[k]}) for r, (a, b) in enumerate(zip(la, lb)) if a != b]
+    for r, (xa, xb) in enumerate(zip(pa, pb)):
+        for q, (x, y) in enumerate(zip(xa, xb)):
+            assert np.array_equal(x, y), (r, q, int(np.count_nonzero(x != y)))
 
 
 def test_full_batch_modelled_collective_matches_oracle():
@@ -512,7 +553,7 @@ def test_full_batch_8way_sharded_optimizer_matches_oracle(precision, name):
     shards = []
     for r in range(world):
         b0, c0 = shard_tasks(T, world, r)
-        e = _engine(spec, precision, b0, c0)
+        e = _engine(spec, precision, b0, c0, cu_slice=(r, world))
         _load(e, st, b0, c0)
         e.set_sharded_optimizer(True)
         shards.append(e)

@@ -43,7 +43,8 @@ def _port():
 def _spawn(args, world, timeout):
     env_base = dict(os.environ, WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()),
                     PYTHONPATH=ROOT + os.pathsep + HERE + os.pathsep + os.environ.get("PYTHONPATH", ""))
-    procs = [subprocess.Popen([sys.executable, "-u"] + args(r), env=dict(env_base, RANK=str(r), LOCAL_RANK="0"))
+    procs = [subprocess.Popen([sys.executable, "-u"] + args(r), env=dict(env_base, RANK=str(r), LOCAL_RANK="0",
+                                                                             MTSAC_CU_SLICE=f"{r}:{world}"))
              for r in range(world)]
     deadline = time.monotonic() + timeout
     rcs = []
