@@ -317,10 +317,13 @@ struct mtsac_engine {
   // the in-launch split-K finish (gemm_x3f / gemm_x3p FIN) is opt-in (MTSAC_SPLITK_FIN=1): at the
   // task-shard shapes its 128-256 KB slabs per tile made it slower than the separate finishing pass
   // (profiles/r3t_fin_bench.txt)
+  // the in-launch finish (MTSAC_SPLITK_FIN=1; split2h: the two-slice pair hand-off, one slab per tile) is
+  // opt-in: on the 7-task shard it measured 1.50 vs 1.43 ms per step against the separate finishing pass
+  // (profiles/r5m_*): the finish then runs serially on half the CUs, latency-bound
   int* fin_cnt() {
     static const bool on = [] {
       const char* e = getenv("MTSAC_SPLITK_FIN");
-      return e && atoi(e) != 0;
+      return e && atoi(e) > 0;
     }();
     return on ? cnt_lane[cur_lane] : nullptr;
   }

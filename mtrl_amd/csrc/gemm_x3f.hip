@@ -218,8 +218,9 @@ bool gemm_x3f_fin(const SplitGemmParams& q, int epi, int bm, dim3 grid, hipStrea
 // the in-launch finish applies to this split launch (counters given, an instance for its outputs,
 // the tiles within the counter array)
 static bool x3f_fin_ok(const SplitGemmParams& p, int epi, int batch) {
-  if (p.cnt == nullptr || p.np == 2) return false;
+  if (p.cnt == nullptr) return false;
   const x3fk::SplitPlan sp = x3fk::split_plan(p.M, p.N, p.K, batch);
+  if (p.np == 2 && sp.s != 2) return false;  // split2h: the two-slice pair hand-off only
   const long long tiles = (long long)((p.M + sp.bm - 1) / sp.bm) * ((p.N + x3fk::BN - 1) / x3fk::BN) * batch;
   return tiles <= GEMM_X3F_CNT && gemm_x3f_fin_supported(p, epi, sp.bm);
 }
@@ -263,8 +264,12 @@ int gemm_x3f(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
     q.kchunk = (p0.K / KS + S - 1) / S * KS;
     q.splits = (p0.K + q.kchunk - 1) / q.kchunk;
     const int bm = split_plan(p0.M, p0.N, p0.K, batch).bm;
-    const dim3 grid((unsigned)(((p0.M + bm - 1) / bm) * ((p0.N + BN - 1) / BN) * batch * q.splits));
-    if (q.splits > 1 && gemm_x3f_fin(q, epi, bm, grid, st)) return q.splits;
+    const unsigned tiles = (unsigned)(((p0.M + bm - 1) / bm) * ((p0.N + BN - 1) / BN) * batch);
+    const dim3 grid(tiles * (unsigned)q.splits);
+    if (q.splits > 1 && (q.np != 2 || q.splits == 2) && gemm_x3f_fin(q, epi, bm, grid, st)) {
+      if (p0.nparts) *p0.nparts = (int)tiles;  // split2h: one partial max per tile (at the tile's index)
+      return q.splits;
+    }
   }
   if (S > 1) {  // raw partial slabs [z][S][M][N] into the workspace, then the epilogue pass
     SplitGemmParams q = p0;

@@ -269,21 +269,22 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   // alike); the scratch for the maxima sits past the epilogue's images and column-sum partials
   float unscale = 1.f, oscale = 1.f;
   float* mscr = img + 2 * EG * 16 * TS + WV * BN;
-  if constexpr (NP == 2) {
-    unscale = exp2i(-p.ra->e) * exp2i(-p.rb->e);
-    if (P_OUT && !FIN) {
-      const int ec = gemm_out_exp(p, mscr);
-      oscale = exp2i(ec);
-      if (blockIdx.x == 0 && t == 0) p.rc->e = ec;
-    }
-  }
+  if constexpr (NP == 2) unscale = exp2i(-p.ra->e) * exp2i(-p.rb->e);
   float omx = 0.f;  // this lane's max |out| (split2h planes)
   const int oc = 8 * (lane & 31);
   const int col = n0 + oc;
   const bool colok = col < p.N;  // N % 8 == 0: a lane's 8 columns are all in or all out
   const long long slab = (long long)p.M * p.N;
   const float* ws_z = FIN ? p.ws + (long long)z * nsplit * slab : nullptr;
-  if constexpr (FIN) {  // this slice's raw partial slab, then the tile's ticket
+  // FIN, two slices ("pair"): the ticket comes FIRST.  The slice drawing 0 publishes its (unscaled)
+  // partial in its slab with write-through (sc1) stores, drains them, and signals by adding 2 to the
+  // tile's counter; the slice drawing 1 (or 3: the partial is already published) polls the counter
+  // until it reads 4, re-arms it, and finishes the tile from its own registers plus the other slab,
+  // read with sc1 loads (the hand-off of MI355X_MICROARCH.md's table, row 1: no acquire needed).  One
+  // slab written instead of two, and the poller waits only on a slice that is already running.
+  // More slices: every slice writes its slab, draws a ticket, and the last one sums the slabs.
+  const bool pair = FIN && nsplit == 2;
+  auto write_slab = [&](bool scale) {  // this slice's partial into its slab (sc1 stores), drained
     const __amdgpu_buffer_rsrc_t slab_rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(p.ws + ((long long)z * nsplit + sl) * slab), (short)0, -1, 0x00020000);
 #pragma unroll
@@ -299,10 +300,14 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
         const int orow = 2 * (wave + WV * rp) + (lane >> 5);
         const int row = m0 + 16 * i + orow;
         if (row >= p.M || !colok) continue;
-        const float4 u = *reinterpret_cast<const float4*>(tb + orow * TS + oc);
-        const float4 v = *reinterpret_cast<const float4*>(tb + orow * TS + oc + 4);
+        float4 u = *reinterpret_cast<const float4*>(tb + orow * TS + oc);
+        float4 v = *reinterpret_cast<const float4*>(tb + orow * TS + oc + 4);
+        if (scale) {
+          u.x *= unscale; u.y *= unscale; u.z *= unscale; u.w *= unscale;
+          v.x *= unscale; v.y *= unscale; v.z *= unscale; v.w *= unscale;
+        }
         // write-through (sc1) stores: the slab leaves the XCD's L2, so no release fence (a
-        // buffer_wbl2 behind 128 KB of dirty lines per workgroup) is needed before the ticket
+        // buffer_wbl2 behind 128 KB of dirty lines per workgroup) is needed before the signal
         const unsigned o = (unsigned)(((long long)row * p.N + col) * 4);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, u), slab_rs, (int)o, 0, 16);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), slab_rs, (int)o + 16, 0, 16);
@@ -310,20 +315,51 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
     __syncthreads();
+  };
+  if constexpr (FIN) {
     int* last = reinterpret_cast<int*>(smem + SMEM0);
-    if (t == 0) {
-      const int tk = __hip_atomic_fetch_add(p.cnt + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int me = tk == nsplit - 1;
-      if (me) __hip_atomic_store(p.cnt + tile_id, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-      *last = me;
+    if (pair) {
+      if (t == 0) *last = __hip_atomic_fetch_add(p.cnt + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int tk = *last;  // block-uniform
+      if (tk == 0) {
+        write_slab(NP == 2);
+        if (t == 0) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_fetch_add(p.cnt + tile_id, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+      }
+      if (t == 0) {
+        if (tk == 1)  // the first slice has not published yet: it is running, so this ends
+          while (__hip_atomic_load(p.cnt + tile_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 4)
+            __builtin_amdgcn_s_sleep(2);
+        __hip_atomic_store(p.cnt + tile_id, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+      }
+      __syncthreads();
+    } else {
+      write_slab(NP == 2);
+      if (t == 0) {
+        const int tk = __hip_atomic_fetch_add(p.cnt + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int me = tk == nsplit - 1;
+        if (me) __hip_atomic_store(p.cnt + tile_id, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+        *last = me;
+      }
+      __syncthreads();
+      if (*last == 0) return;  // block-uniform
+      if (t == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
     }
-    __syncthreads();
-    if (*last == 0) return;  // block-uniform
-    if (t == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  if constexpr (NP == 2) {
+    if (P_OUT) {  // the output planes' exponent: every finishing workgroup derives it alike
+      const int ec = gemm_out_exp(p, mscr);
+      oscale = exp2i(ec);
+      if ((FIN ? tile_id : (int)blockIdx.x) == 0 && t == 0) p.rc->e = ec;
     }
-    __syncthreads();
   }
   float bias[8];
   if (EPI == EPI_BIAS_RELU && colok) {
@@ -340,14 +376,18 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   // per row block
   constexpr int PB = !FIN ? 1 : TI < 8 ? TI : 8;
   float pre[PB][8];
-  const bool two = FIN && nsplit == 2 && RP == 1;
-  auto prefetch = [&](int i0) {
+  static_assert(!FIN || RP == 1, "the in-launch finish runs with 8 waves (one row pair per wave and block)");
+  const bool two = pair;
+  const __amdgpu_buffer_rsrc_t other_rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(ws_z + (1 - sl) * slab), (short)0, -1, 0x00020000);
+  auto prefetch = [&](int i0) {  // the other slice's slab: sc1 loads (the pair hand-off)
 #pragma unroll
     for (int ii = 0; ii < PB; ++ii) {
       const int row = m0 + 16 * (i0 + ii) + 2 * wave + (lane >> 5);
       if (i0 + ii < TI && row < p.M && colok) {
-        const float* w = ws_z + (1 - sl) * slab + (long long)row * p.N + col;
-        const float4 a0 = *reinterpret_cast<const float4*>(w), a1 = *reinterpret_cast<const float4*>(w + 4);
+        const int o = (int)(((long long)row * p.N + col) * 4);
+        const float4 a0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(other_rs, o, 0, 16));
+        const float4 a1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(other_rs, o + 16, 0, 16));
         pre[ii][0] = a0.x; pre[ii][1] = a0.y; pre[ii][2] = a0.z; pre[ii][3] = a0.w;
         pre[ii][4] = a1.x; pre[ii][5] = a1.y; pre[ii][6] = a1.z; pre[ii][7] = a1.w;
       }
@@ -382,7 +422,7 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
     if (row >= p.M || !colok) continue;
     if ((ABL & 128) && p.M > 0) continue;  // ablation: no epilogue stores (p.M > 0 keeps the MFMAs live)
     float e[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-    if constexpr (NP == 2 && !FIN) {
+    if constexpr (NP == 2) {  // FIN: the slabs hold unscaled partials too (pair: s0 + s1 commutes)
 #pragma unroll
       for (int c = 0; c < 8; ++c) e[c] *= unscale;
     }
@@ -469,9 +509,10 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
     }  // row pairs
     }  // row blocks of the group
   }
-  if constexpr (NP == 2 && P_OUT && !FIN) {  // this workgroup's max |out|: the next producer's bound input
-    const float m = block_max_val(omx, mscr);
-    if (t == 0 && blockIdx.x < PLANE_REC_PARTS) p.rc->amax[blockIdx.x] = m;
+  if constexpr (NP == 2 && P_OUT) {  // this workgroup's max |out|: the next producer's bound input
+    const float m = block_max_val(omx, mscr);  // (FIN: one per tile, at the tile's index)
+    const int slot = FIN ? tile_id : (int)blockIdx.x;
+    if (t == 0 && slot < PLANE_REC_PARTS) p.rc->amax[slot] = m;
   }
   if (p.dbp) {  // the tile's column sums: lanes l, l + 32 of every wave hold the same 8 columns
     float* red = img + 2 * EG * 16 * TS;  // [WV waves][256]

@@ -164,18 +164,26 @@ def test_split_k_task_shards(E, M, N, K, epi, m16, bf16):
         np.testing.assert_array_equal(Cs, C)
 
 
-@pytest.mark.parametrize("E,M,N,K,epi,m16,planes", [(2, 896, 2048, 2048, 1, False, True),
-                                                    (2, 896, 2048, 2048, 1, False, False),
-                                                    (2, 768, 2048, 2048, 2, True, True),
-                                                    (1, 1792, 2048, 2048, 1, False, True),
-                                                    (2, 1280, 2040, 512, 2, True, True),
-                                                    (2, 300, 2048, 2048, 2, True, False)],
+@pytest.mark.parametrize("E,M,N,K,epi,m16,planes,h2", [(2, 896, 2048, 2048, 1, False, True, False),
+                                                       (2, 896, 2048, 2048, 1, False, False, False),
+                                                       (2, 768, 2048, 2048, 2, True, True, False),
+                                                       (1, 1792, 2048, 2048, 1, False, True, False),
+                                                       (2, 1280, 2040, 512, 2, True, True, False),
+                                                       (2, 300, 2048, 2048, 2, True, False, False),
+                                                       (2, 896, 2048, 2048, 1, False, True, True),
+                                                       (1, 1792, 2048, 2048, 1, False, False, True),
+                                                       (2, 768, 2048, 2048, 2, True, True, True),
+                                                       (2, 1664, 2048, 2048, 2, True, True, True)],
                          ids=["shard7_fwd_planes", "shard7_fwd_top_fp32", "shard6_dgrad_m16", "shard7_actor_2b",
-                              "mt10_ragged_dgrad_m16", "short_dgrad_fp32_only"])
-def test_split_k_in_launch_finish_bitwise(E, M, N, K, epi, m16, planes):
-    """The in-launch split-K finish (every slice writes its slab and draws a ticket; the last one adds
-    the slabs in slice order with its own partial in its place and applies the epilogue) gives the
-    separate finishing pass's bits exactly, and meets the fp32 bound against float64."""
+                              "mt10_ragged_dgrad_m16", "short_dgrad_fp32_only", "h2_shard7_fwd_planes",
+                              "h2_shard7_actor_top_fp32", "h2_shard6_dgrad_m16", "h2_shard13_dgrad_m16"])
+def test_split_k_in_launch_finish_bitwise(E, M, N, K, epi, m16, planes, h2):
+    """The in-launch split-K finish gives the separate finishing pass's bits exactly and meets the fp32
+    bound against float64.  split3: every slice writes its slab and draws a ticket, the last one adds
+    the slabs in slice order with its own partial in its place.  split2h (the default precision, two
+    slices): the pair hand-off -- the ticket first, the first slice publishes its unscaled partial,
+    the second adds it to its own (fp32 addition commutes) and applies the epilogue; C and the output
+    planes equal the finishing pass's bit for bit."""
     from mtrl_amd import _lib as L
 
     lib = L.load()
@@ -189,13 +197,15 @@ def test_split_k_in_launch_finish_bitwise(E, M, N, K, epi, m16, planes):
     for fin in (0, 4096):
         C = np.zeros((E, M, N), np.float32)
         Cs = np.zeros((E, M, N), np.float32) if planes else None
-        L.check(lib.mtsac_debug_gemm_x3f(epi | (256 if m16 else 0) | 2048 | fin, E, M, N, K, p(A), p(B), C.ctypes.data,
-                                         p(bias), p(mask), None if Cs is None else Cs.ctypes.data))
+        L.check(lib.mtsac_debug_gemm_x3f(epi | (256 if m16 else 0) | 2048 | fin | (8192 if h2 else 0), E, M, N, K,
+                                         p(A), p(B), C.ctypes.data, p(bias), p(mask),
+                                         None if Cs is None else Cs.ctypes.data))
         out.append((C, Cs))
     np.testing.assert_array_equal(out[1][0], out[0][0])
     if planes:
         np.testing.assert_array_equal(out[1][1], out[0][1])
-        np.testing.assert_array_equal(out[1][1], out[1][0])
+        if not h2:  # split3 planes sum to C exactly (split2h's carry 22 bits: test_split2h_products)
+            np.testing.assert_array_equal(out[1][1], out[1][0])
     acc, scale = _ref(A, B)
     if epi == 1:
         want = np.maximum(acc + bias[:, None, :], 0)

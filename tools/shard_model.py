@@ -15,7 +15,10 @@ T, W = 50, 2048
 PREC = {"split3": 1, "bf16": 2, "split2h": 3}
 prec = next((PREC[a] for a in sys.argv[1:] if a in PREC), 1)
 gbps_list = [float(x) for x in ([a for a in sys.argv[1:] if a not in PREC] or ["0", "300", "150"])]
+only = [int(x) for x in __import__("os").environ.get("SHARD_N", "8,4,2").split(",")]  # SHARD_N=8: that N only
 for nr, tl in ((8, 7), (4, 13), (2, 25)):
+    if nr not in only:
+        continue
     cfg = make_config(num_tasks=T, task_begin=0, task_count=tl, obs_dim=39 + T, actor_width=W, critic_width=W,
                       batch_per_task=128, capacity=20_000, clip=0, precision=prec)
     eng = MTSACEngine(cfg, device=0)
