@@ -226,9 +226,10 @@ struct mtsac_engine {
   // split3 planes of the GEMM operands among them (layers 0..D-2 of activations, 1..D-1 of grads)
   bool planes = false;
   // the input layer's weight grad on k-major planes (gemm_x3p; dz[0] planes + bias partials from the
-  // data-grad epilogue) instead of the on-the-fly split kernel, for batches below 4096 rows (measured,
-  // profiles/r3ff_input_wgrad_ab.txt: MT10/W400 +1.5 %, MT50/W2048 at 6400 rows -0.5 %);
-  // MTSAC_INPUT_WGRAD=0 / 1 forces either form (set at create)
+  // data-grad epilogue) instead of the on-the-fly split kernel: split2h always, split3 below 4096 rows
+  // (measured, profiles/r3ff_input_wgrad_ab.txt: MT10/W400 +1.5 %, MT50/W2048 split3 at 6400 rows
+  // -0.5 %; split2h S3 -54 us per step, profiles/r5n_step_ab.txt); MTSAC_INPUT_WGRAD=0 / 1 forces
+  // either form (set at create)
   bool in_wgrad_planes = false;
   int np = 3;  // operand planes the plane GEMMs read: 3 (split3), 1 (bf16) or 2 (split2h: fp16)
   // ---- precision split2h: a device record (kernels.h PlaneRec: exponent + partial maxima) per fp16
@@ -2193,7 +2194,9 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   e->B = c.batch_per_task * c.task_count;
   {
     const char* v = getenv("MTSAC_INPUT_WGRAD");
-    e->in_wgrad_planes = v ? atoi(v) != 0 : e->B < 4096;
+    // split2h planes are 4 B per element, as the fp32 dz[0] is: planes everywhere (S3 -54 us per step,
+    // profiles/r5n_step_ab.txt); split3's 6 B per element pay only below 4096 rows
+    e->in_wgrad_planes = v ? atoi(v) != 0 : (e->B < 4096 || c.precision == MTSAC_FP32_SPLIT2H);
   }
   e->B_glob = c.batch_per_task * c.num_tasks;
   e->R = (int)align_up(2LL * e->D + e->A + 2, 4);

@@ -197,7 +197,12 @@ __global__ __launch_bounds__(256) void colsum_partial_scalar_kernel(const float*
 
 }  // namespace
 
-int g_x3p_geo = -1;  // -1: by operand form; 0: 128x128 k32, 1: 256x128 k32, 2: 256x128 k16, 3: 256x256 k16
+// -1: by operand form; 0: 128x128 k32, 1: 256x128 k32, 2: 256x128 k16, 3: 256x256 k16 (experiments:
+// mtsac_debug_x3p_geo, or MTSAC_X3P_GEO at load)
+int g_x3p_geo = [] {
+  const char* e = getenv("MTSAC_X3P_GEO");
+  return e ? atoi(e) : -1;
+}();
 int g_x3p_dbg = 0;
 
 // tile shape of a geometry id (see Geo aliases above)
@@ -250,14 +255,14 @@ static void x3p_dispatch(int geo, const SplitGemmParams& p, int epi, int batch, 
 // fills the chip there); else 256x128.  g_x3p_geo forces one (experiments).
 static int pick_geo(int M, int N, int K, int batch, bool kmajor, bool a_kmajor) {
   if (g_x3p_geo >= 0) return (g_x3p_geo == 5 && a_kmajor) ? 3 : g_x3p_geo;
-  if (kmajor) {  // weight grads over K = rows: 256 x 256 tiles (+ split-K) at the full MT50 batch;
-                 // 256 x 128 k16 tiles where K is a task shard's or MT10's rows, and for narrow
-                 // trunks (W = 400) -- measured per launch (profiles/r3u_wgrad_geo.txt): W = 2048,
-                 // E = 2, K = 896: 83.9 vs 105.8 us (no split-K, no reduce pass), K = 1664: 153.8
-                 // vs 170.0, K = 3200: 280.3 vs 282.2, K = 6400: 547.7 vs 541.5; W = 400, E = 2,
-                 // K = 1280: 26.0 vs 26.6 (128 x 128), K = 6400: 67.0 vs 73.0
-    const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256) * batch;
-    return (big < 32 || K < 4096) ? 2 : 3;
+  if (kmajor) {  // weight grads over K = rows: 256 x 128 k16 tiles -- measured per launch
+                 // (profiles/r3u_wgrad_geo.txt, split3): W = 2048, E = 2, K = 896: 83.9 vs 105.8 us
+                 // (no split-K, no reduce pass), K = 1664: 153.8 vs 170.0, K = 3200: 280.3 vs 282.2,
+                 // K = 6400: 547.7 vs 541.5 without the 256 x 256 form's slab-reduce pass; W = 400,
+                 // E = 2, K = 1280: 26.0 vs 26.6 (128 x 128), K = 6400: 67.0 vs 73.0.  Round 5, whole S3
+                 // split2h steps: 5.100 vs 5.128 ms (profiles/r5n_step_ab.txt): the critic's 2 x 128
+                 // tiles fill the chip without split-K, so its slabs and reduce pass are gone
+    return 2;
   }
   const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256) * batch;
   if (big < 192) return 1;

@@ -1,7 +1,8 @@
 """A/B of engine-wide switches on whole S3 (or shard) steps in ONE process: for each variant, a fresh
 engine, 5 warm-up steps, then the mean of 3 x 20 timed device-sampled steps (graph replay or eager).
-usage: python tools/step_ab.py [--tl 50] [--prec 3] [--eager] VARIANT...   VARIANT = name:geo
-  geo: mtsac_debug_x3p_geo (-1 auto, 2 = 256x128 k16, 3 = 256x256 k16)"""
+usage: python tools/step_ab.py [--tl 50] [--prec 3] [--eager] VARIANT...   VARIANT = name:geo[:K=V,K=V]
+  geo: mtsac_debug_x3p_geo (-1 auto, 2 = 256x128 k16, 3 = 256x256 k16); K=V: environment variables set
+  while the variant's engine is created (switches the engine reads at create)"""
 import argparse
 import os
 import sys
@@ -23,11 +24,19 @@ lib = L.load()
 res = {}
 for rnd in range(2):
     for v in a.variants:
-        name, geo = v.split(":")
+        name, geo, *envs = v.split(":")
         lib.mtsac_debug_x3p_geo(int(geo))
+        kv = dict(x.split("=", 1) for x in (envs[0].split(",") if envs and envs[0] else []))
+        old = {k: os.environ.get(k) for k in kv}
+        os.environ.update(kv)
         eng = MTSACEngine(make_config(num_tasks=T, task_begin=0, task_count=a.tl, obs_dim=39 + T, actor_width=W,
                                       critic_width=W, batch_per_task=128, capacity=10_000, precision=a.prec))
         ac, cr = init_mtsac(T, 39 + T, 4, W, 3, W, 3, 2, seed=1, task_begin=0, task_count=a.tl)
+        for k, o in old.items():
+            if o is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = o
         eng.set_params(L.ACTOR, ac)
         eng.set_params(L.CRITIC, cr)
         eng.set_params(L.CRITIC_TARGET, cr)
