@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -305,6 +306,13 @@ int mtsac_debug_gemm_x3f(int epi, int batch, int M, int N, int K, const float* A
   } else {
     if (!gemm_x3f_ok(g, epi, batch)) return -95;
     gemm_x3f(g, epi, batch, nullptr);
+  }
+  {
+    const hipError_t le = hipGetLastError();  // a launch the runtime refused leaves C as it was
+    if (le != hipSuccess) {
+      fprintf(stderr, "[mtsac_debug_gemm_x3f] launch refused: %s\n", hipGetErrorString(le));
+      return -6;
+    }
   }
   if (hipDeviceSynchronize() != hipSuccess) return -5;
   if (hipMemcpy(C, dC, sizeof(float) * nC, hipMemcpyDeviceToHost) != hipSuccess) return -5;

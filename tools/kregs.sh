@@ -8,8 +8,10 @@ $B/llvm-readelf --notes $T/co > $T/notes
 python3 - "$T/notes" "${2:-.}" <<'PY'
 import re, sys, subprocess
 t = open(sys.argv[1]).read()
-for e in t.split('.name:')[1:]:
-    name = e.split('\n')[0].strip()
+# one map per kernel, keys in alphabetical order: split where a map starts (.agpr_count comes first)
+for e in t.split('- .agpr_count:')[1:]:
+    e = '.agpr_count:' + e
+    name = (re.search(r'\.name:\s+(\S+)', e) or [None, ''])[1]
     dm = subprocess.run(['c++filt', name], capture_output=True, text=True).stdout.strip()
     if not re.search(sys.argv[2], dm): continue
     g = lambda k: (re.search(r'\.' + k + r':\s+(\d+)', e) or [None, None])[1]
