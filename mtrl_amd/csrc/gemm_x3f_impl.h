@@ -6,6 +6,10 @@
 
 #include "gemm_x3p_impl.h"
 
+#ifndef X3F_STAGGER
+#define X3F_STAGGER 0  // 1: the staggered schedule of the split2h instances (STG below; measured slower, A/B only)
+#endif
+
 #ifndef X3F_EPI_GROUP
 #define X3F_EPI_GROUP 2  // 16-row blocks per epilogue barrier in the plane kernels (4 measured equal: profiles/r4k_*)
 #endif
@@ -98,7 +102,23 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   // input layer's), 1 otherwise
   constexpr int EG = (!FIN && NP >= 2) ? X3F_EPI_GROUP : 1;
   constexpr int EPI_LDS = (2 * EG * 16 * (BN + 4) + WV * BN + 16) * 4;  // + the split2h max scratch
-  constexpr int SMEM0 = 2 * STAGE > EPI_LDS ? 2 * STAGE : EPI_LDS;
+  // STG (split2h, 8 waves, a 3-stage ring that fits): the two waves of each SIMD run half a step apart
+  // (MI355X_MICROARCH.md, 'Two waves per SIMD' item 9).  Waves 0-3 ("early") issue every LDS-DMA piece,
+  // one stage ahead, and meet the step barrier at the start of their steps; waves 4-7 ("late") meet the
+  // same barrier in the MIDDLE of their steps, so while one wave of a SIMD waits at the barrier, loads
+  // its B fragments or reads a fresh stage, its partner is in the middle of its MFMAs.  Stage k lives in
+  // buffer k mod 3: when the early waves refill buffer (k + 1) mod 3 during step k, the late waves are
+  // past step k - 2 (they passed barrier k in the middle of step k - 1).  Same products, same order:
+  // outputs are bitwise those of the unstaggered schedule.  Measured (-DX3F_STAGGER=1 against the
+  // default build on one box, profiles/r5w_*): parity green, but the hidden forward 0.563-0.566 of
+  // the split2h peak against 0.578-0.584 and S3 211.6 against 213.7 steps/s -- the early waves issue
+  // twice the DMA pieces, and the chip's clock under this MFMA load, not the issue schedule, bounds
+  // the loop.  Kept as a build option.
+  constexpr bool STG = X3F_STAGGER && NP == 2 && WV == 8 && (ABL == 0 || ABL == TAG_INPUT) &&
+                       3 * STAGE <= 160 * 1024 - 16 && NJ % 4 == 0;
+  constexpr int NSTG = STG ? 3 : 2;
+  constexpr int PE = NJ / 4;  // STG: DMA pieces per early wave and stage
+  constexpr int SMEM0 = NSTG * STAGE > EPI_LDS ? NSTG * STAGE : EPI_LDS;
   constexpr int SMEM = SMEM0 + (FIN ? 16 : 0);  // FIN: the 'last slice' word after the scratch
   static_assert(BM % 16 == 0 && SMEM <= 160 * 1024, "tile");
   static_assert(PMAX - 1 >= PW || NJ % WV == 0, "every wave issues >= PW pieces in the first half step");
@@ -186,9 +206,17 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
 
   bf16x8 b0[JB][NP], b1[JB][NP];
   if ((ABL & 4) && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  const bool early = wave < 4;
   // prologue: stage 0 + B of the first half step
+  if constexpr (STG) {
+    if (early) {
 #pragma unroll
-  for (int qi = 0; qi < PMAX; ++qi) wave_piece(qi, 0, lds_base);
+      for (int qi = 0; qi < PE; ++qi) piece(wave + 4 * qi, 0, lds_base);
+    }
+  } else {
+#pragma unroll
+    for (int qi = 0; qi < PMAX; ++qi) wave_piece(qi, 0, lds_base);
+  }
   bload(b0, 0);
 
   // one 64-deep step; MORE: the next stage and B half step are loaded during it (all but the last)
@@ -251,8 +279,70 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
       }
     }
   };
-  for (int kt = 0; kt + 1 < nk; ++kt) step(kt, std::integral_constant<bool, true>{});
-  step(nk - 1, std::integral_constant<bool, false>{});
+  // the staggered schedule (STG): stage k in buffer k mod 3; see STG above
+  auto step_stg = [&](int kt, int cb, auto more_c) {
+    constexpr bool MORE = decltype(more_c)::value;
+    // every wave: B(kt, 0) landed (early waves: also their DMA pieces of stage kt); the early waves
+    // (and all at kt = 0) then meet the step barrier, the late waves met it in the middle of step kt - 1.
+    // The waits are single asm sites run by both groups and the branches carry no register operands,
+    // so the allocator never splits the live range of an asm-loaded B fragment (a copy made before
+    // the load lands reads garbage).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (early || kt == 0) asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const int kn = (kt + 1) * KS;
+    const int nb = cb == 2 ? 0 : cb + 1;
+    const unsigned nst = lds_base + nb * STAGE;
+    const char* cur = smem + cb * STAGE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8(&b)[JB][NP] = s == 0 ? b0 : b1;
+      if (s == 0) {
+        bload(b1, kt * KS + 32);  // second half of this step
+      } else {
+        // late waves: everything landed, then the step barrier (mid-step); they hold no DMA pieces
+        if (MORE && !early) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        // B(kt, 1) landed; an early wave's pieces issued after it may not have
+        wait_vm<MORE ? PE : 0, NP, JB>(b1);
+        if (MORE) bload(b0, kn);  // first half of the next step
+      }
+      bf16x8 a[2][NP];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) a[0][q] = afrag(cur, 0, s, q);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        if (i + 1 < TI) {
+#pragma unroll
+          for (int q = 0; q < NP; ++q) a[(i + 1) & 1][q] = afrag(cur, i + 1, s, q);
+        }
+        if (MORE && s == 0 && early) {  // the next stage's pieces, spread over the first half's row tiles
+#pragma unroll
+          for (int qi = (i * PE) / TI; qi < ((i + 1) * PE) / TI; ++qi) piece(wave + 4 * qi, kn, nst);
+        }
+        const bf16x8(&x)[NP] = a[i & 1];
+#pragma unroll
+        for (int j = 0; j < JB; ++j) {
+          f32x4 c = acc[i][j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[0]), __builtin_bit_cast(f16x8, b[j][1]), c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[1]), __builtin_bit_cast(f16x8, b[j][0]), c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[0]), __builtin_bit_cast(f16x8, b[j][0]), c, 0, 0, 0);
+          acc[i][j] = c;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  if constexpr (STG) {
+    int cb = 0;
+    for (int kt = 0; kt + 1 < nk; ++kt) {
+      step_stg(kt, cb, std::integral_constant<bool, true>{});
+      cb = cb == 2 ? 0 : cb + 1;
+    }
+    step_stg(nk - 1, cb, std::integral_constant<bool, false>{});
+  } else {
+    for (int kt = 0; kt + 1 < nk; ++kt) step(kt, std::integral_constant<bool, true>{});
+    step(nk - 1, std::integral_constant<bool, false>{});
+  }
 
   // ---------------------------------------------------------------- epilogue
   // Per 16-row block, the waves' 16 x 16 JB pieces meet in an LDS image of the block's 16 x 256
