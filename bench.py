@@ -56,9 +56,9 @@ GEMM_FAMILIES = {
     "split2h": {
         0: "gemm_x3f_kernel<208, 1, *, *, false, 0, 2> (hidden-layer forward, fp16 planes, bias+ReLU)",
         1: "gemm_x3f_kernel<208, 2, *, *, true, 0, 2> (hidden-layer data grad, fp16 planes, ReLU mask from the planes)",
-        2: "gemm_x3p_kernel<Geo<256, 256, 2, 4, 3, 16, 0>, true, true, 0, false, 2> (hidden-layer weight grad, k-major fp16 planes, split-K)",
+        2: "gemm_x3p_kernel<Geo<256, 128, 4, 2, 4, 16, 0>, true, true, 0, false, 2> (hidden-layer weight grad, k-major fp16 planes, 256 x 128 k16 tiles; the critic's without split-K)",
         3: "gemm_x3f_kernel<208, 1, false, true, false, 8, 2> (input-layer forward, fp16 planes, K = in_dim padded to 64)",
-        4: "gemm_x3_kernel<true, false, 0> (input-layer weight grad, on-the-fly split, split-K)",
+        4: "gemm_x3p_kernel<Geo<256, 128, 4, 2, 4, 16, 0>, true, true, 0, false, 2> (input-layer weight grad, k-major fp16 planes of dz0, split-K)",
     },
     "fp32": {
         0: "gemm_f32_kernel<false, true, 1> (hidden-layer forward, NT vs transposed kernel)",

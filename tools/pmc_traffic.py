@@ -20,14 +20,16 @@ FAMILY_KEYS = {
         3: ("gemm_x3f_kernel<208, 1, false, true, false, 8,",),
         4: ("gemm_x3_kernel<true, false, 0>",),
     },
-    # split2h: the same kernel templates with NP = 2 (the prefixes above match both)
+    # split2h: the same forward / data-grad templates with NP = 2; since round 5 every S3 weight grad
+    # (hidden and input layer) runs on the 256 x 128 k16 tiles: one symbol, and split-K gives the input
+    # layers' launches the hidden layers' grids, so family 2 here is every weight grad (5 hidden-sized
+    # 256-workgroup launches and one 128-workgroup launch per step) and family 4 has no launches
     "split2h": {
         0: ("gemm_x3f_kernel<208, 1, false, true, false, 0,", "gemm_x3f_kernel<208, 1, true, false, false, 0,",
             "gemm_x3f_kernel<208, 1, true, true, false, 0,"),
         1: ("gemm_x3f_kernel<208, 2,",),
-        2: ("gemm_x3p_kernel<mtsac::x3pk::Geo<256, 256, 2, 4, 3, 16, 0>, true, true, 0,",),
+        2: ("gemm_x3p_kernel<mtsac::x3pk::Geo<256, 128, 4, 2, 4, 16, 0>, true, true, 0,",),
         3: ("gemm_x3f_kernel<208, 1, false, true, false, 8,",),
-        4: ("gemm_x3_kernel<true, false, 0>",),
     },
     "fp32": {
         0: ("gemm_f32_kernel<false, true, 1>",),
@@ -40,7 +42,7 @@ FAMILY_KEYS = {
 
 
 def per_dispatch(path, counter):
-    """{dispatch id: (kernel name, value)} for one counter."""
+    """{dispatch id: (kernel name, value, grid size in work-items)} for one counter."""
     out = {}
     with open(path) as f:
         for r in csv.DictReader(f):
@@ -49,17 +51,30 @@ def per_dispatch(path, counter):
             did = r.get("Dispatch_Id") or r.get("Correlation_Id")
             name = r.get("Kernel_Name", "")
             v = float(r.get("Counter_Value", 0.0))
+            grid = int(r.get("Grid_Size", 0) or 0)
             if did in out:
-                out[did] = (name, out[did][1] + v)  # one row per XCD / instance: sum
+                out[did] = (name, out[did][1] + v, grid)  # one row per XCD / instance: sum
             else:
-                out[did] = (name, v)
+                out[did] = (name, v, grid)
     return out
+
+
+def _match(name, grid, k):
+    """k: a kernel-name prefix, or (prefix, min grid, max grid or None)."""
+    if isinstance(k, str):
+        return k in name
+    pre, lo, hi = k
+    return pre in name and grid >= lo and (hi is None or grid <= hi)
+
+
+def _label(k):
+    return k if isinstance(k, str) else f"{k[0]} (grid {k[1]}..{k[2] if k[2] is not None else ''})"
 
 
 def family_means(rows, keys, scale):
     res = {}
     for fam, key in keys.items():
-        vals = [v for (name, v) in rows.values() if any(k in name for k in key)]
+        vals = [v for (name, v, grid) in rows.values() if any(_match(name, grid, k) for k in key)]
         if vals:
             res[fam] = (sum(vals) / len(vals) * scale, len(vals))
     return res
@@ -77,7 +92,7 @@ def main():
     fam_out = {}
     for fam in keys:
         if fam in fetch and fam in write:
-            fam_out[str(fam)] = {"kernel": " | ".join(keys[fam]), "hbm_bytes_per_launch": fetch[fam][0] + write[fam][0],
+            fam_out[str(fam)] = {"kernel": " | ".join(_label(k) for k in keys[fam]), "hbm_bytes_per_launch": fetch[fam][0] + write[fam][0],
                                  "fetch_bytes_per_launch": fetch[fam][0], "write_bytes_per_launch": write[fam][0],
                                  "dispatches": fetch[fam][1],
                                  "correction": "FETCH_SIZE (KiB) x 2 (gfx950 half-count) + WRITE_SIZE (KiB)"}
