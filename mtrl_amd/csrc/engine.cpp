@@ -2212,7 +2212,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   // stream sa -- four, so HIP's default four hardware queues give each its own.  s1 and s3 serve only
   // the experimental 5-lane form and exist only when it is requested (MTSAC_LANES=1).  Streams beyond
   // GPU_MAX_HW_QUEUES share hardware queues, and concurrently active streams on a shared queue were
-  // seen to read stale data ("Shared hardware queues").
+  // seen to read stale data ("Lanes and hardware queues").
   {
     const char* lw = getenv("MTSAC_LANES");
     const bool lanes_wanted = lw && atoi(lw) != 0;
