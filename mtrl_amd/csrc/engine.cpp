@@ -2177,7 +2177,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
       c.precision != MTSAC_FP32_SPLIT2H)
     return fail(-22, "unsupported precision");
   if (c.precision == MTSAC_FP32_SPLIT2H && (long long)c.batch_per_task * c.task_count > 8192)
-    return fail(-22, "split2h: at most 8192 rows per engine (one partial maximum per wave of the action grad)");
+    return fail(-22, "split2h: at most 8192 rows per engine (the sizes its partial-maximum records and plane bounds are validated at; precision split3 has no such limit)");
   if (c.precision == MTSAC_FP32_SPLIT2H && !(c.adam_b1 * c.adam_b1 < c.adam_b2))
     return fail(-22, "split2h bounds an Adam step (|m_hat| / sqrt(v_hat)), which needs adam_b1^2 < adam_b2");
   hipError_t he = hipSetDevice(hip_device);
