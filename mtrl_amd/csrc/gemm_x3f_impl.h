@@ -10,6 +10,15 @@
 #define X3F_STAGGER 0  // 1: the staggered schedule of the split2h instances (STG below; measured slower, A/B only)
 #endif
 
+#ifndef X3F_WT_STORES
+// 1: the epilogue's C and plane stores are write-through (sc1): the lines leave the XCD's L2 as they
+// are written, so no dirty output lingers there for the kernel boundary to write back
+// (MI355X_MICROARCH.md: a dependent boundary costs + B / 6 TB/s for B dirty bytes).  Measured slower
+// (profiles/r5ae_x3f_wt_stores_ab.txt: S3 212.1-212.9 vs 217.4-220.2 steps/s, hidden forward 0.547 vs
+// 0.597 solo): the kernels lose more than the boundaries gain.  0: plain stores (default)
+#define X3F_WT_STORES 0
+#endif
+
 #ifndef X3F_EPI_GROUP
 #define X3F_EPI_GROUP 2  // 16-row blocks per epilogue barrier in the plane kernels (4 measured equal: profiles/r4k_*)
 #endif
@@ -460,6 +469,10 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   }
   float* C = C_OUT ? p.C + z * p.sC + (FIN ? 0ll : (long long)sl * p.M * p.ldc) : nullptr;
   __bf16* Cp = P_OUT ? p.Cp + z * p.sCp : nullptr;
+  // write-through stores (X3F_WT_STORES): buffer stores with the sc1 policy (aux 16) at byte offsets
+  // from the member's C / plane base (< 2^31: at most 2 x 12800 x 2048 x 2 B of planes per member)
+  const __amdgpu_buffer_rsrc_t c_rs = __builtin_amdgcn_make_buffer_rsrc((void*)C, (short)0, -1, 0x00020000);
+  const __amdgpu_buffer_rsrc_t p_rs = __builtin_amdgcn_make_buffer_rsrc((void*)Cp, (short)0, -1, 0x00020000);
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums over this lane's rows (dbp)
   // FIN, two slices (task shards): the other slice's values of the next PB row blocks this lane
   // finishes are loaded in one burst, so the slab reads overlap instead of costing one round trip
@@ -565,9 +578,15 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
 #pragma unroll
     for (int c = 0; c < 8; ++c) csum[c] += e[c];
     if (C_OUT) {
-      float* cp = C + (long long)row * p.ldc + col;
-      *reinterpret_cast<float4*>(cp) = make_float4(e[0], e[1], e[2], e[3]);
-      *reinterpret_cast<float4*>(cp + 4) = make_float4(e[4], e[5], e[6], e[7]);
+      if (X3F_WT_STORES) {
+        const int o = (int)(((long long)row * p.ldc + col) * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_float4(e[0], e[1], e[2], e[3])), c_rs, o, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_float4(e[4], e[5], e[6], e[7])), c_rs, o + 16, 0, 16);
+      } else {
+        float* cp = C + (long long)row * p.ldc + col;
+        *reinterpret_cast<float4*>(cp) = make_float4(e[0], e[1], e[2], e[3]);
+        *reinterpret_cast<float4*>(cp + 4) = make_float4(e[4], e[5], e[6], e[7]);
+      }
     }
     if (P_OUT && NP == 2) {
       f16x8 h, l;
@@ -578,9 +597,15 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
         h[c] = a_; l[c] = b_;
         omx = fmaxf(omx, fabsf(e[c]));
       }
-      __bf16* pp = Cp + (long long)row * p.ldcp + col;
-      *reinterpret_cast<f16x8*>(pp) = h;
-      *reinterpret_cast<f16x8*>(pp + p.pC) = l;
+      if (X3F_WT_STORES) {
+        const int o = (int)(((long long)row * p.ldcp + col) * 2);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h), p_rs, o, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, l), p_rs, o + (int)(p.pC * 2), 0, 16);
+      } else {
+        __bf16* pp = Cp + (long long)row * p.ldcp + col;
+        *reinterpret_cast<f16x8*>(pp) = h;
+        *reinterpret_cast<f16x8*>(pp + p.pC) = l;
+      }
     } else if (P_OUT) {
       bf16x8 h, m, l;
 #pragma unroll
