@@ -118,12 +118,14 @@ void ablate_at(const SplitGemmParams& p, int abl, dim3 grid, hipStream_t st) {
 // 4-wave, 64-column-slab workgroup); precision bf16 runs the 400-row tile
 void gemm_x3f_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t st) {
   using namespace x3fk;
-  const bool wv4 = abl >= 1000 && abl < 2000, short8 = abl >= 2000;
+  const bool wv4 = abl >= 1000 && abl < 2000, short8 = abl >= 2000 && abl < 3000, c2 = abl >= 3000;
   abl %= 1000;
-  const int bm = p.np == 1 && !wv4 && !short8 ? 400 : BM0;  // bf16: + 1000 / + 2000 = 208 rows, 4 / 8 waves
+  // bf16: + 1000 / + 2000 = 208 rows, 4 / 8 waves; + 3000 = the 80-row tile of MT10's 1280 rows (C2)
+  const int bm = c2 ? 80 : p.np == 1 && !wv4 && !short8 ? 400 : BM0;
   const dim3 grid((unsigned)(((p.M + bm - 1) / bm) * ((p.N + BN - 1) / BN) * batch));
   if (p.np == 1) {
-    if (wv4) ablate_at<BM0, 1, 4>(p, abl, grid, st);
+    if (c2) ablate_at<80, 1, 8>(p, abl, grid, st);
+    else if (wv4) ablate_at<BM0, 1, 4>(p, abl, grid, st);
     else if (short8) ablate_at<BM0, 1, 8>(p, abl, grid, st);
     else ablate_at<400, 1, 8>(p, abl, grid, st);
   } else if (p.np == 2) {  // split2h: 8 waves, or (+ 1000) 4 waves x 64-column slabs

@@ -19,6 +19,10 @@
 #define X3F_WT_STORES 0
 #endif
 
+#ifndef X3F_DEEP_B
+#define X3F_DEEP_B 1  // the bf16 instances' four-buffer B ring (DEEP below); 0: build without (A/B)
+#endif
+
 #ifndef X3F_EPI_GROUP
 #define X3F_EPI_GROUP 2  // 16-row blocks per epilogue barrier in the plane kernels (4 measured equal: profiles/r4k_*)
 #endif
@@ -125,6 +129,12 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   // the loop.  Kept as a build option.
   constexpr bool STG = X3F_STAGGER && NP == 2 && WV == 8 && (ABL == 0 || ABL == TAG_INPUT) &&
                        3 * STAGE <= 160 * 1024 - 16 && NJ % 4 == 0;
+  // DEEP (precision bf16, one plane; the non-split epilogue instances of up to 208 rows -- the 400-row
+  // tile has no registers for the ring): B fragments run THREE half steps ahead through a ring of four
+  // register buffers instead of one.  The one-plane step has a third of the MFMAs of a split2h step, so a
+  // half step of MFMAs no longer covers an L2 / MALL load: at MT10's 80-row tile (C2) the kernel
+  // without B reloads took 21.7 against 30.8 us (profiles/r5ah_x3f_c2_ablate.txt).
+  constexpr bool DEEP = NP == 1 && BM <= 208 && ABL == 0 && EPI != EPI_STORE && !FIN && !STG && X3F_DEEP_B;
   constexpr int NSTG = STG ? 3 : 2;
   constexpr int PE = NJ / 4;  // STG: DMA pieces per early wave and stage
   constexpr int SMEM0 = NSTG * STAGE > EPI_LDS ? NSTG * STAGE : EPI_LDS;
@@ -226,7 +236,7 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
 #pragma unroll
     for (int qi = 0; qi < PMAX; ++qi) wave_piece(qi, 0, lds_base);
   }
-  bload(b0, 0);
+  if constexpr (!DEEP) bload(b0, 0);
 
   // one 64-deep step; MORE: the next stage and B half step are loaded during it (all but the last)
   auto step = [&](int kt, auto more_c) {
@@ -341,7 +351,85 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
       }
     }
   };
-  if constexpr (STG) {
+  // DEEP: step kt computes half steps 2kt (buffer 2P) and 2kt + 1 (2P + 1), P = kt & 1, and loads half
+  // steps 2kt + 3 and 2kt + 4 into the buffers freed by 2kt - 1 and 2kt.  Every step issues the same
+  // operations -- B(2kt + 3), the pieces of stage kt + 1 (spread over the first half's row tiles),
+  // B(2kt + 4) -- past the end of K at clamped addresses (a few loads nobody reads; the pieces land in
+  // the buffer the last step does not read, and the epilogue drains them), so every count is a
+  // constant: at the start of step kt only B(2kt + 2) may still be in flight besides what is waited
+  // for (at kt = 0: B(1), B(2)), and at its middle B(2kt + 2), B(2kt + 3) and >= PW pieces.
+  const int klast = p.K - KS;  // (the slice's K: DEEP launches are never split)
+  auto bload_c = [&](bf16x8 (&b)[JB][NP], int k) { bload(b, k < klast + 32 ? k : klast + 32); };
+  auto step_deep = [&](bf16x8 (&bq)[4][JB][NP], int kt, auto par_c, auto first_c) {
+    constexpr int P = decltype(par_c)::value;
+    constexpr bool FIRST = decltype(first_c)::value;
+    constexpr int S0 = 2 * P, S1 = 2 * P + 1, L0 = (2 * P + 3) & 3, L1 = (2 * P + 4) & 3;
+    constexpr int NB = JB * NP;  // B wave-instructions per half step
+    wait_vm<FIRST ? 2 * NB : NB, NP, JB>(bq[S0]);  // B(2kt) and this wave's stage-kt pieces
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const int kn = min((kt + 1) * KS, klast);
+    const unsigned nst = lds_base + ((kt + 1) & 1) * STAGE;
+    const char* cur = smem + (kt & 1) * STAGE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (s == 0) {
+        bload_c(bq[L0], kt * KS + 96);
+      } else {
+        wait_vm<2 * NB + PW, NP, JB>(bq[S1]);
+        bload_c(bq[L1], kt * KS + 128);
+      }
+      bf16x8(&b)[JB][NP] = s == 0 ? bq[S0] : bq[S1];
+      bf16x8 a[2][NP];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) a[0][q] = afrag(cur, 0, s, q);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        if (i + 1 < TI) {
+#pragma unroll
+          for (int q = 0; q < NP; ++q) a[(i + 1) & 1][q] = afrag(cur, i + 1, s, q);
+        }
+        if (s == 0) {
+#pragma unroll
+          for (int qi = (i * PMAX) / TI; qi < ((i + 1) * PMAX) / TI; ++qi)
+            if (qi < mine) wave_piece(qi, kn, nst);
+        }
+        const bf16x8(&x)[NP] = a[i & 1];
+#pragma unroll
+        for (int j = 0; j < JB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][0], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using BT = std::integral_constant<bool, true>;
+  using BF = std::integral_constant<bool, false>;
+  if constexpr (DEEP) {
+    // one self-contained loop per parity of nk: no asm-loaded B register is live across the branch
+    if (nk & 1) {
+      bf16x8 bq[4][JB][NP];
+      bload_c(bq[0], 0);
+      bload_c(bq[1], 32);
+      bload_c(bq[2], 64);
+      step_deep(bq, 0, I0{}, BT{});
+      for (int kt = 1; kt < nk; kt += 2) {
+        step_deep(bq, kt, I1{}, BF{});
+        step_deep(bq, kt + 1, I0{}, BF{});
+      }
+    } else {
+      bf16x8 bq[4][JB][NP];
+      bload_c(bq[0], 0);
+      bload_c(bq[1], 32);
+      bload_c(bq[2], 64);
+      step_deep(bq, 0, I0{}, BT{});
+      step_deep(bq, 1, I1{}, BF{});
+      for (int kt = 2; kt < nk; kt += 2) {
+        step_deep(bq, kt, I0{}, BF{});
+        step_deep(bq, kt + 1, I1{}, BF{});
+      }
+    }
+  } else if constexpr (STG) {
     int cb = 0;
     for (int kt = 0; kt + 1 < nk; ++kt) {
       step_stg(kt, cb, std::integral_constant<bool, true>{});

@@ -11,7 +11,7 @@ from mtrl_amd import _lib as L
 
 lib = L.load()
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-E, M, N, K = 2, 6400, 2048, 2048
+E, M, N, K = 2, int(os.environ.get("X3F_M", "6400")), 2048, 2048  # X3F_M=1280 + ablations 300x: C2's 80-row bf16 tile
 bf16 = os.environ.get("X3F_BF16") == "1"  # precision bf16 at the 400-row tile (peak 2500 TF)
 h2 = os.environ.get("X3F_H2") == "1"  # precision split2h (3 fp16 products, peak 833 TF)
 frag = os.environ.get("X3F_FRAG") == "1"  # B planes in the fragment layout (the engine's weight planes at S3)
