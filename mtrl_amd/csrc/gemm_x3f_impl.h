@@ -22,6 +22,11 @@
 #ifndef X3F_DEEP_B
 #define X3F_DEEP_B 1  // the bf16 instances' four-buffer B ring (DEEP below); 0: build without (A/B)
 #endif
+#ifndef X3F_DEEP_H2
+#define X3F_DEEP_H2 0  // 1: the ring for the split2h tiles of up to 128 rows too (the task shards' split-K
+                       // slices; at 208 rows it spills): parity green, the 7-task shard step unchanged
+                       // (profiles/r5ak_shard_deep_h2_ab.txt), so off
+#endif
 
 #ifndef X3F_EPI_GROUP
 #define X3F_EPI_GROUP 2  // 16-row blocks per epilogue barrier in the plane kernels (4 measured equal: profiles/r4k_*)
@@ -134,7 +139,8 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   // register buffers instead of one.  The one-plane step has a third of the MFMAs of a split2h step, so a
   // half step of MFMAs no longer covers an L2 / MALL load: at MT10's 80-row tile (C2) the kernel
   // without B reloads took 21.7 against 30.8 us (profiles/r5ah_x3f_c2_ablate.txt).
-  constexpr bool DEEP = NP == 1 && BM <= 208 && ABL == 0 && EPI != EPI_STORE && !FIN && !STG && X3F_DEEP_B;
+  constexpr bool DEEP = ((NP == 1 && BM <= 208 && ABL == 0 && EPI != EPI_STORE && !FIN) ||
+                         (NP == 2 && BM <= 128 && X3F_DEEP_H2 && (ABL == 0 || ABL == TAG_INPUT))) && !STG && X3F_DEEP_B;
   constexpr int NSTG = STG ? 3 : 2;
   constexpr int PE = NJ / 4;  // STG: DMA pieces per early wave and stage
   constexpr int SMEM0 = NSTG * STAGE > EPI_LDS ? NSTG * STAGE : EPI_LDS;
@@ -358,7 +364,7 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   // the buffer the last step does not read, and the epilogue drains them), so every count is a
   // constant: at the start of step kt only B(2kt + 2) may still be in flight besides what is waited
   // for (at kt = 0: B(1), B(2)), and at its middle B(2kt + 2), B(2kt + 3) and >= PW pieces.
-  const int klast = p.K - KS;  // (the slice's K: DEEP launches are never split)
+  const int klast = (nk - 1) * KS;  // the last step's k, relative to this slice's A / B
   auto bload_c = [&](bf16x8 (&b)[JB][NP], int k) { bload(b, k < klast + 32 ? k : klast + 32); };
   auto step_deep = [&](bf16x8 (&bq)[4][JB][NP], int kt, auto par_c, auto first_c) {
     constexpr int P = decltype(par_c)::value;
@@ -396,7 +402,17 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
         }
         const bf16x8(&x)[NP] = a[i & 1];
 #pragma unroll
-        for (int j = 0; j < JB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][0], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < JB; ++j) {
+          f32x4 c = acc[i][j];
+          if constexpr (NP == 2) {  // fp16 planes: h*l, l*h, h*h
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[0]), __builtin_bit_cast(f16x8, b[j][1]), c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[1]), __builtin_bit_cast(f16x8, b[j][0]), c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[0]), __builtin_bit_cast(f16x8, b[j][0]), c, 0, 0, 0);
+          } else {
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][0], c, 0, 0, 0);
+          }
+          acc[i][j] = c;
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
