@@ -28,6 +28,11 @@
                        // (profiles/r5ak_shard_deep_h2_ab.txt), so off
 #endif
 
+#ifndef X3F_DEEP3
+#define X3F_DEEP3 0  // 1: the split2h 208-row tiles' three-buffer B ring (DEEP3 below): parity green, S3 not
+                     // faster (211.7-213.1 vs 215.1-216.4 steps/s, profiles/r5al_s3_deep3_ab.txt), so off
+#endif
+
 #ifndef X3F_EPI_GROUP
 #define X3F_EPI_GROUP 2  // 16-row blocks per epilogue barrier in the plane kernels (4 measured equal: profiles/r4k_*)
 #endif
@@ -141,6 +146,9 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   // without B reloads took 21.7 against 30.8 us (profiles/r5ah_x3f_c2_ablate.txt).
   constexpr bool DEEP = ((NP == 1 && BM <= 208 && ABL == 0 && EPI != EPI_STORE && !FIN) ||
                          (NP == 2 && BM <= 128 && X3F_DEEP_H2 && (ABL == 0 || ABL == TAG_INPUT))) && !STG && X3F_DEEP_B;
+  // DEEP3 (split2h tiles of more than 128 rows -- S3's 208, where four buffers spill): the same idea
+  // with a ring of three buffers, B two half steps ahead instead of one
+  constexpr bool DEEP3 = NP == 2 && BM > 128 && (ABL == 0 || ABL == TAG_INPUT) && !STG && !DEEP && X3F_DEEP3;
   constexpr int NSTG = STG ? 3 : 2;
   constexpr int PE = NJ / 4;  // STG: DMA pieces per early wave and stage
   constexpr int SMEM0 = NSTG * STAGE > EPI_LDS ? NSTG * STAGE : EPI_LDS;
@@ -242,7 +250,7 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
 #pragma unroll
     for (int qi = 0; qi < PMAX; ++qi) wave_piece(qi, 0, lds_base);
   }
-  if constexpr (!DEEP) bload(b0, 0);
+  if constexpr (!DEEP && !DEEP3) bload(b0, 0);
 
   // one 64-deep step; MORE: the next stage and B half step are loaded during it (all but the last)
   auto step = [&](int kt, auto more_c) {
@@ -417,11 +425,83 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
       }
     }
   };
+  // DEEP3: step kt computes half steps 2kt (buffer (2kt) mod 3) and 2kt + 1, and loads half steps
+  // 2kt + 2 (into the buffer half 2kt - 1 left) and 2kt + 3 (into the one half 2kt just left); issue
+  // order per step: B(2kt + 2), the pieces of stage kt + 1, B(2kt + 3), past the end of K at clamped
+  // addresses as DEEP does.  At the start of step kt only B(2kt + 1) may still be in flight besides
+  // what is waited for (at kt = 0 too: the prologue issues stage 0, B(0), B(1)), at its middle
+  // B(2kt + 2) and >= PW pieces.  The phase kt mod 3 picks the buffers (compile-time).
+  auto step3 = [&](bf16x8 (&bq)[3][JB][NP], int kt, auto ph_c) {
+    constexpr int PH = decltype(ph_c)::value;
+    constexpr int S0 = (2 * PH) % 3, S1 = (2 * PH + 1) % 3, L0 = (2 * PH + 2) % 3;
+    constexpr int NB = JB * NP;
+    wait_vm<NB, NP, JB>(bq[S0]);  // B(2kt) and this wave's stage-kt pieces
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const int kn = min((kt + 1) * KS, klast);
+    const unsigned nst = lds_base + ((kt + 1) & 1) * STAGE;
+    const char* cur = smem + (kt & 1) * STAGE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (s == 0) {
+        bload_c(bq[L0], kt * KS + 64);
+      } else {
+        wait_vm<NB + PW, NP, JB>(bq[S1]);
+        bload_c(bq[S0], kt * KS + 96);  // half 2kt + 3 into the buffer half 2kt just read
+      }
+      bf16x8(&b)[JB][NP] = s == 0 ? bq[S0] : bq[S1];
+      bf16x8 a[2][NP];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) a[0][q] = afrag(cur, 0, s, q);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        if (i + 1 < TI) {
+#pragma unroll
+          for (int q = 0; q < NP; ++q) a[(i + 1) & 1][q] = afrag(cur, i + 1, s, q);
+        }
+        if (s == 0) {
+#pragma unroll
+          for (int qi = (i * PMAX) / TI; qi < ((i + 1) * PMAX) / TI; ++qi)
+            if (qi < mine) wave_piece(qi, kn, nst);
+        }
+        const bf16x8(&x)[NP] = a[i & 1];
+#pragma unroll
+        for (int j = 0; j < JB; ++j) {
+          f32x4 c = acc[i][j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[0]), __builtin_bit_cast(f16x8, b[j][1]), c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[1]), __builtin_bit_cast(f16x8, b[j][0]), c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[0]), __builtin_bit_cast(f16x8, b[j][0]), c, 0, 0, 0);
+          acc[i][j] = c;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  // one self-contained loop per nk mod 3 (R steps peeled, then whole triples): no asm-loaded B
+  // register is live across a branch
+  auto run3 = [&](auto r_c) {
+    constexpr int R = decltype(r_c)::value;
+    bf16x8 bq[3][JB][NP];
+    bload_c(bq[0], 0);
+    bload_c(bq[1], 32);
+    if constexpr (R >= 1) step3(bq, 0, std::integral_constant<int, 0>{});
+    if constexpr (R >= 2) step3(bq, 1, std::integral_constant<int, 1>{});
+    for (int kt = R; kt < nk; kt += 3) {
+      step3(bq, kt, std::integral_constant<int, R % 3>{});
+      step3(bq, kt + 1, std::integral_constant<int, (R + 1) % 3>{});
+      step3(bq, kt + 2, std::integral_constant<int, (R + 2) % 3>{});
+    }
+  };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using BT = std::integral_constant<bool, true>;
   using BF = std::integral_constant<bool, false>;
-  if constexpr (DEEP) {
+  if constexpr (DEEP3) {
+    const int r = nk % 3;
+    if (r == 0) run3(std::integral_constant<int, 0>{});
+    else if (r == 1) run3(std::integral_constant<int, 1>{});
+    else run3(std::integral_constant<int, 2>{});
+  } else if constexpr (DEEP) {
     // one self-contained loop per parity of nk: no asm-loaded B register is live across the branch
     if (nk & 1) {
       bf16x8 bq[4][JB][NP];
