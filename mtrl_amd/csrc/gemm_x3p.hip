@@ -253,8 +253,12 @@ static void x3p_dispatch(int geo, const SplitGemmParams& p, int epi, int batch, 
 // Auto geometry by size (measured, tools/x3p_bench.py): 256x256 tiles (least operand traffic
 // per MFMA) when they give >= 192 workgroups or the form is the k-major weight gradient (split-K
 // fills the chip there); else 256x128.  g_x3p_geo forces one (experiments).
-static int pick_geo(int M, int N, int K, int batch, bool kmajor, bool a_kmajor) {
+static int pick_geo(int M, int N, int K, int batch, bool kmajor, bool a_kmajor, int np = 3) {
   if (g_x3p_geo >= 0) return (g_x3p_geo == 5 && a_kmajor) ? 3 : g_x3p_geo;
+  // one-plane (bf16) weight grads over few rows (C2: K = 1280): 128 x 128 k32 tiles, two rounds of
+  // 256 workgroups for the twin critic and no split-K for the actor -- C2 978-982 -> 991-1007 steps/s
+  // against the 256 x 128 k16 tiles (profiles/r5ap_c2_wgrad_geo_ab.txt)
+  if (kmajor && np == 1 && K <= 2048) return 0;
   if (kmajor) {  // weight grads over K = rows: 256 x 128 k16 tiles -- measured per launch
                  // (profiles/r3u_wgrad_geo.txt, split3): W = 2048, E = 2, K = 896: 83.9 vs 105.8 us
                  // (no split-K, no reduce pass), K = 1664: 153.8 vs 170.0, K = 3200: 280.3 vs 282.2,
@@ -273,9 +277,9 @@ static int pick_geo(int M, int N, int K, int batch, bool kmajor, bool a_kmajor) 
   return ((tall + ncu - 1) / ncu) * 224 < ((big + ncu - 1) / ncu) * 256 ? 5 : 3;
 }
 
-int gemm_x3p_splits(int M, int N, int K, int batch, bool kmajor) {
+int gemm_x3p_splits(int M, int N, int K, int batch, bool kmajor, int np) {
   int bm, bn;
-  geo_tile(pick_geo(M, N, K, batch, kmajor, kmajor), bm, bn);
+  geo_tile(pick_geo(M, N, K, batch, kmajor, kmajor, np), bm, bn);
   const long long tiles = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch;
   if (tiles >= 192) return 1;
   // slices: least (rounds of tiles x S workgroups on the CUs) / S, plus a share of a round per
@@ -301,8 +305,9 @@ int gemm_x3p_splits(int M, int N, int K, int batch, bool kmajor) {
   return best;
 }
 
-long long gemm_x3p_ws_floats(int M, int N, int K, int batch, bool kmajor) {
-  return gemm_ws_floats(M, N, batch, gemm_x3p_splits(M, N, K, batch, kmajor));
+long long gemm_x3p_ws_floats(int M, int N, int K, int batch, bool kmajor) {  // enough for every plane count
+  return std::max(gemm_ws_floats(M, N, batch, gemm_x3p_splits(M, N, K, batch, kmajor, 3)),
+                  gemm_ws_floats(M, N, batch, gemm_x3p_splits(M, N, K, batch, kmajor, 1)));
 }
 
 namespace {
@@ -511,8 +516,8 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
   SplitGemmParams p = p0;
   p.dbg |= g_x3p_dbg;
   const bool kmajor = p.a_kmajor && p.b_kmajor;
-  const int geo = pick_geo(p.M, p.N, p.K, batch, kmajor, p.a_kmajor != 0);
-  if (p.splits < 0) p.splits = gemm_x3p_splits(p.M, p.N, p.K, batch, kmajor);  // auto
+  const int geo = pick_geo(p.M, p.N, p.K, batch, kmajor, p.a_kmajor != 0, p.np == 0 ? 3 : p.np);
+  if (p.splits < 0) p.splits = gemm_x3p_splits(p.M, p.N, p.K, batch, kmajor, p.np == 0 ? 3 : p.np);  // auto
   // split-K: every epilogue works (the finishing pass applies it); the vector finish needs
   // N, ldc, ldm, ldcp multiples of 4
   const bool vec = p.N % 4 == 0 && (!p.C || p.ldc % 4 == 0) && (epi != EPI_RELU_MASK || p.ldm % 4 == 0) &&

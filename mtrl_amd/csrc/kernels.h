@@ -139,7 +139,8 @@ void gemm_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st);
 // from p.mask16 when set, else p.mask
 void splitk_finish(const SplitGemmParams& p, int epi, int S, int batch, hipStream_t st);
 // auto split-K slices (1 = none) for a plane GEMM; kmajor = the k-major x k-major form
-int gemm_x3p_splits(int M, int N, int K, int batch, bool kmajor);
+// np: operand planes (1 = bf16 picks its own weight-grad tiles); the default sizes for the widest form
+int gemm_x3p_splits(int M, int N, int K, int batch, bool kmajor, int np = 3);
 long long gemm_x3p_ws_floats(int M, int N, int K, int batch, bool kmajor);
 // row-major x row-major plane GEMM on 16x16x32 MFMA, 208 x 256 tiles (gemm_x3f.hip): forward
 // (EPI_BIAS_RELU) and data grad (EPI_RELU_MASK) when gemm_x3f_ok
