@@ -350,11 +350,25 @@ void dispatch(const SplitGemmParams& p, int epi, int batch, hipStream_t st) {
 
 // experiments: the (M, N, batch) forward with planes out on TI = 7, ablations abl (1 no loads,
 // 2 no MFMAs)
+namespace x3sk {
+template <int TI>
+void ablate_ti(const SplitGemmParams& p, int abl, int batch, hipStream_t st) {
+  if (abl == 1) launch<TI, EPI_BIAS_RELU, false, true, false, ABL_NOLOAD>(p, batch, st);
+  else if (abl == 2) launch<TI, EPI_BIAS_RELU, false, true, false, ABL_NOMFMA>(p, batch, st);
+  else launch<TI, EPI_BIAS_RELU, false, true, false>(p, batch, st);
+}
+}  // namespace x3sk
+
 void gemm_x3s_ablate(const SplitGemmParams& p, int abl, int batch, hipStream_t st) {
   using namespace x3sk;
-  if (abl == 1) launch<7, EPI_BIAS_RELU, false, true, false, ABL_NOLOAD>(p, batch, st);
-  else if (abl == 2) launch<7, EPI_BIAS_RELU, false, true, false, ABL_NOMFMA>(p, batch, st);
-  else launch<7, EPI_BIAS_RELU, false, true, false>(p, batch, st);
+  // the row tile the dispatch picks for the shape (4 .. 8 x 16 rows)
+  switch (gemm_x3s_ti(p.M, p.N, batch)) {
+    case 4: ablate_ti<4>(p, abl, batch, st); break;
+    case 5: ablate_ti<5>(p, abl, batch, st); break;
+    case 6: ablate_ti<6>(p, abl, batch, st); break;
+    case 8: ablate_ti<8>(p, abl, batch, st); break;
+    default: ablate_ti<7>(p, abl, batch, st); break;
+  }
 }
 
 // rows per tile / 16: the fewest (rounds of 256 workgroups) x (rows per tile), ties to the smaller
