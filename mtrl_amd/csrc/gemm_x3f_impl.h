@@ -6,33 +6,9 @@
 
 #include "gemm_x3p_impl.h"
 
-#ifndef X3F_STAGGER
-#define X3F_STAGGER 0  // 1: the staggered schedule of the split2h instances (STG below; measured slower, A/B only)
-#endif
-
-#ifndef X3F_WT_STORES
-// 1: the epilogue's C and plane stores are write-through (sc1): the lines leave the XCD's L2 as they
-// are written, so no dirty output lingers there for the kernel boundary to write back
-// (MI355X_MICROARCH.md: a dependent boundary costs + B / 6 TB/s for B dirty bytes).  Measured slower
-// (profiles/r5ae_x3f_wt_stores_ab.txt: S3 212.1-212.9 vs 217.4-220.2 steps/s, hidden forward 0.547 vs
-// 0.597 solo): the kernels lose more than the boundaries gain.  0: plain stores (default)
-#define X3F_WT_STORES 0
-#endif
-
 #ifndef X3F_DEEP_B
 #define X3F_DEEP_B 1  // the bf16 instances' four-buffer B ring (DEEP below); 0: build without (A/B)
 #endif
-#ifndef X3F_DEEP_H2
-#define X3F_DEEP_H2 0  // 1: the ring for the split2h tiles of up to 128 rows too (the task shards' split-K
-                       // slices; at 208 rows it spills): parity green, the 7-task shard step unchanged
-                       // (profiles/r5ak_shard_deep_h2_ab.txt), so off
-#endif
-
-#ifndef X3F_DEEP3
-#define X3F_DEEP3 0  // 1: the split2h 208-row tiles' three-buffer B ring (DEEP3 below): parity green, S3 not
-                     // faster (211.7-213.1 vs 215.1-216.4 steps/s, profiles/r5al_s3_deep3_ab.txt), so off
-#endif
-
 #ifndef X3F_EPI_GROUP
 #define X3F_EPI_GROUP 2  // 16-row blocks per epilogue barrier in the plane kernels (4 measured equal: profiles/r4k_*)
 #endif
@@ -125,33 +101,16 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   // input layer's), 1 otherwise
   constexpr int EG = (!FIN && NP >= 2) ? X3F_EPI_GROUP : 1;
   constexpr int EPI_LDS = (2 * EG * 16 * (BN + 4) + WV * BN + 16) * 4;  // + the split2h max scratch
-  // STG (split2h, 8 waves, a 3-stage ring that fits): the two waves of each SIMD run half a step apart
-  // (MI355X_MICROARCH.md, 'Two waves per SIMD' item 9).  Waves 0-3 ("early") issue every LDS-DMA piece,
-  // one stage ahead, and meet the step barrier at the start of their steps; waves 4-7 ("late") meet the
-  // same barrier in the MIDDLE of their steps, so while one wave of a SIMD waits at the barrier, loads
-  // its B fragments or reads a fresh stage, its partner is in the middle of its MFMAs.  Stage k lives in
-  // buffer k mod 3: when the early waves refill buffer (k + 1) mod 3 during step k, the late waves are
-  // past step k - 2 (they passed barrier k in the middle of step k - 1).  Same products, same order:
-  // outputs are bitwise those of the unstaggered schedule.  Measured (-DX3F_STAGGER=1 against the
-  // default build on one box, profiles/r5w_*): parity green, but the hidden forward 0.563-0.566 of
-  // the split2h peak against 0.578-0.584 and S3 211.6 against 213.7 steps/s -- the early waves issue
-  // twice the DMA pieces, and the chip's clock under this MFMA load, not the issue schedule, bounds
-  // the loop.  Kept as a build option.
-  constexpr bool STG = X3F_STAGGER && NP == 2 && WV == 8 && (ABL == 0 || ABL == TAG_INPUT) &&
-                       3 * STAGE <= 160 * 1024 - 16 && NJ % 4 == 0;
   // DEEP (precision bf16, one plane; the non-split epilogue instances of up to 208 rows -- the 400-row
   // tile has no registers for the ring): B fragments run THREE half steps ahead through a ring of four
   // register buffers instead of one.  The one-plane step has a third of the MFMAs of a split2h step, so a
   // half step of MFMAs no longer covers an L2 / MALL load: at MT10's 80-row tile (C2) the kernel
   // without B reloads took 21.7 against 30.8 us (profiles/r5ah_x3f_c2_ablate.txt).
-  constexpr bool DEEP = ((NP == 1 && BM <= 208 && ABL == 0 && EPI != EPI_STORE && !FIN) ||
-                         (NP == 2 && BM <= 128 && X3F_DEEP_H2 && (ABL == 0 || ABL == TAG_INPUT))) && !STG && X3F_DEEP_B;
-  // DEEP3 (split2h tiles of more than 128 rows -- S3's 208, where four buffers spill): the same idea
-  // with a ring of three buffers, B two half steps ahead instead of one
-  constexpr bool DEEP3 = NP == 2 && BM > 128 && (ABL == 0 || ABL == TAG_INPUT) && !STG && !DEEP && X3F_DEEP3;
-  constexpr int NSTG = STG ? 3 : 2;
-  constexpr int PE = NJ / 4;  // STG: DMA pieces per early wave and stage
-  constexpr int SMEM0 = NSTG * STAGE > EPI_LDS ? NSTG * STAGE : EPI_LDS;
+  // The same ring for the split2h tiles (three buffers at 208 rows, where four spill; four at <= 128)
+  // and a staggered two-waves-per-SIMD schedule with a 3-stage LDS ring were built, passed parity and
+  // measured no faster (commits f56d1da, 5207f51, 6f6b182), so removed.
+  constexpr bool DEEP = NP == 1 && BM <= 208 && ABL == 0 && EPI != EPI_STORE && !FIN && X3F_DEEP_B;
+  constexpr int SMEM0 = 2 * STAGE > EPI_LDS ? 2 * STAGE : EPI_LDS;
   constexpr int SMEM = SMEM0 + (FIN ? 16 : 0);  // FIN: the 'last slice' word after the scratch
   static_assert(BM % 16 == 0 && SMEM <= 160 * 1024, "tile");
   static_assert(PMAX - 1 >= PW || NJ % WV == 0, "every wave issues >= PW pieces in the first half step");
@@ -239,18 +198,10 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
 
   bf16x8 b0[JB][NP], b1[JB][NP];
   if ((ABL & 4) && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  const bool early = wave < 4;
   // prologue: stage 0 + B of the first half step
-  if constexpr (STG) {
-    if (early) {
 #pragma unroll
-      for (int qi = 0; qi < PE; ++qi) piece(wave + 4 * qi, 0, lds_base);
-    }
-  } else {
-#pragma unroll
-    for (int qi = 0; qi < PMAX; ++qi) wave_piece(qi, 0, lds_base);
-  }
-  if constexpr (!DEEP && !DEEP3) bload(b0, 0);
+  for (int qi = 0; qi < PMAX; ++qi) wave_piece(qi, 0, lds_base);
+  if constexpr (!DEEP) bload(b0, 0);
 
   // one 64-deep step; MORE: the next stage and B half step are loaded during it (all but the last)
   auto step = [&](int kt, auto more_c) {
@@ -312,59 +263,6 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
       }
     }
   };
-  // the staggered schedule (STG): stage k in buffer k mod 3; see STG above
-  auto step_stg = [&](int kt, int cb, auto more_c) {
-    constexpr bool MORE = decltype(more_c)::value;
-    // every wave: B(kt, 0) landed (early waves: also their DMA pieces of stage kt); the early waves
-    // (and all at kt = 0) then meet the step barrier, the late waves met it in the middle of step kt - 1.
-    // The waits are single asm sites run by both groups and the branches carry no register operands,
-    // so the allocator never splits the live range of an asm-loaded B fragment (a copy made before
-    // the load lands reads garbage).
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (early || kt == 0) asm volatile("s_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    const int kn = (kt + 1) * KS;
-    const int nb = cb == 2 ? 0 : cb + 1;
-    const unsigned nst = lds_base + nb * STAGE;
-    const char* cur = smem + cb * STAGE;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8(&b)[JB][NP] = s == 0 ? b0 : b1;
-      if (s == 0) {
-        bload(b1, kt * KS + 32);  // second half of this step
-      } else {
-        // late waves: everything landed, then the step barrier (mid-step); they hold no DMA pieces
-        if (MORE && !early) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        // B(kt, 1) landed; an early wave's pieces issued after it may not have
-        wait_vm<MORE ? PE : 0, NP, JB>(b1);
-        if (MORE) bload(b0, kn);  // first half of the next step
-      }
-      bf16x8 a[2][NP];
-#pragma unroll
-      for (int q = 0; q < NP; ++q) a[0][q] = afrag(cur, 0, s, q);
-#pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        if (i + 1 < TI) {
-#pragma unroll
-          for (int q = 0; q < NP; ++q) a[(i + 1) & 1][q] = afrag(cur, i + 1, s, q);
-        }
-        if (MORE && s == 0 && early) {  // the next stage's pieces, spread over the first half's row tiles
-#pragma unroll
-          for (int qi = (i * PE) / TI; qi < ((i + 1) * PE) / TI; ++qi) piece(wave + 4 * qi, kn, nst);
-        }
-        const bf16x8(&x)[NP] = a[i & 1];
-#pragma unroll
-        for (int j = 0; j < JB; ++j) {
-          f32x4 c = acc[i][j];
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[0]), __builtin_bit_cast(f16x8, b[j][1]), c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[1]), __builtin_bit_cast(f16x8, b[j][0]), c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[0]), __builtin_bit_cast(f16x8, b[j][0]), c, 0, 0, 0);
-          acc[i][j] = c;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  };
   // DEEP: step kt computes half steps 2kt (buffer 2P) and 2kt + 1 (2P + 1), P = kt & 1, and loads half
   // steps 2kt + 3 and 2kt + 4 into the buffers freed by 2kt - 1 and 2kt.  Every step issues the same
   // operations -- B(2kt + 3), the pieces of stage kt + 1 (spread over the first half's row tiles),
@@ -372,7 +270,7 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   // the buffer the last step does not read, and the epilogue drains them), so every count is a
   // constant: at the start of step kt only B(2kt + 2) may still be in flight besides what is waited
   // for (at kt = 0: B(1), B(2)), and at its middle B(2kt + 2), B(2kt + 3) and >= PW pieces.
-  const int klast = (nk - 1) * KS;  // the last step's k, relative to this slice's A / B
+  const int klast = (nk - 1) * KS;  // the last step's k
   auto bload_c = [&](bf16x8 (&b)[JB][NP], int k) { bload(b, k < klast + 32 ? k : klast + 32); };
   auto step_deep = [&](bf16x8 (&bq)[4][JB][NP], int kt, auto par_c, auto first_c) {
     constexpr int P = decltype(par_c)::value;
@@ -410,98 +308,16 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
         }
         const bf16x8(&x)[NP] = a[i & 1];
 #pragma unroll
-        for (int j = 0; j < JB; ++j) {
-          f32x4 c = acc[i][j];
-          if constexpr (NP == 2) {  // fp16 planes: h*l, l*h, h*h
-            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[0]), __builtin_bit_cast(f16x8, b[j][1]), c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[1]), __builtin_bit_cast(f16x8, b[j][0]), c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[0]), __builtin_bit_cast(f16x8, b[j][0]), c, 0, 0, 0);
-          } else {
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][0], c, 0, 0, 0);
-          }
-          acc[i][j] = c;
-        }
+        for (int j = 0; j < JB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[0], b[j][0], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
-    }
-  };
-  // DEEP3: step kt computes half steps 2kt (buffer (2kt) mod 3) and 2kt + 1, and loads half steps
-  // 2kt + 2 (into the buffer half 2kt - 1 left) and 2kt + 3 (into the one half 2kt just left); issue
-  // order per step: B(2kt + 2), the pieces of stage kt + 1, B(2kt + 3), past the end of K at clamped
-  // addresses as DEEP does.  At the start of step kt only B(2kt + 1) may still be in flight besides
-  // what is waited for (at kt = 0 too: the prologue issues stage 0, B(0), B(1)), at its middle
-  // B(2kt + 2) and >= PW pieces.  The phase kt mod 3 picks the buffers (compile-time).
-  auto step3 = [&](bf16x8 (&bq)[3][JB][NP], int kt, auto ph_c) {
-    constexpr int PH = decltype(ph_c)::value;
-    constexpr int S0 = (2 * PH) % 3, S1 = (2 * PH + 1) % 3, L0 = (2 * PH + 2) % 3;
-    constexpr int NB = JB * NP;
-    wait_vm<NB, NP, JB>(bq[S0]);  // B(2kt) and this wave's stage-kt pieces
-    asm volatile("s_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    const int kn = min((kt + 1) * KS, klast);
-    const unsigned nst = lds_base + ((kt + 1) & 1) * STAGE;
-    const char* cur = smem + (kt & 1) * STAGE;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      if (s == 0) {
-        bload_c(bq[L0], kt * KS + 64);
-      } else {
-        wait_vm<NB + PW, NP, JB>(bq[S1]);
-        bload_c(bq[S0], kt * KS + 96);  // half 2kt + 3 into the buffer half 2kt just read
-      }
-      bf16x8(&b)[JB][NP] = s == 0 ? bq[S0] : bq[S1];
-      bf16x8 a[2][NP];
-#pragma unroll
-      for (int q = 0; q < NP; ++q) a[0][q] = afrag(cur, 0, s, q);
-#pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        if (i + 1 < TI) {
-#pragma unroll
-          for (int q = 0; q < NP; ++q) a[(i + 1) & 1][q] = afrag(cur, i + 1, s, q);
-        }
-        if (s == 0) {
-#pragma unroll
-          for (int qi = (i * PMAX) / TI; qi < ((i + 1) * PMAX) / TI; ++qi)
-            if (qi < mine) wave_piece(qi, kn, nst);
-        }
-        const bf16x8(&x)[NP] = a[i & 1];
-#pragma unroll
-        for (int j = 0; j < JB; ++j) {
-          f32x4 c = acc[i][j];
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[0]), __builtin_bit_cast(f16x8, b[j][1]), c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[1]), __builtin_bit_cast(f16x8, b[j][0]), c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, x[0]), __builtin_bit_cast(f16x8, b[j][0]), c, 0, 0, 0);
-          acc[i][j] = c;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  };
-  // one self-contained loop per nk mod 3 (R steps peeled, then whole triples): no asm-loaded B
-  // register is live across a branch
-  auto run3 = [&](auto r_c) {
-    constexpr int R = decltype(r_c)::value;
-    bf16x8 bq[3][JB][NP];
-    bload_c(bq[0], 0);
-    bload_c(bq[1], 32);
-    if constexpr (R >= 1) step3(bq, 0, std::integral_constant<int, 0>{});
-    if constexpr (R >= 2) step3(bq, 1, std::integral_constant<int, 1>{});
-    for (int kt = R; kt < nk; kt += 3) {
-      step3(bq, kt, std::integral_constant<int, R % 3>{});
-      step3(bq, kt + 1, std::integral_constant<int, (R + 1) % 3>{});
-      step3(bq, kt + 2, std::integral_constant<int, (R + 2) % 3>{});
     }
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using BT = std::integral_constant<bool, true>;
   using BF = std::integral_constant<bool, false>;
-  if constexpr (DEEP3) {
-    const int r = nk % 3;
-    if (r == 0) run3(std::integral_constant<int, 0>{});
-    else if (r == 1) run3(std::integral_constant<int, 1>{});
-    else run3(std::integral_constant<int, 2>{});
-  } else if constexpr (DEEP) {
+  if constexpr (DEEP) {
     // one self-contained loop per parity of nk: no asm-loaded B register is live across the branch
     if (nk & 1) {
       bf16x8 bq[4][JB][NP];
@@ -525,13 +341,6 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
         step_deep(bq, kt + 1, I1{}, BF{});
       }
     }
-  } else if constexpr (STG) {
-    int cb = 0;
-    for (int kt = 0; kt + 1 < nk; ++kt) {
-      step_stg(kt, cb, std::integral_constant<bool, true>{});
-      cb = cb == 2 ? 0 : cb + 1;
-    }
-    step_stg(nk - 1, cb, std::integral_constant<bool, false>{});
   } else {
     for (int kt = 0; kt + 1 < nk; ++kt) step(kt, std::integral_constant<bool, true>{});
     step(nk - 1, std::integral_constant<bool, false>{});
@@ -653,10 +462,6 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   }
   float* C = C_OUT ? p.C + z * p.sC + (FIN ? 0ll : (long long)sl * p.M * p.ldc) : nullptr;
   __bf16* Cp = P_OUT ? p.Cp + z * p.sCp : nullptr;
-  // write-through stores (X3F_WT_STORES): buffer stores with the sc1 policy (aux 16) at byte offsets
-  // from the member's C / plane base (< 2^31: at most 2 x 12800 x 2048 x 2 B of planes per member)
-  const __amdgpu_buffer_rsrc_t c_rs = __builtin_amdgcn_make_buffer_rsrc((void*)C, (short)0, -1, 0x00020000);
-  const __amdgpu_buffer_rsrc_t p_rs = __builtin_amdgcn_make_buffer_rsrc((void*)Cp, (short)0, -1, 0x00020000);
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums over this lane's rows (dbp)
   // FIN, two slices (task shards): the other slice's values of the next PB row blocks this lane
   // finishes are loaded in one burst, so the slab reads overlap instead of costing one round trip
@@ -762,15 +567,9 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
 #pragma unroll
     for (int c = 0; c < 8; ++c) csum[c] += e[c];
     if (C_OUT) {
-      if (X3F_WT_STORES) {
-        const int o = (int)(((long long)row * p.ldc + col) * 4);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_float4(e[0], e[1], e[2], e[3])), c_rs, o, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_float4(e[4], e[5], e[6], e[7])), c_rs, o + 16, 0, 16);
-      } else {
-        float* cp = C + (long long)row * p.ldc + col;
-        *reinterpret_cast<float4*>(cp) = make_float4(e[0], e[1], e[2], e[3]);
-        *reinterpret_cast<float4*>(cp + 4) = make_float4(e[4], e[5], e[6], e[7]);
-      }
+      float* cp = C + (long long)row * p.ldc + col;
+      *reinterpret_cast<float4*>(cp) = make_float4(e[0], e[1], e[2], e[3]);
+      *reinterpret_cast<float4*>(cp + 4) = make_float4(e[4], e[5], e[6], e[7]);
     }
     if (P_OUT && NP == 2) {
       f16x8 h, l;
@@ -781,15 +580,9 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
         h[c] = a_; l[c] = b_;
         omx = fmaxf(omx, fabsf(e[c]));
       }
-      if (X3F_WT_STORES) {
-        const int o = (int)(((long long)row * p.ldcp + col) * 2);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h), p_rs, o, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, l), p_rs, o + (int)(p.pC * 2), 0, 16);
-      } else {
-        __bf16* pp = Cp + (long long)row * p.ldcp + col;
-        *reinterpret_cast<f16x8*>(pp) = h;
-        *reinterpret_cast<f16x8*>(pp + p.pC) = l;
-      }
+      __bf16* pp = Cp + (long long)row * p.ldcp + col;
+      *reinterpret_cast<f16x8*>(pp) = h;
+      *reinterpret_cast<f16x8*>(pp + p.pC) = l;
     } else if (P_OUT) {
       bf16x8 h, m, l;
 #pragma unroll
