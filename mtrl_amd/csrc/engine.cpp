@@ -93,6 +93,11 @@ struct Net {
   // grad): [E][chunks][width]; dbp_chunks[i] > 0 when the current step's dz[i] came with them
   float* dbp[MAXD] = {};
   int dbp_chunks[MAXD] = {};
+  // one GPU (no collective reads a layer's gradient before the optimizer): the weight grads' finishes
+  // (split-K slab sums, bias grads from column sums) are collected in fin_sink and run in ONE launch at
+  // the start of the network's optimizer; ws_wg[i] holds layer i's slabs until then
+  float* ws_wg[MAXD] = {};
+  FinishSink fin_sink;
   long long wtk(int i) const { return i == 0 ? xld : ald; }  // K (padded in-dim) of layer i
   long long wtps(int i = 1) const { return (long long)width * wtk(i); }
   long long xld = 0;  // input planes' row stride = layer-0 kernel plane rows (in_dim rounded up to 32)
@@ -925,6 +930,11 @@ struct mtsac_engine {
       g.splits = -1;  // by tile count (gemm_x3p_splits); the lane workspace is sized for it
       g.ws = ws_lane[cur_lane];
       g.cnt = fin_cnt();
+      if (defer_finish()) {  // the finish runs at the start of optimize(net); the slabs wait in ws_wg[i]
+        g.ws = net.ws_wg[i];  // (null: this weight grad never splits)
+        g.cnt = nullptr;
+        g.defer = &net.fin_sink;
+      }
       if (net.dbp_chunks[i] > 0) {  // dz[i]'s producer left its column sums: gemm_x3p finishes the bias
         g.cs_part = net.dbp[i];     // grad (in its split-K reduce launch when it has one)
         g.cs_chunks = net.dbp_chunks[i];
@@ -1142,7 +1152,18 @@ struct mtsac_engine {
   // The trunk's partials never mix with the heads' (bitwise-identical replicated trunks and norms
   // on every rank); sharded, the heads' |g|^2 is the all-reduced scalar head_sq() left in the tail.
   // |p_new|^2 partials stay per network and are summed in the last segment (norms_and_logs).
+  // one GPU: no collective reads a layer's gradient between its weight grad and the optimizer, so the
+  // finishes wait for optimize() (MTSAC_DEFER_FINISH=0: each right after its GEMM)
+  bool defer_finish() const {
+    static const bool on = [] {
+      const char* v = getenv("MTSAC_DEFER_FINISH");
+      return !(v && atoi(v) == 0);
+    }();
+    return on && !sharded();
+  }
+
   void optimize(Net& net, float lr, float max_norm, bool polyak, int slot) {
+    finish_many(net.fin_sink, net.E, cur);  // the deferred weight-grad finishes (empty when sharded)
     if (zero_of(net)) {
       optimize_zero(net, lr, max_norm, polyak, slot);
       return;
@@ -2341,6 +2362,13 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
       }
     for (float*& w : e->ws_lane)
       if ((rc = e->alloc(&w, (size_t)std::max(ws, 1LL)))) return bad(rc);
+    if (e->planes)  // the deferred weight-grad finishes' slabs, per layer (Net::fin_sink)
+      for (Net* net : {&e->actor, &e->critic})
+        for (int i = 0; i < net->depth; ++i) {
+          const long long w = gemm_x3p_ws_floats(i == 0 ? net->in_dim : net->width, net->width, (int)net->krows,
+                                                 net->E, true);
+          if (w > 0 && (rc = e->alloc(&net->ws_wg[i], (size_t)w))) return bad(rc);
+        }
     for (int*& c : e->cnt_lane)
       if ((rc = e->alloc(&c, (size_t)GEMM_X3F_CNT))) return bad(rc);
   }

@@ -545,8 +545,11 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
   if (!fin) q.cnt = nullptr;
   x3p_dispatch(geo, q, kepi, batch, st);
   const bool cs = p.cs_part != nullptr && p.cs_chunks > 0;
+  // defer: the caller runs this finish later, with its network's other ones, in one launch
+  const bool defer = epi == EPI_STORE && !p.Cp && p.defer != nullptr && p.defer->n < FINISH_SINK_JOBS;
   if (S == 1 || fin) {
-    if (cs) colsum_finish(p.cs_part, p.N, p.cs_chunks, batch, p.cs_db, p.cs_sdb, st);
+    if (cs && defer) p.defer->job[p.defer->n++] = colsum_job(p.cs_part, p.N, p.cs_chunks, p.cs_db, p.cs_sdb);
+    else if (cs) colsum_finish(p.cs_part, p.N, p.cs_chunks, batch, p.cs_db, p.cs_sdb, st);
     return;
   }
   if (epi == EPI_STORE && !p.Cp) {  // the slab sums and (cs) the bias grad's column sums: one launch
@@ -557,7 +560,8 @@ void gemm_x3p(const SplitGemmParams& p0, int epi, int batch, hipStream_t st) {
     r.ldc = p.ldc;
     r.sC = p.sC;
     r.ws = p.ws;
-    splitk_reduce(r, batch, S, st, cs ? p.cs_part : nullptr, p.cs_chunks, p.cs_db, p.cs_sdb);
+    if (defer) p.defer->job[p.defer->n++] = reduce_job(r, batch, S, cs ? p.cs_part : nullptr, p.cs_chunks, p.cs_db, p.cs_sdb);
+    else splitk_reduce(r, batch, S, st, cs ? p.cs_part : nullptr, p.cs_chunks, p.cs_db, p.cs_sdb);
     return;
   }
   if (cs) colsum_finish(p.cs_part, p.N, p.cs_chunks, batch, p.cs_db, p.cs_sdb, st);

@@ -58,6 +58,25 @@ struct ReduceJob {
 };
 void splitk_reduce(const GemmParams& p, int batch, int splits, hipStream_t st, const float* cs_part = nullptr,
                    int cs_chunks = 0, float* cs_db = nullptr, long long cs_sdb = 0);
+// A weight grad's finish (split-K slab sums and / or the bias grad from column-sum partials), collected
+// instead of launched (SplitGemmParams::defer) and run with the network's other ones in ONE launch
+// before its optimizer (finish_many): the same blocks, sums and order as splitk_finish_all_kernel.
+struct DeferredFinish {
+  ReduceJob j;
+  int nred, ndb, ncs;
+};
+constexpr int FINISH_SINK_JOBS = 8;
+struct FinishSink {
+  DeferredFinish job[FINISH_SINK_JOBS];
+  int n = 0;
+};
+// the job splitk_reduce launches (nred + ndb + ncs blocks per batch entry)
+DeferredFinish reduce_job(const GemmParams& p, int batch, int splits, const float* cs_part, int cs_chunks,
+                          float* cs_db, long long cs_sdb);
+// a bias grad from column-sum partials only (what colsum_finish launches)
+DeferredFinish colsum_job(const float* part, int cols, int chunks, float* db, long long sdb);
+// every job of the sink in one launch (batch entries: grid.y), then the sink is empty
+void finish_many(FinishSink& s, int batch, hipStream_t st);
 // out[z][c][r] = in[z][r][c]  (rows x cols per batch entry, dense)
 void transpose_f32(const float* in, long long s_in, float* out, long long s_out, int rows, int cols, int batch,
                    hipStream_t st);
@@ -132,6 +151,8 @@ struct SplitGemmParams {
   float kmul;             // the number of terms in each output sum (unpadded K)
   long long pMask;        // plane stride of the mask16 planes (np == 2: x > 0 <=> hi > 0 or lo > 0)
   int* nparts;            // host: the launcher stores how many partial maxima it wrote to rc (or null)
+  FinishSink* defer;      // host, gemm_x3p EPI_STORE: collect the finish (slab sums, bias grad) here
+                          // instead of launching it (null: launch), when the sink has room
 };
 constexpr int GEMM_X3F_CNT = 4096;
 void gemm_x3p(const SplitGemmParams& p, int epi, int batch, hipStream_t st);

@@ -42,9 +42,7 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int S, int M,
 // slabs into C (as splitk_reduce_kernel), [nred, nred + ndb) add the per-slice bias sums (as
 // splitk_db_kernel), the rest finish the bias grad from column-sum partials (as colsum_final_kernel,
 // 64 columns per block): the same sums in the same order, two or three launches fewer per layer.
-__global__ __launch_bounds__(256) void splitk_finish_all_kernel(ReduceJob j, int nred, int ndb) {
-  const int z = blockIdx.y;
-  const int bx = blockIdx.x;
+__device__ inline void finish_job(const ReduceJob& j, int nred, int ndb, int bx, int z) {
   if (bx < nred) {
     const long long slab = (long long)j.M * j.N;
     const float* w = j.ws + (long long)z * j.S * slab;
@@ -100,6 +98,23 @@ __global__ __launch_bounds__(256) void splitk_finish_all_kernel(ReduceJob j, int
   if (g == 0 && c < cols) j.cs_db[z * j.cs_sdb + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
 }
 
+__global__ __launch_bounds__(256) void splitk_finish_all_kernel(ReduceJob j, int nred, int ndb) {
+  finish_job(j, nred, ndb, blockIdx.x, blockIdx.y);
+}
+
+// the jobs of a FinishSink: job k owns blocks [start[k], start[k + 1]) (block-uniform branch)
+struct FinishJobs {
+  DeferredFinish job[FINISH_SINK_JOBS];
+  int start[FINISH_SINK_JOBS + 1];
+  int n;
+};
+__global__ __launch_bounds__(256) void splitk_finish_many_kernel(FinishJobs js) {
+  const int bx = blockIdx.x;
+  int k = 0;
+  while (k + 1 < js.n && bx >= js.start[k + 1]) ++k;
+  finish_job(js.job[k].j, js.job[k].nred, js.job[k].ndb, bx - js.start[k], blockIdx.y);
+}
+
 __global__ void splitk_db_kernel(const float* __restrict__ dbws, int S, int N, float* __restrict__ db, long long sDb) {
   const int z = blockIdx.y;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -147,25 +162,55 @@ long long gemm_ws_floats(int M, int N, int batch, int splits) {
   return (long long)batch * splits * ((long long)M * N + N);
 }
 
-void splitk_reduce(const GemmParams& p, int batch, int splits, hipStream_t st, const float* cs_part, int cs_chunks,
-                   float* cs_db, long long cs_sdb) {
+DeferredFinish reduce_job(const GemmParams& p, int batch, int splits, const float* cs_part, int cs_chunks,
+                          float* cs_db, long long cs_sdb) {
   const long long slab = (long long)p.M * p.N;
   const long long work = (p.N % 4 == 0 && p.ldc % 4 == 0) ? slab / 4 : slab;
-  const int nred = std::max(1, (int)std::min<long long>((work + 255) / 256, 1024));
-  ReduceJob j{};
+  DeferredFinish d{};
+  d.nred = std::max(1, (int)std::min<long long>((work + 255) / 256, 1024));
+  ReduceJob& j = d.j;
   j.ws = p.ws; j.S = splits; j.M = p.M; j.N = p.N; j.C = p.C; j.ldc = p.ldc; j.sC = p.sC;
-  int ndb = 0, ncs = 0;
   if (p.db) {
     j.dbws = p.ws + (long long)batch * splits * slab;
     j.db = p.db;
     j.sDb = p.sDb;
-    ndb = (p.N + 255) / 256;
+    d.ndb = (p.N + 255) / 256;
   }
   if (cs_part && cs_chunks > 0) {
     j.cs_part = cs_part; j.cs_chunks = cs_chunks; j.cs_db = cs_db; j.cs_sdb = cs_sdb;
-    ncs = (p.N + 63) / 64;
+    d.ncs = (p.N + 63) / 64;
   }
-  hipLaunchKernelGGL(splitk_finish_all_kernel, dim3(nred + ndb + ncs, batch), dim3(256), 0, st, j, nred, ndb);
+  return d;
+}
+
+DeferredFinish colsum_job(const float* part, int cols, int chunks, float* db, long long sdb) {
+  DeferredFinish d{};
+  d.j.N = cols;
+  d.j.cs_part = part; d.j.cs_chunks = chunks; d.j.cs_db = db; d.j.cs_sdb = sdb;
+  d.ncs = (cols + 63) / 64;
+  return d;
+}
+
+void finish_many(FinishSink& s, int batch, hipStream_t st) {
+  if (s.n <= 0) return;
+  FinishJobs js{};
+  js.n = s.n;
+  int b = 0;
+  for (int k = 0; k < s.n; ++k) {
+    js.job[k] = s.job[k];
+    js.start[k] = b;
+    b += s.job[k].nred + s.job[k].ndb + s.job[k].ncs;
+  }
+  js.start[s.n] = b;
+  s.n = 0;
+  if (b > 0) hipLaunchKernelGGL(splitk_finish_many_kernel, dim3(b, batch), dim3(256), 0, st, js);
+}
+
+void splitk_reduce(const GemmParams& p, int batch, int splits, hipStream_t st, const float* cs_part, int cs_chunks,
+                   float* cs_db, long long cs_sdb) {
+  const DeferredFinish d = reduce_job(p, batch, splits, cs_part, cs_chunks, cs_db, cs_sdb);
+  hipLaunchKernelGGL(splitk_finish_all_kernel, dim3(d.nred + d.ndb + d.ncs, batch), dim3(256), 0, st, d.j, d.nred,
+                     d.ndb);
 }
 
 void transpose_f32(const float* in, long long s_in, float* out, long long s_out, int rows, int cols, int batch,
