@@ -857,8 +857,13 @@ struct mtsac_engine {
 
   // after every write of params: Net::wt[which] (fp32) or the planes wp[which] (split3);
   // fused: the optimizer already wrote them (see optimize())
+  // the optimizer writes the transposed head kernel itself (AdamParams::whT) when its leaf is float4-aligned
+  bool whT_fused(const Net& net) const {
+    return net.whT && net.E == 1 && net.off_hW % 4 == 0 && ((long long)T_l * net.width * net.hd) % 4 == 0;
+  }
   void refresh_wt(Net& net, const float* params, int which, hipStream_t s, bool fused = false) {
-    if (which == 0 && net.whT && net.E == 1) head_transpose(params + net.off_hW, T_l, net.width, net.hd, net.whT, s);
+    if (which == 0 && net.whT && net.E == 1 && !(fused && whT_fused(net)))
+      head_transpose(params + net.off_hW, T_l, net.width, net.hd, net.whT, s);
     if (fused && tiles_fusable(net)) return;  // the optimizer wrote every plane the GEMMs read
     for (int i = planes ? 0 : 1; i < net.depth; ++i) {
       if (!planes) {
@@ -1307,7 +1312,15 @@ struct mtsac_engine {
       a.h2.tparts = polyak ? tparts : nullptr;
     }
     a.n = net.trunk_off;  // heads
+    if (whT_fused(net) && net.off_hW + (long long)T_l * net.width * net.hd <= net.trunk_off) {
+      a.whT = net.whT;
+      a.whT_b4 = net.off_hW / 4;
+      a.whT_e4 = (net.off_hW + (long long)T_l * net.width * net.hd) / 4;
+      a.whT_W = net.width;
+      a.whT_hd = net.hd;
+    }
     at = a;               // trunk
+    at.whT = nullptr;
     at.p += net.trunk_off;
     at.m += net.trunk_off;
     at.v += net.trunk_off;

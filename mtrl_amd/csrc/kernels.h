@@ -452,6 +452,9 @@ struct AdamParams {
   WeightH2 h2;          // np == 2
   int refresh;          // 1: no Adam step -- p is already the new value (the sharded optimizer's all-gathered
                         // trunk); Polyak (target non-null), planes, |p|^2 and maxima as usual
+  float* whT;           // the actor's head kernel transposed per task ([T][hd][W], heads.hip WhT) written
+  long long whT_b4, whT_e4;  // from the new values of the float4 range [whT_b4, whT_e4) of p ([T][W][hd]),
+  int whT_W, whT_hd;         // or null (then head_transpose rewrites it)
 };
 // p_partials accumulate |p_new|^2 over [norm_from, n) only (the replicated trunk range)
 int adam_update(const AdamParams& a, float max_norm, long long norm_from, int max_blocks, hipStream_t st);

@@ -162,6 +162,15 @@ __device__ inline float adam_elems(const AdamParams& a, const AdamConsts& k, lon
       m4[i] = m;
       v4[i] = v;
     }
+    if (a.whT != nullptr && i >= a.whT_b4 && i < a.whT_e4) {  // the head kernel, transposed per task
+      const long long per = (long long)a.whT_W * a.whT_hd, f = 4 * (i - a.whT_b4);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const long long t = (f + c) / per, r = f + c - t * per;
+        const int w = (int)(r / a.whT_hd), o = (int)(r - (long long)w * a.whT_hd);
+        a.whT[(t * a.whT_hd + o) * a.whT_W + w] = pp[c];
+      }
+    }
     if (i >= norm_from4) acc += sq;  // |p|^2 of the replicated (trunk) range only
     pmx = fmaxf(pmx, fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fmaxf(fabsf(p.z), fabsf(p.w))));
     float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
