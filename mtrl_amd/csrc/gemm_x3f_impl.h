@@ -486,9 +486,32 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
     }
   };
   if (two) prefetch(0);
+  // split2h data grad (ReLU mask from the activation's fp16 planes): the mask rows a lane finishes in
+  // the next group of row blocks are loaded one group ahead, so their latency hides behind this
+  // group's image and stores instead of stalling each row (MPF; S3 207.0-208.4 -> 208.6-209.6 steps/s
+  // on one box, profiles/r5ay_x3f_mask_prefetch_ab.txt)
+  constexpr bool MPF = EPI == EPI_RELU_MASK && MASK16 && NP == 2 && !FIN;
+  constexpr int MG = MPF ? EG * RP : 1;
+  i16x8 mbuf[2][MG][2];
+  auto mask_load = [&](int i0, int b) {
+#pragma unroll
+    for (int g = 0; g < EG; ++g)
+#pragma unroll
+      for (int rp = 0; rp < RP; ++rp) {
+        int row = m0 + 16 * (i0 + g) + 2 * (wave + WV * rp) + (lane >> 5);
+        row = row < p.M ? row : p.M - 1;  // (rows past M are not stored)
+        const __bf16* mp = p.mask16 + z * p.sMask + (long long)row * p.ldm + (colok ? col : 0);
+        mbuf[b][g * RP + rp][0] = __builtin_bit_cast(i16x8, *reinterpret_cast<const bf16x8*>(mp));
+        mbuf[b][g * RP + rp][1] = __builtin_bit_cast(i16x8, *reinterpret_cast<const bf16x8*>(mp + p.pMask));
+      }
+  };
+  if constexpr (MPF) mask_load(0, 0);
 #pragma unroll
   for (int i0 = 0; i0 < TI; i0 += EG) {
     float* tb0 = img + ((i0 / EG) & 1) * EG * 16 * TS;
+    if constexpr (MPF) {
+      if (i0 + EG < TI) mask_load(i0 + EG, ((i0 / EG) + 1) & 1);
+    }
 #pragma unroll
     for (int g = 0; g < EG; ++g) {
       if (i0 + g >= TI) break;
@@ -546,7 +569,12 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
       for (int c = 0; c < 8; ++c) e[c] = fmaxf(e[c] + bias[c], 0.f);
     }
     if (EPI == EPI_RELU_MASK) {
-      if (MASK16 && NP == 2) {  // fp16 planes: x > 0 <=> h > 0 or l > 0 (split2h_dev)
+      if (MPF) {  // the prefetched mask rows
+        const i16x8& mh = mbuf[(i0 / EG) & 1][g * RP + rp][0];
+        const i16x8& ml = mbuf[(i0 / EG) & 1][g * RP + rp][1];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) e[c] = (mh[c] > 0 || ml[c] > 0) ? e[c] : 0.f;
+      } else if (MASK16 && NP == 2) {  // fp16 planes: x > 0 <=> h > 0 or l > 0 (split2h_dev)
         const __bf16* mp = p.mask16 + z * p.sMask + (long long)row * p.ldm + col;
         const i16x8 mh = __builtin_bit_cast(i16x8, *reinterpret_cast<const bf16x8*>(mp));
         const i16x8 ml = __builtin_bit_cast(i16x8, *reinterpret_cast<const bf16x8*>(mp + p.pMask));
