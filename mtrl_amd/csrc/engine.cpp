@@ -1520,6 +1520,7 @@ struct mtsac_engine {
     rows = device_batch ? s_rows : inset[inset_cur].rows;
     if (!ev_rotate) ev_next = 0;
     segs.clear();
+    actor.fin_sink.n = critic.fin_sink.n = 0;  // (a step cut short never leaves deferred finishes behind)
     zstep[0] = zero_ok(actor);
     zstep[1] = zero_ok(critic);
     const float* twp = cfg.use_task_weights ? tw : nullptr;
