@@ -24,6 +24,7 @@ from __future__ import annotations
 import argparse
 import json
 import math
+import re
 import os
 import sys
 import time
@@ -82,7 +83,11 @@ def pmc_traffic(precision, family, workload):
     "workload" key is the default mt50_w2048 run), or None."""
     import glob
 
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
+    def recency(path):  # r<round><letters>_...: rounds in order, then a..z, aa..zz (the naming used here)
+        m = re.match(r"r(\d+)([a-z]*)", os.path.basename(path))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=recency, reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
