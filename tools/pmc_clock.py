@@ -13,28 +13,31 @@ from collections import defaultdict
 
 PEAK_GHZ = 2.4
 FAMILIES = [
-    # (label, kernel-name prefix, flops per launch at S3 (MT50/W2048, B = 6400, E = 2), peak TF)
-    ("hidden forward (split2h)", "gemm_x3f_kernel<208, 1, ", 2 * 6400 * 2048 * 2048 * 2, 2500.0 / 3),
-    ("hidden data grad (split2h)", "gemm_x3f_kernel<208, 2, ", 2 * 6400 * 2048 * 2048 * 2, 2500.0 / 3),
+    # (label, kernel-name prefix, flops per launch and ensemble member at S3 (MT50/W2048, B = 6400), peak TF)
+    ("hidden forward (split2h)", "gemm_x3f_kernel<208, 1, ", 2 * 6400 * 2048 * 2048, 2500.0 / 3),
+    ("hidden data grad (split2h)", "gemm_x3f_kernel<208, 2, ", 2 * 6400 * 2048 * 2048, 2500.0 / 3),
 ]
+TILES_PER_MEMBER = 31 * 8  # 208 x 256 tiles of a 6400 x 2048 output
+WG_THREADS = 512
 
 
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
-    acc = defaultdict(lambda: [0, 0.0, 0.0])  # launches, ns, GRBM_GUI_ACTIVE
+    acc = defaultdict(lambda: [0, 0.0, 0.0, 0])  # launches, ns, GRBM_GUI_ACTIVE, ensemble members
     for r in rows:
         if r["Counter_Name"] != "GRBM_GUI_ACTIVE":
             continue
         k = r["Kernel_Name"]
-        a = acc[k]
+        a = acc[k + "|" + r["Grid_Size"]]
+        a[3] = max(1, round(int(r["Grid_Size"]) / WG_THREADS / TILES_PER_MEMBER))
         a[0] += 1
         a[1] += float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
         a[2] += float(r["Counter_Value"])
     out = []
     for label, pre, flops, peak in FAMILIES:
-        n = ns = cyc = 0.0
+        n = ns = cyc = fl = 0.0
         names = []
-        for k, (c, t, g) in acc.items():
+        for k, (c, t, g, e) in acc.items():
             if pre in k:
                 # the hidden layers only: input-layer launches carry TAG (6th parameter) 8
                 params = k[k.index(pre) + len("gemm_x3f_kernel<"):].split(">")[0].split(", ")
@@ -43,20 +46,22 @@ def main():
                 n += c
                 ns += t
                 cyc += g
-                names.append(k.split("(")[0])
+                fl += c * e * flops
+                names.append(k.split("(")[0] + f" (E = {e})")
         if not n:
             continue
         us = ns / n / 1e3
         ghz = cyc / 8 / ns
-        tf = flops / (us * 1e-6) / 1e12
+        tf = fl / (ns * 1e-9) / 1e12
         out.append(f"{label}: {int(n)} launches, {us:.1f} us, clock {ghz:.3f} GHz, {tf:.0f} TF = "
                    f"{tf / peak:.3f} of the nominal peak, {tf / (peak * ghz / PEAK_GHZ):.3f} of the peak at that clock")
         out.extend("    " + s for s in sorted(set(names)))
     # every kernel above 50 us mean, for context
     out.append("kernels with mean duration > 50 us (profiled pass):")
-    for k, (c, t, g) in sorted(acc.items(), key=lambda kv: -kv[1][1]):
+    for k, (c, t, g, e) in sorted(acc.items(), key=lambda kv: -kv[1][1]):
         if t / c > 50e3:
-            out.append(f"  {t / c / 1e3:8.1f} us  {g / 8 / t:.3f} GHz  x{c:<5d} {k.split('(')[0][:150]}")
+            out.append(f"  {t / c / 1e3:8.1f} us  {g / 8 / t:.3f} GHz  x{c:<5d} grid {k.split('|')[1]:>7s} "
+                       f"{k.split('(')[0][:140]}")
     text = "\n".join(out)
     print(text)
     if len(sys.argv) > 2:
