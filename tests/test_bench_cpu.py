@@ -49,3 +49,22 @@ def test_gpus1_is_single_rank():
 def test_world_size_mismatch_is_an_error():
     p = _run(["--gpus", "2", "--dry-run"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode == 2 and "WORLD_SIZE" in p.stderr
+
+
+def test_pmc_traffic_takes_the_newest_round_summary(tmp_path, monkeypatch):
+    """The roofline's `traffic` comes from the newest committed PMC summary of the workload: rounds in
+    order, then a..z, aa..zz (r5x before r5bb), not plain name order."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    for name, v in (("r4zz", 1.0), ("r5x", 2.0), ("r5bb", 3.0), ("r3final3", 0.5)):
+        (prof / f"{name}_pmc_traffic.json").write_text(json.dumps({"split2h": {"0": {"hbm_bytes_per_launch": v}}}))
+    (prof / "r9_pmc_traffic.json").write_text(json.dumps({"workload": "mt10_w400",
+                                                           "split2h": {"0": {"hbm_bytes_per_launch": 9.0}}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    v, src = bench.pmc_traffic("split2h", 0, "mt50_w2048")
+    assert v == 3.0 and src.endswith("r5bb_pmc_traffic.json")
+    assert bench.pmc_traffic("split2h", 0, "mt10_w400")[0] == 9.0
+    assert bench.pmc_traffic("bf16", 0, "mt50_w2048") == (None, None)
