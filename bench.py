@@ -77,17 +77,39 @@ DRQ_METRIC = "DrQ-eps gradient-steps/sec, experiments/atari.py (26 games, IMPALA
 FP32_VALU_PEAK_TF = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector)
 
 
+def _recency(path):  # r<round><letters>_...: rounds in order, then a..z, aa..zz (the naming used here)
+    m = re.match(r"r(\d+)([a-z]*)", os.path.basename(path))
+    return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+
+def pmc_clock(precision, family, workload):
+    """The shader clock the chip held under a GEMM family in the newest committed clock pass of the
+    default workload (profiles/*_clock.json, tools/pmc_clock.py: GRBM_GUI_ACTIVE / 8 / duration), and
+    the family's fraction of the peak at that clock there; None for other workloads."""
+    import glob
+
+    if workload != "mt50_w2048":
+        return None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_clock.json")), key=_recency, reverse=True):
+        try:
+            with open(path) as f:
+                v = json.load(f).get(precision, {}).get(str(family))
+            if v is not None:
+                return {"clock_ghz": v["clock_ghz"], "frac_nominal": v["frac_nominal"],
+                        "frac_at_clock": v["frac_at_clock"], "source": os.path.relpath(path, ROOT),
+                        "basis": "eager pass under rocprofv3 --pmc GRBM_GUI_ACTIVE; peak x clock / 2.4 GHz"}
+        except (OSError, ValueError, KeyError):
+            continue
+    return None
+
+
 def pmc_traffic(precision, family, workload):
     """HBM bytes per launch of a GEMM family from the committed rocprofv3 PMC summary of THIS
     workload (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py; a file without a
     "workload" key is the default mt50_w2048 run), or None."""
     import glob
 
-    def recency(path):  # r<round><letters>_...: rounds in order, then a..z, aa..zz (the naming used here)
-        m = re.match(r"r(\d+)([a-z]*)", os.path.basename(path))
-        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
-
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=recency, reverse=True):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=_recency, reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
@@ -552,6 +574,7 @@ def main():
                                "timed pass runs without events)" if live
                      else "graph replays carry no events: HIP events per launch in one serialised step",
                      "events_pass_ms_per_step": events_ms,
+                     "clock": pmc_clock(args.precision, dom, args.workload),
                      "solo": {"achieved": (solo[dom][2] / max(solo[dom][1], 1)) / (solo[dom][0] / max(solo[dom][1], 1) * 1e-3) / 1e12
                               if solo[dom][0] else None,
                               "avg_launch_us": 1e3 * solo[dom][0] / max(solo[dom][1], 1),

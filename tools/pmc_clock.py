@@ -6,16 +6,20 @@ family's flops reach -- how much of the gap to the nominal peak is the clock rat
 schedule.
 
 usage: python tools/pmc_clock.py <counter_collection.csv> [out.txt]
+With out.txt, also out.json ({precision: {family: {clock_ghz, frac_nominal, frac_at_clock, ...}}}, the
+split2h families 0 = hidden forward, 1 = hidden data grad), which bench.py quotes in its roofline block.
 """
+import json
 import csv
 import sys
 from collections import defaultdict
 
 PEAK_GHZ = 2.4
 FAMILIES = [
-    # (label, kernel-name prefix, flops per launch and ensemble member at S3 (MT50/W2048, B = 6400), peak TF)
-    ("hidden forward (split2h)", "gemm_x3f_kernel<208, 1, ", 2 * 6400 * 2048 * 2048, 2500.0 / 3),
-    ("hidden data grad (split2h)", "gemm_x3f_kernel<208, 2, ", 2 * 6400 * 2048 * 2048, 2500.0 / 3),
+    # (label, kernel-name prefix, flops per launch and ensemble member at S3 (MT50/W2048, B = 6400), peak TF,
+    #  bench family id)
+    ("hidden forward (split2h)", "gemm_x3f_kernel<208, 1, ", 2 * 6400 * 2048 * 2048, 2500.0 / 3, 0),
+    ("hidden data grad (split2h)", "gemm_x3f_kernel<208, 2, ", 2 * 6400 * 2048 * 2048, 2500.0 / 3, 1),
 ]
 TILES_PER_MEMBER = 31 * 8  # 208 x 256 tiles of a 6400 x 2048 output
 WG_THREADS = 512
@@ -34,7 +38,8 @@ def main():
         a[1] += float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
         a[2] += float(r["Counter_Value"])
     out = []
-    for label, pre, flops, peak in FAMILIES:
+    js = {}
+    for label, pre, flops, peak, fam in FAMILIES:
         n = ns = cyc = fl = 0.0
         names = []
         for k, (c, t, g, e) in acc.items():
@@ -53,6 +58,9 @@ def main():
         us = ns / n / 1e3
         ghz = cyc / 8 / ns
         tf = fl / (ns * 1e-9) / 1e12
+        js[str(fam)] = {"label": label, "launches": int(n), "avg_launch_us": us, "clock_ghz": ghz, "tflops": tf,
+                        "frac_nominal": tf / peak, "frac_at_clock": tf / (peak * ghz / PEAK_GHZ),
+                        "source": "rocprofv3 --pmc GRBM_GUI_ACTIVE (eager pass): clock = GRBM_GUI_ACTIVE / 8 / duration"}
         out.append(f"{label}: {int(n)} launches, {us:.1f} us, clock {ghz:.3f} GHz, {tf:.0f} TF = "
                    f"{tf / peak:.3f} of the nominal peak, {tf / (peak * ghz / PEAK_GHZ):.3f} of the peak at that clock")
         out.extend("    " + s for s in sorted(set(names)))
@@ -66,6 +74,8 @@ def main():
     print(text)
     if len(sys.argv) > 2:
         open(sys.argv[2], "w").write(text + "\n")
+        with open(sys.argv[2].rsplit(".", 1)[0] + ".json", "w") as f:
+            json.dump({"split2h": js}, f, indent=1)
 
 
 if __name__ == "__main__":
