@@ -419,21 +419,24 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(AdamParams ah, AdamPara
   __shared__ float stg[POLYAK ? 64 : 1][65];
   __shared__ double red[4];
   __shared__ float gsh;
-  double acc = 0.0;
+  // the global norm: the trunk's and (unsharded) the heads' |g|^2 partials, both summed by the whole
+  // block in a fixed order (the heads' were summed by one thread, a serial chain of up to 256 loads that
+  // every block of the launch waited for)
+  __shared__ double hred[4];
+  double acc = 0.0, hacc = 0.0;
   for (int i = threadIdx.x; i < f.ng; i += 256) acc += (double)f.gparts[i];
+  if (!f.head_sq)
+    for (int i = threadIdx.x; i < f.nh; i += 256) hacc += (double)f.hparts[i];
   acc = wsumd(acc);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  hacc = wsumd(hacc);
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = acc;
+    hred[threadIdx.x >> 6] = hacc;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double tot = (red[0] + red[1]) + (red[2] + red[3]);
-    float head = 0.f;
-    if (f.head_sq) {
-      head = *f.head_sq;
-    } else {
-      double h = 0.0;
-      for (int i = 0; i < f.nh; ++i) h += (double)f.hparts[i];
-      head = (float)h;
-    }
+    const double tot = (red[0] + red[1]) + (red[2] + red[3]);
+    const float head = f.head_sq ? *f.head_sq : (float)((hred[0] + hred[1]) + (hred[2] + hred[3]));
     gsh = (float)sqrt(tot + (double)head);
   }
   __syncthreads();
