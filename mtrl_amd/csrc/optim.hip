@@ -240,22 +240,59 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamParams a, float max_norm,
 // LDS so the transposed planes leave as 2 x 16 B per lane (16 k of one output row).
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// 64 x 64 tile pass over tiles blk, blk + nblk, ... of tp; returns this thread's |p_new|^2
+// A tile's place and (no Polyak target) its four row groups' operands p, g, m, v, fetched ahead of the
+// update: all of a tile's loads in flight together, the next tile's while this one's transposed planes
+// are written, and a block's first tile's before the global norm is known.  Fetched row group by row
+// group inside the update, each group's loads wait behind the previous group's stores (vmcnt counts
+// stores).  Measured at C1 (`profiles/r5bl_*`): the actor's launch 15.3 -> 13.4 us; the critic's (five
+// operands with the target, fetched the same way) 18.8 -> 22.2 us, so a Polyak network keeps the
+// row-group loads.
+struct TileFetch {
+  int L, e, r0, c0;
+  float4 p[4], g[4], m[4], v[4];
+};
+
+template <bool POLYAK>
+__device__ inline void tile_fetch(const AdamParams& a, const TileParams& tp, int tile, TileFetch& F) {
+  int L = 0;
+  while (L + 1 < tp.n && tile >= tp.leaf[L + 1].tile_begin) ++L;
+  const TileLeaf& lf = tp.leaf[L];
+  int loc = tile - lf.tile_begin;
+  const int per = lf.tiles_r * lf.tiles_c;
+  F.L = L;
+  F.e = loc / per;
+  loc -= F.e * per;
+  F.r0 = 64 * (loc / lf.tiles_c);
+  F.c0 = 64 * (loc % lf.tiles_c);
+  const long long base = lf.off + F.e * lf.ms;
+  const int rr = threadIdx.x >> 4, c4 = 4 * (threadIdx.x & 15);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = F.r0 + rr + 16 * j, c = F.c0 + c4;
+    // outside the leaf: the leaf's first float4, loaded and never used (every load unconditional)
+    const long long i4 = (r < lf.rows && c < lf.cols) ? (base + (long long)r * lf.cols + c) >> 2 : base >> 2;
+    if constexpr (!POLYAK) {
+      F.p[j] = reinterpret_cast<const float4*>(a.p)[i4];
+      if (!a.refresh) {
+        F.g[j] = reinterpret_cast<const float4*>(a.g)[i4];
+        F.m[j] = reinterpret_cast<const float4*>(a.m)[i4];
+        F.v[j] = reinterpret_cast<const float4*>(a.v)[i4];
+      }
+    }
+  }
+}
+
+// 64 x 64 tile pass over tiles blk, blk + nblk, ... of tp (F holds tile blk's fetch when blk < total);
+// returns this thread's |p_new|^2
 template <bool POLYAK>
 __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, const AdamConsts& k, int blk, int nblk,
-                                   float (*sp)[65], float (*stg)[65], float& pmx, float& tmx) {
+                                   float (*sp)[65], float (*stg)[65], float& pmx, float& tmx, TileFetch& F) {
   float acc = 0.f;
   const H2Scales hs = h2_scales(a);
   const int t = threadIdx.x, rr = t >> 4, c4 = 4 * (t & 15);
   for (int tile = blk; tile < tp.total; tile += nblk) {
-    int L = 0;
-    while (L + 1 < tp.n && tile >= tp.leaf[L + 1].tile_begin) ++L;
+    const int L = F.L, e = F.e, r0 = F.r0, c0 = F.c0;
     const TileLeaf& lf = tp.leaf[L];
-    int loc = tile - lf.tile_begin;
-    const int per = lf.tiles_r * lf.tiles_c;
-    const int e = loc / per;
-    loc -= e * per;
-    const int r0 = 64 * (loc / lf.tiles_c), c0 = 64 * (loc % lf.tiles_c);
     const long long base = lf.off + e * lf.ms;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -263,7 +300,7 @@ __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, co
       float4 p = make_float4(0.f, 0.f, 0.f, 0.f), tv = p;
       if (r < lf.rows && c < lf.cols) {
         const long long i4 = (base + (long long)r * lf.cols + c) >> 2;
-        p = reinterpret_cast<float4*>(a.p)[i4];
+        p = POLYAK ? reinterpret_cast<float4*>(a.p)[i4] : F.p[j];
         float* pp = &p.x;
         if (a.refresh) {
 #pragma unroll
@@ -272,8 +309,9 @@ __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, co
             pmx = fmaxf(pmx, fabsf(pp[q]));
           }
         } else {
-          float4 g = reinterpret_cast<const float4*>(a.g)[i4];
-          float4 m = reinterpret_cast<float4*>(a.m)[i4], v = reinterpret_cast<float4*>(a.v)[i4];
+          float4 g = POLYAK ? reinterpret_cast<const float4*>(a.g)[i4] : F.g[j];
+          float4 m = POLYAK ? reinterpret_cast<float4*>(a.m)[i4] : F.m[j];
+          float4 v = POLYAK ? reinterpret_cast<float4*>(a.v)[i4] : F.v[j];
           float* gp = &g.x;
           float* mp = &m.x;
           float* vp = &v.x;
@@ -342,6 +380,7 @@ __device__ inline float adam_tiles(const AdamParams& a, const TileParams& tp, co
         stg[lr_][c4] = tv.x; stg[lr_][c4 + 1] = tv.y; stg[lr_][c4 + 2] = tv.z; stg[lr_][c4 + 3] = tv.w;
       }
     }
+    if (tile + nblk < tp.total) tile_fetch<POLYAK>(a, tp, tile + nblk, F);  // F's registers are free now
     __syncthreads();
     {  // transposed planes: output row o (a column of the leaf), k = r0 + 16 (t & 3) .. + 15
       const int oc = t >> 2, kq = 16 * (t & 3);
@@ -400,10 +439,12 @@ template <bool POLYAK>
 __global__ __launch_bounds__(256) void adam_tiles_kernel(AdamParams a, TileParams tp, float max_norm) {
   __shared__ float sp[64][65];
   __shared__ float stg[POLYAK ? 64 : 1][65];
+  TileFetch F;
+  if ((int)blockIdx.x < tp.total) tile_fetch<POLYAK>(a, tp, blockIdx.x, F);
   const OptScalars sc = *a.sc;
   const AdamConsts k = adam_consts(a, sc.gnorm, sc.count, max_norm);
   float pmx = 0.f, tmx = 0.f;
-  float acc = adam_tiles<POLYAK>(a, tp, k, blockIdx.x, gridDim.x, sp, stg, pmx, tmx);
+  float acc = adam_tiles<POLYAK>(a, tp, k, blockIdx.x, gridDim.x, sp, stg, pmx, tmx, F);
   acc = block_sum256(acc);
   if (threadIdx.x == 0) a.p_partials[blockIdx.x] = acc;
 }
@@ -423,6 +464,10 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(AdamParams ah, AdamPara
   // block in a fixed order (the heads' were summed by one thread, a serial chain of up to 256 loads that
   // every block of the launch waited for)
   __shared__ double hred[4];
+  // a tile block's first tile is fetched before the norm's partials: both round trips overlap
+  const int b = blockIdx.x, tb = b - f.bh - f.bt;
+  TileFetch F;
+  if (tb >= 0 && tb < tp.total) tile_fetch<POLYAK>(at, tp, tb, F);
   double acc = 0.0, hacc = 0.0;
   for (int i = threadIdx.x; i < f.ng; i += 256) acc += (double)f.gparts[i];
   if (!f.head_sq)
@@ -443,14 +488,12 @@ __global__ __launch_bounds__(256) void adam_fused_kernel(AdamParams ah, AdamPara
   const float gn = gsh;
   const int count = ah.sc->count;  // incremented by the sum-of-squares launch
   float pa = 0.f, pmx = 0.f, tmx = 0.f;
-  const int b = blockIdx.x;
   if (b < f.bh) {
     pa = adam_elems<POLYAK>(ah, adam_consts(ah, gn, count, f.max_norm), 0, b, f.bh, pmx, tmx);
   } else if (b < f.bh + f.bt) {
     pa = adam_elems<POLYAK>(at, adam_consts(at, gn, count, f.max_norm), 0, b - f.bh, f.bt, pmx, tmx);
   } else {
-    pa = adam_tiles<POLYAK>(at, tp, adam_consts(at, gn, count, f.max_norm), b - f.bh - f.bt, f.btile, sp, stg, pmx,
-                            tmx);
+    pa = adam_tiles<POLYAK>(at, tp, adam_consts(at, gn, count, f.max_norm), tb, f.btile, sp, stg, pmx, tmx, F);
   }
   pa = block_sum256(pa);
   if (threadIdx.x == 0) {
