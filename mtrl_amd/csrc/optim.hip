@@ -603,6 +603,7 @@ __device__ void alpha_tasks(const AlphaParams& a, int wave, int nw) {
   for (int tg0 = wave; tg0 < a.T_glob; tg0 += U * nw) {
     int tl[U], n[U];
     bool ok[U];
+    float la[U];  // log_alpha of the tasks, loaded beside the counts (read after the sums)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int t = tg0 + u * nw - a.task_begin;
@@ -610,23 +611,35 @@ __device__ void alpha_tasks(const AlphaParams& a, int wave, int nw) {
       tl[u] = ok[u] ? t : 0;
       const int c = a.counts[tl[u]];
       n[u] = ok[u] ? c : 0;
+      la[u] = a.log_alpha[min(tg0 + u * nw, a.T_glob - 1)];
     }
     int nmax = 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) nmax = max(nmax, n[u]);  // wave-uniform
     float s[U] = {0.f, 0.f, 0.f, 0.f};
-    for (int j0 = 0; j0 < nmax; j0 += 64) {
-      const int j = j0 + lane;
-      int r[U];
+    // two 64-row chunks a pass (all their loads in flight together), added chunk by chunk in row order
+    // as one chunk a pass did; rows past a task's count add +0 (s is never -0, so that is exact)
+    for (int j0 = 0; j0 < nmax; j0 += 128) {
+      int r[2][U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int rr = a.rows[(long long)tl[u] * a.max_rows + min(j, a.max_rows - 1)];
-        r[u] = j < n[u] ? rr : 0;
+      for (int h = 0; h < 2; ++h) {
+        const int j = j0 + 64 * h + lane;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int rr = a.rows[(long long)tl[u] * a.max_rows + min(j, a.max_rows - 1)];
+          r[h][u] = j < n[u] ? rr : 0;
+        }
       }
+      float lp[2][U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const float lp = a.logpi[r[u]];
-        s[u] += j < n[u] ? lp + a.target_entropy : 0.f;
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int u = 0; u < U; ++u) lp[h][u] = a.logpi[r[h][u]];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = j0 + 64 * h + lane;
+#pragma unroll
+        for (int u = 0; u < U; ++u) s[u] += j < n[u] ? lp[h][u] + a.target_entropy : 0.f;
       }
     }
 #pragma unroll
@@ -637,7 +650,7 @@ __device__ void alpha_tasks(const AlphaParams& a, int wave, int nw) {
         const int tg = tg0 + u * nw;
         if (tg >= a.T_glob) continue;
         a.grad[tg] = ok[u] ? -s[u] / (float)a.B_glob : 0.f;
-        a.task_loss[tg] = ok[u] ? -a.log_alpha[tg] * s[u] : 0.f;
+        a.task_loss[tg] = ok[u] ? -la[u] * s[u] : 0.f;
       }
     }
   }
@@ -657,27 +670,50 @@ __device__ void alpha_grad_block(const AlphaParams& a) {
 
 __global__ __launch_bounds__(1024) void alpha_grad_kernel(AlphaParams a) { alpha_grad_block(a); }
 
-// temperature Adam (optax clip_by_global_norm + adam over log_alpha); one wave
-__device__ void alpha_adam_wave(const AlphaParams& a, float lr, float b1, float b2, float eps, float max_norm) {
+// temperature Adam (optax clip_by_global_norm + adam over log_alpha); one wave.  Returns the alpha log
+// sum(exp(log_alpha_new)) (wave-uniform).  Up to 64 tasks: one task a lane, every operand loaded at
+// once (the strided loops' loads were waited for loop by loop); the same sums, so the same bits.
+__device__ float alpha_adam_wave(const AlphaParams& a, float lr, float b1, float b2, float eps, float max_norm) {
   const int lane = threadIdx.x & 63;
-  float sq = 0.f;
-  for (int i = lane; i < a.T_glob; i += 64) sq += a.grad[i] * a.grad[i];
-  const float gn = sqrtf(wsumf(sq));
-  const bool clip = (max_norm >= 0.f) && !(gn < max_norm);
   const int count = a.sc->count + 1;
   const float bc1 = 1.0f - powf(b1, (float)count), bc2 = 1.0f - powf(b2, (float)count);
-  float es = 0.f;
-  for (int i = lane; i < a.T_glob; i += 64) {
-    float g = a.grad[i];
+  float gn, es = 0.f;
+  bool clip;
+  if (a.T_glob <= 64) {
+    const int i = min(lane, a.T_glob - 1);
+    const bool in = lane < a.T_glob;
+    const float g0 = a.grad[i], m0 = a.m[i], v0 = a.v[i], p0 = a.log_alpha[i];
+    gn = sqrtf(wsumf(in ? 0.f + g0 * g0 : 0.f));
+    clip = (max_norm >= 0.f) && !(gn < max_norm);
+    float g = g0;
     if (clip) g = (g / gn) * max_norm;
-    const float m = (1.0f - b1) * g + b1 * a.m[i];
-    const float v = (1.0f - b2) * (g * g) + b2 * a.v[i];
-    a.m[i] = m;
-    a.v[i] = v;
+    const float m = (1.0f - b1) * g + b1 * m0;
+    const float v = (1.0f - b2) * (g * g) + b2 * v0;
     const float u = (m / bc1) / (sqrtf(v / bc2) + eps);
-    const float p = a.log_alpha[i] + u * (-lr);
-    a.log_alpha[i] = p;
-    es += expf(p);
+    const float p = p0 + u * (-lr);
+    if (in) {
+      a.m[i] = m;
+      a.v[i] = v;
+      a.log_alpha[i] = p;
+    }
+    es = in ? 0.f + expf(p) : 0.f;
+  } else {
+    float sq = 0.f;
+    for (int i = lane; i < a.T_glob; i += 64) sq += a.grad[i] * a.grad[i];
+    gn = sqrtf(wsumf(sq));
+    clip = (max_norm >= 0.f) && !(gn < max_norm);
+    for (int i = lane; i < a.T_glob; i += 64) {
+      float g = a.grad[i];
+      if (clip) g = (g / gn) * max_norm;
+      const float m = (1.0f - b1) * g + b1 * a.m[i];
+      const float v = (1.0f - b2) * (g * g) + b2 * a.v[i];
+      a.m[i] = m;
+      a.v[i] = v;
+      const float u = (m / bc1) / (sqrtf(v / bc2) + eps);
+      const float p = a.log_alpha[i] + u * (-lr);
+      a.log_alpha[i] = p;
+      es += expf(p);
+    }
   }
   es = wsumf(es);
   if (lane == 0) {
@@ -685,25 +721,18 @@ __device__ void alpha_adam_wave(const AlphaParams& a, float lr, float b1, float 
     a.sc->gnorm = gn;
     a.sc->pnorm = es;  // alpha log: sum(exp(log_alpha))  (mtsac.py:730)
   }
+  return es;
 }
 
-// wave 0: the alpha log summed lane-strided (the loads in flight together), then lane 0 writes
-__device__ void write_logs_wave(const LogParams& p) {
-  float s = 0.f;
-  for (int i = threadIdx.x; i < p.T_glob; i += 64) s += expf(p.log_alpha[i]);
-  s = wsumf(s);
-  if (threadIdx.x != 0) return;
-  p.logs[0] = p.critic_sums[1] * p.inv_critic;  // losses/qf_values
-  p.logs[1] = p.critic_sums[0] * p.inv_critic;  // losses/qf_loss
-  p.logs[2] = p.critic->gnorm;              // metrics/critic_grad_magnitude
-  p.logs[3] = p.critic->pnorm;              // metrics/critic_params_norm
-  p.logs[4] = p.actor_sums[0] * p.inv_actor;    // losses/actor_loss
-  p.logs[5] = p.actor->gnorm;               // metrics/actor_grad_magnitude
-  p.logs[6] = p.actor->pnorm;               // metrics/actor_params_norm
-  p.logs[7] = 0.0f;                         // metrics/explore_loss (explore=False, mtsac.py:277)
-  p.logs[8] = *p.alpha_loss_sum * p.inv_b;  // losses/alpha_loss
-  p.logs[9] = s;                            // alpha
-}
+// wave 0: the logs.  Values this launch produced come in as arguments (the alpha log sum, and when the
+// log's source is this launch's output, the row sums, the alpha loss and the parameter norms); the rest
+// are loaded (sharded runs reduce some elsewhere).  One store -> load round trip less per value.
+struct LogLocal {
+  float alpha_sum;
+  float rows[3];        // valid where f.rows[k]
+  float alpha_loss;     // valid with f.alpha_grad
+  float pnorm[2];       // critic, actor
+};
 
 // the step's scalar tail in one block, its independent reductions side by side before ONE barrier:
 // waves 0-7 the temperature gradient's per-task sums (unsharded), waves 8-15 the loss row sums (three
@@ -714,6 +743,14 @@ __global__ __launch_bounds__(1024) void step_finish_kernel(StepFinish f) {
   __shared__ double s[48];  // [8 k + w] row sum k of wave 8 + w; [24 + 2 w + {0,1}] trunk / head |p|^2 of wave 8 + w
   __shared__ float wm[3][8][2];  // split2h: [job][wave 8 + w][heads, trunk] partial weight maxima
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave 0's inputs from earlier launches (the gradient norms, the step counter), loaded up front
+  unsigned long long cnt = 0;
+  float cgn = 0.f, agn = 0.f;
+  if (wave == 0) {
+    cnt = *f.counter;
+    cgn = f.logs.critic->gnorm;
+    agn = f.logs.actor->gnorm;
+  }
   if (wave < 8) {
     if (f.alpha_grad) alpha_tasks(f.alpha, wave, 8);
   } else {
@@ -763,10 +800,12 @@ __global__ __launch_bounds__(1024) void step_finish_kernel(StepFinish f) {
   __syncthreads();
   if (wave != 0) return;
   const AlphaParams& a = f.alpha;
+  LogLocal loc{};
   if (f.alpha_grad) {  // the alpha loss: the per-task terms in task order
     float sl = 0.f;
     for (int t = lane; t < a.T_glob; t += 64) sl += a.task_loss[t];
     sl = wsumf(sl);
+    loc.alpha_loss = sl;
     if (lane == 0) *a.loss_part = sl;
   }
   if (lane == 0) {
@@ -775,7 +814,8 @@ __global__ __launch_bounds__(1024) void step_finish_kernel(StepFinish f) {
       if (!f.rows[k]) continue;
       double t = 0.0;
       for (int w = 0; w < 8; ++w) t += s[8 * k + w];
-      *f.row_out[k] = (float)t;
+      loc.rows[k] = (float)t;
+      *f.row_out[k] = loc.rows[k];
     }
     for (int n = 0; n < 2; ++n) {
       double tt = 0.0, hh = 0.0;
@@ -784,13 +824,40 @@ __global__ __launch_bounds__(1024) void step_finish_kernel(StepFinish f) {
         hh += s[24 + 2 * w + 1];
       }
       const float hs = f.head_sq ? f.head_sq[n] : (float)hh;
-      f.pn.sc[n]->pnorm = sqrtf((float)tt + hs);
+      loc.pnorm[n] = sqrtf((float)tt + hs);
+      f.pn.sc[n]->pnorm = loc.pnorm[n];
     }
   }
-  alpha_adam_wave(f.alpha, f.lr, f.b1, f.b2, f.eps, f.max_norm);
-  __threadfence_block();  // lane 0's scalars above, before the log reads
-  write_logs_wave(f.logs);
-  if (lane == 0) *f.counter += 1ull;
+  loc.alpha_sum = alpha_adam_wave(f.alpha, f.lr, f.b1, f.b2, f.eps, f.max_norm);
+  // the logs: a value this launch produced is taken from registers when the log's source is where it
+  // was stored (the engine's layout); anything else is loaded after a fence
+  const LogParams& p = f.logs;
+  const bool own_c0 = f.rows[0] && p.critic_sums == f.row_out[0];
+  const bool own_c1 = f.rows[1] && p.critic_sums + 1 == f.row_out[1];
+  const bool own_a = f.rows[2] && p.actor_sums == f.row_out[2];
+  const bool own_al = f.alpha_grad && p.alpha_loss_sum == a.loss_part;
+  const bool own_pn = f.pn.sc[0] == p.critic && f.pn.sc[1] == p.actor;
+  const bool own_ls = p.log_alpha == a.log_alpha && p.T_glob == a.T_glob;
+  if (!(own_c0 && own_c1 && own_a && own_al && own_pn && own_ls)) __threadfence_block();
+  float ls = loc.alpha_sum;
+  if (!own_ls) {  // wave 0: the alpha log summed lane-strided (the loads in flight together)
+    float s2 = 0.f;
+    for (int i = lane; i < p.T_glob; i += 64) s2 += expf(p.log_alpha[i]);
+    ls = wsumf(s2);
+  }
+  if (lane == 0) {
+    p.logs[0] = (own_c1 ? loc.rows[1] : p.critic_sums[1]) * p.inv_critic;  // losses/qf_values
+    p.logs[1] = (own_c0 ? loc.rows[0] : p.critic_sums[0]) * p.inv_critic;  // losses/qf_loss
+    p.logs[2] = cgn;                                                          // metrics/critic_grad_magnitude
+    p.logs[3] = own_pn ? loc.pnorm[0] : p.critic->pnorm;                      // metrics/critic_params_norm
+    p.logs[4] = (own_a ? loc.rows[2] : p.actor_sums[0]) * p.inv_actor;      // losses/actor_loss
+    p.logs[5] = agn;                                                          // metrics/actor_grad_magnitude
+    p.logs[6] = own_pn ? loc.pnorm[1] : p.actor->pnorm;                       // metrics/actor_params_norm
+    p.logs[7] = 0.0f;  // metrics/explore_loss (explore=False, mtsac.py:277)
+    p.logs[8] = (own_al ? loc.alpha_loss : *p.alpha_loss_sum) * p.inv_b;      // losses/alpha_loss
+    p.logs[9] = ls;                                                           // alpha
+    *f.counter = cnt + 1ull;
+  }
   // split2h: the optimizer's per-block weight maxima into the weight records (the next update's bound)
   for (int j = 0; j < f.nwmax; ++j) {
     const WeightMaxJob& w = f.wmax[j];
