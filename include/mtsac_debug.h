@@ -89,6 +89,10 @@ int mtsac_debug_check_guards(struct mtsac_engine* engine);
  * gradient head leaves.  count must equal the buffer's float count. */
 int mtsac_debug_snapshot(struct mtsac_engine* engine, int32_t on);
 int mtsac_debug_read(struct mtsac_engine* engine, int32_t id, float* dst, int64_t count);
+/* the head backward's LDS self-check, tested: the last step's actor head weight pass re-run into a
+   scratch output with one cross-wave LDS slot corrupted on purpose; the next mtsac_get_logs /
+   mtsac_synchronize must fail (-5, "head backward self-check failed").  Needs a step first. */
+int mtsac_debug_head_selfcheck(struct mtsac_engine* engine);
 /* Weight planes in the fragment layout (gemm_x3f B operand, engine.cpp Net::bfrag): mode -1 (the
  * default) decides by shape (MTSAC_BFRAG=0 turns it off), 0 / 1 forces it off / allows it, for
  * engines created afterwards.  mtsac_debug_bfrag: bit i actor layer i, bit 8 + i critic layer i. */

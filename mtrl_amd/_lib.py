@@ -161,6 +161,7 @@ SIGNATURES = {
     "mtsac_debug_check_guards": (ctypes.c_int, [P]),
     "mtsac_debug_snapshot": (ctypes.c_int, [P, ctypes.c_int32]),
     "mtsac_debug_read": (ctypes.c_int, [P, ctypes.c_int32, P, ctypes.c_int64]),
+    "mtsac_debug_head_selfcheck": (ctypes.c_int, [P]),
     "mtsac_debug_set_bfrag": (ctypes.c_int, [ctypes.c_int32]),
     "mtsac_debug_bfrag": (ctypes.c_int, [P]),
     "mtsac_debug_force_one_stream": (ctypes.c_int, [P, ctypes.c_int32]),

@@ -69,8 +69,9 @@ class NpzCheckpointManager:
         if buffer is not None:
             ck = buffer.checkpoint()
             arrays.update({f"buffer/{k}": np.asarray(v) for k, v in ck["data"].items()})
-            st = ck["rng_state"]
-            arrays["buffer/rng"] = np.array(json.dumps({**st, "state": {k: str(v) for k, v in st["state"].items()}}))
+            st = ck["rng_state"]  # None (the reference's numpy 2.2 value) or a bit_generator.state dict
+            arrays["buffer/rng"] = np.array(json.dumps(
+                None if st is None else {**st, "state": {k: str(v) for k, v in st["state"].items()}}))
         arrays["metadata"] = np.array(json.dumps(metadata or {}))
         arrays["metrics"] = np.array(json.dumps(metrics or {}))
         arrays.update(_rng_arrays(agent))
@@ -84,7 +85,8 @@ class NpzCheckpointManager:
         buf_ckpt = None
         if buffer is not None and "buffer/obs" in z.files:
             st = json.loads(str(z["buffer/rng"]))
-            st["state"] = {k: int(v) for k, v in st["state"].items()}
+            if st is not None:
+                st["state"] = {k: int(v) for k, v in st["state"].items()}
             buf_ckpt = {"data": {k[len("buffer/"):]: z[k] for k in z.files if k.startswith("buffer/") and k != "buffer/rng"},
                         "rng_state": st}
             buf_ckpt["data"]["pos"] = int(buf_ckpt["data"]["pos"])

@@ -15,6 +15,14 @@ from ..types import ReplayBufferSamples
 
 
 class MultiTaskReplayBuffer:
+    # checkpoint()'s "rng_state": the reference stores self._rng.__getstate__() (buffers.py:323), which
+    # numpy 2.2 (the pinned 2.2.4) returns as None -- its resumed runs restart the index stream from the
+    # fresh default_rng(seed).  False (default): write None too, so a resumed run draws the reference's
+    # indices bit for bit.  True: write the device stream's bit_generator.state dict (numpy's own
+    # Generator.__setstate__ accepts it as well), so a resumed run continues the interrupted stream --
+    # the uninterrupted run's indices, NOT the reference's ("Checkpoints").
+    persist_rng_state: bool = False
+
     def __init__(self, total_capacity: int, num_tasks: int, env_obs_space=None, env_action_space=None,
                  seed: int | None = None, max_steps: int = 500, normalize_rewards: bool = False,
                  reward_norm_eps: float = 1e-8, reward_filter=None, sigma=None, alpha=None, delta=None,
@@ -116,7 +124,7 @@ class MultiTaskReplayBuffer:
             "data": {"obs": obs, "actions": act, "rewards": rew[..., None], "next_obs": nobs,
                      "dones": done[..., None], "pos": pos, "full": full,
                      "returns_min": self._returns_min.copy(), "returns_max": self._returns_max.copy()},
-            "rng_state": self.engine.get_rng_state(),
+            "rng_state": self.engine.get_rng_state() if self.persist_rng_state else None,
         }
 
     def load_checkpoint(self, ckpt: dict) -> None:
@@ -136,5 +144,8 @@ class MultiTaskReplayBuffer:
                                  np.asarray(d["actions"]).reshape(-1, d["actions"].shape[-1]),
                                  np.asarray(d["rewards"]).reshape(-1), np.asarray(d["dones"]).reshape(-1))
         self.engine.set_buffer_state(int(d["pos"]), bool(d["full"]))
-        self.engine.set_rng_state(ckpt["rng_state"])
+        # buffers.py:335, numpy 2.2 Generator.__setstate__: None leaves the stream (seeded by __init__
+        # like the reference's fresh default_rng(seed)); a bit_generator.state dict sets it
+        if ckpt["rng_state"] is not None:
+            self.engine.set_rng_state(ckpt["rng_state"])
         assert T == self.num_tasks

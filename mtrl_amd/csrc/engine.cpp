@@ -457,6 +457,17 @@ struct mtsac_engine {
   size_t tl_next = 0;
   std::vector<void*> allocs;
   float* dbg_snap[2] = {};  // mtsac_debug_snapshot: ha[top] after the actor forward (0) and after the actor-loss pass (1)
+  bool snap_on = false;     // the steps copy into dbg_snap (the buffers stay allocated while off)
+  float* dbg_hw = nullptr;  // mtsac_debug_head_selfcheck's scratch head gradient
+  // the gemm_x3p geometry (mtsac_debug_x3p_geo) the split-K workspaces (ws_lane, ws_wg) were sized for:
+  // a later change could need more slab space than they hold, so the step entry points refuse it
+  int geo_at_create = -1;
+  int geo_guard() const {
+    if (g_x3p_geo == geo_at_create) return 0;
+    return fail(-16, "the gemm_x3p geometry changed after this engine was created (mtsac_debug_x3p_geo " +
+                         std::to_string(geo_at_create) + " -> " + std::to_string(g_x3p_geo) +
+                         "): its split-K workspaces were sized for the old one; restore it or create a new engine");
+  }
 
   ~mtsac_engine() {
     if (gexec) (void)hipGraphExecDestroy(gexec);
@@ -858,8 +869,11 @@ struct mtsac_engine {
   // after every write of params: Net::wt[which] (fp32) or the planes wp[which] (split3);
   // fused: the optimizer already wrote them (see optimize())
   // the optimizer writes the transposed head kernel itself (AdamParams::whT) when its leaf is float4-aligned
+  // (one predicate for both sides of the hand-off: refresh_wt skips head_transpose exactly when
+  // optimize() gives the head pass AdamParams::whT, whose range must lie inside the heads' part)
   bool whT_fused(const Net& net) const {
-    return net.whT && net.E == 1 && net.off_hW % 4 == 0 && ((long long)T_l * net.width * net.hd) % 4 == 0;
+    const long long n = (long long)T_l * net.width * net.hd;
+    return net.whT && net.E == 1 && net.off_hW % 4 == 0 && n % 4 == 0 && net.off_hW + n <= net.trunk_off;
   }
   void refresh_wt(Net& net, const float* params, int which, hipStream_t s, bool fused = false) {
     if (which == 0 && net.whT && net.E == 1 && !(fused && whT_fused(net)))
@@ -1068,11 +1082,7 @@ struct mtsac_engine {
     hp.sWh = net.ms_hW;
     hp.sbh = net.ms_hb;
     hp.sh = (long long)M * net.width;
-    static const int dbg = [] {
-      const char* e = getenv("MTSAC_DBG_HEAD");
-      return e ? atoi(e) : 0;
-    }();
-    hp.dbg = dbg;
+    hp.fault = reinterpret_cast<unsigned*>(err + 1);  // err[1]: the head backward self-check word (check_err)
     return hp;
   }
 
@@ -1312,7 +1322,7 @@ struct mtsac_engine {
       a.h2.tparts = polyak ? tparts : nullptr;
     }
     a.n = net.trunk_off;  // heads
-    if (whT_fused(net) && net.off_hW + (long long)T_l * net.width * net.hd <= net.trunk_off) {
+    if (whT_fused(net)) {
       a.whT = net.whT;
       a.whT_b4 = net.off_hW / 4;
       a.whT_e4 = (net.off_hW + (long long)T_l * net.width * net.hd) / 4;
@@ -1627,7 +1637,7 @@ struct mtsac_engine {
       qn.ap_rec = q.ap_rec;
       qn.logpi = logpi_n;
       policy_head_pair(q, qn, cur);
-      if (dbg_snap[0])
+      if (snap_on)
         (void)hipMemcpyAsync(dbg_snap[0], ha[actor.depth - 1], sizeof(float) * Ma * actor.width,
                              hipMemcpyDeviceToDevice, cur);
     });
@@ -1733,7 +1743,7 @@ struct mtsac_engine {
         ag.dout_parts = &r_dout.n;
       }
       action_grad(ag, cur);
-      if (dbg_snap[1])
+      if (snap_on)
         (void)hipMemcpyAsync(dbg_snap[1], ha[actor.depth - 1], sizeof(float) * Ma * actor.width,
                              hipMemcpyDeviceToDevice, cur);
       if (sharded()) {
@@ -2124,15 +2134,20 @@ struct mtsac_engine {
       comm_error.clear();
       return fail(-5, m);
     }
-    int e = 0;
-    HIP_TRY(hipMemcpyAsync(&e, err, sizeof(int), hipMemcpyDeviceToHost, st));
+    int e[2] = {0, 0};  // [0] the batch check, [1] the head backward's self-check bits (HEAD_FAULT_*)
+    HIP_TRY(hipMemcpyAsync(e, err, sizeof(e), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (e) {
-      int z = 0;
-      HIP_TRY(hipMemcpy(err, &z, sizeof(int), hipMemcpyHostToDevice));
+    if (e[0] || e[1]) {
+      const int z[2] = {0, 0};
+      HIP_TRY(hipMemcpy(err, z, sizeof(z), hipMemcpyHostToDevice));
+    }
+    if (e[1])
+      return fail(-5, std::string("head backward self-check failed (bits ") + std::to_string(e[1]) +
+                          "): a cross-wave LDS reduction slot held other bits than its writer stored, so this "
+                          "step's head gradients are not trustworthy (DESIGN.md section 5)");
+    if (e[0])
       return fail(-22,
                   "batch rows must end in an exact one-hot task id owned by this engine (obs and next_obs agree)");
-    }
     return 0;
   }
 };
@@ -2219,6 +2234,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   if (he != hipSuccess) return fail(-19, std::string("hipSetDevice: ") + hipGetErrorString(he));
 
   auto* e = new mtsac_engine();
+  e->geo_at_create = g_x3p_geo;
   e->cfg = c;
   e->device = hip_device;
   e->T_l = c.task_count;
@@ -2376,8 +2392,9 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
       }
     for (float*& w : e->ws_lane)
       if ((rc = e->alloc(&w, (size_t)std::max(ws, 1LL)))) return bad(rc);
-    if (e->planes)  // the deferred weight-grad finishes' slabs, per layer (Net::fin_sink)
-      for (Net* net : {&e->actor, &e->critic})
+    if (e->planes && e->defer_finish())  // the deferred weight-grad finishes' slabs, per layer (Net::fin_sink);
+      for (Net* net : {&e->actor, &e->critic})  // not with MTSAC_DEFER_FINISH=0 (sharded runs never use them either,
+                                                 // but sharding is set after create)
         for (int i = 0; i < net->depth; ++i) {
           const long long w = gemm_x3p_ws_floats(i == 0 ? net->in_dim : net->width, net->width, (int)net->krows,
                                                  net->E, true);
@@ -2484,7 +2501,7 @@ int mtsac_create(const mtsac_config* cfg, int hip_device, mtsac_engine** out) {
   if ((rc = e->alloc(&e->sc_alpha, 1))) return bad(rc);
   if ((rc = e->alloc(&e->logs, MTSAC_NUM_LOGS))) return bad(rc);
   if ((rc = e->alloc(&e->counter, 1))) return bad(rc);
-  if ((rc = e->alloc(&e->err, 1))) return bad(rc);
+  if ((rc = e->alloc(&e->err, 2))) return bad(rc);  // [0] batch check, [1] self-check
   // rollout workspace
   const int rm = e->roll_max;
   if ((rc = e->alloc(&e->r_obs, (size_t)rm * e->D))) return bad(rc);
@@ -2880,6 +2897,7 @@ int mtsac_sample(mtsac_engine* h, int64_t* indices, float* obs, float* actions, 
 // ---------------------------------------------------------------- update
 int mtsac_update(mtsac_engine* h, const mtsac_batch* b, const float* eps_next, const float* eps_cur) {
   if (!h) return fail(-22, "null engine");
+  if (int rc = h->geo_guard()) return rc;
   if ((eps_next == nullptr) != (eps_cur == nullptr)) return fail(-22, "inject both eps_next and eps_cur or neither");
   const int B = h->B, D = h->D, A = h->A;
   if (b) {
@@ -2912,6 +2930,7 @@ static int task_grad_ready(mtsac_engine* h, int which) {
 
 int mtsac_task_gradients(mtsac_engine* h, const mtsac_batch* b, const float* eps_next, const float* eps_cur) {
   if (!h) return fail(-22, "null engine");
+  if (int rc = h->geo_guard()) return rc;
   if (h->T_l != h->T_g) return fail(-95, "per-task gradients need every task on one engine (unsharded)");
   if ((eps_next == nullptr) != (eps_cur == nullptr)) return fail(-22, "inject both eps_next and eps_cur or neither");
   int rc = h->ensure_task_grad_buffers();
@@ -3018,6 +3037,7 @@ int mtsac_task_gradient_stats(mtsac_engine* h, int which, const float* threshold
 
 int mtsac_update_many(mtsac_engine* h, int32_t steps) {
   if (!h) return fail(-22, "null engine");
+  if (int rc = h->geo_guard()) return rc;
   if (steps <= 0) return 0;
   if (!h->use_graph || h->timing || h->hook || h->chook) {  // events / host hooks need eager issue
     h->tl_next = 0;  // timing records every launch of this call
@@ -3403,10 +3423,26 @@ int mtsac_debug_check_guards(mtsac_engine* h) {
 // 3 the actor head's output gradient dout ([B][2A]), 4 the actor gradient's head leaves.
 int mtsac_debug_snapshot(mtsac_engine* h, int32_t on) {
   if (!h) return fail(-22, "null engine");
-  if (on && !h->dbg_snap[0])
+  if (on && !h->dbg_snap[0])  // allocated once, reused when snapshots are turned on again (freed with the engine)
     for (float*& q : h->dbg_snap)
       if (int rc = h->alloc(&q, (size_t)h->Ma * h->actor.width)) return rc;
-  if (!on) h->dbg_snap[0] = h->dbg_snap[1] = nullptr;  // freed with the engine
+  h->snap_on = on != 0;
+  return 0;
+}
+
+// The head backward's LDS self-check, tested: re-run the actor head's weight pass of the last step on
+// its own buffers with one cross-wave LDS slot corrupted on purpose, into a scratch output (the
+// gradients are untouched); the engine's next check_err (mtsac_get_logs / mtsac_synchronize) must then
+// report HEAD_FAULT_WGRAD.  Needs a step first (the row lists and dout of the last step).
+int mtsac_debug_head_selfcheck(mtsac_engine* h) {
+  if (!h) return fail(-22, "null engine");
+  if (h->actor.hd != 8 || h->actor.width % 4 != 0 || h->counts == nullptr) return fail(-95, "needs hd 8, W % 4 == 0 and a step");
+  if (!h->dbg_hw)
+    if (int rc = h->alloc(&h->dbg_hw, (size_t)h->T_l * h->actor.width * 8 + (size_t)h->T_l * 8)) return rc;
+  const HeadParams ahp = h->head(h->actor, h->actor.p, h->ha[h->actor.depth - 1], h->B, h->task);
+  head_backward_weight_inject(ahp, h->dout_a, 0, h->counts, h->rows, h->B, h->T_l, h->dbg_hw,
+                              h->dbg_hw + (size_t)h->T_l * h->actor.width * 8, h->st);
+  HIP_TRY(hipGetLastError());
   return 0;
 }
 

@@ -368,8 +368,8 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
   const bool colok = col < p.N;  // N % 8 == 0: a lane's 8 columns are all in or all out
   const long long slab = (long long)p.M * p.N;
   const float* ws_z = FIN ? p.ws + (long long)z * nsplit * slab : nullptr;
-  // FIN, two slices ("pair"): the ticket comes FIRST.  The slice drawing 0 publishes its (unscaled)
-  // partial in its slab with write-through (sc1) stores, drains them, and signals by adding 2 to the
+  // FIN, two slices ("pair"): the ticket comes FIRST.  The slice drawing 0 publishes its partial
+  // ALREADY multiplied by unscale = 2^-(eA + eB) (write_slab; true magnitude, not MFMA-scale) in its slab with write-through (sc1) stores, drains them, and signals by adding 2 to the
   // tile's counter; the slice drawing 1 (or 3: the partial is already published) polls the counter
   // until it reads 4, re-arms it, and finishes the tile from its own registers plus the other slab,
   // read with sc1 loads (the hand-off of MI355X_MICROARCH.md's table, row 1: no acquire needed).  One
@@ -537,7 +537,8 @@ __global__ __launch_bounds__(64 * WV, 1) void gemm_x3f_kernel(SplitGemmParams p)
     if (row >= p.M || !colok) continue;
     if ((ABL & 128) && p.M > 0) continue;  // ablation: no epilogue stores (p.M > 0 keeps the MFMAs live)
     float e[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-    if constexpr (NP == 2) {  // FIN: the slabs hold unscaled partials too (pair: s0 + s1 commutes)
+    if constexpr (NP == 2) {  // FIN: scale this slice's registers by unscale, as the slab's partial already is
+                              // (write_slab applied it; pair: s0 + s1 commutes)
 #pragma unroll
       for (int c = 0; c < 8; ++c) e[c] *= unscale;
     }

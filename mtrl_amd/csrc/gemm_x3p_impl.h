@@ -40,8 +40,10 @@ typedef __attribute__((address_space(3))) void lds_void;
 // builtin makes the compiler drain every outstanding ds_read (lgkmcnt(0)) before each DMA, which
 // serialises the fragment reads against the refill spread over the MFMAs.  The ring protocol
 // (counted vmcnt + one barrier per K-step) orders the DMA against the reads instead; M0 carries
-// the wave-uniform LDS byte address (SALU write -> LDS-DMA read of M0 needs one wait state; M0 is
-// reserved, so the compiler never keeps a value of its own there across this).
+// the wave-uniform LDS byte address (SALU write -> LDS-DMA read of M0 needs one wait state).  M0 is a
+// reserved register (clang rejects it in a clobber list: "may not be preserved"), so this relies on the
+// compiler keeping no value of its own there; tests/test_isa_m0.py checks that on the built library's
+// gfx950 machine code: every M0 access is this statement's write and the LDS-DMA right after it.
 __device__ inline void glds16(const void* src, unsigned lds_addr) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src),
                "s"(__builtin_amdgcn_readfirstlane(lds_addr))

@@ -429,12 +429,30 @@ __device__ inline float4 head_bwd_row(const HeadParams& hp, const float* __restr
   return out;
 }
 
-// (bx, by, bz) of a [W / 256][T_l HB_RS][E] grid; red: 4 x 64 float4 of LDS
+// ------------------------------------------------------------------ checked LDS reductions
+// Every cross-wave LDS reduction of the head backward is checked: the wave that reads the other
+// waves' slots keeps a digest of the bits it read, hands it back through `chk`, and after a barrier
+// each writer compares it with the digest of the registers it stored.  A slot that did not hold its
+// writer's bits when it was read ORs a HEAD_FAULT_* bit into HeadParams::fault; the engine turns that
+// into an error at the next sync (engine.cpp check_err), so a recurrence of the round-5 event (one
+// wrong head weight-grad value on an emulated rank whose inputs were right) fails
+// loudly instead of as a tolerance miss.  The digests cost a few VALU ops and one barrier per block.
+__device__ inline unsigned digest4(unsigned d, float4 v) {
+  d = __builtin_rotateleft32(d, 5) ^ __float_as_uint(v.x);
+  d = __builtin_rotateleft32(d, 5) ^ __float_as_uint(v.y);
+  d = __builtin_rotateleft32(d, 5) ^ __float_as_uint(v.z);
+  return __builtin_rotateleft32(d, 5) ^ __float_as_uint(v.w);
+}
+__device__ inline void head_fault(unsigned* fault, unsigned bit) {
+  if (fault) __hip_atomic_fetch_or(fault, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// (bx, by, bz) of a [W / 256][T_l HB_RS][E] grid; red: 4 x 64 float4 of LDS, chk: 4 x 64 digests
 template <int HD>
 __device__ inline void head_bwd_data_body(const HeadParams& hp, const float* __restrict__ dout, long long s_dout,
                                           float* __restrict__ dz, const PlaneOut& po_in, float* __restrict__ dbp,
                                           const int* __restrict__ counts, const int* __restrict__ rows, int max_rows,
-                                          int bx, int by, int bz, int gy, float4 (*red)[64]) {
+                                          int bx, int by, int bz, int gy, float4 (*red)[64], unsigned (*chk)[64]) {
   // split2h: the planes' exponent from the bound kmul * max|dout| * (max|head weight| + w_add), every
   // workgroup alike (red is the scratch of the maxima); the scale rides in po.w_add from here on
   PlaneOut po = po_in;
@@ -481,13 +499,20 @@ __device__ inline void head_bwd_data_body(const HeadParams& hp, const float* __r
   }
   if (dbp == nullptr) return;
   red[rl][lane] = cs;
+  const unsigned own = digest4(0u, cs);
   __syncthreads();
   if (rl == 0 && ok) {
     const float4 a = red[0][lane], b = red[1][lane], c = red[2][lane], d = red[3][lane];
     *reinterpret_cast<float4*>(dbp + ((long long)e * gy + by) * hp.W + w) =
         make_float4(((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y, ((a.z + b.z) + c.z) + d.z,
                     ((a.w + b.w) + c.w) + d.w);
+    chk[0][lane] = digest4(0u, a);
+    chk[1][lane] = digest4(0u, b);
+    chk[2][lane] = digest4(0u, c);
+    chk[3][lane] = digest4(0u, d);
   }
+  __syncthreads();
+  if (ok && chk[rl][lane] != own) head_fault(hp.fault, HEAD_FAULT_COLSUM);
 }
 
 template <int HD>
@@ -496,8 +521,9 @@ __global__ __launch_bounds__(256) void head_bwd_data_kernel(HeadParams hp, const
                                                             float* __restrict__ dbp, const int* __restrict__ counts,
                                                             const int* __restrict__ rows, int max_rows) {
   __shared__ float4 red[4][64];
+  __shared__ unsigned chk[4][64];
   head_bwd_data_body<HD>(hp, dout, s_dout, dz, po, dbp, counts, rows, max_rows, blockIdx.x, blockIdx.y, blockIdx.z,
-                         gridDim.y, red);
+                         gridDim.y, red, chk);
 }
 
 // ------------------------------------------------------------------ head backward (weights)
@@ -560,12 +586,13 @@ __global__ __launch_bounds__(256) void head_bwd_weight_scalar_kernel(HeadParams 
 }
 
 // W % 4 == 0: each lane owns 4 consecutive w (16-B loads), a workgroup 256 w; (bx, by, bz) of a
-// [T_l][W / 256][E] grid; red: 4 x 64 x HD float4 of LDS
-template <int HD>
+// [T_l][W / 256][E] grid; red: HD x 4 x 64 float4 of LDS ([o][wave][lane]: a wave's 64 lanes write one
+// contiguous KiB, no bank conflicts), chk: 4 x 64 digests
+template <int HD, bool INJECT = false>
 __device__ inline void head_bwd_weight_body(const HeadParams& hp, const float* __restrict__ dout, long long s_dout,
                                             const int* __restrict__ counts, const int* __restrict__ rows, int max_rows,
                                             float* __restrict__ dWh, float* __restrict__ dbh, int bx, int by, int bz,
-                                            float4 (*red)[64][HD]) {
+                                            float4 (*red)[4][64], unsigned (*chk)[64]) {
   const int t = bx, e = bz;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int w = by * 256 + 4 * lane;
@@ -591,27 +618,42 @@ __device__ inline void head_bwd_weight_body(const HeadParams& hp, const float* _
       }
     }
   }
+  unsigned own = 0u;
 #pragma unroll
-  for (int o = 0; o < HD; ++o) red[wave][lane][o] = acc[o];
+  for (int o = 0; o < HD; ++o) {
+    red[o][wave][lane] = acc[o];
+    own = digest4(own, acc[o]);
+  }
+  if constexpr (INJECT) {  // the self-check's own test (mtsac_debug_head_selfcheck): one slot gets other bits
+    if (wave == 1 && lane == 48) red[HD - 1][1][48].x = __uint_as_float(__float_as_uint(acc[HD - 1].x) ^ 1u);
+  }
   __syncthreads();
   if (wave == 0 && w < hp.W) {
     float v[4][HD];
+    unsigned dg[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int o = 0; o < HD; ++o) {
-      const float4 a0 = red[0][lane][o], a1 = red[1][lane][o], a2 = red[2][lane][o], a3 = red[3][lane][o];
+      const float4 a0 = red[o][0][lane], a1 = red[o][1][lane], a2 = red[o][2][lane], a3 = red[o][3][lane];
       v[0][o] = a0.x + a1.x + a2.x + a3.x;
       v[1][o] = a0.y + a1.y + a2.y + a3.y;
       v[2][o] = a0.z + a1.z + a2.z + a3.z;
       v[3][o] = a0.w + a1.w + a2.w + a3.w;
+      dg[0] = digest4(dg[0], a0);
+      dg[1] = digest4(dg[1], a1);
+      dg[2] = digest4(dg[2], a2);
+      dg[3] = digest4(dg[3], a3);
     }
     float* out = dWh + e * hp.sWh + ((long long)t * hp.W + w) * HD;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
 #pragma unroll
       for (int o = 0; o < HD; ++o) out[k * HD + o] = v[k][o];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) chk[g][lane] = dg[g];
   }
+  __syncthreads();  // also orders wave 0's reads of red before the bias pass reuses it
+  if (w < hp.W && chk[wave][lane] != own) head_fault(hp.fault, HEAD_FAULT_WGRAD);
   if (by == 0) {  // bias grad: 256 strided partial sums, then a fixed-order tree
-    __syncthreads();
     float* part = reinterpret_cast<float*>(&red[0][0][0]);  // >= 256 * HD floats
 #pragma unroll
     for (int o = 0; o < HD; ++o) {
@@ -635,14 +677,22 @@ __global__ __launch_bounds__(256) void head_bwd_weight_kernel(HeadParams hp, con
                                                               long long s_dout, const int* __restrict__ counts,
                                                               const int* __restrict__ rows, int max_rows,
                                                               float* __restrict__ dWh, float* __restrict__ dbh) {
-  __shared__ float4 red[4][64][HD];
-  if (hp.dbg & 1) {  // diagnostics: drop this CU's L1 before any load (MTSAC_DBG_HEAD=1)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
+  __shared__ float4 red[HD][4][64];
+  __shared__ unsigned chk[4][64];
   head_bwd_weight_body<HD>(hp, dout, s_dout, counts, rows, max_rows, dWh, dbh, blockIdx.x, blockIdx.y, blockIdx.z,
-                           red);
+                           red, chk);
+}
+
+// head_bwd_weight_kernel with one LDS slot corrupted on purpose (the self-check's test, never in a step)
+template <int HD>
+__global__ __launch_bounds__(256) void head_bwd_weight_inject_kernel(HeadParams hp, const float* __restrict__ dout,
+                                                                     long long s_dout, const int* __restrict__ counts,
+                                                                     const int* __restrict__ rows, int max_rows,
+                                                                     float* __restrict__ dWh, float* __restrict__ dbh) {
+  __shared__ float4 red[HD][4][64];
+  __shared__ unsigned chk[4][64];
+  head_bwd_weight_body<HD, true>(hp, dout, s_dout, counts, rows, max_rows, dWh, dbh, blockIdx.x, blockIdx.y,
+                                 blockIdx.z, red, chk);
 }
 
 // Both halves of a head's backward in ONE launch (they read the same dout and are independent):
@@ -654,24 +704,20 @@ __global__ __launch_bounds__(256) void head_bwd_both_kernel(HeadParams hp, const
                                                             float* __restrict__ dbp, const int* __restrict__ counts,
                                                             const int* __restrict__ rows, int max_rows, int T_l,
                                                             float* __restrict__ dWh, float* __restrict__ dbh) {
-  __shared__ float4 red[4][64][HD];
+  __shared__ float4 red[HD][4][64];
+  __shared__ unsigned chk[4][64];
   const int gw = (hp.W + 255) / 256, gy = T_l * HB_RS;
   const int nd = gw * gy * hp.E;
-  if (hp.dbg & 1) {  // diagnostics: drop this CU's L1 before any load (MTSAC_DBG_HEAD=1)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
   int b = blockIdx.x;
   if (b < nd) {
     const int bx = b % gw, by = (b / gw) % gy, bz = b / (gw * gy);
     head_bwd_data_body<HD>(hp, dout, s_dout, dz, po, dbp, counts, rows, max_rows, bx, by, bz, gy,
-                           reinterpret_cast<float4 (*)[64]>(&red[0][0][0]));
+                           reinterpret_cast<float4 (*)[64]>(&red[0][0][0]), chk);
     return;
   }
   b -= nd;
   const int bx = b % T_l, by = (b / T_l) % gw, bz = b / (T_l * gw);
-  head_bwd_weight_body<HD>(hp, dout, s_dout, counts, rows, max_rows, dWh, dbh, bx, by, bz, red);
+  head_bwd_weight_body<HD>(hp, dout, s_dout, counts, rows, max_rows, dWh, dbh, bx, by, bz, red, chk);
 }
 
 // The head backward's data and weight passes reading h ONCE: block (task t, 256 columns bx, member e),
@@ -687,7 +733,8 @@ __global__ __launch_bounds__(256) void head_bwd_fused_kernel(HeadParams hp, cons
                                                              const int* __restrict__ rows, int max_rows, int T_l,
                                                              float* __restrict__ dWh, float* __restrict__ dbh) {
   constexpr int HDL = HD < HB_RS ? HB_RS : HD;  // the column-sum reduction needs [HB_RS][4][64] float4
-  __shared__ float4 red[4][64][HDL];
+  __shared__ float4 red[HDL][4][64];               // weight sums: [o][wave][lane]
+  __shared__ unsigned chk[4][64], rchk[HB_RS][4][64];  // the reductions' digests (checked LDS reductions)
   const int gw = (hp.W + 255) / 256, gy = T_l * HB_RS;
   const int t = blockIdx.x % T_l, bx = (blockIdx.x / T_l) % gw, e = blockIdx.x / (T_l * gw);
   if (po.p && po.rc) {  // split2h: as head_bwd_data_body
@@ -759,40 +806,66 @@ __global__ __launch_bounds__(256) void head_bwd_fused_kernel(HeadParams hp, cons
       }
     }
   }
-  // weight grad: the four waves in order (head_bwd_weight_body)
+  // weight grad: the four waves in order (head_bwd_weight_body), checked
+  unsigned own = 0u;
 #pragma unroll
-  for (int o = 0; o < HD; ++o) red[wave][lane][o] = acc[o];
+  for (int o = 0; o < HD; ++o) {
+    red[o][wave][lane] = acc[o];
+    own = digest4(own, acc[o]);
+  }
   __syncthreads();
   if (wave == 0 && ok) {
     float v[4][HD];
+    unsigned dg[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int o = 0; o < HD; ++o) {
-      const float4 a0 = red[0][lane][o], a1 = red[1][lane][o], a2 = red[2][lane][o], a3 = red[3][lane][o];
+      const float4 a0 = red[o][0][lane], a1 = red[o][1][lane], a2 = red[o][2][lane], a3 = red[o][3][lane];
       v[0][o] = a0.x + a1.x + a2.x + a3.x;
       v[1][o] = a0.y + a1.y + a2.y + a3.y;
       v[2][o] = a0.z + a1.z + a2.z + a3.z;
       v[3][o] = a0.w + a1.w + a2.w + a3.w;
+      dg[0] = digest4(dg[0], a0);
+      dg[1] = digest4(dg[1], a1);
+      dg[2] = digest4(dg[2], a2);
+      dg[3] = digest4(dg[3], a3);
     }
     float* out = dWh + e * hp.sWh + ((long long)t * hp.W + w) * HD;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
 #pragma unroll
       for (int o = 0; o < HD; ++o) out[k * HD + o] = v[k][o];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) chk[g][lane] = dg[g];
   }
   __syncthreads();
-  // the data grad's column sums per row slice rs: waves (a + b) + c + d (head_bwd_data_body)
+  if (ok && chk[wave][lane] != own) head_fault(hp.fault, HEAD_FAULT_WGRAD);
+  // the data grad's column sums per row slice rs: waves (a + b) + c + d (head_bwd_data_body), checked
   if (dbp != nullptr) {
     float4(*cr)[4][64] = reinterpret_cast<float4(*)[4][64]>(&red[0][0][0]);  // [rs][wave][lane]
+    unsigned owns[HB_RS];
 #pragma unroll
-    for (int u = 0; u < HB_RS; ++u) cr[u][wave][lane] = cs[u];
+    for (int u = 0; u < HB_RS; ++u) {
+      cr[u][wave][lane] = cs[u];
+      owns[u] = digest4(0u, cs[u]);
+    }
     __syncthreads();
     if (ok) {  // wave g finishes row slice rs = g
       const float4 a = cr[wave][0][lane], b = cr[wave][1][lane], c = cr[wave][2][lane], dd = cr[wave][3][lane];
       *reinterpret_cast<float4*>(dbp + ((long long)e * gy + t * HB_RS + wave) * hp.W + w) =
           make_float4(((a.x + b.x) + c.x) + dd.x, ((a.y + b.y) + c.y) + dd.y, ((a.z + b.z) + c.z) + dd.z,
                       ((a.w + b.w) + c.w) + dd.w);
+      rchk[wave][0][lane] = digest4(0u, a);
+      rchk[wave][1][lane] = digest4(0u, b);
+      rchk[wave][2][lane] = digest4(0u, c);
+      rchk[wave][3][lane] = digest4(0u, dd);
     }
     __syncthreads();
+    if (ok) {
+      bool bad = false;
+#pragma unroll
+      for (int u = 0; u < HB_RS; ++u) bad |= rchk[u][wave][lane] != owns[u];
+      if (bad) head_fault(hp.fault, HEAD_FAULT_COLSUM);
+    }
   }
   if (bx == 0) {  // head bias grad: as head_bwd_weight_body
     float* part = reinterpret_cast<float*>(&red[0][0][0]);  // >= 256 * HD floats
@@ -1084,6 +1157,13 @@ void head_backward_weight(const HeadParams& hp, const float* dout, long long s_d
     default: if (vec) HBW_LAUNCH(head_bwd_weight_kernel, 8, 256); else HBW_LAUNCH(head_bwd_weight_scalar_kernel, 8, 64); break;
   }
 #undef HBW_LAUNCH
+}
+
+void head_backward_weight_inject(const HeadParams& hp, const float* dout, long long s_dout, const int* counts,
+                                 const int* rows, int max_rows, int T_l, float* dWh, float* dbh, hipStream_t st) {
+  if (hp.hd != 8 || hp.W % 4 != 0) return;  // the instance the round-5 event hit (actor head, hd = 8)
+  hipLaunchKernelGGL(head_bwd_weight_inject_kernel<8>, dim3((unsigned)T_l, (unsigned)((hp.W + 255) / 256), (unsigned)hp.E),
+                     dim3(256), 0, st, hp, dout, s_dout, counts, rows, max_rows, dWh, dbh);
 }
 
 void action_grad(const ActionGradParams& p, hipStream_t st) {

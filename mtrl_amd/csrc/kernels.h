@@ -281,8 +281,12 @@ struct HeadParams {
   const int* task;      // [B]
   int B, W, hd, E;
   long long sWh, sbh, sh;
-  int dbg;              // diagnostics (MTSAC_DBG_HEAD): 1 = an agent-scope acquire at the start of the head backward blocks
+  unsigned* fault;      // nullable: the head backward's LDS-reduction self-checks OR a bit in here on a
+                        // mismatch (HEAD_FAULT_*); the engine reports it at the next sync (check_err)
 };
+// HeadParams::fault bits: which checked cross-wave LDS reduction saw a slot differ from its writer's bits
+constexpr unsigned HEAD_FAULT_WGRAD = 1u;   // the head weight grad's four-wave sum
+constexpr unsigned HEAD_FAULT_COLSUM = 2u;  // the data pass's per-row-slice column sums (bias-grad partials)
 
 // actor head + tanh-normal sample (networks.py:28-45, distributions.py:6-16)
 struct PolicyParams {
@@ -374,6 +378,10 @@ bool head_backward_both(const HeadParams& hp, const float* dout, long long s_dou
                         const int* rows, int max_rows, int T_l, PlaneOut po, float* dbp, float* dWh, float* dbh,
                         hipStream_t st);
 // dWh[e][t][w][o] = sum_{b in t} h[e][b][w] dout[e][b][o];  dbh[e][t][o] = sum dout
+// head_backward_weight with one cross-wave LDS slot corrupted on purpose (hd = 8 only): the self-check's
+// test -- the engine's next check_err must report HEAD_FAULT_WGRAD (mtsac_debug_head_selfcheck)
+void head_backward_weight_inject(const HeadParams& hp, const float* dout, long long s_dout, const int* counts,
+                                 const int* rows, int max_rows, int T_l, float* dWh, float* dbh, hipStream_t st);
 void head_backward_weight(const HeadParams& hp, const float* dout, long long s_dout, const int* counts,
                           const int* rows, int max_rows, float* dWh, float* dbh, hipStream_t st);
 

@@ -136,11 +136,30 @@ class MultiTaskReplayBufferOracle:
         return self.gather(self.sample_indices(batch_size))
 
     def checkpoint(self) -> dict:
+        """buffers.py:308-324.  ``rng_state`` is ``self._rng.__getstate__()`` (:323); under the pinned
+        numpy 2.2.4 (2.2.6 here) ``Generator.__getstate__()`` returns ``None`` -- the stream is NOT
+        persisted by the reference (tests/test_buffer_checkpoint_cpu.py pins this)."""
         return {
             "data": {
                 "obs": self.obs, "actions": self.actions, "rewards": self.rewards,
                 "next_obs": self.next_obs, "dones": self.dones, "pos": self.pos, "full": self.full,
                 "returns_min": self._returns_min, "returns_max": self._returns_max,
             },
-            "rng_state": self.rng.to_numpy_state(),
+            "rng_state": None,
         }
+
+    def load_checkpoint(self, ckpt: dict) -> None:
+        """buffers.py:326-335.  ``self._rng.__setstate__(ckpt["rng_state"])`` (:335) with numpy 2.2's
+        ``Generator.__setstate__``: ``None`` leaves the stream where it is (a resumed reference run
+        continues from the fresh ``default_rng(seed)`` of ``spawn_replay_buffer``, base.py:148); a
+        ``bit_generator.state`` dict (numpy's legacy pickle form) sets it."""
+        for key in ["data", "rng_state"]:
+            assert key in ckpt
+        d = ckpt["data"]
+        for key in ["obs", "actions", "rewards", "next_obs", "dones", "pos", "full"]:
+            assert key in d
+            setattr(self, key, d[key])
+        self._returns_min = d.get("returns_min", self._returns_min)
+        self._returns_max = d.get("returns_max", self._returns_max)
+        if ckpt["rng_state"] is not None:
+            self.rng = PCG64State.from_numpy_state(ckpt["rng_state"])

@@ -65,10 +65,10 @@ def _problem(name):
 
 def _engine(spec, precision, begin=0, count=None, cu_slice=None):
     """cu_slice = (k, n): the engine's streams run on CU slice k of n only (MTSAC_CU_SLICE, read at
-    create).  The in-process multi-rank tests give every emulated rank its own CUs, as ranks on their
-    own GPUs have: with all engines' kernels co-resident on every CU, a handful of values of the head
-    backward's cross-wave LDS reduction came out wrong on some boxes ("Eight
-    engines on one device")."""
+    create), as ranks on their own GPUs have their own CUs.  Round 5 saw, once, a handful of wrong
+    values of the head backward's cross-wave LDS reduction with all engines co-resident on every CU
+    ("Eight engines on one device"); those reductions are now self-checked (a
+    mismatch makes the engine's next logs() raise), and the determinism test below runs co-resident."""
     import os
 
     from mtrl_amd.engine import MTSACEngine, make_config
@@ -143,9 +143,10 @@ def test_full_batch_step_matches_oracle(name, precision):
     e.close()
 
 
-def _run_8way(name, precision, world=8):
-    """The MT50 8-GPU task split as 8 engines on one device (each on its own CU slice), one full-batch
-    step through the in-process all-reduce hook; returns the engines (open) and their logs."""
+def _run_8way(name, precision, world=8, cu_slices=True):
+    """The MT50 8-GPU task split as 8 engines on one device (each on its own CU slice, or all of them
+    co-resident on every CU), one full-batch step through the in-process all-reduce hook; returns the
+    engines (open) and their logs."""
     import threading
 
     from mtrl_amd.shard import InProcessAllReduce, local_rows, shard_tasks
@@ -156,7 +157,7 @@ def _run_8way(name, precision, world=8):
     shards = []
     for r in range(world):
         b0, c0 = shard_tasks(T, world, r)
-        e = _engine(spec, precision, b0, c0, cu_slice=(r, world))
+        e = _engine(spec, precision, b0, c0, cu_slice=(r, world) if cu_slices else None)
         _load(e, st, b0, c0)
         shards.append(e)
     group = InProcessAllReduce(world)
@@ -202,13 +203,19 @@ def test_full_batch_8way_shard_matches_oracle(precision, name):
 
 
 def test_full_batch_8way_shard_split2h_deterministic():
-    """the 8-engine S3 split2h step twice in one process (fresh engines, same
-    inputs) gives bitwise the same logs, parameters and Adam moments on every rank."""
+    """the 8-engine S3 split2h step twice in one process (fresh engines,
+    same inputs), every engine co-resident on every CU (no CU slices: the setting of the round-5
+    event), gives bitwise the same logs, parameters and Adam moments on every rank, and logs within
+    RTOL of the float64 oracle.  The head backward's LDS reductions are self-checked: a recurrence of
+    the round-5 event raises from logs() (engine.cpp check_err) instead of surfacing as a tolerance
+    miss."""
     from mtrl_amd import _lib as L
 
+    *_, want = _problem("s3_mt50_w2048")
     outs = []
-    for _ in range(2):
-        shards, logs = _run_8way("s3_mt50_w2048", 3)
+    for rep in range(2):
+        shards, logs = _run_8way("s3_mt50_w2048", 3, cu_slices=False)
+        _check_logs(logs[0], want, f"shard8-coresident/split2h/rep{rep}")
         outs.append((logs, [[e.get_params(w) for w in (L.ACTOR, L.CRITIC, L.CRITIC_TARGET, L.ACTOR_ADAM_MU,
                                                          L.CRITIC_ADAM_MU, L.ACTOR_ADAM_NU)] for e in shards]))
         for e in shards:
@@ -218,6 +225,30 @@ def test_full_batch_8way_shard_split2h_deterministic():
     for r, (xa, xb) in enumerate(zip(pa, pb)):
         for q, (x, y) in enumerate(zip(xa, xb)):
             assert np.array_equal(x, y), (r, q, int(np.count_nonzero(x != y)))
+
+
+@pytest.mark.parametrize("precision", [1, 3], ids=["split3", "split2h"])
+def test_head_backward_selfcheck_fires(precision):
+    """The head backward's LDS self-check is live end to end: the last step's actor head weight pass,
+    re-run with one cross-wave LDS slot corrupted on purpose (mtsac_debug_head_selfcheck, into a
+    scratch output), makes the next logs() raise the self-check error; the error clears, and the
+    step's own parameters and logs are untouched by the check run."""
+    from mtrl_amd import _lib as L
+
+    name = "s2_mt10_w2048_clip"
+    cfg, st, batch, en, ec, st1, want = _problem(name)
+    e = _engine(CASES[name], precision)
+    _load(e, st)
+    e.update(batch, en, ec)
+    logs = e.logs()  # a clean step: no fault
+    _check_logs(logs, want, f"selfcheck/p{precision}")
+    before = e.get_params(L.ACTOR)
+    L.check(e.lib.mtsac_debug_head_selfcheck(e._h))
+    with pytest.raises(Exception, match="self-check"):
+        e.logs()
+    assert e.logs() == logs  # cleared; the logs buffer was not touched
+    assert np.array_equal(e.get_params(L.ACTOR), before)
+    e.close()
 
 
 def test_full_batch_modelled_collective_matches_oracle():

@@ -272,3 +272,48 @@ def test_return_normalisation_matches_reference():
     np.testing.assert_array_equal(ck["data"]["returns_min"], orc._returns_min)
     np.testing.assert_array_equal(ck["data"]["returns_max"], orc._returns_max)
     eng.close()
+
+
+@pytest.mark.parametrize("persist", [False, True], ids=["reference_dict", "persisted_stream"])
+def test_buffer_resume_from_checkpoint_dict(persist):
+    """a run interrupted after some samples is checkpointed and resumed into a fresh
+    device buffer spawned with the same seed.  With the reference's checkpoint dict (rng_state None:
+    numpy 2.2's Generator.__getstate__, mtrl/rl/buffers.py:323) the resumed buffer's next batches are
+    the oracle's after the same load -- the fresh default_rng(seed) stream, as a resumed reference run
+    draws them -- bit for bit; with persist_rng_state the interrupted stream continues instead."""
+    from mtrl_amd.compat.rl.buffers import MultiTaskReplayBuffer
+    from mtrl_amd.engine import MTSACEngine, make_config
+
+    T, n, cap, A = 3, 8, 64, 4
+    D = 39 + T
+
+    def engine():
+        return MTSACEngine(make_config(num_tasks=T, task_count=T, obs_dim=D, batch_per_task=n, capacity=cap,
+                                       actor_width=16, critic_width=16))
+
+    e1 = engine()
+    buf = MultiTaskReplayBuffer(cap * T, T, seed=1, engine=e1)
+    buf.persist_rng_state = persist
+    orc = MultiTaskReplayBufferOracle(cap * T, T, D, A, seed=1)
+    obs, nobs, act, rew, done = _fill(None, cap, T, D, A, slots=40)
+    for s in range(40):
+        buf.add(obs[s], nobs[s], act[s], rew[s], done[s])
+        orc.add(obs[s], nobs[s], act[s], rew[s], done[s])
+    for _ in range(3):  # the interrupted run advances its stream
+        buf.sample(n * T)
+        orc.sample(n * T)
+    ck = buf.checkpoint()
+    assert (ck["rng_state"] is None) != persist
+    e1.close()
+    e2 = engine()
+    buf2 = MultiTaskReplayBuffer(cap * T, T, seed=1, engine=e2)  # spawn_replay_buffer(seed) on resume
+    buf2.load_checkpoint(ck)
+    ref = MultiTaskReplayBufferOracle(cap * T, T, D, A, seed=1)
+    ref.load_checkpoint({"data": {k: np.asarray(v) for k, v in ck["data"].items()}, "rng_state": ck["rng_state"]})
+    cont = orc  # persisted: the uninterrupted stream
+    for _ in range(3):
+        got = buf2.sample(n * T)
+        want = (cont if persist else ref).sample(n * T)
+        for g, w in zip(got, want):
+            np.testing.assert_array_equal(np.asarray(g).reshape(w.shape), w.astype(np.float32))
+    e2.close()

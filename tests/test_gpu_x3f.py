@@ -181,7 +181,8 @@ def test_split_k_in_launch_finish_bitwise(E, M, N, K, epi, m16, planes, h2):
     """The in-launch split-K finish gives the separate finishing pass's bits exactly and meets the fp32
     bound against float64.  split3: every slice writes its slab and draws a ticket, the last one adds
     the slabs in slice order with its own partial in its place.  split2h (the default precision, two
-    slices): the pair hand-off -- the ticket first, the first slice publishes its unscaled partial,
+    slices): the pair hand-off -- the ticket first, the first slice publishes its partial with the
+    unscale factor 2^-(eA + eB) already applied,
     the second adds it to its own (fp32 addition commutes) and applies the epilogue; C and the output
     planes equal the finishing pass's bit for bit."""
     from mtrl_amd import _lib as L
