@@ -109,6 +109,7 @@ void ablate_at(const SplitGemmParams& p, int abl, dim3 grid, hipStream_t st) {
     case 3: hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_BIAS_RELU, false, true, false, 3, NP, WV>), grid, blk, 0, st, p); break;
     case 64: hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_BIAS_RELU, false, true, false, 64, NP, WV>), grid, blk, 0, st, p); break;
     case 131: hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_BIAS_RELU, false, true, false, 131, NP, WV>), grid, blk, 0, st, p); break;
+    case 128: hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_BIAS_RELU, false, true, false, 128, NP, WV>), grid, blk, 0, st, p); break;
     default: hipLaunchKernelGGL((gemm_x3f_kernel<BM, EPI_BIAS_RELU, false, true, false, 0, NP, WV>), grid, blk, 0, st, p); break;
   }
 }

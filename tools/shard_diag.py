@@ -49,6 +49,11 @@ def leaf_errs(got, ref, shapes, tag):
 
 SNAP = False
 CU_SLICE = False  # --cu-slice: engine r runs on CU slice r of 8 (MTSAC_CU_SLICE)
+FULL_MASK = False  # --full-mask: every engine's streams CU-masked to ALL CUs (MTSAC_CU_SLICE=0:1): engines
+#                   co-resident on every CU as unsliced, but each stream on a queue of its own
+HEADG = {}  # (arm, rank) -> the actor gradient's head leaves of the arm's first repeat (--grad-diff)
+GRAD_DIFF = False
+ARM = ""
 SNAP0 = {}  # rank -> the first repeat's h after the forward
 
 
@@ -69,6 +74,8 @@ def run_sharded(name, precision, world=8):
         b0, c0 = shard_tasks(T, world, r)
         if CU_SLICE:
             os.environ["MTSAC_CU_SLICE"] = f"{r}:{world}"
+        elif FULL_MASK:
+            os.environ["MTSAC_CU_SLICE"] = "0:1"
         e = t._engine(spec, precision, b0, c0)
         t._load(e, st, b0, c0)
         shards.append(e)
@@ -152,6 +159,32 @@ def run_sharded(name, precision, world=8):
             else:
                 SNAP0[r] = bufs[1].copy()
             snaps.append(bufs)
+    if GRAD_DIFF:  # the actor gradient's head leaves against this arm's first repeat, per rank
+        W = t.SHARD_CASES[name]["W"]
+        for r, e in enumerate(shards):
+            b0, c0 = shard_tasks(t.SHARD_CASES[name]["T"], world, r)
+            g = np.empty(snap_count(e, 4), np.float32)
+            L.check(e.lib.mtsac_debug_read(e._h, 4, g.ctypes.data, g.size))
+            key = (ARM, r)
+            if key not in HEADG:
+                HEADG[key] = g.copy()
+                continue
+            off = -(-8 * c0 // 64) * 64  # head_b (T_l x 8, 64-float aligned), then head_W [T_l][W][8]
+            dif = np.flatnonzero(g != HEADG[key])
+            if dif.size == 0:
+                print(f"  [{ARM}] rank {r}: actor head grads bitwise equal to the arm's first repeat", flush=True)
+                continue
+            ref = HEADG[key]
+            rel = np.abs(g[dif] - ref[dif]) / np.abs(ref[off:off + c0 * W * 8]).max()
+            desc = []
+            for i in dif[:24]:
+                if i >= off:
+                    tt, rem = divmod(int(i - off), W * 8)
+                    desc.append(f"W(t{tt},w{rem // 8},o{rem % 8})")
+                else:
+                    desc.append(f"b({int(i) // 8},{int(i) % 8})")
+            print(f"  [{ARM}] rank {r}: {dif.size} head-grad entries differ (max {rel.max():.2e} of the leaf max): "
+                  f"{' '.join(desc)}", flush=True)
     logs = [e.logs() for e in shards]
     mus = [(e.get_params(L.ACTOR_ADAM_MU), e.get_params(L.CRITIC_ADAM_MU)) for e in shards]
     for e in shards:
@@ -168,10 +201,14 @@ def main():
     ap.add_argument("--snap", action="store_true", help="snapshot the actor's top activations in the step")
     ap.add_argument("--cu-slice", action="store_true", help="engine r on CU slice r of 8: no two engines share a CU")
     ap.add_argument("--alternate", action="store_true", help="alternate --cu-slice on / off between repeats")
+    ap.add_argument("--queue-ab", action="store_true",
+                    help="alternate full-mask streams (own queues, all CUs) and plain streams between repeats")
+    ap.add_argument("--grad-diff", action="store_true", help="compare the actor head grads with the arm's first repeat")
     a = ap.parse_args()
-    global SNAP, CU_SLICE
+    global SNAP, CU_SLICE, FULL_MASK, GRAD_DIFF, ARM
     SNAP = a.snap
     CU_SLICE = a.cu_slice
+    GRAD_DIFF = a.grad_diff
     spec = t.SHARD_CASES[a.name]
     cfg, st, batch, en, ec, st1, want = t._problem(a.name)
     T, W = spec["T"], spec["W"]
@@ -185,6 +222,10 @@ def main():
         if a.alternate:  # even repeats on CU slices, odd ones unsliced (same box, interleaved)
             CU_SLICE = rep % 2 == 0
             print(f"rep {rep}: cu slices {CU_SLICE}", flush=True)
+        if a.queue_ab:  # even repeats full-mask (each stream its own queue), odd ones plain streams
+            FULL_MASK = rep % 2 == 0
+            ARM = "fullmask" if FULL_MASK else "plain"
+            print(f"rep {rep}: arm {ARM}", flush=True)
         logs, mus = run_sharded(a.name, a.precision)
         same_ranks = all(lg == logs[0] for lg in logs)
         errs = {k: abs(logs[0][k] - want[k]) / max(abs(want[k]), 1e-30) for k in keys}
