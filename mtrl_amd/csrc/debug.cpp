@@ -133,9 +133,12 @@ int mtsac_debug_gemm_x3p_bench(int epi, int batch, int M, int N, int K, int iter
   const int layout = (epi >> 8) & 3;  // bit 0: A k-major, bit 1: B k-major
   const int splits = (epi >> 16) & 255;  // split-K slices (0/1: none; EPI_STORE: + splitk_reduce; 255: auto)
   const bool fin = (epi >> 12) & 1;      // arrival counters: the weight grads' in-launch reduce
+  const bool h2 = (epi >> 13) & 1;       // precision split2h (zero exponents: operands in [-1, 1])
+  const bool pout = (epi >> 14) & 1;     // output planes too (the forward's: bias+ReLU planes out)
   epi &= 255;
   if (M < 1 || N < 1 || K < 1 || batch < 1 || iters < 1 || !ms_per_launch) return -22;
   DevBuf d;
+  PlaneRec* rec = h2 ? d.get<PlaneRec>(3) : nullptr;
   float* fa = d.get<float>((size_t)M * K);
   float* fb = d.get<float>((size_t)N * K);
   float* C = d.get<float>((size_t)M * N * batch);
@@ -153,13 +156,24 @@ int mtsac_debug_gemm_x3p_bench(int epi, int batch, int M, int N, int K, int iter
   __bf16* Bp = d.get<__bf16>((size_t)3 * pb * batch);
   if (!Ap || !Bp) return -12;
   for (int z = 0; z < batch; ++z) {
-    split_into(fa, M, K, layout & 1, Ap + 3 * pa * z);
-    split_into(fb, N, K, layout & 2, Bp + 3 * pb * z);
+    split_into(fa, M, K, layout & 1, Ap + 3 * pa * z, h2 ? &rec[0].e : nullptr);
+    split_into(fb, N, K, layout & 2, Bp + 3 * pb * z, h2 ? &rec[1].e : nullptr);
   }
   SplitGemmParams g{};
+  if (h2) {
+    g.np = 2;
+    g.ra = rec; g.rb = rec + 1; g.rc = rec + 2;
+    g.kmul = (float)K;
+  }
+  if (pout) {
+    __bf16* Cp = d.get<__bf16>((size_t)3 * M * N * batch);
+    if (!Cp) return -12;
+    g.Cp = Cp; g.ldcp = N; g.pC = (long long)M * N; g.sCp = 3 * g.pC;
+  }
+  const bool planes_only = pout;
   g.A = Ap; g.lda = lda; g.pA = pa; g.sA = 3 * pa; g.a_kmajor = layout & 1;
   g.B = Bp; g.ldb = ldb; g.pB = pb; g.sB = 3 * pb; g.b_kmajor = (layout >> 1) & 1;
-  g.C = C; g.ldc = N; g.sC = (long long)M * N;
+  g.C = planes_only ? nullptr : C; g.ldc = N; g.sC = (long long)M * N;
   g.bias = bias; g.sBias = N;
   g.mask = C; g.ldm = N; g.sMask = (long long)M * N;
   g.M = M; g.N = N; g.K = (int)up32(K);
