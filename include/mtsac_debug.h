@@ -68,6 +68,16 @@ int mtsac_debug_drq_groups(int fwd, int bwd);
 // DrQ convolutions on f32 MFMA (experiment, measured slower than the VALU kernels): bit 1 forward,
 // 2 data grad, 4 weight grad (default 0 = the VALU kernels).  Returns the previous mask; < 0 queries.
 int mtsac_debug_drq_mfma(int mask);
+// The pre-round-6 DrQ conv kernels (one lane per pixel, im2col weight grad) instead of the row-tile
+// ones: bit 1 forward, 2 data grad, 4 weight grad.  Returns the previous mask; < 0 queries.
+int mtsac_debug_drq_legacy(int mask);
+// The row-tile conv weight grad's grid cap (> 0 sets, 0 restores the per-shape default, < 0 queries;
+// returns the previous).  Engines size their partial buffers at creation: change it only before
+// creating one.  Experiments.
+int mtsac_debug_drq_wgrad_blocks(int cap);
+// Mean microseconds per launch of one DrQ conv pass on random operands: kind 0 forward (ReLU in,
+// residual), 1 data gradient (mask, residual), 2 weight-gradient partials.  -22 bad arguments.
+int mtsac_debug_drq_conv_bench(int kind, int B, int H, int W, int ci, int co, int iters, double* us_per_launch);
 
 /* Eager update_many overlaps consecutive steps (the next gather and critic(s, a) forward beside
  * the previous actor backward / all-reduce / Adam): on = 1 always, 0 never (whole steps), -1 the

@@ -156,6 +156,9 @@ SIGNATURES = {
     "mtsac_debug_x3s_ti": (ctypes.c_int, [ctypes.c_int] * 3),
     "mtsac_debug_drq_groups": (ctypes.c_int, [ctypes.c_int] * 2),
     "mtsac_debug_drq_mfma": (ctypes.c_int, [ctypes.c_int]),
+    "mtsac_debug_drq_legacy": (ctypes.c_int, [ctypes.c_int]),
+    "mtsac_debug_drq_wgrad_blocks": (ctypes.c_int, [ctypes.c_int]),
+    "mtsac_debug_drq_conv_bench": (ctypes.c_int, [ctypes.c_int] * 7 + [ctypes.POINTER(ctypes.c_double)]),
     "mtsac_debug_set_pipeline": (ctypes.c_int, [P, I32]),
     "mtsac_debug_lane_mode": (ctypes.c_int, [P]),
     "mtsac_debug_check_guards": (ctypes.c_int, [P]),

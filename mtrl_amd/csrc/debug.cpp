@@ -476,4 +476,31 @@ int mtsac_debug_drq_mfma(int mask) {
   return old;
 }
 
+// the pre-round-6 DrQ conv kernels (bit 1 forward, 2 data grad, 4 weight grad) or the row-tile ones;
+// returns the previous mask (< 0: query only)
+int mtsac_debug_drq_legacy(int mask) {
+  const int old = drq::g_drq_legacy;
+  if (mask >= 0) drq::g_drq_legacy = mask & 7;
+  return old;
+}
+
+// the row-tile conv weight grad's grid cap (> 0 sets, 0 restores the per-shape default; < 0 queries;
+// returns the previous); engines created before a change keep partial buffers sized for the old cap,
+// so set it before creating one (experiments)
+int mtsac_debug_drq_wgrad_blocks(int cap) {
+  const int old = drq::g_drq_wg_blocks;
+  if (cap >= 0) drq::g_drq_wg_blocks = cap;
+  return old;
+}
+
+// mean microseconds per launch of one DrQ conv pass on random operands (drq::conv_bench)
+int mtsac_debug_drq_conv_bench(int kind, int B, int H, int W, int ci, int co, int iters, double* us_per_launch) {
+  if (kind < 0 || kind > 2 || B < 1 || H < 1 || W < 1 || iters < 1 || !us_per_launch || !drq::conv_supported(ci, co))
+    return -22;
+  const double us = drq::conv_bench(kind, B, H, W, ci, co, iters);
+  if (us < 0) return -12;
+  *us_per_launch = us;
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -5;
+}
+
 }  // extern "C"

@@ -12,6 +12,7 @@
 // partials summed in a fixed order (bitwise reproducible).
 #include <algorithm>
 #include <cstdlib>
+#include <vector>
 
 #include "drq_kernels.h"
 
@@ -414,6 +415,267 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* __restrict
   }
 }
 
+// Weight gradient partials on row tiles (round 6, the default; conv_wgrad_kernel above is the
+// im2col form it replaced).  A tile is R consecutive rows of one image; its R + 2 input rows (act
+// applied, one zero column each side, zero outside the image) and its R dout rows are staged in LDS
+// ONCE, and the nine taps read the padded rows at shifted offsets, so the staging moves (R + 2) / R
+// copies of the input instead of im2col's nine, with no per-row index arithmetic (the per-slot
+// offsets are the same for every tile and computed once).  Lane (pg, blk): blk = (tap, block of CB
+// input channels) owns a CB x CO block of dW -- 8 x 16 FMAs per two plus four ds_read_b128, so
+// the loop is VALU-bound, not LDS-bound as the 4 x 4 blocks above were -- over the pixels q = pg,
+// pg + PG, ... of every tile; the next tile is loaded into registers (unconditionally, at a clamped
+// address) while this one is computed.  The PG groups' partials are added in a fixed tree order
+// in LDS and the bias sums as in conv_wgrad_kernel, so the result is reproducible run to run.
+// part[g][9 CI CO + CO] as conv_wgrad_kernel.
+template <int CI, int CO>
+struct WgRows {
+  static constexpr int CB = CI < 8 ? CI : 8;  // input channels per lane block
+  static constexpr int NB = 9 * (CI / CB);    // lane blocks (each: one tap, CB channels, all CO)
+  static constexpr int PG = 256 / NB;         // pixel groups
+  static constexpr int NPF = 8;               // staged float4 per thread per tile
+  static constexpr int E4 = CB * CO / 4;      // float4 of one lane's block
+  static constexpr int RED4 = (PG / 2) * NB * E4;
+  static constexpr int LDS4 = RED4 > NPF * 256 ? RED4 : NPF * 256;
+};
+
+template <int CI, int CO, bool RELU_IN>
+__global__ __launch_bounds__(256) void conv_wgrad_rows_kernel(const float* __restrict__ in, const float* __restrict__ dout,
+                                                              float* __restrict__ part, WgGeo geo) {
+  using P = WgRows<CI, CO>;
+  constexpr int CB = P::CB, NB = P::NB, PG = P::PG, NPF = P::NPF, E4 = P::E4;
+  constexpr int NW = 9 * CI * CO;
+  constexpr int BG = 256 / CO;
+  static_assert(CI % 4 == 0 && CO % 4 == 0 && 256 % CO == 0, "channels");
+  __shared__ float4 lds4[P::LDS4];
+  __shared__ float bred[256];
+  float* const lds = reinterpret_cast<float*>(lds4);
+  const int H = geo.H, W = geo.W, R = geo.R, SR = geo.SR;
+  const int NI = (R + 2) * (W + 2) * (CI / 4), NT = NI + R * W * (CO / 4);
+  const int tpi = (H + R - 1) / R;
+  float* const s_g = lds + (R + 2) * SR;
+  const int t = threadIdx.x;
+  // staging slots k: input float4 (row i, column j, chunk c) or dout float4 (row r, column x, chunk c);
+  // offsets from the tile's base pixel, the row relative to the tile's first row (validity), LDS offset
+  int soff[NPF], loff[NPF], rrel[NPF];
+  bool isg[NPF];
+#pragma unroll
+  for (int k = 0; k < NPF; ++k) {
+    const int s = t + 256 * k;
+    isg[k] = s >= NI;
+    if (s < NI) {
+      const int c = s % (CI / 4), j = (s / (CI / 4)) % (W + 2), i = s / ((CI / 4) * (W + 2));
+      soff[k] = ((i - 1) * W + (j - 1)) * CI + 4 * c;
+      loff[k] = i * SR + j * CI + 4 * c;
+      rrel[k] = (j >= 1 && j <= W) ? i - 1 : -(1 << 20);  // padding columns: never valid
+    } else if (s < NT) {
+      const int u = s - NI, c = u % (CO / 4), q = u / (CO / 4);
+      soff[k] = q * CO + 4 * c;  // q = r W + x
+      loff[k] = (R + 2) * SR + q * CO + 4 * c;
+      rrel[k] = q / W;
+    } else {
+      soff[k] = 0;
+      loff[k] = -1;
+      rrel[k] = -(1 << 20);
+    }
+  }
+  float4 v[NPF];
+  auto load_tile = [&](int tile) {
+    const int b = tile / tpi, y0 = (tile - b * tpi) * R;
+    const long long p0 = ((long long)b * H + y0) * W;
+    const float* ib = in + p0 * CI;
+    const float* gb = dout + p0 * CO;
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const bool ok = (unsigned)(y0 + rrel[k]) < (unsigned)H;
+      const float* src = ok ? (isg[k] ? gb : ib) + soff[k] : ib;  // ib: row y0 of image b, always in range
+      const float4 u = *reinterpret_cast<const float4*>(src);
+      float4 w = ok ? u : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (RELU_IN && !isg[k]) w = make_float4(fmaxf(w.x, 0.f), fmaxf(w.y, 0.f), fmaxf(w.z, 0.f), fmaxf(w.w, 0.f));
+      v[k] = w;
+    }
+  };
+  const int blk = t % NB, pg = t / NB;
+  const int tap = blk / (CI / CB), cb0 = (blk % (CI / CB)) * CB;
+  const int aoff = (tap / 3) * SR + (tap % 3) * CI + cb0;
+  const int bco = t % CO, bg = t / CO;
+  float acc[CB][CO];
+#pragma unroll
+  for (int i = 0; i < CB; ++i)
+#pragma unroll
+    for (int j = 0; j < CO; ++j) acc[i][j] = 0.f;
+  float bacc = 0.f;
+  const int npx = R * W;
+  if ((int)blockIdx.x < geo.tiles) load_tile(blockIdx.x);
+  for (int tile = blockIdx.x; tile < geo.tiles; tile += gridDim.x) {
+    __syncthreads();  // the previous tile's reads are done
+#pragma unroll
+    for (int k = 0; k < NPF; ++k)
+      if (loff[k] >= 0) *reinterpret_cast<float4*>(lds + loff[k]) = v[k];
+    __syncthreads();
+    load_tile(min(tile + (int)gridDim.x, geo.tiles - 1));  // in flight during this tile's FMAs
+    if (t < NB * PG) {
+      for (int q = pg; q < npx; q += PG) {
+        const int r = __umulhi((unsigned)q, geo.magic), x = q - r * W;
+        const float* ap = lds + aoff + r * SR + x * CI;
+        const float* gp = s_g + q * CO;
+        float a[CB], g[CO];
+#pragma unroll
+        for (int c4 = 0; c4 < CB; c4 += 4) {
+          const float4 u = *reinterpret_cast<const float4*>(ap + c4);
+          a[c4] = u.x; a[c4 + 1] = u.y; a[c4 + 2] = u.z; a[c4 + 3] = u.w;
+        }
+#pragma unroll
+        for (int c4 = 0; c4 < CO; c4 += 4) {
+          const float4 u = *reinterpret_cast<const float4*>(gp + c4);
+          g[c4] = u.x; g[c4 + 1] = u.y; g[c4 + 2] = u.z; g[c4 + 3] = u.w;
+        }
+#pragma unroll
+        for (int i = 0; i < CB; ++i)
+#pragma unroll
+          for (int j = 0; j < CO; ++j) acc[i][j] = fmaf(a[i], g[j], acc[i][j]);
+      }
+    }
+    {  // bias: lane group bg sums pixels q = bg, bg + BG, ... of channel bco (rows past H are zero)
+      float s = bacc;
+      for (int q = bg; q < npx; q += BG) s += s_g[q * CO + bco];
+      bacc = s;
+    }
+  }
+  // the PG groups' partials, added in a fixed tree order (group pg + s into group pg)
+  float4* const red = lds4;
+#pragma unroll 1
+  for (int s = 1; s < PG; s *= 2) {
+    __syncthreads();
+    if (t < NB * PG && pg % (2 * s) == s) {
+      float4* d = red + (pg / (2 * s)) * E4 * NB + blk;
+#pragma unroll
+      for (int e = 0; e < E4; ++e) {
+        const int i = (4 * e) / CO, j = (4 * e) % CO;
+        d[e * NB] = make_float4(acc[i][j], acc[i][j + 1], acc[i][j + 2], acc[i][j + 3]);
+      }
+    }
+    __syncthreads();
+    if (t < NB * PG && pg % (2 * s) == 0 && pg + s < PG) {
+      const float4* d = red + (pg / (2 * s)) * E4 * NB + blk;
+#pragma unroll
+      for (int e = 0; e < E4; ++e) {
+        const int i = (4 * e) / CO, j = (4 * e) % CO;
+        const float4 u = d[e * NB];
+        acc[i][j] += u.x; acc[i][j + 1] += u.y; acc[i][j + 2] += u.z; acc[i][j + 3] += u.w;
+      }
+    }
+  }
+  float* pp = part + (long long)blockIdx.x * (NW + CO);
+  if (t < NB)
+#pragma unroll
+    for (int i = 0; i < CB; ++i)
+#pragma unroll
+      for (int j = 0; j < CO; j += 4)
+        *reinterpret_cast<float4*>(pp + (tap * CI + cb0 + i) * CO + j) =
+            make_float4(acc[i][j], acc[i][j + 1], acc[i][j + 2], acc[i][j + 3]);
+  __syncthreads();
+  bred[t] = bacc;
+  __syncthreads();
+  if (t < CO) {
+    float s = bred[t];
+    for (int g = 1; g < BG; ++g) s += bred[g * CO + t];
+    pp[NW + t] = s;
+  }
+}
+
+// Forward and data-gradient convolutions on row tiles (round 6).  One block = one tile of R rows of
+// one image; its R + 2 input rows (zero-padded by one column each side and zero outside the image;
+// act applied) are staged in LDS once, and every lane reads its pixel's nine neighbours from there
+// instead of from L1 (the one-lane-per-pixel kernels above read each input pixel nine times through
+// the texture path, which bounds them next to the FMAs).  Weights stay wave-uniform scalar loads:
+// wave w computes the CG output channels of group w % NG for pixels (w / NG) 64 + lane of the tile.
+//   FWD:  out[p][o] = bias[o] + sum_{tap,k} act(X)[p + off(tap)][k] w[tap][k][o]  (+ res[p][o]),
+//         X = the conv input (KI = ci, KO = co); images [0, B1) take (w_a, bias_a), the rest (w_b, bias_b)
+//   !FWD: din[p][j] = (sum_{tap,k} dout[p + off(tap)][k] w[8 - tap][j][k]) [mask[p][j] > 0] (+ dres[p][j]),
+//         X = dout (KI = co, KO = ci): the transposed conv as a conv with the taps flipped.
+// The per-output summation order (taps, then input channels) is that of the kernels above; a tap
+// outside the image adds fma(0, w, acc) = acc, so the results are theirs.  LDS: a pixel's KI / 4
+// 16-byte chunks are stored XOR-swizzled by column (chunk c of padded column j at
+// c ^ ((j / (64 / KI)) % (KI / 4))), so 16 lanes on consecutive pixels read 16 distinct bank quads.
+constexpr int CR_LDS = 3072;  // floats of the staged rows (12 KB: the benched shapes need <= 2944)
+template <int KI, int KO, int CG, bool FWD, bool RELU_IN, bool MASK, bool ADD_RES>
+__global__ __launch_bounds__(256) void conv_rows_kernel(const float* __restrict__ X, const float* __restrict__ w_a,
+                                                        const float* __restrict__ bias_a, const float* __restrict__ w_b,
+                                                        const float* __restrict__ bias_b, int B1,
+                                                        const float* __restrict__ mask, const float* __restrict__ res,
+                                                        float* __restrict__ out, ConvGeo geo) {
+  constexpr int NG = KO / CG, KC = KI / 4, PPR = 64 / KI;  // groups, chunks per pixel, pixels per 256 B
+  static_assert(KO % CG == 0 && CG % 4 == 0 && KI % 4 == 0 && NG <= 4, "channels");
+  __shared__ float4 lds4[CR_LDS / 4];
+  float* const lds = reinterpret_cast<float*>(lds4);
+  const int H = geo.H, W = geo.W, R = geo.R, SR = geo.SR;
+  const int b = (int)blockIdx.x / geo.n, y0 = ((int)blockIdx.x - b * geo.n) * R;
+  const long long p0 = ((long long)b * H + y0) * W;  // the tile's first pixel
+  const int t = threadIdx.x;
+  {  // stage rows y0 - 1 .. y0 + R: slot s = (row i, padded column j, chunk c)
+    const int NS = (R + 2) * (W + 2) * KC;
+    const float* base = X + p0 * KI;
+#pragma unroll
+    for (int k = 0; k < CR_LDS / 4 / 256; ++k) {
+      const int s = t + 256 * k;
+      const int c = s % KC, u = s / KC;
+      const int i = __umulhi((unsigned)u, geo.magic2), j = u - i * (W + 2);
+      const int yy = y0 + i - 1, xx = j - 1;
+      const bool ok = s < NS && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      const float* src = ok ? base + ((long long)(i - 1) * W + xx) * KI + 4 * c : base;
+      const float4 q = *reinterpret_cast<const float4*>(src);
+      float4 v = ok ? q : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (RELU_IN) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+      if (s < NS) *reinterpret_cast<float4*>(lds + i * SR + j * KI + 4 * (c ^ ((j / PPR) % KC))) = v;
+    }
+  }
+  __syncthreads();
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6), g = wv % NG;  // wave-uniform: scalar weight loads
+  const int q = (wv / NG) * 64 + (t & 63);
+  const int r = __umulhi((unsigned)q, geo.magic), x = q - r * W;
+  if (q >= R * W || y0 + r >= H) return;  // no barrier follows
+  const float* __restrict__ w = (FWD && b >= B1) ? w_b : w_a;
+  float acc[CG];
+#pragma unroll
+  for (int c = 0; c < CG; ++c) acc[c] = FWD ? ((b >= B1) ? bias_b : bias_a)[g * CG + c] : 0.f;
+#pragma unroll
+  for (int tt = 0; tt < 9; ++tt) {  // !FWD: X tap 8 - tt is weight tap tt, in the order above
+    const int tap = FWD ? tt : 8 - tt;
+    const int j = x + tap % 3;
+    const float* xp = lds + (r + tap / 3) * SR + j * KI;
+    const int sw = (j / PPR) % KC;
+    float v[KI];
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const float4 u = *reinterpret_cast<const float4*>(xp + 4 * (c ^ sw));
+      v[4 * c] = u.x; v[4 * c + 1] = u.y; v[4 * c + 2] = u.z; v[4 * c + 3] = u.w;
+    }
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+#pragma unroll
+      for (int c = 0; c < CG; ++c) {
+        const float wk = FWD ? w[(tap * KI + k) * KO + g * CG + c] : w[(tt * KO + g * CG + c) * KI + k];
+        acc[c] = fmaf(v[k], wk, acc[c]);
+      }
+    }
+  }
+  const long long o = (p0 + (long long)r * W + x) * KO + g * CG;
+#pragma unroll
+  for (int c4 = 0; c4 < CG; c4 += 4) {
+    float4 v = make_float4(acc[c4], acc[c4 + 1], acc[c4 + 2], acc[c4 + 3]);
+    if (MASK) {
+      const float4 m = *reinterpret_cast<const float4*>(mask + o + c4);
+      v.x = m.x > 0.f ? v.x : 0.f; v.y = m.y > 0.f ? v.y : 0.f;
+      v.z = m.z > 0.f ? v.z : 0.f; v.w = m.w > 0.f ? v.w : 0.f;
+    }
+    if (ADD_RES) {
+      const float4 a = *reinterpret_cast<const float4*>(res + o + c4);
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+    *reinterpret_cast<float4*>(out + o + c4) = v;
+  }
+}
+
 // ------------------------------------------------------------------ convolutions on f32 MFMA
 // v_mfma_f32_16x16x4_f32 (exact fp32: bit for bit a k-ordered fmaf chain, MI355X_MICROARCH.md) at the
 // FP32 rate, which the VALU kernels above reach only with packed FMAs fed from SGPRs; here the VALU
@@ -676,7 +938,9 @@ __global__ __launch_bounds__(256) void sum_parts_multi_kernel(const SumSeg* __re
 // gradient; jax's select-and-scatter takes the first maximum, as here)
 __global__ void maxpool_fwd_kernel(const float* __restrict__ in, float* __restrict__ out,
                                    unsigned char* __restrict__ arg, int B, int H, int W, int C, int Ho, int Wo, int lo) {
-  // one lane per 4 channels of one output pixel: float4 loads / stores, 32-bit index math
+  // one lane per 4 channels of one output pixel: float4 loads / stores, 32-bit index math.  The nine
+  // window loads are unconditional (clamped into the image, an outside tap then skipped), so they are
+  // all in flight at once: under a branch each was waited for at the branch's end, one latency a tap
   const int C4 = C >> 2;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B * Ho * Wo * C4) return;
@@ -686,17 +950,23 @@ __global__ void maxpool_fwd_kernel(const float* __restrict__ in, float* __restri
   r /= Wo;
   const int oy = r % Ho;
   const int b = r / Ho;
+  float4 v[9];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int y = min(max(2 * oy - lo + tap / 3, 0), H - 1), x = min(max(2 * ox - lo + tap % 3, 0), W - 1);
+    v[tap] = *reinterpret_cast<const float4*>(in + ((b * H + y) * W + x) * C + c);
+  }
   float4 best = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
   uchar4 bi = make_uchar4(0, 0, 0, 0);
+#pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     const int y = 2 * oy - lo + tap / 3, x = 2 * ox - lo + tap % 3;
     if (y < 0 || y >= H || x < 0 || x >= W) continue;
-    const float4 v = *reinterpret_cast<const float4*>(in + ((b * H + y) * W + x) * C + c);
     const unsigned char t = (unsigned char)tap;
-    if (v.x > best.x) { best.x = v.x; bi.x = t; }
-    if (v.y > best.y) { best.y = v.y; bi.y = t; }
-    if (v.z > best.z) { best.z = v.z; bi.z = t; }
-    if (v.w > best.w) { best.w = v.w; bi.w = t; }
+    if (v[tap].x > best.x) { best.x = v[tap].x; bi.x = t; }
+    if (v[tap].y > best.y) { best.y = v[tap].y; bi.y = t; }
+    if (v[tap].z > best.z) { best.z = v[tap].z; bi.z = t; }
+    if (v[tap].w > best.w) { best.w = v[tap].w; bi.w = t; }
   }
   const int o = ((b * Ho + oy) * Wo + ox) * C + c;
   *reinterpret_cast<float4*>(out + o) = best;
@@ -704,7 +974,9 @@ __global__ void maxpool_fwd_kernel(const float* __restrict__ in, float* __restri
 }
 
 // din[b][y][x][c] = sum over the windows whose argmax is (y, x) of dout (a gather: deterministic),
-// one lane per 4 channels of one input pixel
+// one lane per 4 channels of one input pixel.  A pixel lies in at most 2 x 2 windows (stride 2,
+// size 3); their four (arg, dout) pairs are loaded unconditionally at clamped addresses and added in
+// window order, skipping the windows that do not cover the pixel.
 __global__ void maxpool_bwd_kernel(const float* __restrict__ dout, const unsigned char* __restrict__ arg,
                                    float* __restrict__ din, int B, int H, int W, int C, int Ho, int Wo, int lo) {
   const int C4 = C >> 2;
@@ -716,24 +988,33 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ dout, const unsigne
   r /= W;
   const int y = r % H;
   const int b = r / H;
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   // windows o with 2 o - lo <= y <= 2 o - lo + 2, in order
   const int oy0 = y + lo - 2 <= 0 ? 0 : (y + lo - 1) / 2, oy1 = min((y + lo) / 2, Ho - 1);
   const int ox0 = x + lo - 2 <= 0 ? 0 : (x + lo - 1) / 2, ox1 = min((x + lo) / 2, Wo - 1);
-  for (int oy = oy0; oy <= oy1; ++oy) {
-    const int ty = y - (2 * oy - lo);
-    if (ty < 0 || ty > 2) continue;
-    for (int ox = ox0; ox <= ox1; ++ox) {
-      const int tx = x - (2 * ox - lo);
-      if (tx < 0 || tx > 2) continue;
-      const int o = ((b * Ho + oy) * Wo + ox) * C + c;
-      const uchar4 a = *reinterpret_cast<const uchar4*>(arg + o);
-      const float4 d = *reinterpret_cast<const float4*>(dout + o);
+  uchar4 a[2][2];
+  float4 d[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int o = ((b * Ho + min(oy0 + u, Ho - 1)) * Wo + min(ox0 + v, Wo - 1)) * C + c;
+      a[u][v] = *reinterpret_cast<const uchar4*>(arg + o);
+      d[u][v] = *reinterpret_cast<const float4*>(dout + o);
+    }
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int oy = oy0 + u, ty = y - (2 * oy - lo);
+    if (oy > oy1 || ty < 0 || ty > 2) continue;
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int ox = ox0 + v, tx = x - (2 * ox - lo);
+      if (ox > ox1 || tx < 0 || tx > 2) continue;
       const unsigned char t = (unsigned char)(ty * 3 + tx);
-      if (a.x == t) s.x += d.x;
-      if (a.y == t) s.y += d.y;
-      if (a.z == t) s.z += d.z;
-      if (a.w == t) s.w += d.w;
+      if (a[u][v].x == t) s.x += d[u][v].x;
+      if (a[u][v].y == t) s.y += d[u][v].y;
+      if (a[u][v].z == t) s.z += d[u][v].z;
+      if (a[u][v].w == t) s.w += d[u][v].w;
     }
   }
   *reinterpret_cast<float4*>(din + ((b * H + y) * W + x) * C + c) = s;
@@ -1285,6 +1566,40 @@ int g_drq_mfma = [] {
 }();
 constexpr int MFMA_TW = 4;  // 16-pixel tiles per wave of conv_mfma_kernel
 
+// Row-tile forward / data-gradient geometry (conv_rows_kernel): for NG = 1, 2, 4 output-channel groups
+// (CG = KO / NG >= 4 channels a lane) a tile holds up to 256 / NG pixels; R = the rows that fit,
+// balanced over the image; the NG with the best-filled tiles wins (ties: fewer groups, less
+// re-reading).  NG = 0: no fit (W < 2, or a row too wide), the pixel kernels run instead.
+static ConvGeo conv_geo(int H, int W, int KI, int KO, int* ng_out) {
+  ConvGeo best{H, W, 0, (W + 2) * KI, 0, 0u, 0u};
+  double best_u = 0.0;
+  *ng_out = 0;
+  if (W < 2) return best;
+  for (int ng = 1; ng <= 4; ng *= 2) {
+    if (KO % ng || KO / ng < 4) continue;
+    const int cap = 256 / ng;
+    int R = std::min({H, cap / W, CR_LDS / best.SR - 2});
+    if (R < 1) continue;
+    const int n = (H + R - 1) / R;
+    R = (H + n - 1) / n;
+    const double u = (double)(R * W) / cap;
+    if (u > best_u + 1e-9) {
+      best_u = u;
+      best.R = R;
+      best.n = n;
+      *ng_out = ng;
+    }
+  }
+  best.magic = (unsigned)((0x100000000ULL + (unsigned)W - 1) / (unsigned)W);
+  best.magic2 = (unsigned)((0x100000000ULL + (unsigned)W + 1) / (unsigned)(W + 2));
+  return best;
+}
+// a forced channel group (mtsac_debug_drq_groups), the MFMA experiment or the legacy mask selects the
+// one-lane-per-pixel kernels
+static bool conv_rows_on(int ng, int forced_group, int bit) {
+  return ng > 0 && forced_group == 0 && !(g_drq_mfma & bit) && !(g_drq_legacy & bit);
+}
+
 void conv_fwd(const float* in, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
               int ci, int co, bool relu_in, hipStream_t st, const float* w2, const float* bias2, int B1) {
   const long long npix = (long long)B * H * W;
@@ -1293,6 +1608,28 @@ void conv_fwd(const float* in, const float* w, const float* bias, const float* r
     w2 = w;
     bias2 = bias;
     B1 = B;
+  }
+  {
+    int ng = 0;
+    const ConvGeo geo = conv_geo(H, W, ci, co, &ng);
+    if (conv_rows_on(ng, g_drq_fwd_g, 1)) {
+      const dim3 gr((unsigned)(B * geo.n)), tb(256);
+#define C_FR_G(a, b, cg)                                                                                            \
+  if (relu_in && res) hipLaunchKernelGGL((conv_rows_kernel<a, b, cg, true, true, false, true>), gr, tb, 0, st, in, w, bias, w2, bias2, B1, nullptr, res, out, geo); \
+  else if (relu_in) hipLaunchKernelGGL((conv_rows_kernel<a, b, cg, true, true, false, false>), gr, tb, 0, st, in, w, bias, w2, bias2, B1, nullptr, res, out, geo); \
+  else if (res) hipLaunchKernelGGL((conv_rows_kernel<a, b, cg, true, false, false, true>), gr, tb, 0, st, in, w, bias, w2, bias2, B1, nullptr, res, out, geo); \
+  else hipLaunchKernelGGL((conv_rows_kernel<a, b, cg, true, false, false, false>), gr, tb, 0, st, in, w, bias, w2, bias2, B1, nullptr, res, out, geo);
+#define C_FR(a, b)                                   \
+  if (ci == a && co == b) {                          \
+    if (ng == 1) { C_FR_G(a, b, b) }                 \
+    else if (ng == 2) { C_FR_G(a, b, b / 2) }        \
+    else if constexpr (b >= 16) { C_FR_G(a, b, b / 4) } \
+    return;                                          \
+  }
+      CONV_CASES(C_FR)
+#undef C_FR
+#undef C_FR_G
+    }
   }
   if (g_drq_mfma & 1) {
     constexpr int PB = 64 * MFMA_TW;
@@ -1331,6 +1668,32 @@ void conv_fwd(const float* in, const float* w, const float* bias, const float* r
 void conv_bwd_data(const float* dout, const float* w, const float* mask, const float* dres, float* din, int B, int H,
                    int W, int ci, int co, hipStream_t st) {
   const long long npix = (long long)B * H * W;
+  {  // the transposed conv: KI = co (dout channels), KO = ci
+    int ng = 0;
+    const ConvGeo geo = conv_geo(H, W, co, ci, &ng);
+    // measured (r6l): the row-tile data grad wins at 21 x 21 (13.6 vs 28.2 us) and 11 x 11 and loses
+    // at 42 x 42 and 84 x 84 (15.1 vs 13.8, 31.3 vs 27.9, 33.5 vs 31.8): it runs for W <= 32
+    if (W <= 32 && conv_rows_on(ng, g_drq_bwd_g, 2)) {
+      const dim3 gr((unsigned)(B * geo.n)), tb(256);
+#define C_BR_G(a, b, cg)                                                                                            \
+  if (mask && dres) hipLaunchKernelGGL((conv_rows_kernel<b, a, cg, false, false, true, true>), gr, tb, 0, st, dout, w, nullptr, w, nullptr, B, mask, dres, din, geo); \
+  else if (mask) hipLaunchKernelGGL((conv_rows_kernel<b, a, cg, false, false, true, false>), gr, tb, 0, st, dout, w, nullptr, w, nullptr, B, mask, dres, din, geo); \
+  else if (dres) hipLaunchKernelGGL((conv_rows_kernel<b, a, cg, false, false, false, true>), gr, tb, 0, st, dout, w, nullptr, w, nullptr, B, mask, dres, din, geo); \
+  else hipLaunchKernelGGL((conv_rows_kernel<b, a, cg, false, false, false, false>), gr, tb, 0, st, dout, w, nullptr, w, nullptr, B, mask, dres, din, geo);
+#define C_BR(a, b)                                   \
+  if (ci == a && co == b) {                          \
+    if (ng == 1) { C_BR_G(a, b, a) }                 \
+    else if constexpr (a >= 8) {                     \
+      if (ng == 2) { C_BR_G(a, b, a / 2) }           \
+      else if constexpr (a >= 16) { C_BR_G(a, b, a / 4) } \
+    }                                                \
+    return;                                          \
+  }
+      CONV_CASES(C_BR)
+#undef C_BR
+#undef C_BR_G
+    }
+  }
   if (g_drq_mfma & 2) {  // K channels = co, N = ci
     constexpr int PB = 64 * MFMA_TW;
     const dim3 gm((unsigned)((npix + PB - 1) / PB)), tm(256);
@@ -1362,19 +1725,66 @@ void conv_bwd_data(const float* dout, const float* w, const float* mask, const f
 #undef C_BD_G
 }
 
-// enough 64-pixel tiles in flight per CU to cover the staging loads' latency (the partials'
-// reduction is cheap next to them)
-// (the MFMA experiment takes chunks of npix / G pixels, 16-pixel aligned)
-int conv_wgrad_blocks(long long npix) { return (int)std::min<long long>(2048, std::max<long long>(1, (npix + 63) / 64)); }
+// Row-tile weight gradients (conv_wgrad_rows_kernel): the tallest tile whose staging fits the
+// per-thread slots and the kernel's LDS, shortened until the batch gives >= 512 tiles (two blocks
+// per CU), then balanced (equal row counts per image); R = 0 when even one row does not fit (very wide
+// images) or W < 2 (the magic division), where the im2col kernel runs instead.
+static int wg_lds_floats(int ci, int co) {
+#define C_WL(a, b) if (ci == a && co == b) return 4 * WgRows<a, b>::LDS4;
+  CONV_CASES(C_WL)
+#undef C_WL
+  return 0;
+}
+int g_drq_wg_blocks = 0;  // > 0: the row-tile weight grad's grid cap (mtsac_debug_drq_wgrad_blocks)
+static WgGeo wgrad_geo(int B, int H, int W, int ci, int co) {
+  WgGeo g{H, W, 0, (W + 2) * ci + 4, 0, 0u};
+  const int slots = 8 * 256, ldsf = wg_lds_floats(ci, co);
+  auto fits = [&](int R) {
+    return (R + 2) * (W + 2) * (ci / 4) + R * W * (co / 4) <= slots && (R + 2) * g.SR + R * W * co <= ldsf;
+  };
+  if (W < 2 || !fits(1)) return g;
+  int R = H;
+  while (R > 1 && (!fits(R) || (long long)B * ((H + R - 1) / R) < 2 * 256)) --R;
+  const int n = (H + R - 1) / R;
+  g.R = (H + n - 1) / n;
+  g.tiles = B * n;
+  g.magic = (unsigned)((0x100000000ULL + (unsigned)W - 1) / (unsigned)W);
+  return g;
+}
+int g_drq_legacy = [] {  // MTSAC_DRQ_LEGACY=mask in the environment: the same selection (A/B runs)
+  const char* e = getenv("MTSAC_DRQ_LEGACY");
+  return e ? (atoi(e) & 7) : 0;
+}();
+// Measured per shape (profiles/r6l_drq/conv_bench.txt, batch 256): the row-tile weight grad wins from
+// 21 x 21 up (84 x 84 4 -> 8: 41.5 vs 90.1 us) and loses at 11 x 11 (15.5 vs 9.7: one tile per block,
+// where the pixel-group tree is most of the work), so it runs for W >= 16
+static bool wgrad_rows(const WgGeo& g) { return g.R > 0 && g.W >= 16 && !(g_drq_mfma & 4) && !(g_drq_legacy & 4); }
+static int wgrad_cap(const WgGeo& g) {  // grid cap: 1024 at 84 x 84 (35.6 vs 41.5 us at 512), else 512
+  return g_drq_wg_blocks > 0 ? g_drq_wg_blocks : (g.W >= 64 ? 1024 : 512);
+}
+
+// im2col kernel: enough 64-pixel tiles in flight per CU to cover the staging loads' latency (the
+// partials' reduction is cheap next to them); the MFMA experiment takes chunks of npix / G pixels
+int conv_wgrad_blocks(int B, int H, int W, int ci, int co) {
+  const WgGeo g = wgrad_geo(B, H, W, ci, co);
+  if (wgrad_rows(g)) return std::min(g.tiles, wgrad_cap(g));
+  const long long npix = (long long)B * H * W;
+  return (int)std::min<long long>(2048, std::max<long long>(1, (npix + 63) / 64));
+}
 
 void conv_wgrad(const float* in, const float* dout, float* part, float* dw, float* db, int B, int H, int W, int ci,
                 int co, bool relu_in, hipStream_t st, bool defer_sum) {
   const long long npix = (long long)B * H * W;
-  const int G = conv_wgrad_blocks(npix);
+  const WgGeo geo = wgrad_geo(B, H, W, ci, co);
+  const bool rows = wgrad_rows(geo);
+  const int G = conv_wgrad_blocks(B, H, W, ci, co);
   const int chunk = (int)(((npix + G - 1) / G + 15) / 16 * 16);
 #define C_WG(a, b)                                                                                             \
   if (ci == a && co == b) {                                                                                    \
-    if (g_drq_mfma & 4) {                                                                                      \
+    if (rows) {                                                                                                \
+      if (relu_in) hipLaunchKernelGGL((conv_wgrad_rows_kernel<a, b, true>), dim3(G), dim3(256), 0, st, in, dout, part, geo); \
+      else hipLaunchKernelGGL((conv_wgrad_rows_kernel<a, b, false>), dim3(G), dim3(256), 0, st, in, dout, part, geo);      \
+    } else if (g_drq_mfma & 4) {                                                                               \
       if (relu_in) hipLaunchKernelGGL((conv_wgrad_mfma_kernel<a, b, true>), dim3(G), dim3(256), 0, st, in, dout, part, B, H, W, chunk); \
       else hipLaunchKernelGGL((conv_wgrad_mfma_kernel<a, b, false>), dim3(G), dim3(256), 0, st, in, dout, part, B, H, W, chunk);      \
     } else if (relu_in) hipLaunchKernelGGL((conv_wgrad_kernel<a, b, true>), dim3(G), dim3(256), 0, st, in, dout, part, B, H, W); \
@@ -1388,6 +1798,51 @@ void conv_wgrad(const float* in, const float* dout, float* part, float* dw, floa
 }
 
 int sum_parts_blocks(int ci, int co) { return (9 * ci * co + co + 15) / 16; }
+
+// Microbenchmark (debug entry mtsac_debug_drq_conv_bench): kind 0 forward (ReLU in, residual), 1 data
+// gradient (mask, residual), 2 weight-gradient partials; operands uniform in [-1, 1]; returns the mean
+// microseconds per launch over iters launches, or < 0 on an allocation failure
+double conv_bench(int kind, int B, int H, int W, int ci, int co, int iters) {
+  const long long np = (long long)B * H * W;
+  const long long nx = np * (kind == 1 ? co : ci), ny = np * (kind == 1 ? ci : co);
+  const int G = conv_wgrad_blocks(B, H, W, ci, co);
+  const long long nz = kind == 2 ? (long long)G * (9 * ci * co + co) : ny;
+  std::vector<float> hx((size_t)std::max({nx, ny, 9LL * ci * co + co}));
+  unsigned long long z = 88172645463325252ULL;
+  for (float& v : hx) {
+    z ^= z << 13; z ^= z >> 7; z ^= z << 17;
+    v = (float)((double)(z >> 11) / 9007199254740992.0 * 2.0 - 1.0);
+  }
+  float *x = nullptr, *y = nullptr, *o = nullptr, *w = nullptr;
+  if (hipMalloc(&x, nx * 4) != hipSuccess || hipMalloc(&y, ny * 4) != hipSuccess ||
+      hipMalloc(&o, nz * 4) != hipSuccess || hipMalloc(&w, (9LL * ci * co + co) * 4) != hipSuccess)
+    return -1.0;
+  (void)hipMemcpy(x, hx.data(), nx * 4, hipMemcpyHostToDevice);
+  (void)hipMemcpy(y, hx.data(), ny * 4, hipMemcpyHostToDevice);
+  (void)hipMemcpy(w, hx.data(), (9LL * ci * co + co) * 4, hipMemcpyHostToDevice);
+  auto run = [&] {
+    if (kind == 0) conv_fwd(x, w, w + 9 * ci * co, y, o, B, H, W, ci, co, true, nullptr);
+    else if (kind == 1) conv_bwd_data(x, w, y, y, o, B, H, W, ci, co, nullptr);
+    else conv_wgrad(x, y, o, nullptr, nullptr, B, H, W, ci, co, true, nullptr, true);
+  };
+  run();
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, nullptr);
+  for (int i = 0; i < iters; ++i) run();
+  (void)hipEventRecord(e1, nullptr);
+  (void)hipEventSynchronize(e1);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(x);
+  (void)hipFree(y);
+  (void)hipFree(o);
+  (void)hipFree(w);
+  return 1e3 * ms / iters;
+}
 
 void sum_parts_multi(const SumSeg* segs, int nseg, int blocks, hipStream_t st) {
   hipLaunchKernelGGL(sum_parts_multi_kernel, dim3(blocks), dim3(256), 0, st, segs, nseg);

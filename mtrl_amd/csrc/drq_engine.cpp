@@ -561,7 +561,7 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
       for (int j = 0; j < 5; ++j) {
         const Stack& k = e->stk[s];
         const int hh = j == 0 ? k.hin : k.ho, ci = j == 0 ? k.ci : k.co;
-        total += (long long)drq::conv_wgrad_blocks((long long)B * hh * hh) * (9LL * ci * k.co + k.co);
+        total += (long long)drq::conv_wgrad_blocks(B, hh, hh, ci, k.co) * (9LL * ci * k.co + k.co);
       }
     float* all = nullptr;
     if ((rc = e->alloc(&all, total))) return bad(rc);
@@ -570,7 +570,7 @@ int drq_create(const drq_config* c, int device, drq_engine** out) {
       for (int j = 0; j < 5; ++j) {
         const Stack& k = e->stk[s];
         const int hh = j == 0 ? k.hin : k.ho, ci = j == 0 ? k.ci : k.co;
-        const int G = drq::conv_wgrad_blocks((long long)B * hh * hh), n = 9 * ci * k.co + k.co;
+        const int G = drq::conv_wgrad_blocks(B, hh, hh, ci, k.co), n = 9 * ci * k.co + k.co;
         e->wparts[s][j] = all;
         segs.push_back({all, e->g + k.cw[j], e->g + k.cb[j], G, n, 9 * ci * k.co, blk});
         blk += drq::sum_parts_blocks(ci, k.co);

@@ -32,6 +32,11 @@ void aug_draw(unsigned long long seed, unsigned long long ctr, int B, int pad, i
 bool conv_supported(int ci, int co);
 extern int g_drq_fwd_g, g_drq_bwd_g;  // conv channel groups per lane, 0: the engine's choice (experiments)
 extern int g_drq_mfma;  // f32-MFMA convs (experiment): bit 1 forward, 2 data grad, 4 weight grad (default 0)
+// the pre-round-6 conv kernels (one lane per pixel; im2col weight grad) instead of the row-tile
+// ones: bit 1 forward, 2 data grad, 4 weight grad (default 0; tests and A/B)
+extern int g_drq_legacy;
+extern int g_drq_wg_blocks;  // the row-tile weight grad's grid cap (experiments; set before an engine exists)
+double conv_bench(int kind, int B, int H, int W, int ci, int co, int iters);
 // 3x3 / stride 1 / SAME on NHWC, kernel [3][3][ci][co]; relu_in applies ReLU to the input, res
 // (nullable) is added to the output.  w2 / bias2 (nullable): images [B1, B) use that second
 // parameter set (one launch over the online and the target passes)
@@ -41,8 +46,20 @@ void conv_fwd(const float* in, const float* w, const float* bias, const float* r
 // din = conv^T(dout) * [mask > 0] (mask nullable) + dres (nullable)
 void conv_bwd_data(const float* dout, const float* w, const float* mask, const float* dres, float* din, int B, int H,
                    int W, int ci, int co, hipStream_t st);
-int conv_wgrad_blocks(long long npix);
-// dw [3][3][ci][co], db [co] of a conv whose input is act(in); part: conv_wgrad_blocks(B H W) x
+// the row-tile weight-gradient kernel's geometry: tiles of R image rows (tiles = B ceil(H / R)), LDS
+// row stride SR floats, magic = ceil(2^32 / W) (q / W = umulhi(q, magic) for the q < R W it divides)
+struct WgGeo {
+  int H, W, R, SR, tiles;
+  unsigned magic;
+};
+int conv_wgrad_blocks(int B, int H, int W, int ci, int co);
+// the row-tile forward / data-gradient kernels' geometry: n tiles of R rows per image, LDS row
+// stride SR floats, magic = ceil(2^32 / W), magic2 = ceil(2^32 / (W + 2))
+struct ConvGeo {
+  int H, W, R, SR, n;
+  unsigned magic, magic2;
+};
+// dw [3][3][ci][co], db [co] of a conv whose input is act(in); part: conv_wgrad_blocks(...) x
 // (9 ci co + co) floats
 // defer_sum: leave the partials for one sum_parts_multi launch over every conv of the backward
 void conv_wgrad(const float* in, const float* dout, float* part, float* dw, float* db, int B, int H, int W, int ci,

@@ -129,6 +129,61 @@ def test_update_matches_oracle(hw, hidden, B, mfma):
     e.close()
 
 
+@pytest.mark.parametrize("hw,B", [(20, 8), (84, 16), (84, 256)], ids=["small", "reference_geometry", "b256"])
+def test_row_tile_convs_match_the_pixel_kernels(hw, B):
+    """Round 6: the row-tile conv kernels (forward, data grad, weight grad; drq.hip conv_rows_kernel /
+    conv_wgrad_rows_kernel) against the kernels they replaced (mtsac_debug_drq_legacy(7)) on one update.
+    The forward and the data grad keep the per-output summation order, so the loss, the logits and
+    every dense-layer gradient are bitwise equal; the weight grads sum the same products in another
+    order (row tiles, a pixel-group tree), so the conv leaves agree to fp32 rounding of their
+    Sum|terms| (both are held to the float64 oracle in test_update_matches_oracle)."""
+    from mtrl_amd import _lib as L
+
+    lib = L.load()
+    cfg = od.DrQConfig(hw=hw, n_hidden=64 if hw == 20 else 512)
+    st = od.init_state(cfg, 5)
+    batch, aug = _batch(cfg, B, 6)
+    out = {}
+    old = lib.mtsac_debug_drq_legacy(-1)
+    try:
+        for mask in (7, 0):
+            lib.mtsac_debug_drq_legacy(mask)
+            e = _engine(cfg, B)
+            e.set_params(L.DRQ_PARAMS, st.params)
+            e.set_params(L.DRQ_TARGET, st.params)
+            e.update(batch, aug)
+            e.synchronize()
+            out[mask] = (e.logs(), e.get_params(L.DRQ_GRAD))
+            e.close()
+    finally:
+        lib.mtsac_debug_drq_legacy(old)
+    (l_old, g_old), (l_new, g_new) = out[7], out[0]
+    for k in ("losses/online_logits", "losses/critic_loss"):
+        assert l_old[k] == l_new[k], (k, l_old, l_new)
+    o = 0
+    for path, shape in od.param_spec(cfg):
+        n = int(np.prod(shape))
+        a, b = g_new[o:o + n], g_old[o:o + n]
+        o += n
+        if "Conv" in path:
+            scale = float(np.abs(b).max()) + 1e-30
+            assert np.abs(a - b).max() <= 2e-5 * scale, (path, float(np.abs(a - b).max()), scale)
+        else:
+            np.testing.assert_array_equal(a, b, err_msg=path)
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2], ids=["forward", "data_grad", "weight_grad"])
+def test_conv_bench_entry_runs(kind):
+    """mtsac_debug_drq_conv_bench (the per-kernel sweep in tools/drq_conv_bench.py) on one shape."""
+    import ctypes
+
+    from mtrl_amd import _lib as L
+
+    us = ctypes.c_double(0.0)
+    assert L.load().mtsac_debug_drq_conv_bench(kind, 16, 21, 21, 16, 16, 3, ctypes.byref(us)) == 0
+    assert us.value > 0.0
+
+
 def test_deterministic():
     from mtrl_amd import _lib as L
 
