@@ -597,7 +597,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_rows_kernel(const float* __res
 // outside the image adds fma(0, w, acc) = acc, so the results are theirs.  LDS: a pixel's KI / 4
 // 16-byte chunks are stored XOR-swizzled by column (chunk c of padded column j at
 // c ^ ((j / (64 / KI)) % (KI / 4))), so 16 lanes on consecutive pixels read 16 distinct bank quads.
-constexpr int CR_LDS = 3072;  // floats of the staged rows (12 KB: the benched shapes need <= 2944)
+// floats of the staged rows (16 KB; at 12 KB the 16-channel data grad at 42 x 42 got 2-row tiles).  Two
+// output pixels a lane (each scalar weight feeding two FMAs) measured 2-3x slower: the compiler spilled
+// the weights through VGPR lanes (profiles/r6n_drq_two_pixels_per_lane)
+constexpr int CR_LDS = 4096;
 template <int KI, int KO, int CG, bool FWD, bool RELU_IN, bool MASK, bool ADD_RES>
 __global__ __launch_bounds__(256) void conv_rows_kernel(const float* __restrict__ X, const float* __restrict__ w_a,
                                                         const float* __restrict__ bias_a, const float* __restrict__ w_b,
@@ -1671,9 +1674,10 @@ void conv_bwd_data(const float* dout, const float* w, const float* mask, const f
   {  // the transposed conv: KI = co (dout channels), KO = ci
     int ng = 0;
     const ConvGeo geo = conv_geo(H, W, co, ci, &ng);
-    // measured (r6l): the row-tile data grad wins at 21 x 21 (13.6 vs 28.2 us) and 11 x 11 and loses
-    // at 42 x 42 and 84 x 84 (15.1 vs 13.8, 31.3 vs 27.9, 33.5 vs 31.8): it runs for W <= 32
-    if (W <= 32 && conv_rows_on(ng, g_drq_bwd_g, 2)) {
+    // measured (profiles/r6o_drq/conv_bench.txt): the row-tile data grad wins with 16 dout channels
+    // from 21 x 21 up (21 x 21: 13.6 vs 28.2 us, 42 x 42 8 -> 16: 25.0 vs 27.9) and loses with 8 (42 x 42:
+    // 15.2 vs 13.9) and at 11 x 11 (8.5 vs 7.9): it runs for co = 16, W >= 16
+    if (((co >= 16 && W >= 16) || (g_drq_legacy & 8)) && conv_rows_on(ng, g_drq_bwd_g, 2)) {
       const dim3 gr((unsigned)(B * geo.n)), tb(256);
 #define C_BR_G(a, b, cg)                                                                                            \
   if (mask && dres) hipLaunchKernelGGL((conv_rows_kernel<b, a, cg, false, false, true, true>), gr, tb, 0, st, dout, w, nullptr, w, nullptr, B, mask, dres, din, geo); \
@@ -1753,12 +1757,14 @@ static WgGeo wgrad_geo(int B, int H, int W, int ci, int co) {
 }
 int g_drq_legacy = [] {  // MTSAC_DRQ_LEGACY=mask in the environment: the same selection (A/B runs)
   const char* e = getenv("MTSAC_DRQ_LEGACY");
-  return e ? (atoi(e) & 7) : 0;
+  return e ? (atoi(e) & 15) : 0;
 }();
 // Measured per shape (profiles/r6l_drq/conv_bench.txt, batch 256): the row-tile weight grad wins from
 // 21 x 21 up (84 x 84 4 -> 8: 41.5 vs 90.1 us) and loses at 11 x 11 (15.5 vs 9.7: one tile per block,
 // where the pixel-group tree is most of the work), so it runs for W >= 16
-static bool wgrad_rows(const WgGeo& g) { return g.R > 0 && g.W >= 16 && !(g_drq_mfma & 4) && !(g_drq_legacy & 4); }
+static bool wgrad_rows(const WgGeo& g) {
+  return g.R > 0 && (g.W >= 16 || (g_drq_legacy & 8)) && !(g_drq_mfma & 4) && !(g_drq_legacy & 4);
+}
 static int wgrad_cap(const WgGeo& g) {  // grid cap: 1024 at 84 x 84 (35.6 vs 41.5 us at 512), else 512
   return g_drq_wg_blocks > 0 ? g_drq_wg_blocks : (g.W >= 64 ? 1024 : 512);
 }
