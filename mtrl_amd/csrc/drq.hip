@@ -60,30 +60,47 @@ __global__ void augment3_kernel(const unsigned char* __restrict__ obs, const int
                                 const float* __restrict__ noise_o, const unsigned char* __restrict__ nobs,
                                 const int* __restrict__ crop_n, const float* __restrict__ noise_n,
                                 float* __restrict__ out, int B, int C, int H, int W, int pad) {
-  const int n = B * H * W * C;  // < 2^31 (checked at drq_create)
+  // one lane per output pixel (all C channels: one index decomposition, C byte loads in flight, a
+  // float4 store per 4 channels); the arithmetic per element is augment_kernel's
+  const int np = B * H * W;  // B H W C < 2^31 (checked at drq_create)
   int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * n) return;
-  const bool next = i >= n;
-  if (next) i -= n;
+  if (i >= 2 * np) return;
+  const bool next = i >= np;
+  if (next) i -= np;
   const unsigned char* src = next ? nobs : obs;
   const int* crop = next ? crop_n : crop_o;
   const float* noise = next ? noise_n : noise_o;
-  int r = i / C;
-  const int c = i - r * C;
-  int r2 = r / W;
-  const int x = r - r2 * W;
-  r = r2 / H;
-  const int y = r2 - r * H;
-  const int b = r;
+  int r = i / W;
+  const int x = i - r * W;
+  const int b = r / H;
+  const int y = r - b * H;
   const int sy = min(max(y + crop[2 * b] - pad, 0), H - 1);
   const int sx = min(max(x + crop[2 * b + 1] - pad, 0), W - 1);
-  const float v = (float)src[(((long long)b * C + c) * H + sy) * W + sx];
-  const float o = ((v / 255.0f - 0.5f) * 2.0f) * noise[b];
-  if (next) {
-    out[(long long)n + i] = o;
-    out[2LL * n + i] = o;
+  const unsigned char* sp = src + ((long long)b * C * H + sy) * W + sx;  // channel c at sp + c H W
+  const float f = noise[b];
+  const long long o = (long long)i * C, n = (long long)np * C;
+  auto put = [&](long long k, float v) {
+    if (next) {
+      out[n + k] = v;
+      out[2 * n + k] = v;
+    } else {
+      out[k] = v;
+    }
+  };
+  if (C == 4) {
+    float4 v;
+    v.x = (((float)sp[0] / 255.0f - 0.5f) * 2.0f) * f;
+    v.y = (((float)sp[(long long)H * W] / 255.0f - 0.5f) * 2.0f) * f;
+    v.z = (((float)sp[2LL * H * W] / 255.0f - 0.5f) * 2.0f) * f;
+    v.w = (((float)sp[3LL * H * W] / 255.0f - 0.5f) * 2.0f) * f;
+    if (next) {
+      *reinterpret_cast<float4*>(out + n + o) = v;
+      *reinterpret_cast<float4*>(out + 2 * n + o) = v;
+    } else {
+      *reinterpret_cast<float4*>(out + o) = v;
+    }
   } else {
-    out[i] = o;
+    for (int c = 0; c < C; ++c) put(o + c, (((float)sp[(long long)c * H * W] / 255.0f - 0.5f) * 2.0f) * f);
   }
 }
 
@@ -1052,6 +1069,9 @@ __global__ void ln_fwd_kernel(const float* __restrict__ x, const float* __restri
   if (row >= B) return;
   const float* xr = x + (long long)row * ldx;
   float s = 0.f, s2 = 0.f;
+  // unrolled: eight iterations' loads in flight (rolled, each was waited for before the next issued);
+  // the sums keep their order
+#pragma unroll 8
   for (int i = lane; i < F; i += 64) {
     const float v = xr[i] + (xb ? xb[i] : 0.f);
     s += v;
@@ -1062,6 +1082,7 @@ __global__ void ln_fwd_kernel(const float* __restrict__ x, const float* __restri
   const float mu = s / (float)F;
   const float var = fmaxf(s2 / (float)F - mu * mu, 0.f);
   const float r = 1.0f / sqrtf(var + eps);
+#pragma unroll 8
   for (int i = lane; i < F; i += 64) {
     const float v = xr[i] + (xb ? xb[i] : 0.f);
     const float h = (v - mu) * r;
@@ -1081,6 +1102,7 @@ __global__ void ln_bwd_kernel(const float* __restrict__ dy, int lddy, const floa
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= B) return;
   float sg = 0.f, sgx = 0.f;
+#pragma unroll 8
   for (int i = lane; i < F; i += 64) {
     float d = dy[(long long)row * lddy + i];
     if (RELU && !(y[(long long)row * ldy + i] > 0.f)) d = 0.f;
@@ -1091,6 +1113,7 @@ __global__ void ln_bwd_kernel(const float* __restrict__ dy, int lddy, const floa
   sg = wsum(sg) / (float)F;
   sgx = wsum(sgx) / (float)F;
   const float r = rstd[row];
+#pragma unroll 8
   for (int i = lane; i < F; i += 64) {
     float d = dy[(long long)row * lddy + i];
     if (RELU && !(y[(long long)row * ldy + i] > 0.f)) d = 0.f;
@@ -1099,46 +1122,64 @@ __global__ void ln_bwd_kernel(const float* __restrict__ dy, int lddy, const floa
   }
 }
 
-// dscale[i] = sum_b dy xhat, dbias[i] = sum_b dy (masked like ln_bwd): block of 64 columns x 4 row
-// groups (rows g, g + 4, ...), the groups added in order
+// dscale[i] = sum_b dy xhat, dbias[i] = sum_b dy (masked like ln_bwd): block of 16 columns x 16 row
+// groups (rows g, g + 16, ...), the groups added in order
 template <bool RELU>
 __global__ __launch_bounds__(256) void ln_param_grad_kernel(const float* __restrict__ dy, int lddy,
                                                             const float* __restrict__ y, int ldy,
                                                             const float* __restrict__ xhat, int F, int B,
                                                             float* __restrict__ dscale, float* __restrict__ dbias) {
-  __shared__ float red[2][4][64];
-  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + cl;
+  // 16 columns x 16 row groups a block (F / 16 blocks: with 64 columns a block the launch had F / 64
+  // = 8 blocks at F = 512), the groups' partials added in group order
+  __shared__ float red[2][16][16];
+  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + cl;
   float a = 0.f, c = 0.f;
   if (i < F) {
-    for (int b = grp; b < B; b += 4) {
+    auto row = [&](int b) {
       float d = dy[(long long)b * lddy + i];
       if (RELU && !(y[(long long)b * ldy + i] > 0.f)) d = 0.f;
       a += d * xhat[(long long)b * F + i];
       c += d;
+    };
+    if constexpr (RELU) {  // measured: unrolled, this form got slower (7.2 -> 11.7 us), the other faster
+      for (int b = grp; b < B; b += 16) row(b);
+    } else {
+#pragma unroll 8
+      for (int b = grp; b < B; b += 16) row(b);
     }
   }
   red[0][grp][cl] = a;
   red[1][grp][cl] = c;
   __syncthreads();
   if (grp == 0 && i < F) {
-    dscale[i] = ((red[0][0][cl] + red[0][1][cl]) + red[0][2][cl]) + red[0][3][cl];
-    dbias[i] = ((red[1][0][cl] + red[1][1][cl]) + red[1][2][cl]) + red[1][3][cl];
+    float sa = red[0][0][cl], sc = red[1][0][cl];
+    for (int g = 1; g < 16; ++g) {
+      sa += red[0][g][cl];
+      sc += red[1][g][cl];
+    }
+    dscale[i] = sa;
+    dbias[i] = sc;
   }
 }
 
-// column sums (the Dense_0 bias grad) of x[B][ld] over F columns, 4 row groups added in order
+// column sums (the Dense_0 bias grad) of x[B][ld] over F columns, 16 row groups added in order
 __global__ __launch_bounds__(256) void colsum_rows_kernel(const float* __restrict__ x, int ld, int F, int B,
                                                           float* __restrict__ out) {
-  __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + cl;
+  __shared__ float red[16][16];
+  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + cl;
   float s = 0.f;
   if (i < F)
-    for (int b = grp; b < B; b += 4) s += x[(long long)b * ld + i];
+#pragma unroll 8
+    for (int b = grp; b < B; b += 16) s += x[(long long)b * ld + i];
   red[grp][cl] = s;
   __syncthreads();
-  if (grp == 0 && i < F) out[i] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+  if (grp == 0 && i < F) {
+    float v = red[0][cl];
+    for (int g = 1; g < 16; ++g) v += red[g][cl];
+    out[i] = v;
+  }
 }
 
 // ------------------------------------------------------------------ dueling head + C51
@@ -1164,7 +1205,8 @@ __global__ void c51_target_kernel(const float* __restrict__ hc_on, const float* 
   // mean over actions of the advantage (per atom), online and target
   float mon = 0.f, mtg = 0.f;
   if (zl) {
-    for (int a = 0; a < A; ++a) {
+#pragma unroll 6
+    for (int a = 0; a < A; ++a) {  // unrolled: the loads of six actions in flight, sums in order
       mon += on[a * Z + lane] + hb_on[a * Z + lane];
       mtg += tg[a * Z + lane] + hb_tg[a * Z + lane];
     }
@@ -1173,6 +1215,7 @@ __global__ void c51_target_kernel(const float* __restrict__ hc_on, const float* 
   }
   float bestq = -INFINITY;
   int besta = 0;
+#pragma unroll 6
   for (int a = 0; a < A; ++a) {
     const float l = zl ? head_logit(on, hb_on, A, Z, a, lane, mon) : -INFINITY;
     const float mx = wmax(l);
@@ -1215,6 +1258,7 @@ __global__ void q_values_kernel(const float* __restrict__ hc, int ldh, const flo
   const float sup = vmin + (vmax - vmin) / (float)(Z - 1) * (float)lane;
   float madv = 0.f;
   if (zl) {
+#pragma unroll 6
     for (int a = 0; a < A; ++a) madv += h[a * Z + lane] + hb[a * Z + lane];
     madv /= (float)A;
   }
@@ -1242,6 +1286,7 @@ __global__ void c51_loss_kernel(const float* __restrict__ hc, int ldh, const flo
   const bool zl = lane < Z;
   float madv = 0.f;
   if (zl) {
+#pragma unroll 6
     for (int a = 0; a < A; ++a) madv += h[a * Z + lane] + hb[a * Z + lane];
     madv /= (float)A;
   }
@@ -1270,23 +1315,56 @@ __global__ void c51_loss_kernel(const float* __restrict__ hc, int ldh, const flo
 // embedding backward: dE[t] = sum over the task's rows of d(e / (|e| + 1e-8)) / de (rows in order)
 __global__ void embed_bwd_kernel(const float* __restrict__ dfeat, int ldf, int off, const float* __restrict__ emb,
                                  int D, const int* __restrict__ task, int B, float* __restrict__ demb) {
+  // the rows of task t listed once in LDS (all task ids loaded together: read one at a time under
+  // the row loop's branch, each load was waited for), then the same per-row arithmetic in row order
+  __shared__ int rows[1024];
+  __shared__ int nrows;
   const int t = blockIdx.x, lane = threadIdx.x;
   float s = 0.f;
   for (int d = lane; d < D; d += 64) s += emb[t * D + d] * emb[t * D + d];
   s = wsum(s);
   const float n = sqrtf(s), ne = n + 1e-8f;
-  for (int d0 = 0; d0 < D; d0 += 64) {
-    const int d = d0 + lane;
-    float acc = 0.f;
-    for (int b = 0; b < B; ++b) {
-      if (task[b] != t) continue;
-      const float* g = dfeat + (long long)b * ldf + off;
-      float wg = 0.f;
-      for (int k = lane; k < D; k += 64) wg += emb[t * D + k] * g[k];
-      wg = wsum(wg);
-      if (d < D) acc += g[d] / ne - emb[t * D + d] * wg / (n * ne * ne);
+  for (int b0 = 0; b0 < B; b0 += 1024) {
+    const int nb = min(1024, B - b0);
+    if (lane == 0) nrows = 0;
+    __syncthreads();
+    // ordered compaction: each lane owns consecutive rows, a prefix over the lanes' counts
+    const int per = (nb + 63) / 64, lo = min(lane * per, nb), hi = min(lo + per, nb);
+    int cnt = 0;
+    for (int b = lo; b < hi; ++b) cnt += task[b0 + b] == t;
+    int pre = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(pre, o);
+      if (lane >= o) pre += u;
     }
-    if (d < D) demb[t * D + d] = acc;
+    int w = pre - cnt;
+    for (int b = lo; b < hi; ++b)
+      if (task[b0 + b] == t) rows[w++] = b0 + b;
+    if (lane == 63) nrows = pre;
+    __syncthreads();
+    const int m = nrows;
+    // D <= 64 (drq_create): lane d holds element d; four rows' loads and reductions in flight at once,
+    // their contributions added in row order
+    const bool on = lane < D;
+    const float e = on ? emb[t * D + lane] : 0.f;
+    float acc = b0 == 0 || !on ? 0.f : demb[t * D + lane];
+    for (int k2 = 0; k2 < m; k2 += 4) {
+      float gv[4], wg[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* g = dfeat + (long long)rows[min(k2 + u, m - 1)] * ldf + off;
+        gv[u] = on ? g[lane] : 0.f;
+        wg[u] = e * gv[u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) wg[u] = wsum(wg[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k2 + u < m) acc += gv[u] / ne - e * wg[u] / (n * ne * ne);
+    }
+    if (on) demb[t * D + lane] = acc;
+    __syncthreads();
   }
 }
 
@@ -1528,7 +1606,7 @@ void augment(const unsigned char* obs, const int* crop, const float* noise, floa
 
 void augment3(const unsigned char* obs, const int* crop_o, const float* noise_o, const unsigned char* nobs,
               const int* crop_n, const float* noise_n, float* out, int B, int C, int H, int W, int pad, hipStream_t st) {
-  const long long n = 2LL * B * C * H * W;
+  const long long n = 2LL * B * H * W;  // one lane per output pixel of the obs and next-obs halves
   hipLaunchKernelGGL(augment3_kernel, dim3(blocks(n)), dim3(256), 0, st, obs, crop_o, noise_o, nobs, crop_n, noise_n,
                      out, B, C, H, W, pad);
 }
@@ -1889,18 +1967,18 @@ void ln_bwd(const float* dy, int lddy, const float* y, int ldy, const float* xha
   if (relu) {
     hipLaunchKernelGGL(ln_bwd_kernel<true>, dim3((B + 3) / 4), dim3(256), 0, st, dy, lddy, y, ldy, xhat, rstd, scale, F,
                        dx, lddx, B);
-    hipLaunchKernelGGL(ln_param_grad_kernel<true>, dim3((F + 63) / 64), dim3(256), 0, st, dy, lddy, y, ldy, xhat, F,
+    hipLaunchKernelGGL(ln_param_grad_kernel<true>, dim3((F + 15) / 16), dim3(256), 0, st, dy, lddy, y, ldy, xhat, F,
                        B, dscale, dbias);
   } else {
     hipLaunchKernelGGL(ln_bwd_kernel<false>, dim3((B + 3) / 4), dim3(256), 0, st, dy, lddy, y, ldy, xhat, rstd, scale,
                        F, dx, lddx, B);
-    hipLaunchKernelGGL(ln_param_grad_kernel<false>, dim3((F + 63) / 64), dim3(256), 0, st, dy, lddy, y, ldy, xhat, F,
+    hipLaunchKernelGGL(ln_param_grad_kernel<false>, dim3((F + 15) / 16), dim3(256), 0, st, dy, lddy, y, ldy, xhat, F,
                        B, dscale, dbias);
   }
 }
 
 void colsum_rows(const float* x, int ld, int F, int B, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(colsum_rows_kernel, dim3((F + 63) / 64), dim3(256), 0, st, x, ld, F, B, out);
+  hipLaunchKernelGGL(colsum_rows_kernel, dim3((F + 15) / 16), dim3(256), 0, st, x, ld, F, B, out);
 }
 
 void c51_target(const float* hc_on, const float* hc_tg, int ldh, const float* hb_on, const float* hb_tg, int A, int Z,
