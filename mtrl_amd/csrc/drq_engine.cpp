@@ -218,6 +218,17 @@ struct drq_engine {
     drq::q_values(hc_on, NC, p + off_bc, A, Z, cfg.v_min, cfg.v_max, q, n, st);
   }
 
+  // the dense layers' GEMMs: exact fp32 FMAs (gemm_f32), or with MTSAC_DRQ_DENSE=x3 the
+  // fp32-accurate split-bf16 MFMA form (gemm_x3: same contract, error that of an fp32 GEMM)
+  void dense(const GemmParams& gp, GemmKind kind) {
+    static const bool x3 = [] {
+      const char* e = getenv("MTSAC_DRQ_DENSE");
+      return e && std::string(e) == "x3";
+    }();
+    if (x3) gemm_x3(gp, kind, EPI_STORE, 1, st);
+    else gemm_f32(gp, kind, EPI_STORE, 1, st);
+  }
+
   // C[M][N] = A . op(B) with split-K over the few row tiles a batch of 256 gives (EPI_STORE)
   void gemm_store(const float* Aop, int lda, const float* Bop, int ldb, float* C, int ldc, int M, int N, int K,
                   GemmKind kind) {
@@ -228,7 +239,7 @@ struct drq_engine {
     gp.M = M; gp.N = N; gp.K = K;
     gp.splits = gemm_splits(M, N, K, 1);
     gp.ws = ws;
-    gemm_f32(gp, kind, EPI_STORE, 1, st);
+    dense(gp, kind);
   }
 
   void wgrad_gemm(const float* Aop, int lda, const float* Bop, int ldb, float* C, float* db, int M, int N) {
@@ -240,7 +251,7 @@ struct drq_engine {
     gp.M = M; gp.N = N; gp.K = B;
     gp.splits = gemm_splits(M, N, B, 1);
     gp.ws = ws;
-    gemm_f32(gp, GEMM_TN, EPI_STORE, 1, st);
+    dense(gp, GEMM_TN);
   }
 
   // ------------------------------------------------------------------ replay
