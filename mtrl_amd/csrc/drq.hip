@@ -696,6 +696,154 @@ __global__ __launch_bounds__(256) void conv_rows_kernel(const float* __restrict_
   }
 }
 
+// ------------------------------------------------------------------ convolutions on split2h MFMA
+// Forward and data gradient of the 8- and 16-channel convs as implicit GEMMs on v_mfma_f32_16x16x32_f16
+// with the split2h planes of the SAC path (gemm_common.h: x 2^e = h + l in fp16, products h l, l h, h h,
+// fp32 accumulation; the dropped l l is <= 2^-22 relative).  One block = one row tile (conv_rows_kernel's
+// geometry); its R + 2 input rows are loaded, their max |x| taken over the block and the tile's
+// exponent chosen from it, then split ONCE into two fp16 planes in LDS ([plane][row][column][channel],
+// zero-padded) -- the nine taps read the planes at shifted offsets, so nothing is split twice.  The
+// weights' exponent comes from their max |w| (each block reads all of them) and every lane holds
+// its B fragments (k-slices of 32 = taps x channels, N = 16 output channels, zero past 9 KI and KO)
+// split in registers for the whole block.  A lane's A fragment of M-tile m, slice s: pixel 16 m +
+// (lane & 15), k = 32 s + 8 (lane >> 4) .. + 7 = 8 channels of one tap (one ds_read_b128 a plane).
+// The accumulator is unscaled exactly (2^-(ea + ew)) before the bias / residual (FWD) or the ReLU
+// mask / residual gradient (!FWD) is applied.  FWD: X = act(in), KI = ci, KO = co, w[tap][k][n];
+// !FWD: X = dout, KI = co, KO = ci, w[8 - tap][n][k] (the transposed conv).  Not bitwise the VALU
+// kernels (another summation order); held to the float64 oracle like them.
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+typedef float h2acc_t __attribute__((ext_vector_type(4)));
+constexpr int CH_LDS = 6144;   // fp16 elements of one staged plane
+constexpr int CH_SLOTS = 6;    // staged float4 per thread
+__device__ inline int h2_exp(float bound) {  // gemm_common.h plane_exp: |x| 2^e < 2^15
+  bound *= 1.00390625f;
+  if (!(bound > 0.f) || !(bound < 3.0e38f)) return 0;
+  int ex;
+  (void)frexpf(bound, &ex);
+  return min(100, max(-100, 15 - ex));
+}
+__device__ inline void h2_split(float x, float sc, _Float16& h, _Float16& l) {
+  const float y = x * sc;
+  h = (_Float16)y;
+  l = (_Float16)(y - (float)h);
+}
+template <int KI, int KO, bool FWD, bool RELU_IN, bool MASK, bool ADD_RES>
+__global__ __launch_bounds__(256) void conv_h2_kernel(const float* __restrict__ X, const float* __restrict__ w_a,
+                                                      const float* __restrict__ bias_a, const float* __restrict__ w_b,
+                                                      const float* __restrict__ bias_b, int B1,
+                                                      const float* __restrict__ mask, const float* __restrict__ res,
+                                                      float* __restrict__ out, ConvGeo geo) {
+  static_assert(KI == 8 || KI == 16, "input channels");
+  static_assert(KO == 4 || KO == 8 || KO == 16, "output channels");
+  constexpr int NS = (9 * KI + 31) / 32;  // k-slices
+  __shared__ __attribute__((aligned(16))) _Float16 sh[2][CH_LDS];
+  __shared__ float red[2][4];
+  const int H = geo.H, W = geo.W, R = geo.R, WP = W + 2;
+  const int b = (int)blockIdx.x / geo.n, y0 = ((int)blockIdx.x - b * geo.n) * R;
+  const long long p0 = ((long long)b * H + y0) * W;
+  const float* __restrict__ w = (FWD && b >= B1) ? w_b : w_a;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // 1. the tile's rows y0 - 1 .. y0 + R into registers (zero outside the image), their max |x|
+  const int NSL = (R + 2) * WP * (KI / 4);
+  const float* base = X + p0 * KI;
+  float4 v[CH_SLOTS];
+  int lo[CH_SLOTS];
+  float mx = 0.f, mw = 0.f;
+#pragma unroll
+  for (int k = 0; k < CH_SLOTS; ++k) {
+    const int s = t + 256 * k;
+    const int c = s % (KI / 4), u = s / (KI / 4);
+    const int i = __umulhi((unsigned)u, geo.magic2), j = u - i * WP;
+    const int yy = y0 + i - 1, xx = j - 1;
+    const bool ok = s < NSL && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+    const float4 q = *reinterpret_cast<const float4*>(ok ? base + ((long long)(i - 1) * W + xx) * KI + 4 * c : base);
+    float4 x4 = ok ? q : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (RELU_IN) x4 = make_float4(fmaxf(x4.x, 0.f), fmaxf(x4.y, 0.f), fmaxf(x4.z, 0.f), fmaxf(x4.w, 0.f));
+    v[k] = x4;
+    lo[k] = s < NSL ? (i * WP + j) * KI + 4 * c : -1;
+    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(x4.x), fabsf(x4.y)), fmaxf(fabsf(x4.z), fabsf(x4.w))));
+  }
+  for (int e = t; e < 9 * KI * KO; e += 256) mw = fmaxf(mw, fabsf(w[e]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = fmaxf(mx, __shfl_xor(mx, o));
+    mw = fmaxf(mw, __shfl_xor(mw, o));
+  }
+  if (lane == 0) {
+    red[0][wv] = mx;
+    red[1][wv] = mw;
+  }
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+  mw = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+  const int ea = h2_exp(mx), ew = h2_exp(mw);
+  const float sa = ldexpf(1.f, ea), sw = ldexpf(1.f, ew), unscale = ldexpf(1.f, -(ea + ew));
+  // 2. split once into the LDS planes
+#pragma unroll
+  for (int k = 0; k < CH_SLOTS; ++k) {
+    if (lo[k] < 0) continue;
+    _Float16 h0, l0, h1, l1, h2, l2, h3, l3;
+    h2_split(v[k].x, sa, h0, l0);
+    h2_split(v[k].y, sa, h1, l1);
+    h2_split(v[k].z, sa, h2, l2);
+    h2_split(v[k].w, sa, h3, l3);
+    typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<h4_t*>(&sh[0][lo[k]]) = h4_t{h0, h1, h2, h3};
+    *reinterpret_cast<h4_t*>(&sh[1][lo[k]]) = h4_t{l0, l1, l2, l3};
+  }
+  // 3. the B fragments: lane holds B[k = 32 s + 8 (lane >> 4) + e][n = lane & 15], e < 8
+  const int n = lane & 15, kq = 8 * (lane >> 4);
+  h8_t bh[NS], bl[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 32 * s + kq + e, tap = k / KI, c = k % KI;
+      float wk = 0.f;
+      if (k < 9 * KI && n < KO) wk = FWD ? w[(tap * KI + c) * KO + n] : w[((8 - tap) * KO + n) * KI + c];
+      _Float16 hh, ll;
+      h2_split(wk, sw, hh, ll);
+      bh[s][e] = hh;
+      bl[s][e] = ll;
+    }
+  }
+  __syncthreads();
+  // 4. 16-pixel M-tiles, round robin over the waves
+  const int npx = R * W, nmt = (npx + 15) / 16;
+  for (int mt = wv; mt < nmt; mt += 4) {
+    const int q = min(16 * mt + (lane & 15), npx - 1);
+    const int r = __umulhi((unsigned)q, geo.magic), x = q - r * W;
+    h2acc_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int kb = 32 * s + kq;
+      const int tap = min(kb / KI, 8), c0 = kb % KI;  // tap 9..: zero weights, any finite A
+      const int off = ((r + tap / 3) * WP + x + tap % 3) * KI + c0;
+      const h8_t ah = *reinterpret_cast<const h8_t*>(&sh[0][off]);
+      const h8_t al = *reinterpret_cast<const h8_t*>(&sh[1][off]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[s], acc, 0, 0, 0);
+    }
+    // lane holds C[pixel 16 mt + 4 (lane >> 4) + i][channel lane & 15]
+    if (n < KO) {
+      const float bn = FWD ? ((b >= B1) ? bias_b : bias_a)[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qq = 16 * mt + 4 * (lane >> 4) + i;
+        if (qq >= npx) continue;
+        const int rr = __umulhi((unsigned)qq, geo.magic), xx = qq - rr * W;
+        if (y0 + rr >= H) continue;
+        const long long o = (p0 + (long long)rr * W + xx) * KO + n;
+        float val = acc[i] * unscale + bn;
+        if (MASK && !(mask[o] > 0.f)) val = 0.f;
+        if (ADD_RES) val += res[o];
+        out[o] = val;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ convolutions on f32 MFMA
 // v_mfma_f32_16x16x4_f32 (exact fp32: bit for bit a k-ordered fmaf chain, MI355X_MICROARCH.md) at the
 // FP32 rate, which the VALU kernels above reach only with packed FMAs fed from SGPRs; here the VALU
@@ -1681,6 +1829,24 @@ static bool conv_rows_on(int ng, int forced_group, int bit) {
   return ng > 0 && forced_group == 0 && !(g_drq_mfma & bit) && !(g_drq_legacy & bit);
 }
 
+// split2h MFMA geometry (conv_h2_kernel): the tallest balanced row tile whose two fp16 planes fit
+// CH_LDS (the staging slots then fit too); R = 0 (the VALU kernels) for W < 2 or too wide a row
+static ConvGeo conv_h2_geo(int H, int W, int KI) {
+  ConvGeo g{H, W, 0, 0, 0, 0u, 0u};
+  if (W < 2) return g;
+  const int R = std::min(H, CH_LDS / ((W + 2) * KI) - 2);
+  if (R < 1) return g;
+  g.n = (H + R - 1) / R;
+  g.R = (H + g.n - 1) / g.n;
+  g.magic = (unsigned)((0x100000000ULL + (unsigned)W - 1) / (unsigned)W);
+  g.magic2 = (unsigned)((0x100000000ULL + (unsigned)W + 1) / (unsigned)(W + 2));
+  return g;
+}
+// the split2h MFMA convs (legacy bit 16 off: the VALU kernels)
+static bool conv_h2_on(const ConvGeo& g, int bit) {
+  return g.R > 0 && !(g_drq_legacy & 16) && !(g_drq_legacy & bit) && !(g_drq_mfma & bit);
+}
+
 void conv_fwd(const float* in, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
               int ci, int co, bool relu_in, hipStream_t st, const float* w2, const float* bias2, int B1) {
   const long long npix = (long long)B * H * W;
@@ -1689,6 +1855,22 @@ void conv_fwd(const float* in, const float* w, const float* bias, const float* r
     w2 = w;
     bias2 = bias;
     B1 = B;
+  }
+  if (ci >= 8 && g_drq_fwd_g == 0) {
+    const ConvGeo geo = conv_h2_geo(H, W, ci);
+    if (conv_h2_on(geo, 1)) {
+      const dim3 gr((unsigned)(B * geo.n)), tb(256);
+#define C_FH(a, b)                                                                                                   \
+  if (ci == a && co == b) {                                                                                          \
+    if (relu_in && res) hipLaunchKernelGGL((conv_h2_kernel<a, b, true, true, false, true>), gr, tb, 0, st, in, w, bias, w2, bias2, B1, nullptr, res, out, geo); \
+    else if (relu_in) hipLaunchKernelGGL((conv_h2_kernel<a, b, true, true, false, false>), gr, tb, 0, st, in, w, bias, w2, bias2, B1, nullptr, res, out, geo); \
+    else if (res) hipLaunchKernelGGL((conv_h2_kernel<a, b, true, false, false, true>), gr, tb, 0, st, in, w, bias, w2, bias2, B1, nullptr, res, out, geo); \
+    else hipLaunchKernelGGL((conv_h2_kernel<a, b, true, false, false, false>), gr, tb, 0, st, in, w, bias, w2, bias2, B1, nullptr, res, out, geo); \
+    return;                                                                                                          \
+  }
+      C_FH(8, 8) C_FH(8, 16) C_FH(16, 16)
+#undef C_FH
+    }
   }
   {
     int ng = 0;
@@ -1749,6 +1931,22 @@ void conv_fwd(const float* in, const float* w, const float* bias, const float* r
 void conv_bwd_data(const float* dout, const float* w, const float* mask, const float* dres, float* din, int B, int H,
                    int W, int ci, int co, hipStream_t st) {
   const long long npix = (long long)B * H * W;
+  if (co >= 8 && g_drq_bwd_g == 0) {  // the transposed conv on split2h MFMA: KI = co, KO = ci
+    const ConvGeo geo = conv_h2_geo(H, W, co);
+    if (conv_h2_on(geo, 2)) {
+      const dim3 gr((unsigned)(B * geo.n)), tb(256);
+#define C_BH(a, b)                                                                                                   \
+  if (ci == a && co == b) {                                                                                          \
+    if (mask && dres) hipLaunchKernelGGL((conv_h2_kernel<b, a, false, false, true, true>), gr, tb, 0, st, dout, w, nullptr, w, nullptr, B, mask, dres, din, geo); \
+    else if (mask) hipLaunchKernelGGL((conv_h2_kernel<b, a, false, false, true, false>), gr, tb, 0, st, dout, w, nullptr, w, nullptr, B, mask, dres, din, geo); \
+    else if (dres) hipLaunchKernelGGL((conv_h2_kernel<b, a, false, false, false, true>), gr, tb, 0, st, dout, w, nullptr, w, nullptr, B, mask, dres, din, geo); \
+    else hipLaunchKernelGGL((conv_h2_kernel<b, a, false, false, false, false>), gr, tb, 0, st, dout, w, nullptr, w, nullptr, B, mask, dres, din, geo); \
+    return;                                                                                                          \
+  }
+      C_BH(4, 8) C_BH(8, 8) C_BH(8, 16) C_BH(16, 16)
+#undef C_BH
+    }
+  }
   {  // the transposed conv: KI = co (dout channels), KO = ci
     int ng = 0;
     const ConvGeo geo = conv_geo(H, W, co, ci, &ng);
@@ -1835,7 +2033,7 @@ static WgGeo wgrad_geo(int B, int H, int W, int ci, int co) {
 }
 int g_drq_legacy = [] {  // MTSAC_DRQ_LEGACY=mask in the environment: the same selection (A/B runs)
   const char* e = getenv("MTSAC_DRQ_LEGACY");
-  return e ? (atoi(e) & 15) : 0;
+  return e ? (atoi(e) & 31) : 0;
 }();
 // Measured per shape (profiles/r6l_drq/conv_bench.txt, batch 256): the row-tile weight grad wins from
 // 21 x 21 up (84 x 84 4 -> 8: 41.5 vs 90.1 us) and loses at 11 x 11 (15.5 vs 9.7: one tile per block,

@@ -146,7 +146,7 @@ def test_row_tile_convs_match_the_pixel_kernels(hw, B):
     out = {}
     old = lib.mtsac_debug_drq_legacy(-1)
     try:
-        for mask in (7, 0):
+        for mask in (7 | 16, 16):  # 16: no split2h MFMA convs in either arm (their own test below)
             lib.mtsac_debug_drq_legacy(mask)
             e = _engine(cfg, B)
             e.set_params(L.DRQ_PARAMS, st.params)
@@ -157,7 +157,7 @@ def test_row_tile_convs_match_the_pixel_kernels(hw, B):
             e.close()
     finally:
         lib.mtsac_debug_drq_legacy(old)
-    (l_old, g_old), (l_new, g_new) = out[7], out[0]
+    (l_old, g_old), (l_new, g_new) = out[7 | 16], out[16]
     for k in ("losses/online_logits", "losses/critic_loss"):
         assert l_old[k] == l_new[k], (k, l_old, l_new)
     o = 0
@@ -170,6 +170,48 @@ def test_row_tile_convs_match_the_pixel_kernels(hw, B):
             assert np.abs(a - b).max() <= 2e-5 * scale, (path, float(np.abs(a - b).max()), scale)
         else:
             np.testing.assert_array_equal(a, b, err_msg=path)
+
+
+@pytest.mark.parametrize("hw,B", [(20, 8), (84, 16), (84, 256)], ids=["small", "reference_geometry", "b256"])
+def test_split2h_convs_match_the_fp32_kernels(hw, B):
+    """Round 6: the 8- and 16-channel conv forwards and data grads on split2h MFMA (drq.hip
+    conv_h2_kernel, the default) against the fp32 VALU kernels (mtsac_debug_drq_legacy(16)) on one
+    update: losses within 1e-5 relative, every gradient leaf within 1e-4 of its largest entry (conv
+    leaves 1e-3: a conv bias gradient is a sum over B x H x W pixels with heavy cancellation, where
+    two fp32-accurate summation orders differ by up to ~3e-4 of the leaf max at b256).  The strict bar
+    is test_update_matches_oracle's, which holds the default (split2h) path to the float64 oracle:
+    elementwise Sum|terms| floors and the error norm <= 4x a PyTorch fp32 evaluation's."""
+    from mtrl_amd import _lib as L
+
+    lib = L.load()
+    cfg = od.DrQConfig(hw=hw, n_hidden=64 if hw == 20 else 512)
+    st = od.init_state(cfg, 7)
+    batch, aug = _batch(cfg, B, 8)
+    out = {}
+    old = lib.mtsac_debug_drq_legacy(-1)
+    try:
+        for mask in (16, 0):
+            lib.mtsac_debug_drq_legacy(mask)
+            e = _engine(cfg, B)
+            e.set_params(L.DRQ_PARAMS, st.params)
+            e.set_params(L.DRQ_TARGET, st.params)
+            e.update(batch, aug)
+            e.synchronize()
+            out[mask] = (e.logs(), e.get_params(L.DRQ_GRAD).astype(np.float64))
+            e.close()
+    finally:
+        lib.mtsac_debug_drq_legacy(old)
+    (l32, g32), (lh, gh) = out[16], out[0]
+    for k, v in l32.items():
+        assert abs(lh[k] - v) <= 1e-5 * max(1.0, abs(v)), (k, lh[k], v)
+    o = 0
+    for path, shape in od.param_spec(cfg):
+        n = int(np.prod(shape))
+        a, b = gh[o:o + n], g32[o:o + n]
+        o += n
+        scale = float(np.abs(b).max()) + 1e-30
+        tol = 1e-3 if "Conv" in path else 1e-4
+        assert np.abs(a - b).max() <= tol * scale, (path, float(np.abs(a - b).max()), scale)
 
 
 @pytest.mark.parametrize("kind", [0, 1, 2], ids=["forward", "data_grad", "weight_grad"])

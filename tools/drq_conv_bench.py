@@ -1,6 +1,6 @@
 """Per-launch time of every DrQ conv pass at the benched geometry (batch 256, 84x84, IMPALA scale 1):
-the default per-shape choice, the row-tile kernels everywhere and the pre-round-6 ones, in one
-process (mtsac_debug_drq_conv_bench / mtsac_debug_drq_legacy).
+the default per-shape choice, the VALU kernels' per-shape choice (mask 16: no split2h MFMA) and the
+pre-round-6 kernels (mask 7), in one process (mtsac_debug_drq_conv_bench / mtsac_debug_drq_legacy).
 usage: drq_conv_bench.py [iters] [--wg-sweep]"""
 import ctypes
 import os
@@ -16,12 +16,12 @@ B = 256
 shapes = [(3 * B, 84, 4, 8), (3 * B, 42, 8, 8), (3 * B, 42, 8, 16), (3 * B, 21, 16, 16), (3 * B, 11, 16, 16)]
 names = ("forward", "data_grad", "weight_grad")
 us = ctypes.c_double()
-print(f"{'pass':12s} {'B':>4s} {'HxW':>6s} {'ci->co':>7s} {'default':>8s} {'rows us':>8s} {'legacy us':>9s}  GFMA/s(default)")
+print(f"{'pass':12s} {'B':>4s} {'HxW':>6s} {'ci->co':>7s} {'default':>8s} {'VALU us':>8s} {'legacy us':>9s}  GFMA/s(default)")
 for kind in (0, 1, 2):
     for nb, h, ci, co in shapes:
         b = nb if kind == 0 else B
         row = []
-        for legacy in (0, 8, 7):
+        for legacy in (0, 16, 7):
             lib.mtsac_debug_drq_legacy(legacy)
             rc = lib.mtsac_debug_drq_conv_bench(kind, b, h, h, ci, co, it, ctypes.byref(us))
             assert rc == 0, rc
