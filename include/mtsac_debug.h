@@ -70,7 +70,8 @@ int mtsac_debug_drq_groups(int fwd, int bwd);
 int mtsac_debug_drq_mfma(int mask);
 // The pre-round-6 DrQ conv kernels (one lane per pixel, im2col weight grad) instead of the row-tile
 // ones: bit 1 forward, 2 data grad, 4 weight grad; bit 8 runs the row-tile kernels at every shape
-// (past the measured per-shape choice).  Returns the previous mask; < 0 queries.
+// (past the measured per-shape choice); bit 16 turns the split2h MFMA convs off, bit 32 runs them at
+// every shape they support.  Returns the previous mask; < 0 queries.
 int mtsac_debug_drq_legacy(int mask);
 // The row-tile conv weight grad's grid cap (> 0 sets, 0 restores the per-shape default, < 0 queries;
 // returns the previous).  Engines size their partial buffers at creation: change it only before

@@ -480,7 +480,7 @@ int mtsac_debug_drq_mfma(int mask) {
 // returns the previous mask (< 0: query only)
 int mtsac_debug_drq_legacy(int mask) {
   const int old = drq::g_drq_legacy;
-  if (mask >= 0) drq::g_drq_legacy = mask & 31;
+  if (mask >= 0) drq::g_drq_legacy = mask & 63;
   return old;
 }
 

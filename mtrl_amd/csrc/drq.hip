@@ -1842,9 +1842,15 @@ static ConvGeo conv_h2_geo(int H, int W, int KI) {
   g.magic2 = (unsigned)((0x100000000ULL + (unsigned)W + 1) / (unsigned)(W + 2));
   return g;
 }
-// the split2h MFMA convs (legacy bit 16 off: the VALU kernels)
-static bool conv_h2_on(const ConvGeo& g, int bit) {
-  return g.R > 0 && !(g_drq_legacy & 16) && !(g_drq_legacy & bit) && !(g_drq_mfma & bit);
+// the split2h MFMA convs (legacy bit 16: the VALU kernels).  Measured per shape (batch 256,
+// profiles/r6w_drq_h2/conv_bench.txt, us per launch, split2h vs the VALU choice): they win with 16
+// input channels on the small images (forward 21 x 21: 27.3 vs 30.7, 11 x 11: 9.5 vs 9.9; data grad
+// 11.9 vs 14.0, 7.2 vs 8.0) and lose elsewhere (42 x 42 8 -> 8 forward 46.5 vs 30.1; the data grads
+// at 42 and 84: 22-58 vs 14-32): the per-block weight gather and split and the staging's max
+// reduction cost more than the MFMAs save there.  They run for KI = 16, W <= 32.
+static bool conv_h2_on(const ConvGeo& g, int KI, int bit) {
+  const bool shape = (KI == 16 && g.W <= 32) || (g_drq_legacy & 32);  // bit 32: every supported shape
+  return g.R > 0 && shape && !(g_drq_legacy & 16) && !(g_drq_legacy & bit) && !(g_drq_mfma & bit);
 }
 
 void conv_fwd(const float* in, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
@@ -1858,7 +1864,7 @@ void conv_fwd(const float* in, const float* w, const float* bias, const float* r
   }
   if (ci >= 8 && g_drq_fwd_g == 0) {
     const ConvGeo geo = conv_h2_geo(H, W, ci);
-    if (conv_h2_on(geo, 1)) {
+    if (conv_h2_on(geo, ci, 1)) {
       const dim3 gr((unsigned)(B * geo.n)), tb(256);
 #define C_FH(a, b)                                                                                                   \
   if (ci == a && co == b) {                                                                                          \
@@ -1933,7 +1939,7 @@ void conv_bwd_data(const float* dout, const float* w, const float* mask, const f
   const long long npix = (long long)B * H * W;
   if (co >= 8 && g_drq_bwd_g == 0) {  // the transposed conv on split2h MFMA: KI = co, KO = ci
     const ConvGeo geo = conv_h2_geo(H, W, co);
-    if (conv_h2_on(geo, 2)) {
+    if (conv_h2_on(geo, co, 2)) {
       const dim3 gr((unsigned)(B * geo.n)), tb(256);
 #define C_BH(a, b)                                                                                                   \
   if (ci == a && co == b) {                                                                                          \
@@ -2033,7 +2039,7 @@ static WgGeo wgrad_geo(int B, int H, int W, int ci, int co) {
 }
 int g_drq_legacy = [] {  // MTSAC_DRQ_LEGACY=mask in the environment: the same selection (A/B runs)
   const char* e = getenv("MTSAC_DRQ_LEGACY");
-  return e ? (atoi(e) & 31) : 0;
+  return e ? (atoi(e) & 63) : 0;
 }();
 // Measured per shape (profiles/r6l_drq/conv_bench.txt, batch 256): the row-tile weight grad wins from
 // 21 x 21 up (84 x 84 4 -> 8: 41.5 vs 90.1 us) and loses at 11 x 11 (15.5 vs 9.7: one tile per block,

@@ -34,7 +34,8 @@ extern int g_drq_fwd_g, g_drq_bwd_g;  // conv channel groups per lane, 0: the en
 extern int g_drq_mfma;  // f32-MFMA convs (experiment): bit 1 forward, 2 data grad, 4 weight grad (default 0)
 // the pre-round-6 conv kernels (one lane per pixel; im2col weight grad) instead of the row-tile
 // ones: bit 1 forward, 2 data grad, 4 weight grad; bit 8: the row-tile kernels at every shape (past
-// the measured per-shape choice) where bits 1-4 are clear (default 0; tests and A/B)
+// the measured per-shape choice) where bits 1-4 are clear; bit 16: no split2h MFMA convs; bit 32: the
+// split2h MFMA convs at every shape they support (default 0; tests and A/B)
 extern int g_drq_legacy;
 extern int g_drq_wg_blocks;  // the row-tile weight grad's grid cap (experiments; set before an engine exists)
 double conv_bench(int kind, int B, int H, int W, int ci, int co, int iters);

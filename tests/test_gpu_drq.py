@@ -175,8 +175,8 @@ def test_row_tile_convs_match_the_pixel_kernels(hw, B):
 @pytest.mark.parametrize("hw,B", [(20, 8), (84, 16), (84, 256)], ids=["small", "reference_geometry", "b256"])
 def test_split2h_convs_match_the_fp32_kernels(hw, B):
     """Round 6: the 8- and 16-channel conv forwards and data grads on split2h MFMA (drq.hip
-    conv_h2_kernel, the default) against the fp32 VALU kernels (mtsac_debug_drq_legacy(16)) on one
-    update: losses within 1e-5 relative, every gradient leaf within 1e-4 of its largest entry (conv
+    conv_h2_kernel; the default for 16 input channels at W <= 32, here forced everywhere) against the
+    fp32 VALU kernels (mtsac_debug_drq_legacy(16)) on one update: losses within 1e-5 relative, every gradient leaf within 1e-4 of its largest entry (conv
     leaves 1e-3: a conv bias gradient is a sum over B x H x W pixels with heavy cancellation, where
     two fp32-accurate summation orders differ by up to ~3e-4 of the leaf max at b256).  The strict bar
     is test_update_matches_oracle's, which holds the default (split2h) path to the float64 oracle:
@@ -190,7 +190,7 @@ def test_split2h_convs_match_the_fp32_kernels(hw, B):
     out = {}
     old = lib.mtsac_debug_drq_legacy(-1)
     try:
-        for mask in (16, 0):
+        for mask in (16, 32):  # 32: the split2h convs at every shape they support (default: 16 ch, W <= 32)
             lib.mtsac_debug_drq_legacy(mask)
             e = _engine(cfg, B)
             e.set_params(L.DRQ_PARAMS, st.params)
@@ -201,7 +201,7 @@ def test_split2h_convs_match_the_fp32_kernels(hw, B):
             e.close()
     finally:
         lib.mtsac_debug_drq_legacy(old)
-    (l32, g32), (lh, gh) = out[16], out[0]
+    (l32, g32), (lh, gh) = out[16], out[32]
     for k, v in l32.items():
         assert abs(lh[k] - v) <= 1e-5 * max(1.0, abs(v)), (k, lh[k], v)
     o = 0
