@@ -763,7 +763,11 @@ __global__ __launch_bounds__(256) void conv_h2_kernel(const float* __restrict__ 
     lo[k] = s < NSL ? (i * WP + j) * KI + 4 * c : -1;
     mx = fmaxf(mx, fmaxf(fmaxf(fabsf(x4.x), fabsf(x4.y)), fmaxf(fabsf(x4.z), fabsf(x4.w))));
   }
-  for (int e = t; e < 9 * KI * KO; e += 256) mw = fmaxf(mw, fabsf(w[e]));
+#pragma unroll
+  for (int e0 = 0; e0 < 9 * KI * KO; e0 += 256) {  // unrolled: the weight loads in flight together
+    const int e = min(e0 + t, 9 * KI * KO - 1);
+    mw = fmaxf(mw, fabsf(w[e]));
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     mx = fmaxf(mx, __shfl_xor(mx, o));
